@@ -1,0 +1,212 @@
+/*
+ * scd.h — C-ABI of the MI355X (gfx950) Siamese change-detection kernel library (libscd.so).
+ *
+ * The reference (SebastianHafner/multimodal_siamese_cd) has no native code and no FFI: its hot path
+ * is the torch module stack in utils/networks.py (DoubleConv 386-402, InConv 405-412, Down 415-426,
+ * Up 429-451, OutConv 454-461, SiameseUNet.forward 139-154) and power_jaccard_loss
+ * (utils/loss_functions.py:141-150).  Every aten op those modules call is replaced by one entry
+ * point below; the "replaces" line of each cites the reference call site.  The Python host layer
+ * (multimodal_siamese_cd_amd/hip.py, ctypes) binds exactly these symbols.
+ *
+ * Conventions
+ *  - Every function returns int: 0 = ok, negative = error; scd_last_error() (thread-local) has text.
+ *  - Activations are NHWC fp32.  An scd_nhwc_t is a *channel slice* view: element (n,y,x,c) lives at
+ *    data[((n*h + y)*w + x)*ldc + c].  data must be 16-byte aligned, c and ldc multiples of 4.
+ *  - The library never allocates, frees or synchronises.  Workspaces are caller-owned (torch caching
+ *    allocator); size them with the *_workspace_bytes() queries.  All launches are asynchronous on the
+ *    caller's stream (a hipStream_t passed as void*; NULL = legacy default stream).
+ *  - Stateless and re-entrant; one GPU per process.
+ */
+#ifndef SCD_H_
+#define SCD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *scd_stream_t; /* hipStream_t */
+
+enum scd_status {
+    SCD_OK = 0,
+    SCD_ERR_ARG = -1,         /* bad shape / null pointer / unsupported combination   */
+    SCD_ERR_ALIGN = -2,       /* pointer or channel stride not 16-byte aligned          */
+    SCD_ERR_LAUNCH = -3,      /* hipGetLastError() after launch                         */
+    SCD_ERR_DEVICE = -4,      /* device is not gfx950                                   */
+    SCD_ERR_WORKSPACE = -5,   /* workspace too small                                    */
+};
+
+/* NHWC channel-slice view. */
+typedef struct scd_nhwc {
+    void *data;
+    int32_t n, h, w, c, ldc;
+} scd_nhwc_t;
+
+/* ---------------------------------------------------------------------------------------------
+ * Info
+ * ------------------------------------------------------------------------------------------- */
+const char *scd_version(void);
+const char *scd_last_error(void);
+/* 0 if `device` is a gfx950 (MI355X); SCD_ERR_DEVICE otherwise. */
+int scd_device_check(int device);
+
+/* ---------------------------------------------------------------------------------------------
+ * Layout / weight packing
+ * ------------------------------------------------------------------------------------------- */
+/* dst[n, y, x, 0:c_count] = src[n, c_begin:c_begin+c_count, y, x]  (NCHW -> NHWC slice);
+ * dst[n, y, x, c_count:dst.c] = 0 (channel padding to the MFMA K granule).
+ * replaces: the .to(device) input hand-off + implicit NCHW layout (train_supervised.py:68-69) and
+ * the channel slicing/concats of DualStreamUNet/WhateverNet (networks.py:105-106,113-114,236,247). */
+int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, int32_t w, int32_t c_begin,
+                  int32_t c_count, scd_nhwc_t dst, scd_stream_t stream);
+
+/* Conv2d 3x3 weight OIHW [co][ci][3][3] ->
+ *   mode 0 (forward):   [co][9][ci_pad]           (zero for ci >= ci)
+ *   mode 1 (data grad): [ci][9][co], taps flipped (W[co][ci][2-ky][2-kx])
+ * replaces: nn.Conv2d(in,out,3,padding=1) parameter layout (networks.py:392,395). */
+int scd_pack_conv3x3(const float *w, int32_t co, int32_t ci, int32_t ci_pad, int32_t mode, float *out,
+                     scd_stream_t stream);
+
+/* ConvTranspose2d weight [ci][co][2][2] ->
+ *   mode 0 (forward):   [(i*2+j)*co + o][ci]
+ *   mode 1 (data grad): [ci][(i*2+j)*co + o]
+ * replaces: nn.ConvTranspose2d(C,C,2,stride=2) parameter layout (networks.py:433). */
+int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, float *out, scd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+ *   out[m, o] = bias[o] + sum_{t<ntaps, c<src.c} src[img, oy*stride+dy[t], ox*stride+dx[t], c] * wpk[o][t*src.c + c]
+ *   m = (img, oy, ox) over src.n x out_h x out_w; out-of-range source pixels read as 0 (zero padding).
+ * store_mode 0: dst[img, oy, ox, o]                            (dst.h == out_h, dst.w == out_w)
+ * store_mode 1: 2x2 pixel shuffle, o = (i*2+j)*co + oc -> dst[img, 2oy+i, 2ox+j, oc], bias[oc]
+ * Used for: Conv2d 3x3 forward (taps -1..1, stride 1), Conv2d 3x3 data-grad (flipped weights),
+ *           ConvTranspose2d forward (1 tap, store_mode 1) and its data-grad (4 taps 0..1, stride 2).
+ * replaces: aten::convolution / mkldnn_convolution (networks.py:392,395,433) and the data-grad half
+ *           of aten::convolution_backward.  `cat([x2, x1], 1)` (networks.py:449) is zero-copy: dst may
+ *           be a channel slice of the concat buffer.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct scd_igemm {
+    scd_nhwc_t src;
+    int32_t out_h, out_w;
+    int32_t stride;
+    int32_t ntaps;
+    int8_t dy[9], dx[9];
+    const float *wpk;   /* [n_out][ntaps*src.c] */
+    int32_t n_out;
+    const float *bias;  /* [n_out] (store_mode 0) or [n_out/4] (store_mode 1) or NULL */
+    scd_nhwc_t dst;
+    int32_t store_mode;
+} scd_igemm_t;
+
+int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Weight gradient (split-K implicit GEMM on fp32 MFMA), deterministic two-stage reduction.
+ *   slab[s][r][t*src.c + c] = sum_{m in split s} rows[m, r] * src[img, oy*stride+dy[t], ox*stride+dx[t], c]
+ *   m = (img, oy, ox) over rows.n x rows.h x rows.w.
+ * Conv2d 3x3: rows = dY, src = X (taps -1..1).  ConvTranspose2d: rows = X, src = dOut (stride 2, taps 0..1).
+ * The Siamese shared encoder runs both branches as one 2B batch, so the two-branch weight-grad
+ * accumulation (networks.py:141-145 shared inc/encoder) is the K-sum itself.
+ * replaces: the weight-grad half of aten::convolution_backward.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct scd_wgrad {
+    scd_nhwc_t rows;
+    scd_nhwc_t src;
+    int32_t stride;
+    int32_t ntaps;
+    int8_t dy[9], dx[9];
+} scd_wgrad_t;
+
+/* Number of K-splits the library will use and the slab bytes it needs. */
+int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes);
+int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream);
+/* Sum the slabs and unpack to the parameter layout.
+ * mode 0: out OIHW [R][c_valid][3][3]  (slab cols (ky*3+kx)*C + c)
+ * mode 1: out ConvT [R][C][2][2]       (slab cols (i*2+j)*C + c)                                  */
+int scd_wgrad_finalize(const float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C, int32_t mode,
+                       int32_t c_valid, float *out, scd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * BatchNorm2d (train: batch statistics per segment; eval: running statistics) + ReLU.
+ * A "segment" is a contiguous range of images normalised as one BN batch: the Siamese encoder runs
+ * t1 and t2 as one 2B buffer with nseg = 2, matching the reference's two separate module calls
+ * (networks.py:141-145) — per-branch batch statistics and two running-stat updates, t1 first.
+ * replaces: aten::native_batch_norm (networks.py:393,396), aten::relu_ (394,397).
+ * ------------------------------------------------------------------------------------------- */
+size_t scd_bn_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t c, int32_t nseg);
+
+/* Batch statistics of y per segment -> save_mean/save_invstd [nseg][C], scale/shift [nseg][C]
+ * (scale = gamma*invstd, shift = beta - mean*scale).  If update_running != 0 the running buffers are
+ * updated once per segment in segment order: r = (1-momentum)*r + momentum*stat (unbiased var). */
+int scd_bn_train_stats(scd_nhwc_t y, int32_t nseg, const float *gamma, const float *beta, float eps,
+                       float momentum, int32_t update_running, float *running_mean, float *running_var,
+                       float *save_mean, float *save_invstd, float *scale, float *shift, void *ws,
+                       size_t ws_bytes, scd_stream_t stream);
+/* Eval: scale/shift [C] from running statistics. */
+int scd_bn_eval_coeffs(int32_t c, const float *gamma, const float *beta, const float *running_mean,
+                       const float *running_var, float eps, float *scale, float *shift, scd_stream_t stream);
+/* a = max(y*scale[seg] + shift[seg], 0); nseg = 1 with [C] coefficients in eval mode. */
+int scd_bn_relu_apply(scd_nhwc_t y, int32_t nseg, const float *scale, const float *shift, scd_nhwc_t a,
+                      scd_stream_t stream);
+/* Backward of a = relu(bn(y)) given da:
+ *   dz = da * [y*scale+shift > 0]; xhat = (y-mean)*invstd
+ *   dgamma = sum dz*xhat, dbeta = sum dz (summed over segments); dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat))
+ * dbias_prev (optional, [C]) receives sum(dy): the bias grad of the conv that produced y.
+ * replaces: native_batch_norm_backward + threshold_backward (+ the conv bias-grad reduction). */
+int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
+                         const float *save_invstd, const float *gamma, const float *scale, const float *shift,
+                         float *dgamma, float *dbeta, float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes,
+                         scd_stream_t stream);
+
+/* out[c] = sum over all pixels of x[., c] (ConvTranspose2d bias grad, networks.py:433); workspace as
+ * scd_bn_workspace_bytes(n, h, w, c, 1).  replaces: the bias-grad reduction of convolution_backward. */
+int scd_channel_sum(scd_nhwc_t x, float *out, void *ws, size_t ws_bytes, scd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * MaxPool2d(2) (kernel 2, stride 2, floor) with 2-bit argmax per output element (first max wins,
+ * NaN propagates, as aten::max_pool2d_with_indices).  replaces: nn.MaxPool2d(2) (networks.py:420).
+ * ------------------------------------------------------------------------------------------- */
+int scd_maxpool2_fwd(scd_nhwc_t x, scd_nhwc_t y, uint8_t *idx, scd_stream_t stream);
+
+/* Gradient into an encoder feature map (both Siamese branches):
+ *   gx[img] = maxpool_bwd(gy, idx)[img]   (if gy.data != NULL)
+ *           + sgn(img) * gskip[img % gskip.n]   (if gskip.data != NULL)
+ * skip_mode 0: sgn = +1 (plain skip), 1: Siamese difference, sgn = -1 for img < gskip.n (t1), +1 (t2).
+ * replaces: max_pool2d_with_indices_backward + the autograd of torch.sub(f_t2, f_t1)
+ * (networks.py:147-150) + the skip-half of cat backward (networks.py:449). */
+int scd_feature_grad(scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip, int32_t skip_mode, scd_nhwc_t gx,
+                     int32_t accumulate, scd_stream_t stream);
+
+/* d[b] = a[half + b] - a[b], half = d.n (a.n == 2*d.n): f_t2 - f_t1 (networks.py:147-150).  d may be the
+ * skip slice [0:C) of the decoder concat buffer (networks.py:449). */
+int scd_siamese_diff(scd_nhwc_t a, scd_nhwc_t d, scd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * OutConv 1x1 head (networks.py:454-461): out NCHW [n][n_out][h][w] = b + x . w   (n_out <= 4)
+ * ------------------------------------------------------------------------------------------- */
+int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int32_t n_out, float *out,
+                    scd_stream_t stream);
+size_t scd_conv1x1_workspace_bytes(scd_nhwc_t x, int32_t n_out);
+/* gx (+)= gout . w ; gw = sum gout*x ; gb = sum gout. */
+int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, int32_t n_out, scd_nhwc_t gx,
+                    int32_t accumulate, float *gw, float *gb, void *ws, size_t ws_bytes, scd_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * power_jaccard_loss (utils/loss_functions.py:141-150): p = sigmoid(logit); I = sum p*t;
+ * D = sum(p^2 + t^2) - I + 1e-6; loss = 1 - I/D, reduced over the whole batch.
+ * sums_out = {I, sum(p^2+t^2), D} (device, float[3]); loss_out device float[1].
+ * ------------------------------------------------------------------------------------------- */
+size_t scd_pjaccard_workspace_bytes(int64_t n);
+int scd_pjaccard_fwd(const float *logits, const float *target, int64_t n, float *sums_out, float *loss_out,
+                     void *ws, size_t ws_bytes, scd_stream_t stream);
+/* glogits = gloss * dL/dlogit; if gtarget != NULL also the soft-target grad (MMCR consistency loss,
+ * train_semisupervised.py:107, where the target sigma(logits_s2) is not detached). */
+int scd_pjaccard_bwd(const float *logits, const float *target, int64_t n, const float *sums,
+                     const float *gloss, float *glogits, float *gtarget, scd_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCD_H_ */

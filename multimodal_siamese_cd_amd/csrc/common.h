@@ -1,0 +1,66 @@
+// Internal helpers shared by the libscd translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/scd.h"
+
+namespace scd {
+
+void set_error(const char *fmt, ...);
+void clear_error();
+
+inline hipStream_t as_stream(scd_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Validate an NHWC view used with 16-byte vector accesses.
+inline int check_view(const scd_nhwc_t &v, const char *name, bool allow_null = false) {
+    if (v.data == nullptr) {
+        if (allow_null) return SCD_OK;
+        set_error("%s: null data", name);
+        return SCD_ERR_ARG;
+    }
+    if (v.n <= 0 || v.h <= 0 || v.w <= 0 || v.c <= 0 || v.ldc < v.c) {
+        set_error("%s: bad shape n=%d h=%d w=%d c=%d ldc=%d", name, v.n, v.h, v.w, v.c, v.ldc);
+        return SCD_ERR_ARG;
+    }
+    if ((v.c & 3) || (v.ldc & 3) || !aligned16(v.data)) {
+        set_error("%s: c=%d / ldc=%d must be multiples of 4 and data 16-byte aligned", name, v.c, v.ldc);
+        return SCD_ERR_ALIGN;
+    }
+    return SCD_OK;
+}
+
+inline int64_t pixels(const scd_nhwc_t &v) { return int64_t(v.n) * v.h * v.w; }
+
+inline int launch_status(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+        return SCD_ERR_LAUNCH;
+    }
+    return SCD_OK;
+}
+
+#define SCD_TRY(expr)                 \
+    do {                              \
+        int _rc = (expr);             \
+        if (_rc != SCD_OK) return _rc; \
+    } while (0)
+
+// Device-side NHWC element pointer helpers.
+struct View {
+    float *p;
+    int n, h, w, c, ldc;
+};
+
+inline View make_view(const scd_nhwc_t &v) {
+    return View{static_cast<float *>(v.data), v.n, v.h, v.w, v.c, v.ldc};
+}
+
+}  // namespace scd

@@ -1,0 +1,653 @@
+// Implicit-GEMM convolution kernels on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces aten::convolution / convolution_backward for the reference's Conv2d(3x3, pad 1),
+// ConvTranspose2d(2x2, stride 2) (utils/networks.py:392,395,433).  Two kernel families:
+//
+//   igemm_f32  : out[m, o] = bias + sum_k A[m, k] * Wpk[o, k]  with A gathered on the fly from an NHWC
+//                source (k = (tap, c)); used for conv forward, conv data-grad (flipped weights), ConvT
+//                forward (1 tap + 2x2 pixel-shuffle store into the concat buffer slice) and ConvT
+//                data-grad (4 taps, stride 2).
+//   wgrad_f32  : slab[s][r][(tap, c)] = sum_{m in split s} P[m, r] * Q[src(m, tap), c]; split-K over the
+//                pixel dimension into fp32 slabs, summed deterministically by wgrad_finalize.
+//
+// MFMA operand trick (fp32, 32x32x2): instruction s of an 8-deep K chunk takes k = 4h + s from lane
+// half h = lane>>5, so every lane reads its 4 k-values for a row with ONE ds_read_b128 from a
+// [row][k] LDS image (row stride BK+4 floats: conflict-free b128 reads).
+#include "common.h"
+
+namespace scd {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Loads/stores through the global address space (kernel-arg structs otherwise yield flat_* ops).
+__device__ __forceinline__ f32x4 gload4(const float *p) {
+    return *(const __attribute__((address_space(1))) f32x4 *)(p);
+}
+__device__ __forceinline__ void gstore1(float *p, float v) { *(__attribute__((address_space(1))) float *)(p) = v; }
+__device__ __forceinline__ f32x4 lload4(const float *p) { return *reinterpret_cast<const f32x4 *>(p); }
+__device__ __forceinline__ void lstore4(float *p, f32x4 v) { *reinterpret_cast<f32x4 *>(p) = v; }
+
+// Division by a runtime constant: n / d = (umulhi(n, mul) + n) >> shr, valid for n < 2^31.
+struct FastDiv {
+    uint32_t d, mul, shr;
+};
+
+static FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    uint32_t s = 0;
+    while ((1ull << s) < d) ++s;
+    f.shr = s;
+    f.mul = uint32_t(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
+    return (__umulhi(n, f.mul) + n) >> f.shr;
+}
+
+// 9 taps packed as signed 4-bit fields.
+__device__ __forceinline__ int tap_at(uint64_t packed, int t) {
+    int v = int((packed >> (4 * t)) & 15ull);
+    return v >= 8 ? v - 16 : v;
+}
+
+static uint64_t pack_taps(const int8_t *v, int n) {
+    uint64_t p = 0;
+    for (int i = 0; i < n; ++i) p |= uint64_t(uint8_t(v[i]) & 15u) << (4 * i);
+    return p;
+}
+
+// ------------------------------------------------------------------------------------------------
+// igemm
+// ------------------------------------------------------------------------------------------------
+struct IgemmArgs {
+    const float *src;
+    int n_img, hs, ws, c, ldc_s;
+    int ho, wo, stride, ntaps;
+    uint64_t tdy, tdx;
+    const float *w;
+    int n_out, K;
+    const float *bias;
+    float *dst;
+    int ldc_d, dst_h, dst_w, store_mode, cout;
+    int M;
+    FastDiv div_hw, div_w;
+};
+
+template <int WAVES_M, int WAVES_N, int TM, int TN, int BK>
+__global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_f32(IgemmArgs a) {
+    constexpr int NT = 64 * WAVES_M * WAVES_N;
+    constexpr int BM = WAVES_M * TM * 32;
+    constexpr int BN = WAVES_N * TN * 32;
+    constexpr int LS = BK + 4;  // LDS row stride (floats)
+    constexpr int KC = BK / 4;  // 16-byte chunks per row
+    constexpr int A_CH = BM * KC;
+    constexpr int B_CH = BN * KC;
+    constexpr int A_PER = (A_CH + NT - 1) / NT;
+    constexpr int B_PER = (B_CH + NT - 1) / NT;
+    constexpr int STAGE = (BM + BN) * LS;
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid % WAVES_M;
+    const int wn = wid / WAVES_M;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+
+    // Per-thread A-chunk bookkeeping (fixed across the K loop).
+    int a_img[A_PER], a_sy[A_PER], a_sx[A_PER], a_off[A_PER];
+    bool a_ok[A_PER];
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+        const int ch = tid + i * NT;
+        const int row = ch / KC, col = ch % KC;
+        const int m = m0 + row;
+        a_ok[i] = (ch < A_CH) && (m < a.M);
+        const uint32_t mm = a_ok[i] ? uint32_t(m) : 0u;
+        const uint32_t img = fdiv(mm, a.div_hw);
+        const uint32_t r = mm - img * uint32_t(a.ho * a.wo);
+        const uint32_t oy = fdiv(r, a.div_w);
+        const uint32_t ox = r - oy * uint32_t(a.wo);
+        a_img[i] = int(img);
+        a_sy[i] = int(oy) * a.stride;
+        a_sx[i] = int(ox) * a.stride;
+        a_off[i] = row * LS + col * 4;
+    }
+    int b_row[B_PER], b_off[B_PER];
+    bool b_ok[B_PER], b_in[B_PER];
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+        const int ch = tid + i * NT;
+        const int row = ch / KC, col = ch % KC;
+        b_in[i] = ch < B_CH;
+        b_ok[i] = b_in[i] && (n0 + row < a.n_out);
+        b_row[i] = (n0 + row) * a.K + col * 4;
+        b_off[i] = BM * LS + row * LS + col * 4;
+    }
+
+    f32x4 ra[A_PER], rb[B_PER];
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+    auto load_stage = [&](int t, int c0) {
+        const int dyt = tap_at(a.tdy, t), dxt = tap_at(a.tdx, t);
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            const int sy = a_sy[i] + dyt, sx = a_sx[i] + dxt;
+            const bool v = a_ok[i] && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+            const int col4 = ((tid + i * NT) % KC) * 4;
+            if (v) {
+                const size_t pix = size_t(a_img[i] * a.hs + sy) * a.ws + sx;
+                ra[i] = gload4(a.src + pix * a.ldc_s + c0 + col4);
+            } else {
+                ra[i] = zero4;
+            }
+        }
+        const int k0 = t * a.c + c0;
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            rb[i] = b_ok[i] ? gload4(a.w + size_t(b_row[i]) + k0) : zero4;
+        }
+    };
+    auto store_stage = [&](int buf) {
+        float *S = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i)
+            if (tid + i * NT < A_CH) lstore4(S + a_off[i], ra[i]);
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i)
+            if (b_in[i]) lstore4(S + b_off[i], rb[i]);
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int csteps = a.c / BK;
+    const int nsteps = a.ntaps * csteps;
+    const int a_lane = (wm * TM * 32 + (lane & 31)) * LS + 4 * (lane >> 5);
+    const int b_lane = BM * LS + (wn * TN * 32 + (lane & 31)) * LS + 4 * (lane >> 5);
+
+    int t = 0, cs = 0;
+    load_stage(0, 0);
+    store_stage(0);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const bool more = s + 1 < nsteps;
+        if (more) {
+            if (++cs == csteps) {
+                cs = 0;
+                ++t;
+            }
+            load_stage(t, cs * BK);
+        }
+        const float *S = smem + (s & 1) * STAGE;
+#pragma unroll
+        for (int q = 0; q < BK / 8; ++q) {
+            f32x4 av[TM], bv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                av[i] = lload4(S + a_lane + i * 32 * LS + 8 * q);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bv[j] = lload4(S + b_lane + j * 32 * LS + 8 * q);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][0], bv[j][0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][1], bv[j][1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][2], bv[j][2], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][3], bv[j][3], acc[i][j], 0, 0, 0);
+                }
+        }
+        if (more) store_stage((s + 1) & 1);
+        __syncthreads();
+    }
+
+    // Epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+        if (n >= a.n_out) continue;
+        if (a.store_mode == 0) {
+            const float bias = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    if (m < a.M) gstore1(a.dst + size_t(m) * a.ldc_d + n, acc[i][j][r] + bias);
+                }
+        } else {
+            const int ij = n / a.cout, oc = n - ij * a.cout;
+            const int di = ij >> 1, dj = ij & 1;
+            const float bias = a.bias ? a.bias[oc] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    if (m < a.M) {
+                        const uint32_t img = fdiv(uint32_t(m), a.div_hw);
+                        const uint32_t rr = uint32_t(m) - img * uint32_t(a.ho * a.wo);
+                        const uint32_t oy = fdiv(rr, a.div_w);
+                        const uint32_t ox = rr - oy * uint32_t(a.wo);
+                        const size_t pix = size_t(int(img) * a.dst_h + 2 * int(oy) + di) * a.dst_w + 2 * int(ox) + dj;
+                        gstore1(a.dst + pix * a.ldc_d + oc, acc[i][j][r] + bias);
+                    }
+                }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// wgrad
+// ------------------------------------------------------------------------------------------------
+struct WgradArgs {
+    const float *rows;
+    int ho, wo, R, ldc_r;
+    const float *src;
+    int hs, ws, C, ldc_s;
+    int stride, ntaps;
+    uint64_t tdy, tdx;
+    int Ng, M, kchunk;
+    float *slabs;
+    FastDiv div_hw, div_w, div_c;
+};
+
+template <int WAVES_M, int WAVES_N, int TM, int TN, int BK>
+__global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) {
+    constexpr int NT = 64 * WAVES_M * WAVES_N;
+    constexpr int BM = WAVES_M * TM * 32;
+    constexpr int BN = WAVES_N * TN * 32;
+    constexpr int AQ = BM / 4;  // 16-byte chunks per A row (one pixel)
+    constexpr int BQ = BN / 4;
+    constexpr int A_CH = BK * AQ;
+    constexpr int B_CH = BK * BQ;
+    constexpr int A_PER = (A_CH + NT - 1) / NT;
+    constexpr int B_PER = (B_CH + NT - 1) / NT;
+    constexpr int STAGE = BK * (BM + BN);
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid % WAVES_M;
+    const int wn = wid / WAVES_M;
+    const int r0 = blockIdx.x * BM;
+    const int j0 = blockIdx.y * BN;
+    const int kbeg = blockIdx.z * a.kchunk;
+    const int kend = min(a.M, kbeg + a.kchunk);
+
+    int a_k[A_PER], a_r[A_PER];
+    bool a_in[A_PER], a_ok[A_PER];
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+        const int ch = tid + i * NT;
+        a_in[i] = ch < A_CH;
+        a_k[i] = ch / AQ;
+        a_r[i] = r0 + (ch % AQ) * 4;
+        a_ok[i] = a_in[i] && a_r[i] < a.R;
+    }
+    int b_k[B_PER], b_dy[B_PER], b_dx[B_PER], b_c[B_PER];
+    bool b_in[B_PER], b_ok[B_PER];
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+        const int ch = tid + i * NT;
+        b_in[i] = ch < B_CH;
+        b_k[i] = ch / BQ;
+        const int j = j0 + (ch % BQ) * 4;
+        b_ok[i] = b_in[i] && j < a.Ng;
+        const int t = b_ok[i] ? int(fdiv(uint32_t(j), a.div_c)) : 0;
+        b_c[i] = j - t * a.C;
+        b_dy[i] = tap_at(a.tdy, t);
+        b_dx[i] = tap_at(a.tdx, t);
+    }
+
+    f32x4 ra[A_PER], rb[B_PER];
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    auto load_stage = [&](int kb) {
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            const int m = kb + a_k[i];
+            ra[i] = (a_ok[i] && m < kend) ? gload4(a.rows + size_t(m) * a.ldc_r + a_r[i]) : zero4;
+        }
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            const int m = kb + b_k[i];
+            bool v = b_ok[i] && m < kend;
+            const uint32_t mm = v ? uint32_t(m) : 0u;
+            const uint32_t img = fdiv(mm, a.div_hw);
+            const uint32_t rr = mm - img * uint32_t(a.ho * a.wo);
+            const uint32_t oy = fdiv(rr, a.div_w);
+            const uint32_t ox = rr - oy * uint32_t(a.wo);
+            const int sy = int(oy) * a.stride + b_dy[i];
+            const int sx = int(ox) * a.stride + b_dx[i];
+            v = v && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+            if (v) {
+                const size_t pix = size_t(int(img) * a.hs + sy) * a.ws + sx;
+                rb[i] = gload4(a.src + pix * a.ldc_s + b_c[i]);
+            } else {
+                rb[i] = zero4;
+            }
+        }
+    };
+    auto store_stage = [&](int buf) {
+        float *S = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i)
+            if (a_in[i]) lstore4(S + (tid + i * NT) * 4, ra[i]);
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i)
+            if (b_in[i]) lstore4(S + BK * BM + (tid + i * NT) * 4, rb[i]);
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int h = lane >> 5;
+    const int a_lane = h * BM + wm * TM * 32 + (lane & 31);
+    const int b_lane = BK * BM + h * BN + wn * TN * 32 + (lane & 31);
+
+    const int nsteps = (kend > kbeg) ? (kend - kbeg + BK - 1) / BK : 0;
+    if (nsteps > 0) {
+        load_stage(kbeg);
+        store_stage(0);
+        __syncthreads();
+        for (int s = 0; s < nsteps; ++s) {
+            const bool more = s + 1 < nsteps;
+            if (more) load_stage(kbeg + (s + 1) * BK);
+            const float *S = smem + (s & 1) * STAGE;
+#pragma unroll
+            for (int kk = 0; kk < BK / 2; ++kk) {
+                float av[TM], bv[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = S[a_lane + 2 * kk * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = S[b_lane + 2 * kk * BN + j * 32];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+            }
+            if (more) store_stage((s + 1) & 1);
+            __syncthreads();
+        }
+    }
+
+    float *slab = a.slabs + size_t(blockIdx.z) * a.R * a.Ng;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = j0 + wn * TN * 32 + j * 32 + (lane & 31);
+        if (col >= a.Ng) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = r0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (row < a.R) gstore1(slab + size_t(row) * a.Ng + col, acc[i][j][r]);
+            }
+    }
+}
+
+__global__ void wgrad_finalize_kernel(const float *__restrict__ slabs, int nsplit, int R, int ntaps, int C,
+                                      int mode, int c_valid, float *__restrict__ out) {
+    const int Ng = ntaps * C;
+    const size_t total = size_t(R) * Ng;
+    const size_t stride = total;
+    for (size_t e = blockIdx.x * size_t(blockDim.x) + threadIdx.x; e < total; e += size_t(gridDim.x) * blockDim.x) {
+        const int r = int(e / Ng);
+        const int col = int(e - size_t(r) * Ng);
+        const int t = col / C;
+        const int c = col - t * C;
+        if (c >= c_valid) continue;
+        float s = 0.f;
+        for (int k = 0; k < nsplit; ++k) s += slabs[e + k * stride];
+        size_t o;
+        if (mode == 0)
+            o = (size_t(r) * c_valid + c) * ntaps + t;  // OIHW [R][c_valid][3][3], t = ky*3+kx
+        else
+            o = (size_t(r) * C + c) * ntaps + t;        // ConvT [R][C][2][2], t = i*2+j
+        out[o] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host launchers
+// ------------------------------------------------------------------------------------------------
+template <int WM, int WN, int TM, int TN, int BK>
+static void launch_igemm(const IgemmArgs &a, hipStream_t s) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    dim3 grid((a.M + BM - 1) / BM, (a.n_out + BN - 1) / BN);
+    hipLaunchKernelGGL((igemm_f32<WM, WN, TM, TN, BK>), grid, dim3(64 * WM * WN), 0, s, a);
+}
+
+template <int WM, int WN, int TM, int TN>
+static void launch_igemm_bk(const IgemmArgs &a, hipStream_t s) {
+    if (a.c % 16 == 0)
+        launch_igemm<WM, WN, TM, TN, 16>(a, s);
+    else
+        launch_igemm<WM, WN, TM, TN, 8>(a, s);
+}
+
+static int check_taps(int ntaps, const int8_t *dy, const int8_t *dx) {
+    if (ntaps < 1 || ntaps > 9) {
+        set_error("ntaps=%d out of range [1,9]", ntaps);
+        return SCD_ERR_ARG;
+    }
+    for (int i = 0; i < ntaps; ++i)
+        if (dy[i] < -8 || dy[i] > 7 || dx[i] < -8 || dx[i] > 7) {
+            set_error("tap %d offset (%d,%d) out of range", i, dy[i], dx[i]);
+            return SCD_ERR_ARG;
+        }
+    return SCD_OK;
+}
+
+}  // namespace scd
+
+using namespace scd;
+
+extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
+    clear_error();
+    if (!d) {
+        set_error("scd_conv_igemm: null descriptor");
+        return SCD_ERR_ARG;
+    }
+    SCD_TRY(check_view(d->src, "igemm.src"));
+    SCD_TRY(check_view(d->dst, "igemm.dst"));
+    SCD_TRY(check_taps(d->ntaps, d->dy, d->dx));
+    if (d->src.c % 8) {
+        set_error("igemm: src.c=%d must be a multiple of 8 (pad channels)", d->src.c);
+        return SCD_ERR_ARG;
+    }
+    if (!d->wpk || !aligned16(d->wpk) || d->n_out <= 0 || d->out_h <= 0 || d->out_w <= 0 || d->stride < 1) {
+        set_error("igemm: bad weights/n_out/out grid/stride");
+        return SCD_ERR_ARG;
+    }
+    const int64_t M = int64_t(d->src.n) * d->out_h * d->out_w;
+    if (M >= (int64_t(1) << 31) || pixels(d->src) >= (int64_t(1) << 31)) {
+        set_error("igemm: problem too large for 32-bit pixel indexing");
+        return SCD_ERR_ARG;
+    }
+    if (d->dst.n != d->src.n) {
+        set_error("igemm: dst.n=%d != src.n=%d", d->dst.n, d->src.n);
+        return SCD_ERR_ARG;
+    }
+    if (d->store_mode == 0) {
+        if (d->dst.h != d->out_h || d->dst.w != d->out_w || d->dst.c != d->n_out) {
+            set_error("igemm: dst view (%d,%d,%d) != out grid (%d,%d,%d)", d->dst.h, d->dst.w, d->dst.c, d->out_h,
+                      d->out_w, d->n_out);
+            return SCD_ERR_ARG;
+        }
+    } else if (d->store_mode == 1) {
+        if (d->n_out % 4 || d->dst.c != d->n_out / 4 || d->dst.h != 2 * d->out_h || d->dst.w != 2 * d->out_w) {
+            set_error("igemm: shuffle store needs dst (2h,2w,n_out/4)");
+            return SCD_ERR_ARG;
+        }
+    } else {
+        set_error("igemm: store_mode %d", d->store_mode);
+        return SCD_ERR_ARG;
+    }
+    IgemmArgs a;
+    a.src = static_cast<const float *>(d->src.data);
+    a.n_img = d->src.n;
+    a.hs = d->src.h;
+    a.ws = d->src.w;
+    a.c = d->src.c;
+    a.ldc_s = d->src.ldc;
+    a.ho = d->out_h;
+    a.wo = d->out_w;
+    a.stride = d->stride;
+    a.ntaps = d->ntaps;
+    a.tdy = pack_taps(d->dy, d->ntaps);
+    a.tdx = pack_taps(d->dx, d->ntaps);
+    a.w = d->wpk;
+    a.n_out = d->n_out;
+    a.K = d->ntaps * d->src.c;
+    a.bias = d->bias;
+    a.dst = static_cast<float *>(d->dst.data);
+    a.ldc_d = d->dst.ldc;
+    a.dst_h = d->dst.h;
+    a.dst_w = d->dst.w;
+    a.store_mode = d->store_mode;
+    a.cout = d->store_mode == 1 ? d->n_out / 4 : d->n_out;
+    a.M = int(M);
+    a.div_hw = make_fastdiv(uint32_t(d->out_h * d->out_w));
+    a.div_w = make_fastdiv(uint32_t(d->out_w));
+    hipStream_t s = as_stream(stream);
+    if (d->n_out >= 128)
+        launch_igemm_bk<2, 2, 2, 2>(a, s);  // 128 x 128
+    else if (d->n_out >= 64)
+        launch_igemm_bk<4, 1, 2, 2>(a, s);  // 256 x 64
+    else
+        launch_igemm_bk<4, 1, 2, 1>(a, s);  // 256 x 32
+    return launch_status("scd_conv_igemm");
+}
+
+namespace scd {
+struct WgradTile {
+    int bm, bn;
+};
+static WgradTile wgrad_tile(int R) {
+    if (R >= 128) return {128, 128};
+    if (R >= 64) return {64, 256};
+    return {32, 128};
+}
+static int wgrad_validate(const scd_wgrad_t *d) {
+    if (!d) {
+        set_error("wgrad: null descriptor");
+        return SCD_ERR_ARG;
+    }
+    SCD_TRY(check_view(d->rows, "wgrad.rows"));
+    SCD_TRY(check_view(d->src, "wgrad.src"));
+    SCD_TRY(check_taps(d->ntaps, d->dy, d->dx));
+    if (d->rows.n != d->src.n || d->stride < 1) {
+        set_error("wgrad: rows.n=%d src.n=%d stride=%d", d->rows.n, d->src.n, d->stride);
+        return SCD_ERR_ARG;
+    }
+    if (pixels(d->rows) >= (int64_t(1) << 31) || pixels(d->src) >= (int64_t(1) << 31)) {
+        set_error("wgrad: problem too large for 32-bit pixel indexing");
+        return SCD_ERR_ARG;
+    }
+    return SCD_OK;
+}
+static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
+    const WgradTile t = wgrad_tile(d->rows.c);
+    const int Ng = d->ntaps * d->src.c;
+    const int64_t M = pixels(d->rows);
+    const int64_t tiles = int64_t((d->rows.c + t.bm - 1) / t.bm) * ((Ng + t.bn - 1) / t.bn);
+    int64_t want = (1024 + tiles - 1) / tiles;
+    const int64_t maxsplit = (M + 511) / 512;  // keep >= 512 pixels per split
+    if (want > maxsplit) want = maxsplit;
+    if (want < 1) want = 1;
+    int64_t kc = (M + want - 1) / want;
+    kc = (kc + 15) / 16 * 16;
+    *kchunk = int(kc);
+    *nsplit = int((M + kc - 1) / kc);
+}
+}  // namespace scd
+
+extern "C" int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes) {
+    clear_error();
+    SCD_TRY(wgrad_validate(d));
+    int ns, kc;
+    wgrad_split(d, &ns, &kc);
+    if (nsplit) *nsplit = ns;
+    if (slab_bytes) *slab_bytes = size_t(ns) * d->rows.c * d->ntaps * d->src.c * sizeof(float);
+    return SCD_OK;
+}
+
+extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(wgrad_validate(d));
+    int ns, kc;
+    wgrad_split(d, &ns, &kc);
+    const int Ng = d->ntaps * d->src.c;
+    const size_t need = size_t(ns) * d->rows.c * Ng * sizeof(float);
+    if (!slabs || slab_bytes < need) {
+        set_error("wgrad: slab workspace %zu < %zu bytes", slab_bytes, need);
+        return SCD_ERR_WORKSPACE;
+    }
+    WgradArgs a;
+    a.rows = static_cast<const float *>(d->rows.data);
+    a.ho = d->rows.h;
+    a.wo = d->rows.w;
+    a.R = d->rows.c;
+    a.ldc_r = d->rows.ldc;
+    a.src = static_cast<const float *>(d->src.data);
+    a.hs = d->src.h;
+    a.ws = d->src.w;
+    a.C = d->src.c;
+    a.ldc_s = d->src.ldc;
+    a.stride = d->stride;
+    a.ntaps = d->ntaps;
+    a.tdy = pack_taps(d->dy, d->ntaps);
+    a.tdx = pack_taps(d->dx, d->ntaps);
+    a.Ng = Ng;
+    a.M = int(pixels(d->rows));
+    a.kchunk = kc;
+    a.slabs = slabs;
+    a.div_hw = make_fastdiv(uint32_t(d->rows.h * d->rows.w));
+    a.div_w = make_fastdiv(uint32_t(d->rows.w));
+    a.div_c = make_fastdiv(uint32_t(d->src.c));
+    hipStream_t s = as_stream(stream);
+    const WgradTile t = wgrad_tile(a.R);
+    dim3 grid((a.R + t.bm - 1) / t.bm, (Ng + t.bn - 1) / t.bn, ns);
+    if (t.bm == 128)
+        hipLaunchKernelGGL((wgrad_f32<2, 2, 2, 2, 16>), grid, dim3(256), 0, s, a);
+    else if (t.bm == 64)
+        hipLaunchKernelGGL((wgrad_f32<1, 4, 2, 2, 16>), grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((wgrad_f32<1, 4, 1, 1, 16>), grid, dim3(256), 0, s, a);
+    return launch_status("scd_conv_wgrad");
+}
+
+extern "C" int scd_wgrad_finalize(const float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C,
+                                  int32_t mode, int32_t c_valid, float *out, scd_stream_t stream) {
+    clear_error();
+    if (!slabs || !out || nsplit < 1 || R < 1 || ntaps < 1 || C < 1 || (mode != 0 && mode != 1) || c_valid < 1 ||
+        c_valid > C) {
+        set_error("wgrad_finalize: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    const size_t total = size_t(R) * ntaps * C;
+    int blocks = int((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), slabs, nsplit, R, ntaps,
+                       C, mode, c_valid, out);
+    return launch_status("scd_wgrad_finalize");
+}

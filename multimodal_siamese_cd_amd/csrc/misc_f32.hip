@@ -1,0 +1,582 @@
+// Memory-bound kernels of the Siamese U-Net path (fp32 NHWC) + library info / error handling.
+//
+// Reference call sites: input hand-off (train_supervised.py:68-69), nn.MaxPool2d(2) (networks.py:420),
+// torch.sub(f_t2, f_t1) (networks.py:149), OutConv 1x1 (networks.py:454-461), power_jaccard_loss
+// (utils/loss_functions.py:141-150), the parameter layouts of Conv2d / ConvTranspose2d.
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+namespace scd {
+
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+void clear_error() { g_err.clear(); }
+
+constexpr int RED_CHUNK = 4096;
+
+static int grid_for(int64_t total, int cap = 4096) {
+    int64_t b = (total + 255) / 256;
+    if (b > cap) b = cap;
+    if (b < 1) b = 1;
+    return int(b);
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ void pack_nchw_kernel(const float *__restrict__ src, int n, int c, int hw, int c_begin, int c_count,
+                                 float *__restrict__ dst, int dc, int ldc) {
+    // one thread per (pixel, dst channel); scalar stores so any channel offset works (5-band inputs)
+    const int64_t total = int64_t(n) * hw * dc;
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        const int cc = int(e % dc);
+        const int64_t p = e / dc;
+        const int64_t img = p / hw, pix = p % hw;
+        dst[p * ldc + cc] = cc < c_count ? src[(img * c + c_begin + cc) * hw + pix] : 0.f;
+    }
+}
+
+__global__ void pack_conv3x3_kernel(const float *__restrict__ w, int co, int ci, int ci_pad, int mode,
+                                    float *__restrict__ out) {
+    const int64_t total = mode == 0 ? int64_t(co) * 9 * ci_pad : int64_t(ci) * 9 * co;
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        if (mode == 0) {  // out[o][t][c]
+            const int c = int(e % ci_pad);
+            const int t = int((e / ci_pad) % 9);
+            const int o = int(e / (int64_t(9) * ci_pad));
+            out[e] = c < ci ? w[(int64_t(o) * ci + c) * 9 + t] : 0.f;
+        } else {  // out[c][t'][o] = w[o][c][8-t']
+            const int o = int(e % co);
+            const int t = int((e / co) % 9);
+            const int c = int(e / (int64_t(9) * co));
+            out[e] = w[(int64_t(o) * ci + c) * 9 + (8 - t)];
+        }
+    }
+}
+
+__global__ void pack_convT_kernel(const float *__restrict__ w, int ci, int co, int mode, float *__restrict__ out) {
+    const int64_t total = int64_t(ci) * co * 4;
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        if (mode == 0) {  // out[(t*co + o)][c]
+            const int c = int(e % ci);
+            const int r = int(e / ci);
+            const int t = r / co, o = r % co;
+            out[e] = w[(int64_t(c) * co + o) * 4 + t];
+        } else {  // out[c][t*co + o]
+            const int col = int(e % (4 * co));
+            const int c = int(e / (4 * co));
+            const int t = col / co, o = col % co;
+            out[e] = w[(int64_t(c) * co + o) * 4 + t];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void pool_pick(float v, int k, float &mx, int &idx) {
+    if (v > mx || isnan(v)) {
+        mx = v;
+        idx = k;
+    }
+}
+
+__global__ void maxpool2_fwd_kernel(const float *__restrict__ x, int hx, int wx, int ldx, float *__restrict__ y,
+                                   int hy, int wy, int ldy, uint8_t *__restrict__ idx, int C, int64_t total) {
+    const int cq = C / 4;
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        const int c = int(e % cq) * 4;
+        const int64_t p = e / cq;  // output pixel
+        const int ox = int(p % wy);
+        const int oy = int((p / wy) % hy);
+        const int64_t img = p / (int64_t(wy) * hy);
+        const float *base = x + ((img * hx + 2 * oy) * wx + 2 * ox) * ldx + c;
+        const float4 v0 = *reinterpret_cast<const float4 *>(base);
+        const float4 v1 = *reinterpret_cast<const float4 *>(base + ldx);
+        const float4 v2 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx);
+        const float4 v3 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx + ldx);
+        const float a0[4] = {v0.x, v0.y, v0.z, v0.w}, a1[4] = {v1.x, v1.y, v1.z, v1.w};
+        const float a2[4] = {v2.x, v2.y, v2.z, v2.w}, a3[4] = {v3.x, v3.y, v3.z, v3.w};
+        float o[4];
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float mx = -INFINITY;
+            int id = 0;
+            pool_pick(a0[k], 0, mx, id);
+            pool_pick(a1[k], 1, mx, id);
+            pool_pick(a2[k], 2, mx, id);
+            pool_pick(a3[k], 3, mx, id);
+            o[k] = mx;
+            packed |= uint32_t(id) << (8 * k);
+        }
+        *reinterpret_cast<float4 *>(y + p * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<uint32_t *>(idx + p * C + c) = packed;
+    }
+}
+
+__global__ void feature_grad_kernel(const float *__restrict__ gy, int hy, int wy, int ldgy,
+                                    const uint8_t *__restrict__ idx, const float *__restrict__ gs, int gsn, int ldgs,
+                                    int skip_mode, float *__restrict__ gx, int hx, int wx, int ldgx, int C,
+                                    int accumulate, int64_t total) {
+    const int cq = C / 4;
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        const int c = int(e % cq) * 4;
+        const int64_t p = e / cq;
+        const int x = int(p % wx);
+        const int yy = int((p / wx) % hx);
+        const int64_t img = p / (int64_t(wx) * hx);
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gy) {
+            const int oy = yy >> 1, ox = x >> 1;
+            if (oy < hy && ox < wy) {
+                const int64_t q = (img * hy + oy) * wy + ox;
+                const uint32_t pk = *reinterpret_cast<const uint32_t *>(idx + q * C + c);
+                const float4 g = *reinterpret_cast<const float4 *>(gy + q * ldgy + c);
+                const uint32_t want = uint32_t((yy & 1) * 2 + (x & 1));
+                r.x = ((pk >> 0) & 0xff) == want ? g.x : 0.f;
+                r.y = ((pk >> 8) & 0xff) == want ? g.y : 0.f;
+                r.z = ((pk >> 16) & 0xff) == want ? g.z : 0.f;
+                r.w = ((pk >> 24) & 0xff) == want ? g.w : 0.f;
+            }
+        }
+        if (gs) {
+            const int64_t simg = img % gsn;
+            const float sg = (skip_mode == 1 && img < gsn) ? -1.f : 1.f;
+            const float4 s = *reinterpret_cast<const float4 *>(gs + ((simg * hx + yy) * wx + x) * ldgs + c);
+            r.x += sg * s.x;
+            r.y += sg * s.y;
+            r.z += sg * s.z;
+            r.w += sg * s.w;
+        }
+        float4 *dst = reinterpret_cast<float4 *>(gx + p * ldgx + c);
+        if (accumulate) {
+            const float4 o = *dst;
+            r.x += o.x;
+            r.y += o.y;
+            r.z += o.z;
+            r.w += o.w;
+        }
+        *dst = r;
+    }
+}
+
+__global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float *__restrict__ d, int ldd, int C,
+                                    int64_t half_pixels, int64_t total) {
+    const int cq = C / 4;
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        const int c = int(e % cq) * 4;
+        const int64_t p = e / cq;
+        const float4 v1 = *reinterpret_cast<const float4 *>(a + p * lda + c);
+        const float4 v2 = *reinterpret_cast<const float4 *>(a + (p + half_pixels) * lda + c);
+        *reinterpret_cast<float4 *>(d + p * ldd + c) = make_float4(v2.x - v1.x, v2.y - v1.y, v2.z - v1.z, v2.w - v1.w);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ void conv1x1_fwd_kernel(const float *__restrict__ x, int ldx, int C, int hw, int64_t npix,
+                                   const float *__restrict__ w, const float *__restrict__ b, int n_out,
+                                   float *__restrict__ out) {
+    for (int64_t p = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; p < npix; p += int64_t(gridDim.x) * blockDim.x) {
+        const float *xr = x + p * ldx;
+        const int64_t img = p / hw, pix = p % hw;
+        for (int o = 0; o < n_out; ++o) {
+            const float *wr = w + int64_t(o) * C;
+            float s = 0.f;
+            for (int c = 0; c < C; c += 4) {
+                const float4 v = *reinterpret_cast<const float4 *>(xr + c);
+                s = fmaf(v.x, wr[c], s);
+                s = fmaf(v.y, wr[c + 1], s);
+                s = fmaf(v.z, wr[c + 2], s);
+                s = fmaf(v.w, wr[c + 3], s);
+            }
+            out[(img * n_out + o) * hw + pix] = s + (b ? b[o] : 0.f);
+        }
+    }
+}
+
+__global__ void conv1x1_bwd_dx_kernel(const float *__restrict__ gout, int n_out, int hw, const float *__restrict__ w,
+                                      float *__restrict__ gx, int ldgx, int C, int accumulate, int64_t total) {
+    const int cq = C / 4;
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        const int c = int(e % cq) * 4;
+        const int64_t p = e / cq;
+        const int64_t img = p / hw, pix = p % hw;
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int o = 0; o < n_out; ++o) {
+            const float g = gout[(img * n_out + o) * hw + pix];
+            const float *wr = w + int64_t(o) * C + c;
+            r.x = fmaf(g, wr[0], r.x);
+            r.y = fmaf(g, wr[1], r.y);
+            r.z = fmaf(g, wr[2], r.z);
+            r.w = fmaf(g, wr[3], r.w);
+        }
+        float4 *dst = reinterpret_cast<float4 *>(gx + p * ldgx + c);
+        if (accumulate) {
+            const float4 o4 = *dst;
+            r.x += o4.x;
+            r.y += o4.y;
+            r.z += o4.z;
+            r.w += o4.w;
+        }
+        *dst = r;
+    }
+}
+
+// partial gw: rec[chunk][o][C]; grid (chunks, channel groups of 64 quads), block 256 = 64 quads x 4 pixel lanes
+__global__ __launch_bounds__(256) void conv1x1_bwd_dw_partial(const float *__restrict__ x, int ldx, int C, int hw,
+                                                              int64_t npix, const float *__restrict__ gout, int n_out,
+                                                              float *__restrict__ rec) {
+    __shared__ float4 sh[4][256];
+    const int tid = threadIdx.x;
+    const int q = tid & 63, pl = tid >> 6;
+    const int cq = blockIdx.y * 64 + q;
+    const int64_t pbeg = int64_t(blockIdx.x) * RED_CHUNK;
+    const int64_t pend = min(pbeg + RED_CHUNK, npix);
+    float4 acc[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) acc[o] = make_float4(0, 0, 0, 0);
+    if (cq * 4 < C) {
+        for (int64_t p = pbeg + pl; p < pend; p += 4) {
+            const float4 v = *reinterpret_cast<const float4 *>(x + p * ldx + cq * 4);
+            const int64_t img = p / hw, pix = p % hw;
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                if (o < n_out) {
+                    const float g = gout[(img * n_out + o) * hw + pix];
+                    acc[o].x = fmaf(g, v.x, acc[o].x);
+                    acc[o].y = fmaf(g, v.y, acc[o].y);
+                    acc[o].z = fmaf(g, v.z, acc[o].z);
+                    acc[o].w = fmaf(g, v.w, acc[o].w);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) sh[o][tid] = acc[o];
+    __syncthreads();
+    if (pl == 0 && cq * 4 < C) {
+        for (int o = 0; o < n_out; ++o) {
+            float4 s = sh[o][q];
+            for (int k = 1; k < 4; ++k) {
+                const float4 t = sh[o][q + 64 * k];
+                s.x += t.x;
+                s.y += t.y;
+                s.z += t.z;
+                s.w += t.w;
+            }
+            *reinterpret_cast<float4 *>(rec + (size_t(blockIdx.x) * n_out + o) * C + cq * 4) = s;
+        }
+    }
+}
+
+// partial sums of gout per output channel: rec[block][o]
+__global__ __launch_bounds__(256) void conv1x1_bwd_db_partial(const float *__restrict__ gout, int n_out, int hw,
+                                                              int64_t npix, float *__restrict__ rec) {
+    __shared__ float sh[256];
+    const int o = blockIdx.y;
+    float s = 0.f;
+    for (int64_t p = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; p < npix; p += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t img = p / hw, pix = p % hw;
+        s += gout[(img * n_out + o) * hw + pix];
+    }
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rec[size_t(blockIdx.x) * n_out + o] = sh[0];
+}
+
+__global__ void sum_rows_kernel(const float *__restrict__ rec, int nrec, int width, float *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= width) return;
+    double s = 0;
+    for (int k = 0; k < nrec; ++k) s += rec[size_t(k) * width + i];
+    out[i] = float(s);
+}
+
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ __launch_bounds__(256) void pjaccard_partial(const float *__restrict__ logits, const float *__restrict__ t,
+                                                        int64_t n, float *__restrict__ rec) {
+    __shared__ float s1[256], s2[256];
+    float a = 0.f, b = 0.f;
+    for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+        const float p = sigmoidf_(logits[i]);
+        const float tt = t[i];
+        a = fmaf(p, tt, a);
+        b += p * p + tt * tt;
+    }
+    s1[threadIdx.x] = a;
+    s2[threadIdx.x] = b;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (threadIdx.x < off) {
+            s1[threadIdx.x] += s1[threadIdx.x + off];
+            s2[threadIdx.x] += s2[threadIdx.x + off];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        rec[2 * blockIdx.x] = s1[0];
+        rec[2 * blockIdx.x + 1] = s2[0];
+    }
+}
+
+__global__ void pjaccard_finalize(const float *__restrict__ rec, int nrec, float *sums, float *loss) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double I = 0, A = 0;
+    for (int k = 0; k < nrec; ++k) {
+        I += rec[2 * k];
+        A += rec[2 * k + 1];
+    }
+    const float If = float(I);
+    const float Df = float(A) - If + 1e-6f;
+    sums[0] = If;
+    sums[1] = float(A);
+    sums[2] = Df;
+    loss[0] = 1.f - If / Df;
+}
+
+__global__ void pjaccard_bwd_kernel(const float *__restrict__ logits, const float *__restrict__ t, int64_t n,
+                                    const float *__restrict__ sums, const float *__restrict__ gloss,
+                                    float *__restrict__ gl, float *__restrict__ gt) {
+    const float I = sums[0], D = sums[2];
+    const float g = gloss ? gloss[0] : 1.f;
+    const float invD2 = 1.f / (D * D);
+    for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+        const float p = sigmoidf_(logits[i]);
+        const float tt = t[i];
+        const float dLdp = -(tt * D - I * (2.f * p - tt)) * invD2;
+        gl[i] = g * dLdp * (p * (1.f - p));
+        if (gt) gt[i] = g * (-(p * D - I * (2.f * tt - p)) * invD2);
+    }
+}
+
+}  // namespace scd
+
+using namespace scd;
+
+// ------------------------------------------------------------------------------------------------
+extern "C" const char *scd_version(void) { return "libscd 0.1.0 (gfx950, fp32 MFMA implicit-GEMM)"; }
+extern "C" const char *scd_last_error(void) { return g_err.c_str(); }
+
+extern "C" int scd_device_check(int device) {
+    clear_error();
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) {
+        set_error("hipGetDeviceProperties(%d): %s", device, hipGetErrorString(e));
+        return SCD_ERR_DEVICE;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error("device %d is %s, libscd is built for gfx950 only", device, prop.gcnArchName);
+        return SCD_ERR_DEVICE;
+    }
+    return SCD_OK;
+}
+
+extern "C" int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, int32_t w, int32_t c_begin,
+                             int32_t c_count, scd_nhwc_t dst, scd_stream_t stream) {
+    clear_error();
+    // dst may start at any channel offset (scalar stores): only shape checks here.
+    if (!src || !dst.data || n != dst.n || h != dst.h || w != dst.w || dst.c < 1 || dst.ldc < dst.c || c_begin < 0 ||
+        c_count < 0 || c_begin + c_count > c || c_count > dst.c) {
+        set_error("pack_nchw: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    const int64_t total = int64_t(n) * h * w * dst.c;
+    hipLaunchKernelGGL(pack_nchw_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), src, n, c, h * w,
+                       c_begin, c_count, static_cast<float *>(dst.data), dst.c, dst.ldc);
+    return launch_status("scd_pack_nchw");
+}
+
+extern "C" int scd_pack_conv3x3(const float *w, int32_t co, int32_t ci, int32_t ci_pad, int32_t mode, float *out,
+                                scd_stream_t stream) {
+    clear_error();
+    if (!w || !out || co < 1 || ci < 1 || ci_pad < ci || (mode != 0 && mode != 1)) {
+        set_error("pack_conv3x3: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    const int64_t total = mode == 0 ? int64_t(co) * 9 * ci_pad : int64_t(ci) * 9 * co;
+    hipLaunchKernelGGL(pack_conv3x3_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), w, co, ci, ci_pad,
+                       mode, out);
+    return launch_status("scd_pack_conv3x3");
+}
+
+extern "C" int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, float *out,
+                                 scd_stream_t stream) {
+    clear_error();
+    if (!w || !out || co < 1 || ci < 1 || (mode != 0 && mode != 1)) {
+        set_error("pack_convT2x2: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    hipLaunchKernelGGL(pack_convT_kernel, dim3(grid_for(int64_t(ci) * co * 4)), dim3(256), 0, as_stream(stream), w, ci,
+                       co, mode, out);
+    return launch_status("scd_pack_convT2x2");
+}
+
+extern "C" int scd_maxpool2_fwd(scd_nhwc_t x, scd_nhwc_t y, uint8_t *idx, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(x, "maxpool.x"));
+    SCD_TRY(check_view(y, "maxpool.y"));
+    if (!idx || y.n != x.n || y.c != x.c || y.h != x.h / 2 || y.w != x.w / 2 || (reinterpret_cast<uintptr_t>(idx) & 3)) {
+        set_error("maxpool2_fwd: y must be (n, h/2, w/2, c); idx 4-byte aligned");
+        return SCD_ERR_ARG;
+    }
+    const int64_t total = pixels(y) * (y.c / 4);
+    hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(x.data), x.h, x.w, x.ldc, static_cast<float *>(y.data), y.h, y.w,
+                       y.ldc, idx, y.c, total);
+    return launch_status("scd_maxpool2_fwd");
+}
+
+extern "C" int scd_feature_grad(scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip, int32_t skip_mode,
+                                scd_nhwc_t gx, int32_t accumulate, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(gx, "feature_grad.gx"));
+    SCD_TRY(check_view(gy, "feature_grad.gy", true));
+    SCD_TRY(check_view(gskip, "feature_grad.gskip", true));
+    if (gy.data) {
+        if (!idx || gy.n != gx.n || gy.c != gx.c || gy.h != gx.h / 2 || gy.w != gx.w / 2) {
+            set_error("feature_grad: gy must be (n, h/2, w/2, c) with idx");
+            return SCD_ERR_ARG;
+        }
+    }
+    if (gskip.data) {
+        if (gskip.c != gx.c || gskip.h != gx.h || gskip.w != gx.w || gx.n % gskip.n ||
+            (skip_mode == 1 && gx.n != 2 * gskip.n) || (skip_mode != 0 && skip_mode != 1)) {
+            set_error("feature_grad: gskip shape/mode mismatch");
+            return SCD_ERR_ARG;
+        }
+    }
+    const int64_t total = pixels(gx) * (gx.c / 4);
+    hipLaunchKernelGGL(feature_grad_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(gy.data), gy.h, gy.w, gy.ldc, idx,
+                       static_cast<const float *>(gskip.data), gskip.n > 0 ? gskip.n : 1, gskip.ldc, skip_mode,
+                       static_cast<float *>(gx.data), gx.h, gx.w, gx.ldc, gx.c, accumulate, total);
+    return launch_status("scd_feature_grad");
+}
+
+extern "C" int scd_siamese_diff(scd_nhwc_t a, scd_nhwc_t d, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(a, "diff.a"));
+    SCD_TRY(check_view(d, "diff.d"));
+    if (a.n != 2 * d.n || a.h != d.h || a.w != d.w || a.c != d.c) {
+        set_error("siamese_diff: a must be (2n, h, w, c) of d");
+        return SCD_ERR_ARG;
+    }
+    const int64_t total = pixels(d) * (d.c / 4);
+    hipLaunchKernelGGL(siamese_diff_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(a.data), a.ldc, static_cast<float *>(d.data), d.ldc, d.c, pixels(d),
+                       total);
+    return launch_status("scd_siamese_diff");
+}
+
+extern "C" int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int32_t n_out, float *out,
+                               scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(x, "conv1x1.x"));
+    if (!w || !out || n_out < 1 || n_out > 4) {
+        set_error("conv1x1_fwd: bad arguments (n_out in [1,4])");
+        return SCD_ERR_ARG;
+    }
+    const int64_t npix = pixels(x);
+    hipLaunchKernelGGL(conv1x1_fwd_kernel, dim3(grid_for(npix)), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(x.data), x.ldc, x.c, x.h * x.w, npix, w, b, n_out, out);
+    return launch_status("scd_conv1x1_fwd");
+}
+
+extern "C" size_t scd_conv1x1_workspace_bytes(scd_nhwc_t x, int32_t n_out) {
+    const int64_t nchunk = (pixels(x) + RED_CHUNK - 1) / RED_CHUNK;
+    return size_t(nchunk) * n_out * x.c * sizeof(float) + size_t(1024) * n_out * sizeof(float) + 256;
+}
+
+extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, int32_t n_out, scd_nhwc_t gx,
+                               int32_t accumulate, float *gw, float *gb, void *ws, size_t ws_bytes,
+                               scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(x, "conv1x1_bwd.x"));
+    SCD_TRY(check_view(gx, "conv1x1_bwd.gx", true));
+    if (!w || !gout || n_out < 1 || n_out > 4) {
+        set_error("conv1x1_bwd: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    if (gx.data && (gx.n != x.n || gx.h != x.h || gx.w != x.w || gx.c != x.c)) {
+        set_error("conv1x1_bwd: gx shape mismatch");
+        return SCD_ERR_ARG;
+    }
+    if ((gw || gb) && (!ws || ws_bytes < scd_conv1x1_workspace_bytes(x, n_out))) {
+        set_error("conv1x1_bwd: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    hipStream_t s = as_stream(stream);
+    const int64_t npix = pixels(x);
+    const int hw = x.h * x.w;
+    if (gx.data) {
+        const int64_t total = npix * (x.c / 4);
+        hipLaunchKernelGGL(conv1x1_bwd_dx_kernel, dim3(grid_for(total)), dim3(256), 0, s, gout, n_out, hw, w,
+                           static_cast<float *>(gx.data), gx.ldc, x.c, accumulate, total);
+    }
+    const int nchunk = int((npix + RED_CHUNK - 1) / RED_CHUNK);
+    float *rec = static_cast<float *>(ws);
+    if (gw) {
+        hipLaunchKernelGGL(conv1x1_bwd_dw_partial, dim3(nchunk, (x.c / 4 + 63) / 64), dim3(256), 0, s,
+                           static_cast<const float *>(x.data), x.ldc, x.c, hw, npix, gout, n_out, rec);
+        hipLaunchKernelGGL(sum_rows_kernel, dim3((n_out * x.c + 127) / 128), dim3(128), 0, s, rec, nchunk, n_out * x.c,
+                           gw);
+    }
+    if (gb) {
+        float *brec = rec + size_t(nchunk) * n_out * x.c;
+        const int nb = 1024;
+        hipLaunchKernelGGL(conv1x1_bwd_db_partial, dim3(nb, n_out), dim3(256), 0, s, gout, n_out, hw, npix, brec);
+        hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(128), 0, s, brec, nb, n_out, gb);
+    }
+    return launch_status("scd_conv1x1_bwd");
+}
+
+static constexpr int PJ_BLOCKS = 1024;
+
+extern "C" size_t scd_pjaccard_workspace_bytes(int64_t n) {
+    (void)n;
+    return size_t(PJ_BLOCKS) * 2 * sizeof(float) + 256;
+}
+
+extern "C" int scd_pjaccard_fwd(const float *logits, const float *target, int64_t n, float *sums_out,
+                                float *loss_out, void *ws, size_t ws_bytes, scd_stream_t stream) {
+    clear_error();
+    if (!logits || !target || n < 1 || !sums_out || !loss_out) {
+        set_error("pjaccard_fwd: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    if (!ws || ws_bytes < scd_pjaccard_workspace_bytes(n)) {
+        set_error("pjaccard_fwd: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    hipStream_t s = as_stream(stream);
+    float *rec = static_cast<float *>(ws);
+    hipLaunchKernelGGL(pjaccard_partial, dim3(PJ_BLOCKS), dim3(256), 0, s, logits, target, n, rec);
+    hipLaunchKernelGGL(pjaccard_finalize, dim3(1), dim3(64), 0, s, rec, PJ_BLOCKS, sums_out, loss_out);
+    return launch_status("scd_pjaccard_fwd");
+}
+
+extern "C" int scd_pjaccard_bwd(const float *logits, const float *target, int64_t n, const float *sums,
+                                const float *gloss, float *glogits, float *gtarget, scd_stream_t stream) {
+    clear_error();
+    if (!logits || !target || n < 1 || !sums || !glogits) {
+        set_error("pjaccard_bwd: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    hipLaunchKernelGGL(pjaccard_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), logits, target, n, sums,
+                       gloss, glogits, gtarget);
+    return launch_status("scd_pjaccard_bwd");
+}

@@ -1,0 +1,446 @@
+"""Stage executors of the Siamese U-Net hot path: torch.autograd.Functions over libscd (HIP, gfx950).
+
+Each Function runs a whole stage of the reference's forward (utils/networks.py) as a sequence of C-ABI
+calls on NHWC fp32 device buffers, and its backward as the reverse sequence:
+
+  pack_pair / pack_stream  input NCHW -> NHWC (+ channel padding)        train_supervised.py:68-69
+  EncoderFn                InConv + Encoder (Down x L)                    networks.py:313-343, 405-426
+  SiameseDiffFn            f_t2 - f_t1                                     networks.py:147-150
+  DecoderFn                Up x L (ConvT -> cat -> DoubleConv)             networks.py:346-382, 429-451
+  HeadFn                   OutConv 1x1                                     networks.py:454-461
+  CatFn                    torch.cat(..., dim=1) of decoder outputs        networks.py:119, 258
+  PJaccardFn               power_jaccard_loss                              loss_functions.py:141-150
+
+The Siamese encoder runs both branches as ONE 2B-image batch (weights shared) with BatchNorm
+statistics segmented per branch (nseg = 2), which reproduces the reference's two separate module calls
+exactly: per-branch batch statistics, two running-stat updates (t1 first), summed weight grads.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import hip
+from .hip import TAPS_1, TAPS_2X2, TAPS_3X3, nhwc
+
+_F32 = torch.float32
+
+
+def _empty(shape, like: torch.Tensor, dtype=_F32):
+    return torch.empty(shape, device=like.device, dtype=dtype)
+
+
+def _ws(nbytes: int, like: torch.Tensor):
+    return torch.empty(int(nbytes), device=like.device, dtype=torch.uint8)
+
+
+def pad8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+# ------------------------------------------------------------------------------------------------
+# BatchNorm + ReLU
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class _BNSaved:
+    smean: torch.Tensor
+    sinv: torch.Tensor
+    scale: torch.Tensor
+    shift: torch.Tensor
+    nseg: int
+
+
+def _bn_forward(y: torch.Tensor, bn: torch.nn.BatchNorm2d, nseg: int, training: bool) -> _BNSaved:
+    """Batch statistics (train) or running statistics (eval) -> per-segment scale/shift."""
+    n, h, w, c = y.shape
+    use_batch = training or not bn.track_running_stats or bn.running_mean is None
+    if use_batch:
+        smean, sinv, scale, shift = (_empty((nseg * c,), y) for _ in range(4))
+        ws = _ws(hip.bn_workspace_bytes(n, h, w, c, nseg), y)
+        update = training and bn.track_running_stats and bn.running_mean is not None
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        if update and bn.momentum is None:
+            raise NotImplementedError("BatchNorm2d(momentum=None) cumulative averaging is not supported")
+        hip.bn_train_stats(nhwc(y), nseg, bn.weight, bn.bias, bn.eps, mom, update, bn.running_mean,
+                           bn.running_var, smean, sinv, scale, shift, ws)
+        if update:
+            bn.num_batches_tracked.add_(nseg)
+        return _BNSaved(smean, sinv, scale, shift, nseg)
+    scale, shift = _empty((c,), y), _empty((c,), y)
+    hip.bn_eval_coeffs(c, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, scale, shift)
+    return _BNSaved(None, None, scale, shift, 1)
+
+
+# ------------------------------------------------------------------------------------------------
+# DoubleConv (networks.py:386-402): (conv3x3 -> BN -> ReLU) x 2
+# ------------------------------------------------------------------------------------------------
+def dc_params(dc) -> list:
+    s = dc.conv
+    return [s[0].weight, s[0].bias, s[1].weight, s[1].bias, s[3].weight, s[3].bias, s[4].weight, s[4].bias]
+
+
+def _conv3x3(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int) -> torch.Tensor:
+    n, h, w, _ = x.shape
+    y = _empty((n, h, w, n_out), x)
+    hip.conv_igemm(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, bias, nhwc(y))
+    return y
+
+
+def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool):
+    s = dc.conv
+    conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
+    cin = x.shape[3]
+    if conv0.in_channels > cin:
+        raise ValueError(f"DoubleConv expects {conv0.in_channels} input channels, got {cin}")
+    y0 = _conv3x3(x, hip.pack_conv3x3(conv0.weight.detach(), 0, ci_pad=cin), conv0.bias, conv0.out_channels)
+    st0 = _bn_forward(y0, bn0, nseg, training)
+    a0 = torch.empty_like(y0)
+    hip.bn_relu_apply(nhwc(y0), st0.nseg, st0.scale, st0.shift, nhwc(a0))
+    y1 = _conv3x3(a0, hip.pack_conv3x3(conv1.weight.detach(), 0), conv1.bias, conv1.out_channels)
+    st1 = _bn_forward(y1, bn1, nseg, training)
+    a1 = torch.empty_like(y1)
+    hip.bn_relu_apply(nhwc(y1), st1.nseg, st1.scale, st1.shift, nhwc(a1))
+    saved = (x, y0, a0, st0, y1, st1) if save else None
+    return a1, saved
+
+
+def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3)
+    slabs = _empty((nbytes // 4,), dy)
+    hip.conv_wgrad(d, slabs)
+    gw = torch.empty_like(weight)
+    hip.wgrad_finalize(slabs, nsplit, dy.shape[3], 9, x.shape[3], 0, weight.shape[1], gw)
+    return gw
+
+
+def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool):
+    c = y.shape[3]
+    dy = torch.empty_like(y)
+    dgamma = _empty((c,), y)
+    dbeta = _empty((c,), y)
+    dbias = _empty((c,), y) if conv_bias_grad else None
+    n, h, w, _ = y.shape
+    ws = _ws(hip.bn_workspace_bytes(n, h, w, c, st.nseg), y)
+    hip.bn_relu_backward(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift, dgamma, dbeta,
+                         dbias, nhwc(dy), ws)
+    return dy, dgamma, dbeta, dbias
+
+
+def _dc_backward(g_out: torch.Tensor, saved, dc, need_dx: bool):
+    """Returns (grad wrt DoubleConv input or None, [8 param grads in dc_params order])."""
+    x, y0, a0, st0, y1, st1 = saved
+    s = dc.conv
+    conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
+    if st1.smean is None:
+        raise RuntimeError("backward through an eval-mode BatchNorm is not supported (call net.train())")
+    dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None)
+    gw1 = _wgrad3x3(dy1, a0, conv1.weight)
+    ga0 = _conv3x3(dy1, hip.pack_conv3x3(conv1.weight.detach(), 1), None, conv1.in_channels)
+    dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None)
+    gw0 = _wgrad3x3(dy0, x, conv0.weight)
+    gx = None
+    if need_dx:
+        if x.shape[3] != conv0.in_channels:
+            raise RuntimeError("input-gradient through a channel-padded first layer is not supported")
+        gx = _conv3x3(dy0, hip.pack_conv3x3(conv0.weight.detach(), 1), None, conv0.in_channels)
+    return gx, [gw0, dbias0, dg0, db0, gw1, dbias1, dg1, db1]
+
+
+# ------------------------------------------------------------------------------------------------
+# Input packing
+# ------------------------------------------------------------------------------------------------
+def pack_pair(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:
+    """Siamese input: [2B, H, W, pad8(C)] NHWC with t1 images first (one shared-encoder batch)."""
+    hip.ensure_device(x_t1)
+    if x_t1.requires_grad or x_t2.requires_grad:
+        raise NotImplementedError("input gradients are not computed by the HIP path")
+    b, c, h, w = x_t1.shape
+    c_count = c - c_begin if c_count is None else c_count
+    out = torch.empty((2 * b, h, w, pad8(c_count)), device=x_t1.device, dtype=_F32)
+    hip.pack_nchw(x_t1.float(), c_begin, c_count, out[:b])
+    hip.pack_nchw(x_t2.float(), c_begin, c_count, out[b:])
+    return out
+
+
+def pack_stream(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:
+    """Early-fusion input cat((t1[bands], t2[bands]), dim=1) as [B, H, W, pad8(2*nb)] NHWC."""
+    hip.ensure_device(x_t1)
+    if x_t1.requires_grad or x_t2.requires_grad:
+        raise NotImplementedError("input gradients are not computed by the HIP path")
+    b, c, h, w = x_t1.shape
+    c_count = c - c_begin if c_count is None else c_count
+    cp = pad8(2 * c_count)
+    out = torch.empty((b, h, w, cp), device=x_t1.device, dtype=_F32)
+    # t1 bands -> channels [0, nb) (zero-padding the rest), then t2 bands -> [nb, 2nb)
+    hip.pack_nchw(x_t1.float(), c_begin, c_count, out, 0, cp)  # t1 bands -> [0, nb), zero-pad to cp
+    hip.pack_nchw(x_t2.float(), c_begin, c_count, out, c_count, c_count)  # t2 bands -> [nb, 2nb)
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Encoder: InConv + Down x L
+# ------------------------------------------------------------------------------------------------
+class _Meta:
+    """Non-tensor arguments of a stage Function."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def encoder_blocks(inc, encoder) -> list:
+    return [inc.conv] + [down.mpconv[1] for down in encoder.down_seq.values()]
+
+
+class EncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, meta, *params):
+        ctx.set_materialize_grads(False)
+        blocks = meta.blocks
+        feats, saved = [], []
+        cur = x
+        for level, dc in enumerate(blocks):
+            idx = None
+            if level > 0:
+                prev = feats[-1]
+                n, h, w, c = prev.shape
+                cur = _empty((n, h // 2, w // 2, c), prev)
+                idx = _empty((n, h // 2, w // 2, c), prev, dtype=torch.uint8)
+                hip.maxpool2_fwd(nhwc(prev), nhwc(cur), idx)
+            a, sv = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save)
+            feats.append(a)
+            saved.append((idx, sv))
+        if meta.save:
+            ctx.meta = meta
+            ctx.saved = saved
+            ctx.feat_shapes = [f.shape for f in feats]
+        return tuple(feats)
+
+    @staticmethod
+    def backward(ctx, *g_feats):
+        meta, saved = ctx.meta, ctx.saved
+        blocks = meta.blocks
+        L = len(blocks) - 1
+        grads = [None] * (8 * len(blocks))
+        g_pool = None
+        dev_like = saved[0][1][1]
+        for level in range(L, -1, -1):
+            shape = ctx.feat_shapes[level]
+            ga = _empty(tuple(shape), dev_like)
+            idx_next = saved[level + 1][0] if level < L else None
+            gf = g_feats[level]
+            hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL, idx_next if g_pool is not None else None,
+                             nhwc(gf) if gf is not None else hip._NULL, 0, nhwc(ga))
+            gx, pg = _dc_backward(ga, saved[level][1], blocks[level], need_dx=level > 0)
+            grads[8 * level:8 * level + 8] = pg
+            g_pool = gx
+        ctx.saved = None
+        return (None, None, *grads)
+
+
+def run_encoder(inc, encoder, x: torch.Tensor, nseg: int, training: bool) -> list:
+    blocks = encoder_blocks(inc, encoder)
+    params = [p for dc in blocks for p in dc_params(dc)]
+    save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+    meta = _Meta(blocks=blocks, nseg=nseg, training=training, save=save)
+    return list(EncoderFn.apply(x, meta, *params))
+
+
+# ------------------------------------------------------------------------------------------------
+# Siamese feature difference
+# ------------------------------------------------------------------------------------------------
+class SiameseDiffFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat):
+        n2, h, w, c = feat.shape
+        d = _empty((n2 // 2, h, w, c), feat)
+        hip.siamese_diff(nhwc(feat), nhwc(d))
+        ctx.shape = feat.shape
+        return d
+
+    @staticmethod
+    def backward(ctx, g):
+        gf = _empty(tuple(ctx.shape), g)
+        hip.feature_grad(hip._NULL, None, nhwc(g), 1, nhwc(gf))
+        return gf
+
+
+def siamese_diff(feat: torch.Tensor) -> torch.Tensor:
+    return SiameseDiffFn.apply(feat)
+
+
+# ------------------------------------------------------------------------------------------------
+# Decoder: Up x L
+# ------------------------------------------------------------------------------------------------
+def up_params(up) -> list:
+    return [up.up.weight, up.up.bias] + dc_params(up.conv)
+
+
+class DecoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, meta, x_deep, *rest):
+        ctx.set_materialize_grads(False)
+        ups = meta.ups
+        skips = rest[:len(ups)]
+        cur = x_deep
+        saved = []
+        for k, up in enumerate(ups):
+            skip = skips[k]
+            b, h, w, cs = skip.shape
+            _, hc, wc, cu = cur.shape
+            convT = up.up
+            cto = convT.out_channels
+            if (h, w) != (2 * hc, 2 * wc):
+                raise NotImplementedError(
+                    f"Up: non-zero F.pad (skip {h}x{w} vs upsampled {2 * hc}x{2 * wc}) is not supported yet; "
+                    "use tile sizes divisible by 2**len(TOPOLOGY)")
+            cat = _empty((b, h, w, cs + cto), skip)
+            hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
+            wT = hip.pack_convT2x2(convT.weight.detach(), 0)
+            hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto), store_mode=1)
+            a, sv = _dc_forward(cat, up.conv, 1, meta.training, meta.save)
+            saved.append((cur, cat, cs, sv))
+            cur = a
+        if meta.save:
+            ctx.meta = meta
+            ctx.saved = saved
+        return cur
+
+    @staticmethod
+    def backward(ctx, g_out):
+        meta, saved = ctx.meta, ctx.saved
+        ups = meta.ups
+        n = len(ups)
+        g_skips = [None] * n
+        grads = [None] * (10 * n)
+        g = g_out
+        if g is None:
+            return (None, None, *g_skips, *grads)
+        for k in range(n - 1, -1, -1):
+            up = ups[k]
+            cur, cat, cs, sv = saved[k]
+            g_cat, pg = _dc_backward(g, sv, up.conv, need_dx=True)
+            g_skips[k] = g_cat[..., :cs]
+            convT = up.up
+            cto = convT.out_channels
+            b, hc, wc, cu = cur.shape
+            g_up = nhwc(g_cat, cs, cto)
+            # ConvT data grad: 4-tap stride-2 gather of g_cat's up half
+            g_cur = torch.empty_like(cur)
+            hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, hip.pack_convT2x2(convT.weight.detach(), 1), cu, None,
+                           nhwc(g_cur))
+            # ConvT weight grad: rows = convT input, src = g_up gathered with stride 2
+            d, nsplit, nbytes = hip.wgrad_plan(nhwc(cur), g_up, 2, TAPS_2X2)
+            slabs = _empty((nbytes // 4,), cur)
+            hip.conv_wgrad(d, slabs)
+            gwT = torch.empty_like(convT.weight)
+            hip.wgrad_finalize(slabs, nsplit, cu, 4, cto, 1, cto, gwT)
+            gbT = _empty((cto,), cur)
+            bb, hh, ww, _ = g_cat.shape
+            hip.channel_sum(g_up, gbT, _ws(hip.bn_workspace_bytes(bb, hh, ww, cto, 1), cur))
+            grads[10 * k:10 * k + 10] = [gwT, gbT] + pg
+            g = g_cur
+        ctx.saved = None
+        return (None, g, *g_skips, *grads)
+
+
+def run_decoder(decoder, features: list, training: bool) -> torch.Tensor:
+    """`features` in the reference's order: [deepest, ..., level 0] (Encoder.forward's reversed list)."""
+    ups = list(decoder.up_seq.values())
+    params = [p for up in ups for p in up_params(up)]
+    save = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or any(f.requires_grad for f in features))
+    meta = _Meta(ups=ups, training=training, save=save)
+    return DecoderFn.apply(meta, features[0], *features[1:1 + len(ups)], *params)
+
+
+# ------------------------------------------------------------------------------------------------
+# OutConv 1x1 head
+# ------------------------------------------------------------------------------------------------
+class HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        n, h, w, c = x.shape
+        n_out = weight.shape[0]
+        out = _empty((n, n_out, h, w), x)
+        w2 = weight.detach().reshape(n_out, c).contiguous()
+        hip.conv1x1_fwd(nhwc(x), w2, bias, n_out, out)
+        ctx.save_for_backward(x, w2)
+        ctx.n_out = n_out
+        ctx.wshape = weight.shape
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w2 = ctx.saved_tensors
+        n_out = ctx.n_out
+        gx = torch.empty_like(x)
+        gw = _empty(tuple(ctx.wshape), x)
+        gb = _empty((n_out,), x) if ctx.has_bias else None
+        ws = _ws(hip.conv1x1_workspace_bytes(nhwc(x), n_out), x)
+        hip.conv1x1_bwd(nhwc(x), w2, g.contiguous(), n_out, nhwc(gx), False, gw, gb, ws)
+        return gx, gw, gb
+
+
+def run_head(outc, x: torch.Tensor) -> torch.Tensor:
+    return HeadFn.apply(x, outc.conv.weight, outc.conv.bias)
+
+
+# ------------------------------------------------------------------------------------------------
+# Channel concatenation of NHWC stage outputs (fusion heads)
+# ------------------------------------------------------------------------------------------------
+class CatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        n, h, w, _ = xs[0].shape
+        cs = [x.shape[3] for x in xs]
+        out = _empty((n, h, w, sum(cs)), xs[0])
+        off = 0
+        for x, c in zip(xs, cs):
+            hip.feature_grad(hip._NULL, None, nhwc(x), 0, nhwc(out, off, c))
+            off += c
+        ctx.cs = cs
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        outs, off = [], 0
+        for c in ctx.cs:
+            outs.append(g[..., off:off + c])
+            off += c
+        return tuple(outs)
+
+
+def cat_channels(*xs) -> torch.Tensor:
+    return CatFn.apply(*xs)
+
+
+# ------------------------------------------------------------------------------------------------
+# power_jaccard_loss
+# ------------------------------------------------------------------------------------------------
+class PJaccardFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target):
+        logits = logits.contiguous().float()
+        target = target.contiguous().float()
+        if logits.numel() != target.numel():
+            raise ValueError(f"power_jaccard_loss: {logits.numel()} logits vs {target.numel()} targets")
+        sums = _empty((3,), logits)
+        loss = _empty((), logits)
+        ws = _ws(hip.pjaccard_workspace_bytes(logits.numel()), logits)
+        hip.pjaccard_fwd(logits, target, sums, loss, ws)
+        ctx.save_for_backward(logits, target, sums)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target, sums = ctx.saved_tensors
+        gl = torch.empty_like(logits)
+        gt = torch.empty_like(target) if ctx.needs_input_grad[1] else None
+        hip.pjaccard_bwd(logits, target, sums, g.contiguous(), gl, gt)
+        return gl, gt
+
+
+def power_jaccard(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    hip.ensure_device(logits)
+    return PJaccardFn.apply(logits, target)

@@ -1,0 +1,302 @@
+"""ctypes binding of libscd.so (include/scd.h) — the only way the Python host reaches the GPU kernels.
+
+Every function here takes torch tensors that already live on the current HIP device, converts them
+to the C-ABI views (plain pointers + sizes) and launches on ``torch.cuda.current_stream()``.  There
+is no fallback: if the library is missing or the device is not gfx950 the first call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int8, c_int32, c_int64, c_size_t, c_uint8, c_void_p
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libscd.so")
+
+
+class NHWC(ctypes.Structure):
+    """scd_nhwc_t: channel-slice view of an NHWC fp32 tensor."""
+
+    _fields_ = [("data", c_void_p), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32), ("ldc", c_int32)]
+
+
+class IGEMM(ctypes.Structure):
+    _fields_ = [
+        ("src", NHWC),
+        ("out_h", c_int32),
+        ("out_w", c_int32),
+        ("stride", c_int32),
+        ("ntaps", c_int32),
+        ("dy", c_int8 * 9),
+        ("dx", c_int8 * 9),
+        ("wpk", c_void_p),
+        ("n_out", c_int32),
+        ("bias", c_void_p),
+        ("dst", NHWC),
+        ("store_mode", c_int32),
+    ]
+
+
+class WGRAD(ctypes.Structure):
+    _fields_ = [
+        ("rows", NHWC),
+        ("src", NHWC),
+        ("stride", c_int32),
+        ("ntaps", c_int32),
+        ("dy", c_int8 * 9),
+        ("dx", c_int8 * 9),
+    ]
+
+
+# Tap sets (dy, dx) used by the network.
+TAPS_3X3 = ([-1, -1, -1, 0, 0, 0, 1, 1, 1], [-1, 0, 1, -1, 0, 1, -1, 0, 1])  # t = ky*3 + kx
+TAPS_1 = ([0], [0])
+TAPS_2X2 = ([0, 0, 1, 1], [0, 1, 0, 1])  # t = i*2 + j
+
+_NULL = NHWC(None, 0, 0, 0, 0, 0)
+
+_lib = None
+_dev_checked: set = set()
+
+_SIGS = {
+    "scd_version": ([], c_char_p),
+    "scd_last_error": ([], c_char_p),
+    "scd_device_check": ([c_int], c_int),
+    "scd_pack_nchw": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, NHWC, c_void_p], c_int),
+    "scd_pack_conv3x3": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
+    "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
+    "scd_conv_wgrad": ([POINTER(WGRAD), c_void_p, c_size_t, c_void_p], c_int),
+    "scd_wgrad_finalize": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_bn_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32], c_size_t),
+    "scd_bn_train_stats": (
+        [NHWC, c_int32, c_void_p, c_void_p, c_float, c_float, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+        c_int,
+    ),
+    "scd_bn_eval_coeffs": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p], c_int),
+    "scd_bn_relu_apply": ([NHWC, c_int32, c_void_p, c_void_p, NHWC, c_void_p], c_int),
+    "scd_bn_relu_backward": (
+        [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC,
+         c_void_p, c_size_t, c_void_p],
+        c_int,
+    ),
+    "scd_channel_sum": ([NHWC, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
+    "scd_maxpool2_fwd": ([NHWC, NHWC, c_void_p, c_void_p], c_int),
+    "scd_feature_grad": ([NHWC, c_void_p, NHWC, c_int32, NHWC, c_int32, c_void_p], c_int),
+    "scd_siamese_diff": ([NHWC, NHWC, c_void_p], c_int),
+    "scd_conv1x1_fwd": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p], c_int),
+    "scd_conv1x1_workspace_bytes": ([NHWC, c_int32], c_size_t),
+    "scd_conv1x1_bwd": (
+        [NHWC, c_void_p, c_void_p, c_int32, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+        c_int,
+    ),
+    "scd_pjaccard_workspace_bytes": ([c_int64], c_size_t),
+    "scd_pjaccard_fwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
+    "scd_pjaccard_bwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libscd.so and bind every C-ABI symbol (no GPU work is done here)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libscd.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback."
+        )
+    lib = ctypes.CDLL(path)
+    for name, (argtypes, restype) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load_library()
+
+
+def version() -> str:
+    return lib().scd_version().decode()
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().scd_last_error().decode()
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ensure_device(t: torch.Tensor):
+    """Fail loudly unless `t` lives on a gfx950 HIP device."""
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            "multimodal_siamese_cd_amd runs only on MI355X (gfx950) HIP devices; got a tensor on "
+            f"{t.device}. The CPU restatement under oracle/ is test infrastructure, not a fallback."
+        )
+    idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    if idx not in _dev_checked:
+        _check(lib().scd_device_check(idx), "scd_device_check")
+        _dev_checked.add(idx)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def nhwc(t: torch.Tensor, c_off: int = 0, c: int | None = None) -> NHWC:
+    """View a 4-D [n, h, w, C] tensor (stride(3) == 1, rows of ldc = stride(2)) as scd_nhwc_t."""
+    if t is None:
+        return _NULL
+    if t.dim() != 4 or t.dtype != torch.float32 or t.stride(3) != 1:
+        raise ValueError(f"expected fp32 NHWC tensor with unit channel stride, got {tuple(t.shape)} {t.stride()}")
+    n, h, w, cc = t.shape
+    ldc = t.stride(2)
+    if (h > 1 and t.stride(1) != w * ldc) or (n > 1 and t.stride(0) != h * w * ldc):
+        raise ValueError(f"tensor is not an NHWC channel slice: shape {tuple(t.shape)} stride {t.stride()}")
+    if c is None:
+        c = cc - c_off
+    return NHWC(t.data_ptr() + 4 * c_off, n, h, w, c, ldc)
+
+
+def _taps(taps):
+    dy, dx = taps
+    a = (c_int8 * 9)(*dy, *([0] * (9 - len(dy))))
+    b = (c_int8 * 9)(*dx, *([0] * (9 - len(dx))))
+    return len(dy), a, b
+
+
+# ------------------------------------------------------------------------------------------------
+# thin wrappers
+# ------------------------------------------------------------------------------------------------
+def pack_nchw(src: torch.Tensor, c_begin: int, c_count: int, dst: torch.Tensor, dst_c_off: int = 0, dst_c=None):
+    n, c, h, w = src.shape
+    src = src.contiguous()
+    cc = dst.shape[3] - dst_c_off if dst_c is None else dst_c
+    v = NHWC(dst.data_ptr() + 4 * dst_c_off, dst.shape[0], dst.shape[1], dst.shape[2], cc, dst.stride(2))
+    _check(lib().scd_pack_nchw(src.data_ptr(), n, c, h, w, c_begin, c_count, v, _stream()), "scd_pack_nchw")
+
+
+def pack_conv3x3(w: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch.Tensor:
+    co, ci = w.shape[0], w.shape[1]
+    ci_pad = ci if ci_pad is None else ci_pad
+    out = torch.empty((co * 9 * ci_pad) if mode == 0 else (ci * 9 * co), device=w.device, dtype=torch.float32)
+    _check(lib().scd_pack_conv3x3(w.contiguous().data_ptr(), co, ci, ci_pad, mode, out.data_ptr(), _stream()),
+           "scd_pack_conv3x3")
+    return out
+
+
+def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:
+    ci, co = w.shape[0], w.shape[1]
+    out = torch.empty(ci * co * 4, device=w.device, dtype=torch.float32)
+    _check(lib().scd_pack_convT2x2(w.contiguous().data_ptr(), ci, co, mode, out.data_ptr(), _stream()),
+           "scd_pack_convT2x2")
+    return out
+
+
+def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
+               bias, dst: NHWC, store_mode: int = 0):
+    nt, dy, dx = _taps(taps)
+    d = IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode)
+    _check(lib().scd_conv_igemm(ctypes.byref(d), _stream()), "scd_conv_igemm")
+
+
+def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps):
+    nt, dy, dx = _taps(taps)
+    d = WGRAD(rows, src, stride, nt, dy, dx)
+    ns = c_int32(0)
+    nb = c_size_t(0)
+    _check(lib().scd_wgrad_plan(ctypes.byref(d), ctypes.byref(ns), ctypes.byref(nb)), "scd_wgrad_plan")
+    return d, ns.value, nb.value
+
+
+def conv_wgrad(d: WGRAD, slabs: torch.Tensor):
+    _check(lib().scd_conv_wgrad(ctypes.byref(d), slabs.data_ptr(), slabs.numel() * 4, _stream()), "scd_conv_wgrad")
+
+
+def wgrad_finalize(slabs, nsplit, R, ntaps, C, mode, c_valid, out: torch.Tensor):
+    _check(lib().scd_wgrad_finalize(slabs.data_ptr(), nsplit, R, ntaps, C, mode, c_valid, out.data_ptr(), _stream()),
+           "scd_wgrad_finalize")
+
+
+def bn_workspace_bytes(n, h, w, c, nseg) -> int:
+    return lib().scd_bn_workspace_bytes(n, h, w, c, nseg)
+
+
+def bn_train_stats(y: NHWC, nseg, gamma, beta, eps, momentum, update, rmean, rvar, smean, sinv, scale, shift, ws):
+    _check(
+        lib().scd_bn_train_stats(y, nseg, _ptr(gamma), _ptr(beta), eps, momentum, int(update), _ptr(rmean), _ptr(rvar),
+                                 smean.data_ptr(), sinv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(),
+                                 ws.numel(), _stream()),
+        "scd_bn_train_stats")
+
+
+def bn_eval_coeffs(c, gamma, beta, rmean, rvar, eps, scale, shift):
+    _check(lib().scd_bn_eval_coeffs(c, _ptr(gamma), _ptr(beta), rmean.data_ptr(), rvar.data_ptr(), eps,
+                                    scale.data_ptr(), shift.data_ptr(), _stream()), "scd_bn_eval_coeffs")
+
+
+def bn_relu_apply(y: NHWC, nseg, scale, shift, a: NHWC):
+    _check(lib().scd_bn_relu_apply(y, nseg, scale.data_ptr(), shift.data_ptr(), a, _stream()), "scd_bn_relu_apply")
+
+
+def bn_relu_backward(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, dgamma, dbeta, dbias, dy: NHWC, ws):
+    _check(
+        lib().scd_bn_relu_backward(y, da, nseg, smean.data_ptr(), sinv.data_ptr(), _ptr(gamma), scale.data_ptr(),
+                                   shift.data_ptr(), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), dy, ws.data_ptr(),
+                                   ws.numel(), _stream()),
+        "scd_bn_relu_backward")
+
+
+def channel_sum(x: NHWC, out: torch.Tensor, ws: torch.Tensor):
+    _check(lib().scd_channel_sum(x, out.data_ptr(), ws.data_ptr(), ws.numel(), _stream()), "scd_channel_sum")
+
+
+def maxpool2_fwd(x: NHWC, y: NHWC, idx: torch.Tensor):
+    _check(lib().scd_maxpool2_fwd(x, y, idx.data_ptr(), _stream()), "scd_maxpool2_fwd")
+
+
+def feature_grad(gy: NHWC, idx, gskip: NHWC, skip_mode: int, gx: NHWC, accumulate: bool = False):
+    _check(lib().scd_feature_grad(gy, _ptr(idx), gskip, skip_mode, gx, int(accumulate), _stream()), "scd_feature_grad")
+
+
+def siamese_diff(a: NHWC, d: NHWC):
+    _check(lib().scd_siamese_diff(a, d, _stream()), "scd_siamese_diff")
+
+
+def conv1x1_fwd(x: NHWC, w, b, n_out, out: torch.Tensor):
+    _check(lib().scd_conv1x1_fwd(x, w.data_ptr(), _ptr(b), n_out, out.data_ptr(), _stream()), "scd_conv1x1_fwd")
+
+
+def conv1x1_workspace_bytes(x: NHWC, n_out) -> int:
+    return lib().scd_conv1x1_workspace_bytes(x, n_out)
+
+
+def conv1x1_bwd(x: NHWC, w, gout, n_out, gx: NHWC, accumulate, gw, gb, ws):
+    _check(lib().scd_conv1x1_bwd(x, w.data_ptr(), gout.data_ptr(), n_out, gx, int(accumulate), _ptr(gw), _ptr(gb),
+                                 ws.data_ptr(), ws.numel(), _stream()), "scd_conv1x1_bwd")
+
+
+def pjaccard_workspace_bytes(n) -> int:
+    return lib().scd_pjaccard_workspace_bytes(n)
+
+
+def pjaccard_fwd(logits, target, sums, loss, ws):
+    _check(lib().scd_pjaccard_fwd(logits.data_ptr(), target.data_ptr(), logits.numel(), sums.data_ptr(),
+                                  loss.data_ptr(), ws.data_ptr(), ws.numel(), _stream()), "scd_pjaccard_fwd")
+
+
+def pjaccard_bwd(logits, target, sums, gloss, glogits, gtarget=None):
+    _check(lib().scd_pjaccard_bwd(logits.data_ptr(), target.data_ptr(), logits.numel(), sums.data_ptr(),
+                                  _ptr(gloss), glogits.data_ptr(), _ptr(gtarget), _stream()), "scd_pjaccard_bwd")

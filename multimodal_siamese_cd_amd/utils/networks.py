@@ -1,0 +1,349 @@
+"""Drop-in replacement for the reference's `utils.networks` (utils/networks.py), MI355X-native.
+
+Same public surface as the reference: `create_network(cfg)` (networks.py:12-27), `save_checkpoint`
+(30-38), `load_checkpoint` (41-56) and the model classes UNet (59-79), DualStreamUNet (82-120),
+SiameseUNet (123-154), DualTaskSiameseUNet (157-197), WhateverNet (200-263), WhateverNet2 (266-310),
+Encoder (313-343), Decoder (346-382), DoubleConv (386-402), InConv (405-412), Down (415-426),
+Up (429-451), OutConv (454-461).  Constructor arguments, submodule attribute paths, parameter shapes
+(OIHW) and default initialisation are identical, so `state_dict()` keys and checkpoints interchange
+(e.g. `module.inc.conv.conv.0.weight`).
+
+What differs is the execution: the model-level forward runs every stage through the HIP kernels of
+libscd (via multimodal_siamese_cd_amd.engine) on NHWC fp32 buffers, with the Siamese encoder run as one
+2B-image batch whose BatchNorm statistics are segmented per branch.  torch.nn modules are used only as
+parameter/buffer containers; their own forward is never called on the hot path.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from pathlib import Path
+
+import torch
+import torch.nn as nn
+
+from .. import engine
+
+
+def _check_topology(cfg):
+    topo = list(cfg.MODEL.TOPOLOGY)
+    bad = [t for t in topo if t % 8]
+    if bad:
+        raise ValueError(f"MODEL.TOPOLOGY entries must be multiples of 8 for the MFMA kernels, got {topo}")
+    if cfg.MODEL.OUT_CHANNELS > 4:
+        raise ValueError("OUT_CHANNELS > 4 is not supported by the 1x1 head kernel")
+
+
+class ModelWrapper(nn.Module):
+    """Single-process stand-in for the reference's `nn.DataParallel(model)` (networks.py:27).
+
+    On one device DataParallel is a pass-through (torch/nn/parallel/data_parallel.py:146-149); this
+    wrapper keeps its observable contract — `.module` and the `module.` state_dict prefix.  Multi-GPU
+    training uses one process per GPU (multimodal_siamese_cd_amd.parallel.wrap_ddp) instead.
+    """
+
+    def __init__(self, module: nn.Module):
+        super().__init__()
+        self.module = module
+
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+
+def create_network(cfg):
+    t = cfg.MODEL.TYPE
+    if t == 'unet':
+        model = UNet(cfg)
+    elif t == 'dualstreamunet':
+        model = DualStreamUNet(cfg)
+    elif t == 'siameseunet':
+        model = SiameseUNet(cfg)
+    elif t == 'dtsiameseunet':
+        model = DualTaskSiameseUNet(cfg)
+    elif t == 'whatevernet':
+        model = WhateverNet(cfg)
+    elif t == 'whatevernet2':
+        model = WhateverNet2(cfg)
+    else:
+        raise Exception(f'Unknown network ({t}).')
+    return ModelWrapper(model)
+
+
+def save_checkpoint(network, optimizer, epoch, step, cfg):
+    save_file = Path(cfg.PATHS.OUTPUT) / 'networks' / f'{cfg.NAME}_checkpoint{epoch}.pt'
+    save_file.parent.mkdir(exist_ok=True)
+    torch.save({'step': step, 'network': network.state_dict(), 'optimizer': optimizer.state_dict()}, save_file)
+
+
+def load_checkpoint(epoch, cfg, device, net_file: Path = None):
+    net = create_network(cfg)
+    net.to(device)
+    save_file = net_file if net_file is not None else Path(cfg.PATHS.OUTPUT) / 'networks' / f'{cfg.NAME}_checkpoint{epoch}.pt'
+    checkpoint = torch.load(save_file, map_location=device, weights_only=True)
+    optimizer = torch.optim.AdamW(net.parameters(), lr=cfg.TRAINER.LR, weight_decay=0.01)
+    net.load_state_dict(checkpoint['network'])
+    optimizer.load_state_dict(checkpoint['optimizer'])
+    return net, optimizer, checkpoint['step']
+
+
+def _band_counts(cfg):
+    return len(cfg.DATALOADER.S1_BANDS), len(cfg.DATALOADER.S2_BANDS)
+
+
+def _stream(inc, encoder, decoder, x, nseg, training, siamese):
+    """inc + encoder (+ Siamese diff) + decoder of one stream; returns (decoder output, features)."""
+    feats = engine.run_encoder(inc, encoder, x, nseg, training)
+    if siamese:
+        feats = [engine.siamese_diff(f) for f in feats]
+    feats = feats[::-1]  # Encoder.forward returns the reversed list (networks.py:342)
+    return engine.run_decoder(decoder, feats, training), feats
+
+
+class UNet(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        _check_topology(cfg)
+        self.cfg = cfg
+        topology = cfg.MODEL.TOPOLOGY
+        self.inc = InConv(cfg.MODEL.IN_CHANNELS * 2, topology[0], DoubleConv)
+        self.encoder = Encoder(cfg)
+        self.decoder = Decoder(cfg)
+        self.outc = OutConv(topology[0], cfg.MODEL.OUT_CHANNELS)
+
+    def forward(self, x_t1, x_t2):
+        x = engine.pack_stream(x_t1, x_t2)  # torch.cat((x_t1, x_t2), dim=1) (networks.py:74)
+        dec, _ = _stream(self.inc, self.encoder, self.decoder, x, 1, self.training, siamese=False)
+        return engine.run_head(self.outc, dec)
+
+
+class DualStreamUNet(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        _check_topology(cfg)
+        self.cfg = cfg
+        topology = cfg.MODEL.TOPOLOGY
+        n1, n2 = _band_counts(cfg)
+        self.inc_stream1 = InConv(2 * n1, topology[0], DoubleConv)
+        self.encoder_stream1 = Encoder(cfg)
+        self.decoder_stream1 = Decoder(cfg)
+        self.inc_stream2 = InConv(2 * n2, topology[0], DoubleConv)
+        self.encoder_stream2 = Encoder(cfg)
+        self.decoder_stream2 = Decoder(cfg)
+        self.outc = OutConv(2 * topology[0], cfg.MODEL.OUT_CHANNELS)
+
+    def forward(self, x_t1, x_t2):
+        n1, _ = _band_counts(self.cfg)
+        c = x_t1.shape[1]
+        x1 = engine.pack_stream(x_t1, x_t2, 0, n1)
+        d1, _ = _stream(self.inc_stream1, self.encoder_stream1, self.decoder_stream1, x1, 1, self.training, False)
+        x2 = engine.pack_stream(x_t1, x_t2, n1, c - n1)
+        d2, _ = _stream(self.inc_stream2, self.encoder_stream2, self.decoder_stream2, x2, 1, self.training, False)
+        return engine.run_head(self.outc, engine.cat_channels(d1, d2))
+
+
+class SiameseUNet(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        _check_topology(cfg)
+        self.cfg = cfg
+        topology = cfg.MODEL.TOPOLOGY
+        self.inc = InConv(cfg.MODEL.IN_CHANNELS, topology[0], DoubleConv)
+        self.encoder = Encoder(cfg)
+        self.decoder = Decoder(cfg)
+        self.outc = OutConv(topology[0], cfg.MODEL.OUT_CHANNELS)
+
+    def forward(self, x_t1, x_t2):
+        x = engine.pack_pair(x_t1, x_t2)
+        dec, _ = _stream(self.inc, self.encoder, self.decoder, x, 2, self.training, siamese=True)
+        return engine.run_head(self.outc, dec)
+
+
+class DualTaskSiameseUNet(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        _check_topology(cfg)
+        self.cfg = cfg
+        topology = cfg.MODEL.TOPOLOGY
+        n_classes = cfg.MODEL.OUT_CHANNELS
+        self.inc = InConv(cfg.MODEL.IN_CHANNELS, topology[0], DoubleConv)
+        self.encoder = Encoder(cfg)
+        self.decoder_change = Decoder(cfg)
+        self.decoder_sem = Decoder(cfg)
+        self.outc_change = OutConv(topology[0], n_classes)
+        self.outc_sem = OutConv(topology[0], n_classes)
+        self.outc_sem_change = OutConv(2, 1)  # present in the reference, unused by forward (networks.py:174)
+
+    def forward(self, x_t1, x_t2):
+        b = x_t1.shape[0]
+        x = engine.pack_pair(x_t1, x_t2)
+        feats = engine.run_encoder(self.inc, self.encoder, x, 2, self.training)
+        diffs = [engine.siamese_diff(f) for f in feats][::-1]
+        out_change = engine.run_head(self.outc_change, engine.run_decoder(self.decoder_change, diffs, self.training))
+        f_t2 = [f[b:] for f in feats][::-1]
+        out_sem_t2 = engine.run_head(self.outc_sem, engine.run_decoder(self.decoder_sem, f_t2, self.training))
+        f_t1 = [f[:b] for f in feats][::-1]
+        out_sem_t1 = engine.run_head(self.outc_sem, engine.run_decoder(self.decoder_sem, f_t1, self.training))
+        return out_change, out_sem_t1, out_sem_t2
+
+
+class WhateverNet(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        _check_topology(cfg)
+        self.cfg = cfg
+        topology = cfg.MODEL.TOPOLOGY
+        n_classes = cfg.MODEL.OUT_CHANNELS
+        n1, n2 = _band_counts(cfg)
+        self.inc_stream1 = InConv(n1, topology[0], DoubleConv)
+        self.encoder_stream1 = Encoder(cfg)
+        self.decoder_stream1 = Decoder(cfg)
+        self.outc_stream1 = OutConv(topology[0], n_classes)
+        self.inc_stream2 = InConv(n2, topology[0], DoubleConv)
+        self.encoder_stream2 = Encoder(cfg)
+        self.decoder_stream2 = Decoder(cfg)
+        self.outc_stream2 = OutConv(topology[0], n_classes)
+        self.outc_fusion = OutConv(2 * topology[0], n_classes)
+
+    def forward(self, x_t1, x_t2):
+        n1, _ = _band_counts(self.cfg)
+        c = x_t1.shape[1]
+        x1 = engine.pack_pair(x_t1, x_t2, 0, n1)
+        d1, _ = _stream(self.inc_stream1, self.encoder_stream1, self.decoder_stream1, x1, 2, self.training, True)
+        out_stream1 = engine.run_head(self.outc_stream1, d1)
+        x2 = engine.pack_pair(x_t1, x_t2, n1, c - n1)
+        d2, _ = _stream(self.inc_stream2, self.encoder_stream2, self.decoder_stream2, x2, 2, self.training, True)
+        out_stream2 = engine.run_head(self.outc_stream2, d2)
+        out_fusion = engine.run_head(self.outc_fusion, engine.cat_channels(d1, d2))
+        if self.training:
+            return out_fusion, out_stream1, out_stream2
+        return out_fusion
+
+
+class WhateverNet2(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        _check_topology(cfg)
+        self.cfg = cfg
+        topology = cfg.MODEL.TOPOLOGY
+        n_classes = cfg.MODEL.OUT_CHANNELS
+        n1, n2 = _band_counts(cfg)
+        self.inc_stream1 = InConv(2 * n1, topology[0], DoubleConv)
+        self.encoder_stream1 = Encoder(cfg)
+        self.decoder_stream1 = Decoder(cfg)
+        self.outc_stream1 = OutConv(topology[0], n_classes)
+        self.inc_stream2 = InConv(2 * n2, topology[0], DoubleConv)
+        self.encoder_stream2 = Encoder(cfg)
+        self.decoder_stream2 = Decoder(cfg)
+        self.outc_stream2 = OutConv(topology[0], n_classes)
+        self.outc_fusion = OutConv(2 * topology[0], n_classes)
+
+    def forward(self, x_t1, x_t2):
+        n1, _ = _band_counts(self.cfg)
+        c = x_t1.shape[1]
+        x1 = engine.pack_stream(x_t1, x_t2, 0, n1)
+        d1, _ = _stream(self.inc_stream1, self.encoder_stream1, self.decoder_stream1, x1, 1, self.training, False)
+        out_stream1 = engine.run_head(self.outc_stream1, d1)
+        x2 = engine.pack_stream(x_t1, x_t2, n1, c - n1)
+        d2, _ = _stream(self.inc_stream2, self.encoder_stream2, self.decoder_stream2, x2, 1, self.training, False)
+        out_stream2 = engine.run_head(self.outc_stream2, d2)
+        out_fusion = engine.run_head(self.outc_fusion, engine.cat_channels(d1, d2))
+        if self.training:
+            return out_fusion, out_stream1, out_stream2
+        return out_fusion
+
+
+# ------------------------------------------------------------------------------------------------
+# Building blocks: parameter containers with the reference's attribute paths.
+# ------------------------------------------------------------------------------------------------
+_STAGE_ONLY = ("{} is executed as part of a model-level stage on the HIP path "
+               "(multimodal_siamese_cd_amd.engine); call the model's forward instead")
+
+
+class Encoder(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        down_topo = cfg.MODEL.TOPOLOGY
+        n_layers = len(down_topo)
+        down_dict = OrderedDict()
+        for idx in range(n_layers):
+            in_dim = down_topo[idx]
+            out_dim = down_topo[idx + 1] if idx != n_layers - 1 else down_topo[idx]
+            down_dict[f'down{idx + 1}'] = Down(in_dim, out_dim, DoubleConv)
+        self.down_seq = nn.ModuleDict(down_dict)
+
+    def forward(self, x1):
+        raise NotImplementedError(_STAGE_ONLY.format("Encoder"))
+
+
+class Decoder(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        topology = cfg.MODEL.TOPOLOGY
+        n_layers = len(topology)
+        up_topo = [topology[0]]
+        for idx in range(n_layers):
+            up_topo.append(topology[idx + 1] if idx != n_layers - 1 else topology[idx])
+        up_dict = OrderedDict()
+        for idx in reversed(range(n_layers)):
+            x2_idx = idx - 1 if idx != 0 else idx
+            up_dict[f'up{idx + 1}'] = Up(up_topo[idx] * 2, up_topo[x2_idx], DoubleConv)
+        self.up_seq = nn.ModuleDict(up_dict)
+
+    def forward(self, features):
+        raise NotImplementedError(_STAGE_ONLY.format("Decoder"))
+
+
+class DoubleConv(nn.Module):
+    '''(conv => BN => ReLU) * 2'''
+
+    def __init__(self, in_ch, out_ch):
+        super().__init__()
+        self.conv = nn.Sequential(
+            nn.Conv2d(in_ch, out_ch, 3, padding=1),
+            nn.BatchNorm2d(out_ch),
+            nn.ReLU(inplace=True),
+            nn.Conv2d(out_ch, out_ch, 3, padding=1),
+            nn.BatchNorm2d(out_ch),
+            nn.ReLU(inplace=True),
+        )
+
+    def forward(self, x):
+        raise NotImplementedError(_STAGE_ONLY.format("DoubleConv"))
+
+
+class InConv(nn.Module):
+    def __init__(self, in_ch, out_ch, conv_block):
+        super().__init__()
+        self.conv = conv_block(in_ch, out_ch)
+
+    def forward(self, x):
+        raise NotImplementedError(_STAGE_ONLY.format("InConv"))
+
+
+class Down(nn.Module):
+    def __init__(self, in_ch, out_ch, conv_block):
+        super().__init__()
+        self.mpconv = nn.Sequential(nn.MaxPool2d(2), conv_block(in_ch, out_ch))
+
+    def forward(self, x):
+        raise NotImplementedError(_STAGE_ONLY.format("Down"))
+
+
+class Up(nn.Module):
+    def __init__(self, in_ch, out_ch, conv_block):
+        super().__init__()
+        self.up = nn.ConvTranspose2d(in_ch // 2, in_ch // 2, 2, stride=2)
+        self.conv = conv_block(in_ch, out_ch)
+
+    def forward(self, x1, x2):
+        raise NotImplementedError(_STAGE_ONLY.format("Up"))
+
+
+class OutConv(nn.Module):
+    def __init__(self, in_ch, out_ch):
+        super().__init__()
+        self.conv = nn.Conv2d(in_ch, out_ch, 1)
+
+    def forward(self, x):
+        raise NotImplementedError(_STAGE_ONLY.format("OutConv"))

@@ -1,0 +1,175 @@
+"""Generate golden fixtures by running the REFERENCE implementation itself (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py  [--ref /root/reference]
+
+Imports the reference's utils/networks.py and utils/loss_functions.py from /root/reference (a local
+stub stands in for the missing `fvcore` package, which networks.py only uses for type annotations via
+utils/experiment_manager.py:7), builds each model with `networks.create_network` (networks.py:12-27),
+loads a deterministic parameter fill (oracle.siamese_oracle.deterministic_params), and records on CPU
+fp32 one training step of the reference trainers:
+
+  train-mode outputs, loss, every parameter gradient, BatchNorm buffers after the step,
+  eval-mode outputs (running statistics), then two more AdamW steps (loss trajectory + final params).
+
+Only data (inputs and expected outputs) is written to tests/golden/*.npz; no reference source travels.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import siamese_oracle as O  # noqa: E402
+
+CONFIGS = [
+    # name, model type, topology, in_channels, S1 bands, S2 bands, batch, hw, labeled
+    ('siamese_t8-16', 'siameseunet', [8, 16], 5, [0, 1], [2, 1, 0], 2, 64, None),
+    ('siamese_t8-16-32', 'siameseunet', [8, 16, 32], 5, [0, 1], [2, 1, 0], 2, 32, None),
+    ('unet_t8-16', 'unet', [8, 16], 5, [0, 1], [2, 1, 0], 2, 32, None),
+    ('dualstream_t8-16', 'dualstreamunet', [8, 16], 5, [0, 1], [2, 1, 0], 2, 32, None),
+    ('dtsiamese_t8-16', 'dtsiameseunet', [8, 16], 5, [0, 1], [2, 1, 0], 2, 32, None),
+    ('whatevernet_t8-16', 'whatevernet', [8, 16], 5, [0, 1], [2, 1, 0], 2, 32, [True, False]),
+]
+LR = 1e-3
+WD = 0.01
+ALPHA = 0.5
+SEED = 7
+
+
+def import_reference(ref):
+    fv = types.ModuleType('fvcore')
+    fvc = types.ModuleType('fvcore.common')
+    fvcc = types.ModuleType('fvcore.common.config')
+
+    class _CfgNode(dict):  # annotation-only stand-in
+        pass
+
+    fvcc.CfgNode = _CfgNode
+    sys.modules.setdefault('fvcore', fv)
+    sys.modules.setdefault('fvcore.common', fvc)
+    sys.modules.setdefault('fvcore.common.config', fvcc)
+    sys.path.insert(0, ref)
+    from utils import loss_functions, networks  # noqa: E402
+    return networks, loss_functions
+
+
+def ns_cfg(d):
+    from types import SimpleNamespace as NS
+    return NS(MODEL=NS(TYPE=d['TYPE'], IN_CHANNELS=d['IN_CHANNELS'], OUT_CHANNELS=d['OUT_CHANNELS'],
+                       TOPOLOGY=list(d['TOPOLOGY'])),
+              DATALOADER=NS(S1_BANDS=list(d['S1_BANDS']), S2_BANDS=list(d['S2_BANDS'])))
+
+
+def outputs_list(o):
+    return list(o) if isinstance(o, (tuple, list)) else [o]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--ref', default='/root/reference')
+    ap.add_argument('--only', default=None)
+    args = ap.parse_args()
+    networks, loss_functions = import_reference(args.ref)
+    pj = loss_functions.get_criterion('PowerJaccardLoss')
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+    for name, mtype, topo, cin, s1, s2, b, hw, labeled in CONFIGS:
+        if args.only and args.only != name:
+            continue
+        cfgd = dict(TYPE=mtype, IN_CHANNELS=cin, OUT_CHANNELS=1, TOPOLOGY=topo, S1_BANDS=s1, S2_BANDS=s2)
+        net = networks.create_network(ns_cfg(cfgd))
+        module = net.module
+        shapes = O.param_shapes(mtype, cfgd)
+        ref_shapes = [(k, tuple(p.shape)) for k, p in module.named_parameters()]
+        assert ref_shapes == list(shapes.items()), f'{name}: oracle parameter table differs from the reference'
+        P0 = O.deterministic_params(shapes, SEED)
+        with torch.no_grad():
+            for k, p in module.named_parameters():
+                p.copy_(P0[k])
+        batch = O.synthetic_batch(cfgd, b, hw, SEED + 1, labeled)
+        rec = {}
+        for k in ('x_t1', 'x_t2', 'y_change', 'y_sem_t1', 'y_sem_t2'):
+            rec[k] = batch[k].numpy()
+        rec['is_labeled'] = batch['is_labeled'].numpy()
+        for k, v in P0.items():
+            rec['p0/' + k] = v.numpy()
+
+        opt = torch.optim.AdamW(net.parameters(), lr=LR, weight_decay=WD)
+        net.train()
+        opt.zero_grad()
+        out = net(batch['x_t1'], batch['x_t2'])
+        # the loss recipes of the reference trainers, evaluated with the REFERENCE loss function
+        loss = _ref_step_loss(mtype, out, batch, pj)
+        loss.backward()
+        for i, o in enumerate(outputs_list(out)):
+            rec[f'out/{i}'] = o.detach().numpy()
+        rec['loss0'] = np.float32(loss.item())
+        for k, p in module.named_parameters():
+            if p.grad is not None:  # outc_sem_change is unused by DualTaskSiameseUNet.forward
+                rec['g/' + k] = p.grad.detach().numpy().copy()
+        for k, v in module.state_dict().items():
+            if 'running' in k or 'num_batches' in k:
+                rec['r1/' + k] = v.detach().numpy().copy()
+        net.eval()
+        with torch.no_grad():
+            ev = net(batch['x_t1'], batch['x_t2'])
+        for i, o in enumerate(outputs_list(ev)):
+            rec[f'eval/{i}'] = o.numpy()
+        net.train()
+        losses = [loss.item()]
+        opt.step()
+        for _ in range(2):
+            opt.zero_grad()
+            out = net(batch['x_t1'], batch['x_t2'])
+            loss = _ref_step_loss(mtype, out, batch, pj)
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        rec['losses'] = np.array(losses, dtype=np.float32)
+        for k, p in module.named_parameters():
+            rec['p3/' + k] = p.detach().numpy().copy()
+        for k, v in module.state_dict().items():
+            if 'running' in k or 'num_batches' in k:
+                rec['r3/' + k] = v.detach().numpy().copy()
+        meta = dict(name=name, cfg=cfgd, batch=b, hw=hw, seed=SEED, lr=LR, wd=WD, alpha=ALPHA, labeled=labeled,
+                    generator='reference utils/networks.py + utils/loss_functions.py (CPU fp32, torch '
+                              + torch.__version__ + ')')
+        rec['meta'] = np.array(json.dumps(meta))
+        path = os.path.join(HERE, f'{name}.npz')
+        np.savez_compressed(path, **rec)
+        print(f'{name}: loss0={losses[0]:.6f} losses={losses} -> {os.path.getsize(path) / 1024:.0f} KiB')
+
+
+def _ref_step_loss(mtype, out, batch, pj):
+    """Loss recipes of train_supervised.py:75, train_supervised_dualtask.py:73-85, train_semisupervised.py:82-113."""
+    y = batch['y_change']
+    if mtype in ('siameseunet', 'unet', 'dualstreamunet'):
+        return pj(out, y)
+    if mtype == 'dtsiameseunet':
+        c, s1, s2 = out
+        return (pj(c, y) + (pj(s1, batch['y_sem_t1']) + pj(s2, batch['y_sem_t2'])) / 2) / 2
+    if mtype == 'whatevernet':
+        f, s1, s2 = out
+        lab = batch['is_labeled']
+        loss = None
+        if lab.any():
+            loss = ALPHA * ((pj(f[lab], y[lab]) + pj(s1[lab], y[lab]) + pj(s2[lab], y[lab])) / 3)
+        if not lab.all():
+            nl = torch.logical_not(lab)
+            cons = (1 - ALPHA) * pj(s1[nl], torch.sigmoid(s2[nl]))
+            loss = cons if loss is None else loss + cons
+        return loss
+    raise ValueError(mtype)
+
+
+if __name__ == '__main__':
+    main()

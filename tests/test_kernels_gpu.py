@@ -1,0 +1,303 @@
+"""Per-kernel parity on MI355X: each libscd entry point vs the torch fp32 CPU op it replaces.
+
+Tolerance: max|hip - ref| / max|ref| <= 1e-5 for single ops (fp32 MFMA = exact fp32 fmaf chains; the
+residual is summation order), argmax indices bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import siamese_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+@pytest.fixture(scope='module')
+def dev():
+    from multimodal_siamese_cd_amd import hip
+    hip.load_library()
+    d = torch.device('cuda:0')
+    hip.ensure_device(torch.empty(1, device=d))
+    return d
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def nhwc_t(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+CONV_SHAPES = [  # n, h, w, cin, cout
+    (2, 16, 16, 8, 8),
+    (2, 9, 13, 16, 40),
+    (1, 8, 8, 64, 128),
+    (2, 32, 32, 128, 64),
+    (3, 5, 7, 24, 200),
+    (2, 16, 16, 512, 512),
+]
+
+
+@pytest.mark.parametrize('n,h,w,ci,co', CONV_SHAPES)
+def test_conv3x3_forward(dev, n, h, w, ci, co):
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * 1000 + ci + co)
+    x = torch.randn(n, h, w, ci, generator=g)
+    wt = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
+    b = torch.randn(co, generator=g)
+    ref = nhwc_t(F.conv2d(nchw(x), wt, b, padding=1))
+    xd, wd, bd = x.to(dev), wt.to(dev), b.to(dev)
+    y = torch.empty(n, h, w, co, device=dev)
+    hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wd, 0), co, bd, hip.nhwc(y))
+    assert rel(y, ref) < TOL
+
+
+@pytest.mark.parametrize('n,h,w,ci,co', CONV_SHAPES)
+def test_conv3x3_data_and_weight_grad(dev, n, h, w, ci, co):
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(7 + n + ci * co)
+    x = torch.randn(n, h, w, ci, generator=g)
+    wt = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
+    dy = torch.randn(n, h, w, co, generator=g)
+    ref_dx = nhwc_t(torch.nn.grad.conv2d_input((n, ci, h, w), wt, nchw(dy), padding=1))
+    ref_dw = torch.nn.grad.conv2d_weight(nchw(x), wt.shape, nchw(dy), padding=1)
+    xd, wd, dyd = x.to(dev), wt.to(dev), dy.to(dev)
+    dx = torch.empty(n, h, w, ci, device=dev)
+    hip.conv_igemm(hip.nhwc(dyd), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wd, 1), ci, None, hip.nhwc(dx))
+    assert rel(dx, ref_dx) < TOL
+    d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dyd), hip.nhwc(xd), 1, hip.TAPS_3X3)
+    slabs = torch.empty(nbytes // 4, device=dev)
+    hip.conv_wgrad(d, slabs)
+    dw = torch.empty(co, ci, 3, 3, device=dev)
+    hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
+    assert rel(dw, ref_dw) < TOL
+
+
+def test_conv3x3_channel_padded_input(dev):
+    """First layer: 5 real input channels padded to 8 in NHWC (zero channels, zero weights)."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(3)
+    n, h, w, ci, co = 2, 12, 20, 5, 16
+    x = torch.rand(n, ci, h, w, generator=g)
+    wt = torch.randn(co, ci, 3, 3, generator=g)
+    b = torch.randn(co, generator=g)
+    ref = nhwc_t(F.conv2d(x, wt, b, padding=1))
+    xp = torch.empty(n, h, w, 8, device=dev)
+    hip.pack_nchw(x.to(dev), 0, ci, xp)
+    assert torch.equal(xp[..., 5:].cpu(), torch.zeros(n, h, w, 3))
+    y = torch.empty(n, h, w, co, device=dev)
+    hip.conv_igemm(hip.nhwc(xp), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wt.to(dev), 0, ci_pad=8), co, b.to(dev),
+                   hip.nhwc(y))
+    assert rel(y, ref) < TOL
+    dy = torch.randn(n, h, w, co, generator=g)
+    ref_dw = torch.nn.grad.conv2d_weight(x, wt.shape, nchw(dy), padding=1)
+    d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dy.to(dev)), hip.nhwc(xp), 1, hip.TAPS_3X3)
+    slabs = torch.empty(nbytes // 4, device=dev)
+    hip.conv_wgrad(d, slabs)
+    dw = torch.empty(co, ci, 3, 3, device=dev)
+    hip.wgrad_finalize(slabs, nsplit, co, 9, 8, 0, ci, dw)
+    assert rel(dw, ref_dw) < TOL
+
+
+@pytest.mark.parametrize('n,h,w,c,cs', [(2, 8, 8, 16, 16), (1, 16, 16, 64, 64), (2, 4, 6, 512, 512), (2, 3, 5, 8, 24)])
+def test_convT2x2_forward_into_concat_slice(dev, n, h, w, c, cs):
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(c + h)
+    x = torch.randn(n, h, w, c, generator=g)
+    wt = torch.randn(c, c, 2, 2, generator=g) / c ** 0.5
+    b = torch.randn(c, generator=g)
+    ref = nhwc_t(F.conv_transpose2d(nchw(x), wt, b, stride=2))
+    cat = torch.full((n, 2 * h, 2 * w, cs + c), float('nan'), device=dev)
+    hip.conv_igemm(hip.nhwc(x.to(dev)), h, w, 1, hip.TAPS_1, hip.pack_convT2x2(wt.to(dev), 0), 4 * c, b.to(dev),
+                   hip.nhwc(cat, cs, c), store_mode=1)
+    assert rel(cat[..., cs:], ref) < TOL
+    assert torch.isnan(cat[..., :cs]).all(), 'wrote outside its channel slice'
+
+
+@pytest.mark.parametrize('n,h,w,c,cs', [(2, 8, 8, 16, 16), (1, 16, 16, 64, 64), (2, 4, 6, 512, 512)])
+def test_convT2x2_backward(dev, n, h, w, c, cs):
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(11 + c)
+    x = torch.randn(n, c, h, w, generator=g, requires_grad=True)
+    wt = (torch.randn(c, c, 2, 2, generator=g) / c ** 0.5).requires_grad_(True)
+    b = torch.randn(c, generator=g, requires_grad=True)
+    out = F.conv_transpose2d(x, wt, b, stride=2)
+    gy = torch.randn(out.shape, generator=g)
+    out.backward(gy)
+    gcat = torch.randn(n, 2 * h, 2 * w, cs + c, generator=g)
+    gcat[..., cs:] = nhwc_t(gy)
+    gd = gcat.to(dev)
+    gup = hip.nhwc(gd, cs, c)
+    xd = nhwc_t(x.detach()).to(dev)
+    gx = torch.empty(n, h, w, c, device=dev)
+    hip.conv_igemm(gup, h, w, 2, hip.TAPS_2X2, hip.pack_convT2x2(wt.detach().to(dev), 1), c, None, hip.nhwc(gx))
+    assert rel(gx, nhwc_t(x.grad)) < TOL
+    d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(xd), gup, 2, hip.TAPS_2X2)
+    slabs = torch.empty(nbytes // 4, device=dev)
+    hip.conv_wgrad(d, slabs)
+    gw = torch.empty(c, c, 2, 2, device=dev)
+    hip.wgrad_finalize(slabs, nsplit, c, 4, c, 1, c, gw)
+    assert rel(gw, wt.grad) < TOL
+    gb = torch.empty(c, device=dev)
+    hip.channel_sum(gup, gb, torch.empty(hip.bn_workspace_bytes(n, 2 * h, 2 * w, c, 1), dtype=torch.uint8, device=dev))
+    assert rel(gb, b.grad) < TOL
+
+
+@pytest.mark.parametrize('n,h,w,c,nseg', [(4, 16, 16, 8, 2), (2, 33, 17, 64, 2), (2, 64, 64, 16, 1), (6, 8, 8, 512, 2)])
+def test_batchnorm_relu_train_forward_backward(dev, n, h, w, c, nseg):
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * h + c)
+    y = (torch.randn(n, h, w, c, generator=g) * 3 + 5).requires_grad_(True)  # mean >> std stresses the variance
+    gamma = (1 + 0.1 * torch.randn(c, generator=g)).requires_grad_(True)
+    beta = (0.1 * torch.randn(c, generator=g)).requires_grad_(True)
+    rm0, rv0 = torch.randn(c, generator=g), torch.rand(c, generator=g) + 0.5
+    rm, rv = rm0.clone(), rv0.clone()
+    outs = []
+    per = n // nseg
+    for s in range(nseg):
+        ys = nchw(y[s * per:(s + 1) * per])
+        outs.append(nhwc_t(F.relu(F.batch_norm(ys, rm, rv, gamma, beta, True, 0.1, 1e-5))))
+    ref = torch.cat(outs)
+    ga = torch.randn(n, h, w, c, generator=g)
+    ref.backward(ga)
+
+    yd = y.detach().to(dev)
+    smean, sinv, scale, shift = (torch.empty(nseg * c, device=dev) for _ in range(4))
+    rmd, rvd = rm0.to(dev), rv0.to(dev)
+    ws = torch.empty(hip.bn_workspace_bytes(n, h, w, c, nseg), dtype=torch.uint8, device=dev)
+    gd, bd = gamma.detach().to(dev), beta.detach().to(dev)
+    hip.bn_train_stats(hip.nhwc(yd), nseg, gd, bd, 1e-5, 0.1, True, rmd, rvd, smean, sinv, scale, shift, ws)
+    a = torch.empty_like(yd)
+    hip.bn_relu_apply(hip.nhwc(yd), nseg, scale, shift, hip.nhwc(a))
+    assert rel(a, ref) < 1e-5
+    assert rel(rmd, rm) < 1e-6 and rel(rvd, rv) < 1e-6
+    dy = torch.empty_like(yd)
+    dgam, dbet, dbias = (torch.empty(c, device=dev) for _ in range(3))
+    hip.bn_relu_backward(hip.nhwc(yd), hip.nhwc(ga.to(dev)), nseg, smean, sinv, gd, scale, shift, dgam, dbet, dbias,
+                         hip.nhwc(dy), ws)
+    assert rel(dy, y.grad) < 1e-4
+    assert rel(dgam, gamma.grad) < 1e-5 and rel(dbet, beta.grad) < 1e-5
+    assert (dbias.cpu() - y.grad.sum((0, 1, 2))).abs().max() < 1e-3 * y.grad.abs().max()
+
+
+def test_batchnorm_eval(dev):
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(5)
+    n, h, w, c = 2, 8, 8, 32
+    y = torch.randn(n, h, w, c, generator=g)
+    gamma, beta = torch.randn(c, generator=g), torch.randn(c, generator=g)
+    rm, rv = torch.randn(c, generator=g), torch.rand(c, generator=g) + 0.1
+    ref = nhwc_t(F.relu(F.batch_norm(nchw(y), rm, rv, gamma, beta, False, 0.1, 1e-5)))
+    scale, shift = torch.empty(c, device=dev), torch.empty(c, device=dev)
+    hip.bn_eval_coeffs(c, gamma.to(dev), beta.to(dev), rm.to(dev), rv.to(dev), 1e-5, scale, shift)
+    a = torch.empty(n, h, w, c, device=dev)
+    hip.bn_relu_apply(hip.nhwc(y.to(dev)), 1, scale, shift, hip.nhwc(a))
+    assert rel(a, ref) < 1e-5
+
+
+@pytest.mark.parametrize('n,h,w,c', [(2, 16, 16, 8), (2, 7, 9, 64), (1, 32, 32, 512)])
+def test_maxpool_forward_indices_and_feature_grad(dev, n, h, w, c):
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(h * w + c)
+    x = F.relu(torch.randn(n, h, w, c, generator=g))  # ReLU outputs: many ties at 0 (first max wins)
+    x[0, 0, 1, 0] = float('nan')
+    xc = nchw(x).requires_grad_(True)
+    ref, ref_idx = F.max_pool2d(xc, 2, return_indices=True)
+    ho, wo = h // 2, w // 2
+    xd = x.to(dev)
+    y = torch.empty(n, ho, wo, c, device=dev)
+    idx = torch.empty(n, ho, wo, c, dtype=torch.uint8, device=dev)
+    hip.maxpool2_fwd(hip.nhwc(xd), hip.nhwc(y), idx)
+    yc = y.cpu()
+    assert torch.equal(torch.isnan(yc), torch.isnan(nhwc_t(ref.detach())))
+    assert torch.equal(torch.nan_to_num(yc, 0.0), torch.nan_to_num(nhwc_t(ref.detach()), 0.0))
+    # decode aten's flat indices to window positions
+    ri = nhwc_t(ref_idx)
+    oy = torch.arange(ho).view(1, ho, 1, 1)
+    ox = torch.arange(wo).view(1, 1, wo, 1)
+    win = ((ri // w) - 2 * oy) * 2 + ((ri % w) - 2 * ox)
+    assert torch.equal(idx.cpu().long(), win)
+    # backward + Siamese skip add: gx = pool_bwd(gy) + sign * gskip
+    gy = torch.randn(n, ho, wo, c, generator=g)
+    ref.backward(nchw(gy))
+    gskip = torch.randn(n // 2 if n > 1 else 1, h, w, c, generator=g)
+    gx = torch.empty(n, h, w, c, device=dev)
+    mode = 1 if n % 2 == 0 else 0
+    hip.feature_grad(hip.nhwc(gy.to(dev)), idx, hip.nhwc(gskip.to(dev)), mode, hip.nhwc(gx))
+    sgn = torch.ones(n, 1, 1, 1)
+    if mode == 1:
+        sgn[: n // 2] = -1
+    want = nhwc_t(xc.grad) + sgn * gskip.repeat(n // gskip.shape[0], 1, 1, 1)
+    assert torch.allclose(gx.cpu(), want, atol=1e-6)
+
+
+def test_siamese_diff(dev):
+    from multimodal_siamese_cd_amd import hip
+    a = torch.randn(6, 5, 7, 16)
+    d = torch.empty(3, 5, 7, 16, device=dev)
+    hip.siamese_diff(hip.nhwc(a.to(dev)), hip.nhwc(d))
+    assert torch.equal(d.cpu(), a[3:] - a[:3])
+
+
+@pytest.mark.parametrize('c,n_out', [(64, 1), (8, 1), (128, 1), (16, 3)])
+def test_head_conv1x1(dev, c, n_out):
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(c + n_out)
+    n, h, w = 2, 16, 24
+    x = torch.randn(n, c, h, w, generator=g, requires_grad=True)
+    wt = torch.randn(n_out, c, 1, 1, generator=g, requires_grad=True)
+    b = torch.randn(n_out, generator=g, requires_grad=True)
+    out = F.conv2d(x, wt, b)
+    gout = torch.randn(out.shape, generator=g)
+    out.backward(gout)
+    xd = nhwc_t(x.detach()).to(dev)
+    o = torch.empty(n, n_out, h, w, device=dev)
+    wd = wt.detach().reshape(n_out, c).contiguous().to(dev)
+    hip.conv1x1_fwd(hip.nhwc(xd), wd, b.detach().to(dev), n_out, o)
+    assert rel(o, out) < TOL
+    gx = torch.empty_like(xd)
+    gw = torch.empty(n_out, c, 1, 1, device=dev)
+    gb = torch.empty(n_out, device=dev)
+    ws = torch.empty(hip.conv1x1_workspace_bytes(hip.nhwc(xd), n_out), dtype=torch.uint8, device=dev)
+    hip.conv1x1_bwd(hip.nhwc(xd), wd, gout.to(dev), n_out, hip.nhwc(gx), False, gw, gb, ws)
+    assert rel(gx, nhwc_t(x.grad)) < TOL
+    assert rel(gw, wt.grad) < TOL and rel(gb, b.grad) < TOL
+
+
+@pytest.mark.parametrize('n,soft', [(2 * 64 * 64, False), (3 * 97 * 31, False), (2 * 32 * 32, True)])
+def test_power_jaccard(dev, n, soft):
+    from multimodal_siamese_cd_amd import engine
+    g = torch.Generator().manual_seed(n)
+    logits = (torch.randn(n, generator=g) * 3).requires_grad_(True)
+    if soft:
+        t = torch.sigmoid(torch.randn(n, generator=g)).requires_grad_(True)
+    else:
+        t = (torch.rand(n, generator=g) > 0.9).float()
+    ref = O.power_jaccard_loss(logits, t)
+    ref.backward()
+    ld = logits.detach().to(dev).requires_grad_(True)
+    td = t.detach().to(dev).requires_grad_(soft)
+    loss = engine.power_jaccard(ld, td)
+    loss.backward()
+    assert abs(loss.item() - ref.item()) < 1e-6
+    assert rel(ld.grad, logits.grad) < 1e-5
+    if soft:
+        assert rel(td.grad, t.grad) < 1e-5
+
+
+def test_errors_are_reported(dev):
+    from multimodal_siamese_cd_amd import hip
+    x = torch.zeros(1, 4, 4, 6, device=dev)  # c=6 not a multiple of 4
+    y = torch.zeros(1, 4, 4, 8, device=dev)
+    with pytest.raises(RuntimeError, match='multiples of 4'):
+        hip.conv_igemm(hip.nhwc(x), 4, 4, 1, hip.TAPS_3X3, torch.zeros(8 * 9 * 6, device=dev), 8, None, hip.nhwc(y))
