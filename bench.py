@@ -1,0 +1,253 @@
+"""Throughput benchmark of the Siamese U-Net training step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config baseline_siamese] [--batch B]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+One step = zero_grad -> SiameseUNet forward (HIP) -> power_jaccard_loss -> backward (HIP) -> AdamW step,
+on synthetic 256x256 SAR(2)+optical(3) pairs generated on the device (weak scaling: every rank draws its
+own batch).  Rank 0 prints ONE JSON line; `value` is pairs/s of the whole job (all ranks' pairs / max rank time).
+
+Measurement extras (rank 0, after the timed region):
+  roofline      the MFMA conv kernels (igemm_f32 + wgrad_f32, every conv launch of one step) bracketed by
+                HIP events on the launch stream: algorithmic conv FLOPs per step / summed kernel time vs the
+                gfx950 fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
+  cpu_baseline  the CPU oracle (oracle/siamese_oracle.py, torch fp32 on host cores) running the same training
+                step on a bounded sample (bs=2, 256x256).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from multimodal_siamese_cd_amd import engine, hip, parallel  # noqa: E402
+from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_functions, networks  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3
+METRIC = "image-pairs/sec training step, 256×256 SAR+optical Siamese U-Net, 1/2/4/8 MI355X"
+
+
+def conv_flops(cfg, batch: int, size: int):
+    """Algorithmic train FLOPs per step: 2*M*N*K per conv for fwd, data-grad (not for the input layer) and
+    weight-grad; 3x3 stack and ConvTranspose counted separately."""
+    topo = list(cfg.MODEL.TOPOLOGY)
+    cin = cfg.MODEL.IN_CHANNELS
+    L = len(topo)
+    ch = [topo[0]] + [topo[i + 1] if i != L - 1 else topo[i] for i in range(L)]
+    f3 = 0.0
+    fT = 0.0
+    n_enc = 2 * batch  # Siamese: both branches through the shared encoder
+    for lvl in range(L + 1):
+        hw = (size >> lvl) ** 2
+        c_in = cin if lvl == 0 else ch[lvl - 1]
+        for k, (a, b) in enumerate(((c_in, ch[lvl]), (ch[lvl], ch[lvl]))):
+            fwd = 2.0 * n_enc * hw * b * 9 * a
+            f3 += fwd * (2 if (lvl == 0 and k == 0) else 3)
+    for idx in reversed(range(L)):  # decoder up{idx+1}
+        hw = (size >> idx) ** 2
+        c = ch[idx]
+        out = ch[idx - 1] if idx != 0 else ch[0]
+        fT += 3 * 2.0 * batch * (hw // 4) * (4 * c) * c
+        f3 += 3 * 2.0 * batch * hw * out * 9 * (2 * c)
+        f3 += 3 * 2.0 * batch * hw * out * 9 * out
+    return f3, fT
+
+
+class KernelTimer:
+    """HIP-event brackets around every MFMA conv launch (on torch's current stream, where libscd launches)."""
+
+    def __init__(self):
+        self.events = []
+        self.active = False
+        self._igemm = hip.conv_igemm
+        self._wgrad = hip.conv_wgrad
+
+    def install(self):
+        timer = self
+
+        def igemm(*a, **k):
+            if not timer.active:
+                return timer._igemm(*a, **k)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = timer._igemm(*a, **k)
+            e.record()
+            timer.events.append(('igemm', s, e))
+            return r
+
+        def wgrad(*a, **k):
+            if not timer.active:
+                return timer._wgrad(*a, **k)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = timer._wgrad(*a, **k)
+            e.record()
+            timer.events.append(('wgrad', s, e))
+            return r
+
+        hip.conv_igemm = igemm
+        hip.conv_wgrad = wgrad
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, s, e in self.events:
+            n, t = out.get(name, (0, 0.0))
+            out[name] = (n + 1, t + s.elapsed_time(e))
+        return out
+
+
+def cpu_baseline(cfg, steps: int = 2, batch: int = 2, size: int = 256):
+    """The CPU oracle (torch fp32 on host cores) running the same training step on a bounded sample."""
+    from oracle import siamese_oracle as O
+
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    ocfg = dict(TOPOLOGY=list(cfg.MODEL.TOPOLOGY), IN_CHANNELS=cfg.MODEL.IN_CHANNELS, OUT_CHANNELS=1,
+                S1_BANDS=list(cfg.DATALOADER.S1_BANDS), S2_BANDS=list(cfg.DATALOADER.S2_BANDS))
+    shapes = O.param_shapes('siameseunet', ocfg)
+    P = {k: v.requires_grad_(True) for k, v in O.deterministic_params(shapes, 7).items()}
+    B = O.fresh_buffers(shapes)
+    b = O.synthetic_batch(ocfg, batch, size, 8)
+    opt = torch.optim.AdamW(list(P.values()), lr=1e-4, weight_decay=0.01)
+
+    def step():
+        opt.zero_grad()
+        out = O.forward('siameseunet', P, B, b['x_t1'], b['x_t2'], ocfg, True)
+        loss = O.power_jaccard_loss(out, b['y_change'])
+        loss.backward()
+        opt.step()
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * steps / dt, 4), "unit": "image-pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} timed training steps (after 1 warm-up) of the CPU oracle, bs={batch}, "
+                      f"{size}x{size}, {cfg.MODEL.IN_CHANNELS}-ch, TOPOLOGY {list(cfg.MODEL.TOPOLOGY)}, fp32, "
+                      f"torch {torch.__version__} with {threads} threads ({dt:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--config', default='baseline_siamese')
+    ap.add_argument('--batch', type=int, default=None, help='per-GPU batch (default: config TRAINER.BATCH_SIZE)')
+    ap.add_argument('--size', type=int, default=None)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-kernel-timing', action='store_true')
+    args = ap.parse_args()
+
+    rank, local_rank, world = parallel.init_distributed()
+    torch.cuda.set_device(local_rank)
+    dev = torch.device('cuda', local_rank)
+    hip.load_library()
+
+    cfg = experiment_manager.load_cfg(args.config)
+    batch = args.batch or int(cfg.TRAINER.BATCH_SIZE)
+    size = args.size or int(cfg.AUGMENTATION.CROP_SIZE)
+    torch.manual_seed(cfg.SEED)
+    net = networks.create_network(cfg).to(dev)
+    net = parallel.wrap_ddp(net, dev)
+    net.train()
+    try:
+        opt = torch.optim.AdamW(net.parameters(), lr=float(cfg.TRAINER.LR), weight_decay=0.01, fused=True)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.AdamW(net.parameters(), lr=float(cfg.TRAINER.LR), weight_decay=0.01)
+    crit = loss_functions.get_criterion(cfg.MODEL.LOSS_TYPE)
+    gen = torch.Generator(device=dev).manual_seed(parallel.rank_seed(cfg.SEED, rank))
+    b = datasets.synthetic_batch(cfg, batch, dev, gen, size)
+    hip.ensure_device(b['x_t1'])
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        logits = net(b['x_t1'], b['x_t2'])
+        loss = crit(logits, b['y_change'])
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    first_loss = float(loss.item())
+
+    parallel.barrier(dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    parallel.barrier(dev)
+    dt = time.perf_counter() - t0
+    dt = parallel.allreduce_max(dt, dev)
+    last_loss = float(loss.item())
+
+    value = batch * world * args.steps / dt
+    ms = 1000.0 * dt / args.steps
+    f3, fT = conv_flops(cfg, batch, size)
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "image-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (on-device U[0,1) pairs, Bernoulli(0.05) change masks; random-init weights)",
+        "config": {"workload": f"{args.config}: siameseunet TOPOLOGY {list(cfg.MODEL.TOPOLOGY)}, "
+                               f"{cfg.MODEL.IN_CHANNELS}-ch SAR+optical, {size}x{size}, bs={batch}/GPU, fp32, "
+                               f"train step incl. AdamW",
+                   "global_batch": batch * world, "tile": size, "parallelism": f"dp{world}",
+                   "topology": list(cfg.MODEL.TOPOLOGY)},
+        "loss_first_last": [round(first_loss, 6), round(last_loss, 6)],
+        "step_roofline": {"formula": "3x3-stack train FLOP/pair x pairs/s/GPU / fp32 MFMA peak",
+                          "gflop_per_pair_3x3": round(f3 / batch / 1e9, 2),
+                          "frac": round(f3 / batch * (value / world) / (FP32_MFMA_PEAK_TFLOPS * 1e12), 4)},
+    }
+
+    if rank == 0 and not args.no_kernel_timing:
+        timer = KernelTimer()
+        timer.install()
+        reps = 2
+        timer.active = True
+        for _ in range(reps):
+            step()
+        timer.active = False
+        summ = timer.summary()
+        t_ms = sum(t for _, t in summ.values()) / reps
+        achieved = (f3 + fT) / (t_ms * 1e-3) / 1e12
+        result["roofline"] = {
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": "igemm_f32 + wgrad_f32 (all conv launches of one training step: 3x3 fwd/dgrad/wgrad, "
+                      "ConvT fwd/dgrad/wgrad)",
+            "flop_per_step": f3 + fT,
+            "kernel_ms_per_step": round(t_ms, 3),
+            "launches_per_step": {k: v[0] // reps for k, v in summ.items()},
+            "ms_per_family": {k: round(v[1] / reps, 3) for k, v in summ.items()},
+        }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, size=size)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if parallel.is_distributed():
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -167,7 +167,9 @@ def nhwc(t: torch.Tensor, c_off: int = 0, c: int | None = None) -> NHWC:
         raise ValueError(f"tensor is not an NHWC channel slice: shape {tuple(t.shape)} stride {t.stride()}")
     if c is None:
         c = cc - c_off
-    return NHWC(t.data_ptr() + 4 * c_off, n, h, w, c, ldc)
+    v = NHWC(t.data_ptr() + 4 * c_off, n, h, w, c, ldc)
+    v._owner = t  # keep the storage alive at least until the view has been handed to a launch
+    return v
 
 
 def _taps(taps):

@@ -1,0 +1,72 @@
+"""One process per GPU data parallelism over RCCL (torch.distributed backend "nccl" = librccl on ROCm).
+
+Replaces the reference's single-process `nn.DataParallel(model)` (utils/networks.py:27).  Each rank owns a
+full replica and its own shard of image pairs (independent synthetic generator seeded per rank); the only
+data-path collective is the gradient all-reduce that DistributedDataParallel buckets and launches as the
+Siamese stage Functions return their gradients.  BatchNorm statistics stay per rank (like DataParallel's
+per-replica statistics) and running statistics are broadcast from rank 0 each forward
+(`broadcast_buffers=True`, DataParallel's replica-0 semantics, torch/nn/parallel/data_parallel.py:88-90).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    return int(os.environ.get('RANK', 0)), int(os.environ.get('LOCAL_RANK', 0)), int(os.environ.get('WORLD_SIZE', 1))
+
+
+def init_distributed(backend: str | None = None):
+    """Initialise the process group from torchrun's env; returns (rank, local_rank, world_size)."""
+    rank, local_rank, world = env_rank()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        if backend == 'nccl':
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group(backend, device_id=torch.device('cuda', local_rank))
+        else:
+            dist.init_process_group(backend)
+    return rank, local_rank, world
+
+
+def is_distributed() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def rank_seed(seed: int, rank: int) -> int:
+    """Independent per-rank data stream (weak scaling: each rank draws its own pairs)."""
+    return int(seed) * 1_000_003 + 7919 * int(rank)
+
+
+def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 64):
+    """Replace the DataParallel-style wrapper's pass-through by DDP when running under torchrun.
+
+    Keeps the `.module` attribute and `module.` state_dict prefix of the reference's wrapper.
+    """
+    if not is_distributed():
+        return wrapper
+    module = wrapper.module if hasattr(wrapper, 'module') else wrapper
+    ids = [device.index] if (device is not None and device.type == 'cuda') else None
+    return torch.nn.parallel.DistributedDataParallel(module, device_ids=ids, broadcast_buffers=True,
+                                                     bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+
+
+def allreduce_max(value: float, device) -> float:
+    if not is_distributed():
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(device=None):
+    if is_distributed():
+        if device is not None and device.type == 'cuda':
+            dist.barrier(device_ids=[device.index])
+        else:
+            dist.barrier()

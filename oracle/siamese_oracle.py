@@ -56,9 +56,14 @@ def decoder_layers(topology):
 # --------------------------------------------------------------------------------------------------
 # blocks
 # --------------------------------------------------------------------------------------------------
+RECORD = None  # set to a list to capture (bn key, pre-activation) pairs (used to find ReLU-kink pixels)
+
+
 def _bn(x, P, B, key, training):
     rm, rv = B[key + '.running_mean'], B[key + '.running_var']
     y = F.batch_norm(x, rm, rv, P[key + '.weight'], P[key + '.bias'], training, BN_MOMENTUM, BN_EPS)
+    if RECORD is not None:
+        RECORD.append((key, y.detach()))
     if training:
         B[key + '.num_batches_tracked'] += 1
     return y

@@ -118,8 +118,9 @@ def test_convT2x2_forward_into_concat_slice(dev, n, h, w, c, cs):
     b = torch.randn(c, generator=g)
     ref = nhwc_t(F.conv_transpose2d(nchw(x), wt, b, stride=2))
     cat = torch.full((n, 2 * h, 2 * w, cs + c), float('nan'), device=dev)
-    hip.conv_igemm(hip.nhwc(x.to(dev)), h, w, 1, hip.TAPS_1, hip.pack_convT2x2(wt.to(dev), 0), 4 * c, b.to(dev),
-                   hip.nhwc(cat, cs, c), store_mode=1)
+    xd, wd, bd = x.to(dev), wt.to(dev), b.to(dev)
+    hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_1, hip.pack_convT2x2(wd, 0), 4 * c, bd, hip.nhwc(cat, cs, c),
+                   store_mode=1)
     assert rel(cat[..., cs:], ref) < TOL
     assert torch.isnan(cat[..., :cs]).all(), 'wrote outside its channel slice'
 
@@ -233,7 +234,8 @@ def test_maxpool_forward_indices_and_feature_grad(dev, n, h, w, c):
     gskip = torch.randn(n // 2 if n > 1 else 1, h, w, c, generator=g)
     gx = torch.empty(n, h, w, c, device=dev)
     mode = 1 if n % 2 == 0 else 0
-    hip.feature_grad(hip.nhwc(gy.to(dev)), idx, hip.nhwc(gskip.to(dev)), mode, hip.nhwc(gx))
+    gyd, gsd = gy.to(dev), gskip.to(dev)
+    hip.feature_grad(hip.nhwc(gyd), idx, hip.nhwc(gsd), mode, hip.nhwc(gx))
     sgn = torch.ones(n, 1, 1, 1)
     if mode == 1:
         sgn[: n // 2] = -1
