@@ -2,9 +2,14 @@
 //
 // Replaces aten::native_batch_norm / native_batch_norm_backward / relu_ / threshold_backward for the
 // reference's `Conv2d -> BatchNorm2d -> ReLU(inplace)` pairs (utils/networks.py:392-397).
-// Reductions are chunked: each workgroup reduces one (segment, pixel-chunk, channel-group) tile
-// (Welford in registers, Chan merges in LDS), then one thread per channel merges the chunk records in
-// double, in chunk order — deterministic and free of E[x^2]-E[x]^2 cancellation.
+//
+// Reductions are two-stage and deterministic:
+//   partial  : one workgroup per (segment, 4096-pixel chunk, channel group); every thread owns one channel
+//              quad (float4) and walks pixels with 4 independent 16-byte loads in flight; forward stats use
+//              shifted sums (shift = the chunk's first value of the channel) turned into (n, mean, M2) and
+//              Chan-merged in LDS, so there is no E[x^2]-E[x]^2 cancellation.  Records are written
+//              channel-major, rec[c][chunk][field].
+//   finalize : one workgroup per channel merges its chunk records in double with a fixed-shape tree.
 #include "common.h"
 
 namespace scd {
@@ -13,16 +18,18 @@ constexpr int BN_THREADS = 256;
 constexpr int BN_CHUNK = 4096;  // pixels per reduction chunk
 
 struct BnGeom {
-    int64_t pseg;   // pixels per segment
-    int ncps;       // chunks per segment
-    int qpb;        // channel quads per block (power of two)
-    int cgroups;    // channel groups (grid.y)
+    int64_t pseg;  // pixels per segment
+    int ncps;      // chunks per segment
+    int nrec;      // nseg * ncps
+    int qpb;       // channel quads per block (power of two)
+    int cgroups;   // channel groups (grid.y)
 };
 
 static BnGeom bn_geom(const scd_nhwc_t &y, int nseg) {
     BnGeom g;
     g.pseg = pixels(y) / nseg;
     g.ncps = int((g.pseg + BN_CHUNK - 1) / BN_CHUNK);
+    g.nrec = nseg * g.ncps;
     const int cq = y.c / 4;
     int q = 1;
     while (q * 2 <= cq && q * 2 <= 64) q *= 2;
@@ -31,56 +38,97 @@ static BnGeom bn_geom(const scd_nhwc_t &y, int nseg) {
     return g;
 }
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 ld4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
+__device__ __forceinline__ void st4(float *p, f4 v) { *reinterpret_cast<f4 *>(p) = v; }
+// Keep a batch of loads in flight: an opaque use of the loaded registers right after issuing them stops
+// hipcc from sinking each load next to its consumer (which serialised the loop at vmcnt(0) per load).
+#define PIN4(a, b, c, d) asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d))
+
 struct Welford4 {
     float n;
-    float mean[4], m2[4];
+    f4 mean, m2;
 };
 
 __device__ __forceinline__ void chan_merge(Welford4 &a, const Welford4 &b) {
-    const float n = a.n + b.n;
     if (b.n == 0.f) return;
     if (a.n == 0.f) {
         a = b;
         return;
     }
+    const float n = a.n + b.n;
     const float fb = b.n / n;
     const float fab = a.n * b.n / n;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float d = b.mean[k] - a.mean[k];
-        a.mean[k] += d * fb;
-        a.m2[k] += b.m2[k] + d * d * fab;
-    }
+    const f4 d = b.mean - a.mean;
+    a.mean += d * fb;
+    a.m2 += b.m2 + d * d * fab;
     a.n = n;
 }
 
-// records: [nseg*ncps][C][3] = {count, mean, m2}
+// Chunk bounds of this block.
+struct Chunk {
+    int64_t beg, end;
+    int seg;
+};
+__device__ __forceinline__ Chunk chunk_of(int64_t pseg, int ncps) {
+    Chunk c;
+    c.seg = blockIdx.x / ncps;
+    const int k = blockIdx.x % ncps;
+    c.beg = c.seg * pseg + int64_t(k) * BN_CHUNK;
+    c.end = min(c.beg + BN_CHUNK, (c.seg + 1) * pseg);
+    return c;
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward statistics
+// ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const float *__restrict__ y, int ldc, int C,
-                                                               int64_t pseg, int ncps, int qpb,
+                                                               int64_t pseg, int ncps, int nrec, int qpb,
                                                                float *__restrict__ rec) {
     __shared__ Welford4 sh[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
-    const int cq = blockIdx.y * qpb + q;
-    const int seg = blockIdx.x / ncps, chunk = blockIdx.x % ncps;
-    const int64_t pbeg = seg * pseg + int64_t(chunk) * BN_CHUNK;
-    const int64_t pend = min(pbeg + BN_CHUNK, (seg + 1) * pseg);
+    const int c = (blockIdx.y * qpb + q) * 4;
+    const Chunk ch = chunk_of(pseg, ncps);
     Welford4 w;
     w.n = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) w.mean[k] = w.m2[k] = 0.f;
-    if (cq * 4 < C) {
-        for (int64_t p = pbeg + pl; p < pend; p += npl) {
-            const float4 v = *reinterpret_cast<const float4 *>(y + p * ldc + cq * 4);
-            w.n += 1.f;
-            const float inv = 1.f / w.n;
-            const float x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float d = x[k] - w.mean[k];
-                w.mean[k] += d * inv;
-                w.m2[k] += d * (x[k] - w.mean[k]);
-            }
+    w.mean = f4{0.f, 0.f, 0.f, 0.f};
+    w.m2 = w.mean;
+    if (c < C) {
+        const f4 K = ld4(y + ch.beg * ldc + c);
+        f4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
+        int n = 0;
+        int64_t p = ch.beg + pl;
+        for (; p + 3 * npl < ch.end; p += 4 * npl) {
+            f4 a = ld4(y + p * ldc + c), b = ld4(y + (p + npl) * ldc + c);
+            f4 d = ld4(y + (p + 2 * npl) * ldc + c), e = ld4(y + (p + 3 * npl) * ldc + c);
+            PIN4(a, b, d, e);
+            a -= K;
+            b -= K;
+            d -= K;
+            e -= K;
+            s1 += (a + b) + (d + e);
+            s2 += (a * a + b * b) + (d * d + e * e);
+            n += 4;
+        }
+        for (; p < ch.end; p += npl) {
+            const f4 a = ld4(y + p * ldc + c) - K;
+            s1 += a;
+            s2 += a * a;
+            n += 1;
+        }
+        if (n > 0) {
+            const float fn = float(n);
+            w.n = fn;
+            const f4 m = s1 / fn;
+            w.mean = K + m;
+            f4 m2 = s2 - s1 * m;
+            m2.x = fmaxf(m2.x, 0.f);
+            m2.y = fmaxf(m2.y, 0.f);
+            m2.z = fmaxf(m2.z, 0.f);
+            m2.w = fmaxf(m2.w, 0.f);
+            w.m2 = m2;
         }
     }
     sh[tid] = w;
@@ -93,48 +141,79 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const float *__re
         }
         __syncthreads();
     }
-    if (pl == 0 && cq * 4 < C) {
+    if (pl == 0 && c < C) {
         const Welford4 a = sh[tid];
-        float *r = rec + (size_t(blockIdx.x) * C + cq * 4) * 3;
+        const float mv[4] = {a.mean.x, a.mean.y, a.mean.z, a.mean.w};
+        const float qv[4] = {a.m2.x, a.m2.y, a.m2.z, a.m2.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            r[3 * k + 0] = a.n;
-            r[3 * k + 1] = a.mean[k];
-            r[3 * k + 2] = a.m2[k];
+            float *r = rec + (size_t(c + k) * nrec + blockIdx.x) * 3;
+            r[0] = a.n;
+            r[1] = mv[k];
+            r[2] = qv[k];
         }
     }
 }
 
-__global__ void bn_stats_finalize(const float *__restrict__ rec, int C, int nseg, int ncps, const float *gamma,
-                                  const float *beta, float eps, float momentum, int update, float *rmean,
-                                  float *rvar, float *smean, float *sinv, float *scale, float *shift) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    const double g = gamma ? gamma[c] : 1.0, b = beta ? beta[c] : 0.0;
+struct DWelford {
+    double n, mean, m2;
+};
+__device__ __forceinline__ void dmerge(DWelford &a, const DWelford &b) {
+    if (b.n == 0) return;
+    if (a.n == 0) {
+        a = b;
+        return;
+    }
+    const double n = a.n + b.n;
+    const double d = b.mean - a.mean;
+    a.mean += d * b.n / n;
+    a.m2 += b.m2 + d * d * a.n * b.n / n;
+    a.n = n;
+}
+
+// one workgroup per channel; segments in order (t1 first), running stats updated once per segment
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_finalize(const float *__restrict__ rec, int C, int nseg,
+                                                                int ncps, int nrec, const float *gamma,
+                                                                const float *beta, float eps, float momentum,
+                                                                int update, float *rmean, float *rvar, float *smean,
+                                                                float *sinv, float *scale, float *shift) {
+    __shared__ DWelford sh[BN_THREADS];
+    const int c = blockIdx.x;
+    const int t = threadIdx.x;
+    const float *rc = rec + size_t(c) * nrec * 3;
     for (int s = 0; s < nseg; ++s) {
-        double n = 0, mean = 0, m2 = 0;
-        for (int k = 0; k < ncps; ++k) {
-            const float *r = rec + (size_t(s * ncps + k) * C + c) * 3;
-            const double nb = r[0];
-            if (nb == 0) continue;
-            const double d = r[1] - mean;
-            const double nn = n + nb;
-            mean += d * nb / nn;
-            m2 += r[2] + d * d * n * nb / nn;
-            n = nn;
+        DWelford w{0, 0, 0};
+        for (int k = t; k < ncps; k += BN_THREADS) {
+            const float *r = rc + size_t(s * ncps + k) * 3;
+            dmerge(w, DWelford{r[0], r[1], r[2]});
         }
-        const double var = n > 0 ? m2 / n : 0.0;
-        const double inv = 1.0 / sqrt(var + double(eps));
-        smean[s * C + c] = float(mean);
-        sinv[s * C + c] = float(inv);
-        const float sc = float(g * inv);
-        scale[s * C + c] = sc;
-        shift[s * C + c] = float(b - mean * double(sc));
-        if (update) {
-            const double uvar = n > 1 ? m2 / (n - 1) : var;
-            rmean[c] = float((1.0 - momentum) * rmean[c] + momentum * mean);
-            rvar[c] = float((1.0 - momentum) * rvar[c] + momentum * uvar);
+        sh[t] = w;
+        __syncthreads();
+        for (int off = BN_THREADS / 2; off > 0; off >>= 1) {
+            if (t < off) {
+                DWelford a = sh[t];
+                dmerge(a, sh[t + off]);
+                sh[t] = a;
+            }
+            __syncthreads();
         }
+        if (t == 0) {
+            const DWelford a = sh[0];
+            const double g = gamma ? gamma[c] : 1.0, b = beta ? beta[c] : 0.0;
+            const double var = a.n > 0 ? a.m2 / a.n : 0.0;
+            const double inv = 1.0 / sqrt(var + double(eps));
+            smean[s * C + c] = float(a.mean);
+            sinv[s * C + c] = float(inv);
+            const float sc = float(g * inv);
+            scale[s * C + c] = sc;
+            shift[s * C + c] = float(b - a.mean * double(sc));
+            if (update) {
+                const double uvar = a.n > 1 ? a.m2 / (a.n - 1) : var;
+                rmean[c] = float((1.0 - momentum) * rmean[c] + momentum * a.mean);
+                rvar[c] = float((1.0 - momentum) * rvar[c] + momentum * uvar);
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -149,6 +228,9 @@ __global__ void bn_eval_coeffs_kernel(int C, const float *gamma, const float *be
 }
 
 __device__ __forceinline__ float bn_relu(float y, float sc, float sh) { return fmaxf(fmaf(y, sc, sh), 0.f); }
+__device__ __forceinline__ f4 bn_relu4(f4 y, f4 sc, f4 sh) {
+    return f4{bn_relu(y.x, sc.x, sh.x), bn_relu(y.y, sc.y, sh.y), bn_relu(y.z, sc.z, sh.z), bn_relu(y.w, sc.w, sh.w)};
+}
 
 // grid: (chunks, segments); each thread walks quads of its segment's pixels.
 __global__ __launch_bounds__(256) void bn_relu_apply_kernel(const float *__restrict__ y, int ldy, float *__restrict__ a,
@@ -162,54 +244,51 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(const float *__restr
     for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
         const int64_t p = seg * pseg + e / cq;
         const int c = int(e % cq) * 4;
-        const float4 v = *reinterpret_cast<const float4 *>(y + p * ldy + c);
-        const float4 s4 = *reinterpret_cast<const float4 *>(sc + c);
-        const float4 h4 = *reinterpret_cast<const float4 *>(sh + c);
-        float4 o;
-        o.x = bn_relu(v.x, s4.x, h4.x);
-        o.y = bn_relu(v.y, s4.y, h4.y);
-        o.z = bn_relu(v.z, s4.z, h4.z);
-        o.w = bn_relu(v.w, s4.w, h4.w);
-        *reinterpret_cast<float4 *>(a + p * lda + c) = o;
+        st4(a + p * lda + c, bn_relu4(ld4(y + p * ldy + c), ld4(sc + c), ld4(sh + c)));
     }
 }
 
-// Backward reduce: per (chunk, C) record {sum dz, sum dz*xhat}.
+// ------------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ f4 relu_mask(f4 y, f4 sc, f4 sf, f4 g) {
+    return f4{fmaf(y.x, sc.x, sf.x) > 0.f ? g.x : 0.f, fmaf(y.y, sc.y, sf.y) > 0.f ? g.y : 0.f,
+              fmaf(y.z, sc.z, sf.z) > 0.f ? g.z : 0.f, fmaf(y.w, sc.w, sf.w) > 0.f ? g.w : 0.f};
+}
+
+// per (chunk) record {sum dz, sum dz*xhat}, rec[c][chunk][2]
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__restrict__ y, int ldy,
                                                              const float *__restrict__ da, int ldda, int C,
-                                                             int64_t pseg, int ncps, int qpb, const float *smean,
-                                                             const float *sinv, const float *scale, const float *shift,
-                                                             float *__restrict__ rec) {
-    __shared__ float4 sh1[BN_THREADS], sh2[BN_THREADS];
+                                                             int64_t pseg, int ncps, int nrec, int qpb,
+                                                             const float *smean, const float *sinv, const float *scale,
+                                                             const float *shift, float *__restrict__ rec) {
+    __shared__ f4 sh1[BN_THREADS], sh2[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
-    const int cq = blockIdx.y * qpb + q;
-    const int seg = blockIdx.x / ncps, chunk = blockIdx.x % ncps;
-    const int64_t pbeg = seg * pseg + int64_t(chunk) * BN_CHUNK;
-    const int64_t pend = min(pbeg + BN_CHUNK, (seg + 1) * pseg);
-    float4 s1 = make_float4(0, 0, 0, 0), s2 = make_float4(0, 0, 0, 0);
-    if (cq * 4 < C) {
-        const int c = cq * 4;
-        const float4 mu = *reinterpret_cast<const float4 *>(smean + seg * C + c);
-        const float4 iv = *reinterpret_cast<const float4 *>(sinv + seg * C + c);
-        const float4 sc = *reinterpret_cast<const float4 *>(scale + seg * C + c);
-        const float4 sf = *reinterpret_cast<const float4 *>(shift + seg * C + c);
-        for (int64_t p = pbeg + pl; p < pend; p += npl) {
-            const float4 v = *reinterpret_cast<const float4 *>(y + p * ldy + c);
-            const float4 g = *reinterpret_cast<const float4 *>(da + p * ldda + c);
-            float dz;
-            dz = fmaf(v.x, sc.x, sf.x) > 0.f ? g.x : 0.f;
-            s1.x += dz;
-            s2.x += dz * ((v.x - mu.x) * iv.x);
-            dz = fmaf(v.y, sc.y, sf.y) > 0.f ? g.y : 0.f;
-            s1.y += dz;
-            s2.y += dz * ((v.y - mu.y) * iv.y);
-            dz = fmaf(v.z, sc.z, sf.z) > 0.f ? g.z : 0.f;
-            s1.z += dz;
-            s2.z += dz * ((v.z - mu.z) * iv.z);
-            dz = fmaf(v.w, sc.w, sf.w) > 0.f ? g.w : 0.f;
-            s1.w += dz;
-            s2.w += dz * ((v.w - mu.w) * iv.w);
+    const int c = (blockIdx.y * qpb + q) * 4;
+    const Chunk ch = chunk_of(pseg, ncps);
+    f4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
+    if (c < C) {
+        const int o = ch.seg * C + c;
+        const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
+        int64_t p = ch.beg + pl;
+        for (; p + 3 * npl < ch.end; p += 4 * npl) {
+            f4 y0 = ld4(y + p * ldy + c), y1 = ld4(y + (p + npl) * ldy + c);
+            f4 y2 = ld4(y + (p + 2 * npl) * ldy + c), y3 = ld4(y + (p + 3 * npl) * ldy + c);
+            f4 g0 = ld4(da + p * ldda + c), g1 = ld4(da + (p + npl) * ldda + c);
+            f4 g2 = ld4(da + (p + 2 * npl) * ldda + c), g3 = ld4(da + (p + 3 * npl) * ldda + c);
+            PIN4(y0, y1, y2, y3);
+            PIN4(g0, g1, g2, g3);
+            const f4 z0 = relu_mask(y0, sc, sf, g0), z1 = relu_mask(y1, sc, sf, g1);
+            const f4 z2 = relu_mask(y2, sc, sf, g2), z3 = relu_mask(y3, sc, sf, g3);
+            s1 += (z0 + z1) + (z2 + z3);
+            s2 += (z0 * ((y0 - mu) * iv) + z1 * ((y1 - mu) * iv)) + (z2 * ((y2 - mu) * iv) + z3 * ((y3 - mu) * iv));
+        }
+        for (; p < ch.end; p += npl) {
+            const f4 y0 = ld4(y + p * ldy + c);
+            const f4 z0 = relu_mask(y0, sc, sf, ld4(da + p * ldda + c));
+            s1 += z0;
+            s2 += z0 * ((y0 - mu) * iv);
         }
     }
     sh1[tid] = s1;
@@ -217,153 +296,175 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__rest
     __syncthreads();
     for (int off = npl / 2; off > 0; off >>= 1) {
         if (pl < off) {
-            float4 a = sh1[tid], b = sh1[tid + off * qpb];
-            sh1[tid] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-            a = sh2[tid];
-            b = sh2[tid + off * qpb];
-            sh2[tid] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+            sh1[tid] += sh1[tid + off * qpb];
+            sh2[tid] += sh2[tid + off * qpb];
         }
         __syncthreads();
     }
-    if (pl == 0 && cq * 4 < C) {
-        float *r = rec + (size_t(blockIdx.x) * C + cq * 4) * 2;
-        const float4 a = sh1[tid], b = sh2[tid];
-        r[0] = a.x; r[1] = b.x;
-        r[2] = a.y; r[3] = b.y;
-        r[4] = a.z; r[5] = b.z;
-        r[6] = a.w; r[7] = b.w;
+    if (pl == 0 && c < C) {
+        const f4 a = sh1[tid], b = sh2[tid];
+        const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float *r = rec + (size_t(c + k) * nrec + blockIdx.x) * 2;
+            r[0] = av[k];
+            r[1] = bv[k];
+        }
     }
 }
 
-// coef[seg][C][2] = {mean(dz), mean(dz*xhat)}; dgamma/dbeta summed over segments.
-__global__ void bn_bwd_finalize(const float *__restrict__ rec, int C, int nseg, int ncps, int64_t pseg,
-                                float *coef, float *dgamma, float *dbeta) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// one workgroup per channel: coef[seg][C][2] = {mean(dz), mean(dz*xhat)}; dgamma/dbeta summed over segments
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__restrict__ rec, int C, int nseg,
+                                                              int ncps, int nrec, int64_t pseg, float *coef,
+                                                              float *dgamma, float *dbeta) {
+    __shared__ double a1[BN_THREADS], a2[BN_THREADS];
+    const int c = blockIdx.x;
+    const int t = threadIdx.x;
+    const float *rc = rec + size_t(c) * nrec * 2;
     double tg = 0, tb = 0;
     for (int s = 0; s < nseg; ++s) {
         double s1 = 0, s2 = 0;
-        for (int k = 0; k < ncps; ++k) {
-            const float *r = rec + (size_t(s * ncps + k) * C + c) * 2;
-            s1 += r[0];
-            s2 += r[1];
+        for (int k = t; k < ncps; k += BN_THREADS) {
+            s1 += rc[size_t(s * ncps + k) * 2];
+            s2 += rc[size_t(s * ncps + k) * 2 + 1];
         }
-        coef[(s * C + c) * 2 + 0] = float(s1 / double(pseg));
-        coef[(s * C + c) * 2 + 1] = float(s2 / double(pseg));
-        tg += s2;
-        tb += s1;
+        a1[t] = s1;
+        a2[t] = s2;
+        __syncthreads();
+        for (int off = BN_THREADS / 2; off > 0; off >>= 1) {
+            if (t < off) {
+                a1[t] += a1[t + off];
+                a2[t] += a2[t + off];
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            coef[(s * C + c) * 2 + 0] = float(a1[0] / double(pseg));
+            coef[(s * C + c) * 2 + 1] = float(a2[0] / double(pseg));
+            tb += a1[0];
+            tg += a2[0];
+        }
+        __syncthreads();
     }
-    if (dgamma) dgamma[c] = float(tg);
-    if (dbeta) dbeta[c] = float(tb);
+    if (t == 0) {
+        if (dgamma) dgamma[c] = float(tg);
+        if (dbeta) dbeta[c] = float(tb);
+    }
 }
 
-// dy = gamma*invstd*(dz - k1 - xhat*k2); optional per-chunk sums of dy (conv bias grad).
+// dy = gamma*invstd*(dz - k1 - xhat*k2); optional per-chunk sums of dy (conv bias grad), brec[c][chunk]
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restrict__ y, int ldy,
                                                            const float *__restrict__ da, int ldda,
                                                            float *__restrict__ dy, int lddy, int C, int64_t pseg,
-                                                           int ncps, int qpb, const float *smean, const float *sinv,
-                                                           const float *gamma, const float *scale, const float *shift,
-                                                           const float *coef, float *__restrict__ brec) {
-    __shared__ float4 sh[BN_THREADS];
+                                                           int ncps, int nrec, int qpb, const float *smean,
+                                                           const float *sinv, const float *gamma, const float *scale,
+                                                           const float *shift, const float *coef,
+                                                           float *__restrict__ brec) {
+    __shared__ f4 sh[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
-    const int cq = blockIdx.y * qpb + q;
-    const int seg = blockIdx.x / ncps, chunk = blockIdx.x % ncps;
-    const int64_t pbeg = seg * pseg + int64_t(chunk) * BN_CHUNK;
-    const int64_t pend = min(pbeg + BN_CHUNK, (seg + 1) * pseg);
-    float4 acc = make_float4(0, 0, 0, 0);
-    if (cq * 4 < C) {
-        const int c = cq * 4;
-        const float4 mu = *reinterpret_cast<const float4 *>(smean + seg * C + c);
-        const float4 iv = *reinterpret_cast<const float4 *>(sinv + seg * C + c);
-        const float4 sc = *reinterpret_cast<const float4 *>(scale + seg * C + c);
-        const float4 sf = *reinterpret_cast<const float4 *>(shift + seg * C + c);
-        const float *cf = coef + (seg * C + c) * 2;
-        const float k1[4] = {cf[0], cf[2], cf[4], cf[6]};
-        const float k2[4] = {cf[1], cf[3], cf[5], cf[7]};
-        const float gm[4] = {gamma ? gamma[c] : 1.f, gamma ? gamma[c + 1] : 1.f, gamma ? gamma[c + 2] : 1.f,
-                             gamma ? gamma[c + 3] : 1.f};
-        const float mul[4] = {gm[0] * iv.x, gm[1] * iv.y, gm[2] * iv.z, gm[3] * iv.w};
-        const float mus[4] = {mu.x, mu.y, mu.z, mu.w};
-        const float ivs[4] = {iv.x, iv.y, iv.z, iv.w};
-        const float scs[4] = {sc.x, sc.y, sc.z, sc.w};
-        const float sfs[4] = {sf.x, sf.y, sf.z, sf.w};
-        for (int64_t p = pbeg + pl; p < pend; p += npl) {
-            const float4 v4 = *reinterpret_cast<const float4 *>(y + p * ldy + c);
-            const float4 g4 = *reinterpret_cast<const float4 *>(da + p * ldda + c);
-            const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-            const float g[4] = {g4.x, g4.y, g4.z, g4.w};
-            float o[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float dz = fmaf(v[k], scs[k], sfs[k]) > 0.f ? g[k] : 0.f;
-                const float xh = (v[k] - mus[k]) * ivs[k];
-                o[k] = mul[k] * (dz - k1[k] - xh * k2[k]);
-            }
-            *reinterpret_cast<float4 *>(dy + p * lddy + c) = make_float4(o[0], o[1], o[2], o[3]);
-            acc.x += o[0];
-            acc.y += o[1];
-            acc.z += o[2];
-            acc.w += o[3];
+    const int c = (blockIdx.y * qpb + q) * 4;
+    const Chunk ch = chunk_of(pseg, ncps);
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (c < C) {
+        const int o = ch.seg * C + c;
+        const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
+        const float *cf = coef + size_t(o) * 2;
+        const f4 k1 = {cf[0], cf[2], cf[4], cf[6]};
+        const f4 k2 = {cf[1], cf[3], cf[5], cf[7]};
+        const f4 gm = gamma ? ld4(gamma + c) : f4{1.f, 1.f, 1.f, 1.f};
+        const f4 mul = gm * iv;
+        int64_t p = ch.beg + pl;
+        for (; p + 3 * npl < ch.end; p += 4 * npl) {
+            f4 y0 = ld4(y + p * ldy + c), y1 = ld4(y + (p + npl) * ldy + c);
+            f4 y2 = ld4(y + (p + 2 * npl) * ldy + c), y3 = ld4(y + (p + 3 * npl) * ldy + c);
+            f4 g0 = ld4(da + p * ldda + c), g1 = ld4(da + (p + npl) * ldda + c);
+            f4 g2 = ld4(da + (p + 2 * npl) * ldda + c), g3 = ld4(da + (p + 3 * npl) * ldda + c);
+            PIN4(y0, y1, y2, y3);
+            PIN4(g0, g1, g2, g3);
+            const f4 o0 = mul * (relu_mask(y0, sc, sf, g0) - k1 - ((y0 - mu) * iv) * k2);
+            const f4 o1 = mul * (relu_mask(y1, sc, sf, g1) - k1 - ((y1 - mu) * iv) * k2);
+            const f4 o2 = mul * (relu_mask(y2, sc, sf, g2) - k1 - ((y2 - mu) * iv) * k2);
+            const f4 o3 = mul * (relu_mask(y3, sc, sf, g3) - k1 - ((y3 - mu) * iv) * k2);
+            st4(dy + p * lddy + c, o0);
+            st4(dy + (p + npl) * lddy + c, o1);
+            st4(dy + (p + 2 * npl) * lddy + c, o2);
+            st4(dy + (p + 3 * npl) * lddy + c, o3);
+            acc += (o0 + o1) + (o2 + o3);
+        }
+        for (; p < ch.end; p += npl) {
+            const f4 y0 = ld4(y + p * ldy + c);
+            const f4 o0 = mul * (relu_mask(y0, sc, sf, ld4(da + p * ldda + c)) - k1 - ((y0 - mu) * iv) * k2);
+            st4(dy + p * lddy + c, o0);
+            acc += o0;
         }
     }
     if (!brec) return;  // uniform
     sh[tid] = acc;
     __syncthreads();
     for (int off = npl / 2; off > 0; off >>= 1) {
-        if (pl < off) {
-            const float4 a = sh[tid], b = sh[tid + off * qpb];
-            sh[tid] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-        }
+        if (pl < off) sh[tid] += sh[tid + off * qpb];
         __syncthreads();
     }
-    if (pl == 0 && cq * 4 < C) {
-        const float4 a = sh[tid];
-        float *r = brec + size_t(blockIdx.x) * C + cq * 4;
-        r[0] = a.x;
-        r[1] = a.y;
-        r[2] = a.z;
-        r[3] = a.w;
+    if (pl == 0 && c < C) {
+        const f4 a = sh[tid];
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) brec[size_t(c + k) * nrec + blockIdx.x] = av[k];
     }
 }
 
-__global__ void sum_records(const float *__restrict__ rec, int nrec, int C, float *out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// out[c] = sum_r rec[c][r] (double, fixed tree); one workgroup per channel
+__global__ __launch_bounds__(BN_THREADS) void sum_records(const float *__restrict__ rec, int nrec, float *out) {
+    __shared__ double sh[BN_THREADS];
+    const int c = blockIdx.x;
+    const int t = threadIdx.x;
     double s = 0;
-    for (int k = 0; k < nrec; ++k) s += rec[size_t(k) * C + c];
-    out[c] = float(s);
+    for (int k = t; k < nrec; k += BN_THREADS) s += rec[size_t(c) * nrec + k];
+    sh[t] = s;
+    __syncthreads();
+    for (int off = BN_THREADS / 2; off > 0; off >>= 1) {
+        if (t < off) sh[t] += sh[t + off];
+        __syncthreads();
+    }
+    if (t == 0) out[c] = float(sh[0]);
 }
 
-// Per-chunk channel sums (ConvTranspose2d bias grad): rec[chunk][C].
+// Per-chunk channel sums (ConvTranspose2d bias grad) and weighted sums (1x1 head weight grad):
+//   rec[c][chunk] = sum_p w(p) * x[p][c],  w(p) = 1 or gout[img][o][pix]
 __global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const float *__restrict__ x, int ldx, int C,
-                                                               int64_t npix, int qpb, float *__restrict__ rec) {
-    __shared__ float4 sh[BN_THREADS];
+                                                               int64_t npix, int nrec, int qpb,
+                                                               const float *__restrict__ wgt, int hw, int n_out,
+                                                               int o, float *__restrict__ rec) {
+    __shared__ f4 sh[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
-    const int cq = blockIdx.y * qpb + q;
+    const int c = (blockIdx.y * qpb + q) * 4;
     const int64_t pbeg = int64_t(blockIdx.x) * BN_CHUNK;
     const int64_t pend = min(pbeg + BN_CHUNK, npix);
-    float4 acc = make_float4(0, 0, 0, 0);
-    if (cq * 4 < C) {
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (c < C) {
         for (int64_t p = pbeg + pl; p < pend; p += npl) {
-            const float4 v = *reinterpret_cast<const float4 *>(x + p * ldx + cq * 4);
-            acc.x += v.x;
-            acc.y += v.y;
-            acc.z += v.z;
-            acc.w += v.w;
+            f4 v = ld4(x + p * ldx + c);
+            if (wgt) {
+                const int64_t img = p / hw, pix = p - img * hw;
+                v *= wgt[(img * n_out + o) * hw + pix];
+            }
+            acc += v;
         }
     }
     sh[tid] = acc;
     __syncthreads();
     for (int off = npl / 2; off > 0; off >>= 1) {
-        if (pl < off) {
-            const float4 a = sh[tid], b = sh[tid + off * qpb];
-            sh[tid] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-        }
+        if (pl < off) sh[tid] += sh[tid + off * qpb];
         __syncthreads();
     }
-    if (pl == 0 && cq * 4 < C) *reinterpret_cast<float4 *>(rec + size_t(blockIdx.x) * C + cq * 4) = sh[tid];
+    if (pl == 0 && c < C) {
+        const f4 a = sh[tid];
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rec[size_t(c + k) * nrec + blockIdx.x] = av[k];
+    }
 }
 
 static int bn_check(const scd_nhwc_t &y, int nseg) {
@@ -375,6 +476,25 @@ static int bn_check(const scd_nhwc_t &y, int nseg) {
     return SCD_OK;
 }
 
+// Shared with misc_f32.hip (1x1 head weight grad).
+int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o, float *out, void *ws,
+                         size_t ws_bytes, hipStream_t s);
+
+int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o, float *out, void *ws,
+                         size_t ws_bytes, hipStream_t s) {
+    const BnGeom g = bn_geom(x, 1);
+    if (!ws || ws_bytes < size_t(g.nrec) * x.c * sizeof(float)) {
+        set_error("channel_sum: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    float *rec = static_cast<float *>(ws);
+    hipLaunchKernelGGL(chan_sum_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       static_cast<const float *>(x.data), x.ldc, x.c, pixels(x), g.nrec, g.qpb, wgt, x.h * x.w, n_out,
+                       o, rec);
+    hipLaunchKernelGGL(sum_records, dim3(x.c), dim3(BN_THREADS), 0, s, rec, g.nrec, out);
+    return SCD_OK;
+}
+
 }  // namespace scd
 
 using namespace scd;
@@ -383,10 +503,9 @@ extern "C" size_t scd_bn_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_
     if (nseg < 1) nseg = 1;
     scd_nhwc_t v{nullptr, n, h, w, c, c};
     const BnGeom g = bn_geom(v, nseg);
-    const size_t nrec = size_t(nseg) * g.ncps;
     // stats: 3 floats/rec/channel; backward: 2 (+1 bias) floats/rec/channel + coef 2/seg/channel.
-    const size_t a = nrec * c * 3;
-    const size_t b = nrec * c * 3 + size_t(nseg) * c * 2;
+    const size_t a = size_t(g.nrec) * c * 3;
+    const size_t b = size_t(g.nrec) * c * 3 + size_t(nseg) * c * 2;
     return (a > b ? a : b) * sizeof(float) + 256;
 }
 
@@ -407,11 +526,11 @@ extern "C" int scd_bn_train_stats(scd_nhwc_t y, int32_t nseg, const float *gamma
     const BnGeom g = bn_geom(y, nseg);
     hipStream_t s = as_stream(stream);
     float *rec = static_cast<float *>(ws);
-    hipLaunchKernelGGL(bn_stats_partial, dim3(nseg * g.ncps, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, y.c, g.pseg, g.ncps, g.qpb, rec);
-    hipLaunchKernelGGL(bn_stats_finalize, dim3((y.c + 127) / 128), dim3(128), 0, s, rec, y.c, nseg, g.ncps, gamma,
-                       beta, eps, momentum, update_running, running_mean, running_var, save_mean, save_invstd,
-                       scale, shift);
+    hipLaunchKernelGGL(bn_stats_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       static_cast<const float *>(y.data), y.ldc, y.c, g.pseg, g.ncps, g.nrec, g.qpb, rec);
+    hipLaunchKernelGGL(bn_stats_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, gamma,
+                       beta, eps, momentum, update_running, running_mean, running_var, save_mean, save_invstd, scale,
+                       shift);
     return launch_status("scd_bn_train_stats");
 }
 
@@ -465,22 +584,20 @@ extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, c
         return SCD_ERR_WORKSPACE;
     }
     const BnGeom g = bn_geom(y, nseg);
-    const int nrec = nseg * g.ncps;
     float *rec = static_cast<float *>(ws);
-    float *brec = rec + size_t(nrec) * y.c * 2;
-    float *coef = brec + size_t(nrec) * y.c;
+    float *brec = rec + size_t(g.nrec) * y.c * 2;
+    float *coef = brec + size_t(g.nrec) * y.c;
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(bn_bwd_partial, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+    hipLaunchKernelGGL(bn_bwd_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        static_cast<const float *>(y.data), y.ldc, static_cast<const float *>(da.data), da.ldc, y.c,
-                       g.pseg, g.ncps, g.qpb, save_mean, save_invstd, scale, shift, rec);
-    hipLaunchKernelGGL(bn_bwd_finalize, dim3((y.c + 127) / 128), dim3(128), 0, s, rec, y.c, nseg, g.ncps, g.pseg, coef,
-                       dgamma, dbeta);
-    hipLaunchKernelGGL(bn_bwd_apply, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       g.pseg, g.ncps, g.nrec, g.qpb, save_mean, save_invstd, scale, shift, rec);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
+                       coef, dgamma, dbeta);
+    hipLaunchKernelGGL(bn_bwd_apply, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        static_cast<const float *>(y.data), y.ldc, static_cast<const float *>(da.data), da.ldc,
-                       static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.qpb, save_mean, save_invstd, gamma,
-                       scale, shift, coef, dbias_prev ? brec : nullptr);
-    if (dbias_prev)
-        hipLaunchKernelGGL(sum_records, dim3((y.c + 127) / 128), dim3(128), 0, s, brec, nrec, y.c, dbias_prev);
+                       static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.nrec, g.qpb, save_mean,
+                       save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr);
+    if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
     return launch_status("scd_bn_relu_backward");
 }
 
@@ -491,15 +608,6 @@ extern "C" int scd_channel_sum(scd_nhwc_t x, float *out, void *ws, size_t ws_byt
         set_error("channel_sum: null output");
         return SCD_ERR_ARG;
     }
-    if (!ws || ws_bytes < scd_bn_workspace_bytes(x.n, x.h, x.w, x.c, 1)) {
-        set_error("channel_sum: workspace too small");
-        return SCD_ERR_WORKSPACE;
-    }
-    const BnGeom g = bn_geom(x, 1);
-    float *rec = static_cast<float *>(ws);
-    hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(chan_sum_partial, dim3(g.ncps, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(x.data), x.ldc, x.c, pixels(x), g.qpb, rec);
-    hipLaunchKernelGGL(sum_records, dim3((x.c + 127) / 128), dim3(128), 0, s, rec, g.ncps, x.c, out);
+    SCD_TRY(weighted_channel_sum(x, nullptr, 1, 0, out, ws, ws_bytes, as_stream(stream)));
     return launch_status("scd_channel_sum");
 }

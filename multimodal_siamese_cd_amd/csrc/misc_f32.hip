@@ -22,7 +22,11 @@ void set_error(const char *fmt, ...) {
 }
 void clear_error() { g_err.clear(); }
 
-constexpr int RED_CHUNK = 4096;
+constexpr int RED_CHUNK = 4096;  // pixels per reduction chunk (matches bn_f32.hip)
+
+// bn_f32.hip: sum_p w(p) x[p][c] over all pixels (w = 1 or gout[img][o][pix]).
+int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o, float *out, void *ws,
+                         size_t ws_bytes, hipStream_t s);
 
 static int grid_for(int64_t total, int cap = 4096) {
     int64_t b = (total + 255) / 256;
@@ -180,23 +184,37 @@ __global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float 
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ void conv1x1_fwd_kernel(const float *__restrict__ x, int ldx, int C, int hw, int64_t npix,
-                                   const float *__restrict__ w, const float *__restrict__ b, int n_out,
-                                   float *__restrict__ out) {
-    for (int64_t p = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; p < npix; p += int64_t(gridDim.x) * blockDim.x) {
-        const float *xr = x + p * ldx;
-        const int64_t img = p / hw, pix = p % hw;
-        for (int o = 0; o < n_out; ++o) {
-            const float *wr = w + int64_t(o) * C;
-            float s = 0.f;
-            for (int c = 0; c < C; c += 4) {
-                const float4 v = *reinterpret_cast<const float4 *>(xr + c);
-                s = fmaf(v.x, wr[c], s);
-                s = fmaf(v.y, wr[c + 1], s);
-                s = fmaf(v.z, wr[c + 2], s);
-                s = fmaf(v.w, wr[c + 3], s);
+// Wave-cooperative 1x1 conv: G = pow2 >= C/4 lanes share a pixel (each a channel quad, coalesced 16-byte
+// loads), partial dots are combined with a fixed xor-shuffle tree.  grid-stride over pixel groups.
+__global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restrict__ x, int ldx, int C, int hw,
+                                                          int64_t npix, const float *__restrict__ w,
+                                                          const float *__restrict__ b, int n_out, int G,
+                                                          float *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int q = lane % G, pp = lane / G, ppw = 64 / G;
+    const int cq = C / 4;
+    const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+    for (int64_t p0 = wave * ppw; p0 < npix; p0 += nwaves * ppw) {
+        const int64_t p = p0 + pp;
+        const bool ok = p < npix;
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int qq = q; qq < cq; qq += G) {
+            const float4 v = ok ? *reinterpret_cast<const float4 *>(x + p * ldx + 4 * qq) : make_float4(0, 0, 0, 0);
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                if (o < n_out) {
+                    const float4 wv = *reinterpret_cast<const float4 *>(w + int64_t(o) * C + 4 * qq);
+                    s[o] = fmaf(v.x, wv.x, fmaf(v.y, wv.y, fmaf(v.z, wv.z, fmaf(v.w, wv.w, s[o]))));
+                }
             }
-            out[(img * n_out + o) * hw + pix] = s + (b ? b[o] : 0.f);
+        }
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+            for (int off = G / 2; off > 0; off >>= 1) s[o] += __shfl_xor(s[o], off, 64);
+        if (ok && q == 0) {
+            const int64_t img = p / hw, pix = p - img * hw;
+            for (int o = 0; o < n_out; ++o) out[(img * n_out + o) * hw + pix] = s[o] + (b ? b[o] : 0.f);
         }
     }
 }
@@ -229,61 +247,14 @@ __global__ void conv1x1_bwd_dx_kernel(const float *__restrict__ gout, int n_out,
     }
 }
 
-// partial gw: rec[chunk][o][C]; grid (chunks, channel groups of 64 quads), block 256 = 64 quads x 4 pixel lanes
-__global__ __launch_bounds__(256) void conv1x1_bwd_dw_partial(const float *__restrict__ x, int ldx, int C, int hw,
-                                                              int64_t npix, const float *__restrict__ gout, int n_out,
-                                                              float *__restrict__ rec) {
-    __shared__ float4 sh[4][256];
-    const int tid = threadIdx.x;
-    const int q = tid & 63, pl = tid >> 6;
-    const int cq = blockIdx.y * 64 + q;
-    const int64_t pbeg = int64_t(blockIdx.x) * RED_CHUNK;
-    const int64_t pend = min(pbeg + RED_CHUNK, npix);
-    float4 acc[4];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) acc[o] = make_float4(0, 0, 0, 0);
-    if (cq * 4 < C) {
-        for (int64_t p = pbeg + pl; p < pend; p += 4) {
-            const float4 v = *reinterpret_cast<const float4 *>(x + p * ldx + cq * 4);
-            const int64_t img = p / hw, pix = p % hw;
-#pragma unroll
-            for (int o = 0; o < 4; ++o) {
-                if (o < n_out) {
-                    const float g = gout[(img * n_out + o) * hw + pix];
-                    acc[o].x = fmaf(g, v.x, acc[o].x);
-                    acc[o].y = fmaf(g, v.y, acc[o].y);
-                    acc[o].z = fmaf(g, v.z, acc[o].z);
-                    acc[o].w = fmaf(g, v.w, acc[o].w);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int o = 0; o < 4; ++o) sh[o][tid] = acc[o];
-    __syncthreads();
-    if (pl == 0 && cq * 4 < C) {
-        for (int o = 0; o < n_out; ++o) {
-            float4 s = sh[o][q];
-            for (int k = 1; k < 4; ++k) {
-                const float4 t = sh[o][q + 64 * k];
-                s.x += t.x;
-                s.y += t.y;
-                s.z += t.z;
-                s.w += t.w;
-            }
-            *reinterpret_cast<float4 *>(rec + (size_t(blockIdx.x) * n_out + o) * C + cq * 4) = s;
-        }
-    }
-}
-
-// partial sums of gout per output channel: rec[block][o]
+// partial sums of gout per output channel: rec[o][block]
 __global__ __launch_bounds__(256) void conv1x1_bwd_db_partial(const float *__restrict__ gout, int n_out, int hw,
                                                               int64_t npix, float *__restrict__ rec) {
     __shared__ float sh[256];
     const int o = blockIdx.y;
     float s = 0.f;
     for (int64_t p = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; p < npix; p += int64_t(gridDim.x) * blockDim.x) {
-        const int64_t img = p / hw, pix = p % hw;
+        const int64_t img = p / hw, pix = p - img * hw;
         s += gout[(img * n_out + o) * hw + pix];
     }
     sh[threadIdx.x] = s;
@@ -292,20 +263,28 @@ __global__ __launch_bounds__(256) void conv1x1_bwd_db_partial(const float *__res
         if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
         __syncthreads();
     }
-    if (threadIdx.x == 0) rec[size_t(blockIdx.x) * n_out + o] = sh[0];
+    if (threadIdx.x == 0) rec[size_t(o) * gridDim.x + blockIdx.x] = sh[0];
 }
 
-__global__ void sum_rows_kernel(const float *__restrict__ rec, int nrec, int width, float *__restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= width) return;
+// out[i] = sum_k rec[i][k] in double with a fixed tree; one workgroup per output
+__global__ __launch_bounds__(256) void sum_rows_block(const float *__restrict__ rec, int n, float *__restrict__ out) {
+    __shared__ double sh[256];
+    const int t = threadIdx.x;
     double s = 0;
-    for (int k = 0; k < nrec; ++k) s += rec[size_t(k) * width + i];
-    out[i] = float(s);
+    for (int k = t; k < n; k += 256) s += rec[size_t(blockIdx.x) * n + k];
+    sh[t] = s;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (t < off) sh[t] += sh[t + off];
+        __syncthreads();
+    }
+    if (t == 0) out[blockIdx.x] = float(sh[0]);
 }
 
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
 
+// rec[0][block] = sum p*t, rec[1][block] = sum p^2 + t^2
 __global__ __launch_bounds__(256) void pjaccard_partial(const float *__restrict__ logits, const float *__restrict__ t,
                                                         int64_t n, float *__restrict__ rec) {
     __shared__ float s1[256], s2[256];
@@ -327,24 +306,38 @@ __global__ __launch_bounds__(256) void pjaccard_partial(const float *__restrict_
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        rec[2 * blockIdx.x] = s1[0];
-        rec[2 * blockIdx.x + 1] = s2[0];
+        rec[blockIdx.x] = s1[0];
+        rec[gridDim.x + blockIdx.x] = s2[0];
     }
 }
 
-__global__ void pjaccard_finalize(const float *__restrict__ rec, int nrec, float *sums, float *loss) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(256) void pjaccard_finalize(const float *__restrict__ rec, int nrec, float *sums,
+                                                         float *loss) {
+    __shared__ double sI[256], sA[256];
+    const int t = threadIdx.x;
     double I = 0, A = 0;
-    for (int k = 0; k < nrec; ++k) {
-        I += rec[2 * k];
-        A += rec[2 * k + 1];
+    for (int k = t; k < nrec; k += 256) {
+        I += rec[k];
+        A += rec[nrec + k];
     }
-    const float If = float(I);
-    const float Df = float(A) - If + 1e-6f;
-    sums[0] = If;
-    sums[1] = float(A);
-    sums[2] = Df;
-    loss[0] = 1.f - If / Df;
+    sI[t] = I;
+    sA[t] = A;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (t < off) {
+            sI[t] += sI[t + off];
+            sA[t] += sA[t + off];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const float If = float(sI[0]);
+        const float Df = float(sA[0]) - If + 1e-6f;
+        sums[0] = If;
+        sums[1] = float(sA[0]);
+        sums[2] = Df;
+        loss[0] = 1.f - If / Df;
+    }
 }
 
 __global__ void pjaccard_bwd_kernel(const float *__restrict__ logits, const float *__restrict__ t, int64_t n,
@@ -491,14 +484,19 @@ extern "C" int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int
         return SCD_ERR_ARG;
     }
     const int64_t npix = pixels(x);
-    hipLaunchKernelGGL(conv1x1_fwd_kernel, dim3(grid_for(npix)), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(x.data), x.ldc, x.c, x.h * x.w, npix, w, b, n_out, out);
+    int G = 1;
+    while (G < x.c / 4 && G < 64) G *= 2;
+    const int64_t waves = (npix + (64 / G) - 1) / (64 / G);
+    int blocks = int((waves + 3) / 4);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(conv1x1_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(x.data), x.ldc, x.c, x.h * x.w, npix, w, b, n_out, G, out);
     return launch_status("scd_conv1x1_fwd");
 }
 
 extern "C" size_t scd_conv1x1_workspace_bytes(scd_nhwc_t x, int32_t n_out) {
     const int64_t nchunk = (pixels(x) + RED_CHUNK - 1) / RED_CHUNK;
-    return size_t(nchunk) * n_out * x.c * sizeof(float) + size_t(1024) * n_out * sizeof(float) + 256;
+    return size_t(nchunk) * x.c * sizeof(float) + size_t(1024) * n_out * sizeof(float) + 256;
 }
 
 extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, int32_t n_out, scd_nhwc_t gx,
@@ -529,17 +527,15 @@ extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, 
     }
     const int nchunk = int((npix + RED_CHUNK - 1) / RED_CHUNK);
     float *rec = static_cast<float *>(ws);
-    if (gw) {
-        hipLaunchKernelGGL(conv1x1_bwd_dw_partial, dim3(nchunk, (x.c / 4 + 63) / 64), dim3(256), 0, s,
-                           static_cast<const float *>(x.data), x.ldc, x.c, hw, npix, gout, n_out, rec);
-        hipLaunchKernelGGL(sum_rows_kernel, dim3((n_out * x.c + 127) / 128), dim3(128), 0, s, rec, nchunk, n_out * x.c,
-                           gw);
-    }
+    const size_t wbytes = size_t(nchunk) * x.c * sizeof(float);
+    if (gw)
+        for (int o = 0; o < n_out; ++o)  // stream-ordered reuse of the record buffer
+            SCD_TRY(weighted_channel_sum(x, gout, n_out, o, gw + size_t(o) * x.c, ws, wbytes, s));
     if (gb) {
-        float *brec = rec + size_t(nchunk) * n_out * x.c;
+        float *brec = rec + size_t(nchunk) * x.c;
         const int nb = 1024;
         hipLaunchKernelGGL(conv1x1_bwd_db_partial, dim3(nb, n_out), dim3(256), 0, s, gout, n_out, hw, npix, brec);
-        hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(128), 0, s, brec, nb, n_out, gb);
+        hipLaunchKernelGGL(sum_rows_block, dim3(n_out), dim3(256), 0, s, brec, nb, gb);
     }
     return launch_status("scd_conv1x1_bwd");
 }
@@ -565,7 +561,7 @@ extern "C" int scd_pjaccard_fwd(const float *logits, const float *target, int64_
     hipStream_t s = as_stream(stream);
     float *rec = static_cast<float *>(ws);
     hipLaunchKernelGGL(pjaccard_partial, dim3(PJ_BLOCKS), dim3(256), 0, s, logits, target, n, rec);
-    hipLaunchKernelGGL(pjaccard_finalize, dim3(1), dim3(64), 0, s, rec, PJ_BLOCKS, sums_out, loss_out);
+    hipLaunchKernelGGL(pjaccard_finalize, dim3(1), dim3(256), 0, s, rec, PJ_BLOCKS, sums_out, loss_out);
     return launch_status("scd_pjaccard_fwd");
 }
 

@@ -1,0 +1,86 @@
+"""Training entry point — counterpart of the reference's train_supervised.py (also covers the dual-task and
+MMCR trainers' per-step losses, train_supervised_dualtask.py / train_semisupervised.py).
+
+    python -m multimodal_siamese_cd_amd.train_supervised -c baseline_siamese -p proj -o out/ -d data/ [KEY VALUE ...]
+    torchrun --nproc-per-node 8 -m multimodal_siamese_cd_amd.train_supervised -c baseline_dualstream ...
+
+Step loop (train_supervised.py:63-79): net.train(); zero_grad; forward; loss; backward; AdamW(lr, wd=0.01).
+Differences, by design: data are synthetic pairs generated on the device (the SpaceNet7 GeoTIFF reader is out
+of scope), wandb logging is replaced by stdout, the per-step `loss.item()` host sync happens only every
+LOG_FREQ steps, and multi-GPU is one process per GPU (DDP over RCCL) instead of nn.DataParallel.
+"""
+from __future__ import annotations
+
+import sys
+import timeit
+
+import numpy as np
+import torch
+
+from . import hip, parallel, trainers
+from .utils import datasets, experiment_manager, networks, parsers
+
+
+def run_training(cfg, device, max_steps: int | None = None):
+    rank, _, world = parallel.env_rank()
+    net = networks.create_network(cfg)
+    net.to(device)
+    net = parallel.wrap_ddp(net, device)
+    optimizer = torch.optim.AdamW(net.parameters(), lr=float(cfg.TRAINER.LR), weight_decay=0.01)
+    gen = torch.Generator(device=device).manual_seed(parallel.rank_seed(cfg.SEED, rank))
+    steps_per_epoch = int(cfg.TRAINER.get('STEPS_PER_EPOCH', 100))
+    epochs = int(cfg.TRAINER.EPOCHS)
+    global_step = 0
+    if rank == 0:
+        print(f"run config {cfg.NAME}: model {cfg.MODEL.TYPE} topology {list(cfg.MODEL.TOPOLOGY)} "
+              f"bs {cfg.TRAINER.BATCH_SIZE}/GPU x {world} GPU, lr {cfg.TRAINER.LR}, epochs {epochs}", flush=True)
+    for epoch in range(1, epochs + 1):
+        start = timeit.default_timer()
+        losses = []
+        for _ in range(steps_per_epoch):
+            batch = datasets.synthetic_batch(cfg, int(cfg.TRAINER.BATCH_SIZE), device, gen)
+            net.train()
+            optimizer.zero_grad(set_to_none=True)
+            out = net(batch['x_t1'], batch['x_t2'])
+            loss = trainers.step_loss(cfg, out, batch)
+            loss.backward()
+            optimizer.step()
+            losses.append(loss.detach())
+            global_step += 1
+            if global_step % int(cfg.LOG_FREQ) == 0 and rank == 0:
+                t = timeit.default_timer() - start
+                print(f'step {global_step} epoch {global_step / steps_per_epoch:.2f} '
+                      f'loss {torch.stack(losses).mean().item():.5f} time {t:.1f}s', flush=True)
+            if cfg.DEBUG or (max_steps is not None and global_step >= max_steps):
+                break
+        if rank == 0:
+            print(f'epoch {epoch}: mean loss {torch.stack(losses).mean().item():.5f}', flush=True)
+            if epoch in list(cfg.SAVE_CHECKPOINTS) and not cfg.DEBUG:
+                networks.save_checkpoint(net, optimizer, epoch, global_step, cfg)
+        if cfg.DEBUG or (max_steps is not None and global_step >= max_steps):
+            break
+    return net, optimizer, global_step
+
+
+def main(argv=None):
+    args = parsers.training_argument_parser().parse_known_args(argv)[0]
+    cfg = experiment_manager.setup_cfg(args)
+    torch.manual_seed(cfg.SEED)
+    np.random.seed(cfg.SEED)
+    rank, local_rank, world = parallel.init_distributed()
+    if not torch.cuda.is_available():
+        raise SystemExit('train_supervised: needs an MI355X (gfx950) GPU; the HIP path has no CPU fallback')
+    device = torch.device('cuda', local_rank)
+    torch.cuda.set_device(device)
+    hip.load_library()
+    try:
+        run_training(cfg, device)
+    except KeyboardInterrupt:
+        sys.exit(0)
+    finally:
+        if parallel.is_distributed():
+            torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

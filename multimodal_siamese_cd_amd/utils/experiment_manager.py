@@ -162,8 +162,10 @@ def _merge_into(a, b):
     """Recursively merge CfgNode a into b, decoding string values (yacs _merge_a_into_b)."""
     for k, v in a.items():
         v = _decode(v) if not isinstance(v, CfgNode) else v
-        if isinstance(v, CfgNode) and isinstance(b.get(k), CfgNode):
-            _merge_into(v, b[k])
+        if isinstance(v, CfgNode):
+            if not isinstance(b.get(k), CfgNode):
+                b[k] = CfgNode()
+            _merge_into(v, b[k])  # decodes the strings of new subtrees too
         else:
             b[k] = copy.deepcopy(v)
 

@@ -1,0 +1,92 @@
+"""Config API parity with the reference's fvcore/yacs-based experiment_manager (CPU only)."""
+import argparse
+from pathlib import Path
+
+import pytest
+
+from multimodal_siamese_cd_amd.utils import experiment_manager as em
+from multimodal_siamese_cd_amd.utils import parsers
+
+
+def test_base_chain_and_literal_eval_of_strings():
+    cfg = em.load_cfg('siamese_mmcr_alpha0500')  # -> siamese_mmcr_base.yaml -> base.yaml
+    assert cfg.MODEL.TYPE == 'whatevernet'
+    assert cfg.CONSISTENCY_TRAINER.LOSS_FACTOR == 0.5
+    assert cfg.TRAINER.BATCH_SIZE == 4
+    assert isinstance(cfg.TRAINER.LR, float) and cfg.TRAINER.LR == 1e-4  # '1e-4' is a string for PyYAML
+    assert cfg.NAME == 'siamese_mmcr_alpha0500'
+    assert list(cfg.MODEL.TOPOLOGY) == [64, 128, 256, 512]
+
+
+def test_baseline_configs_exist():
+    for name in ('debug', 'baseline_siamese', 'baseline_dualstream', 'dtsiamese', 'siamese_mmcr_alpha0500'):
+        cfg = em.load_cfg(name)
+        assert cfg.MODEL.TYPE in ('siameseunet', 'dualstreamunet', 'dtsiameseunet', 'whatevernet')
+    assert em.load_cfg('baseline_siamese').TRAINER.BATCH_SIZE == 32
+
+
+def test_merge_from_list_decodes_and_coerces():
+    cfg = em.load_cfg('baseline_siamese')
+    cfg.merge_from_list(['TRAINER.LR', '3e-4', 'MODEL.TOPOLOGY', '[8, 16]', 'TRAINER.BATCH_SIZE', '2',
+                         'NEW.KEY', 'hello'])
+    assert cfg.TRAINER.LR == 3e-4 and cfg.MODEL.TOPOLOGY == [8, 16] and cfg.TRAINER.BATCH_SIZE == 2
+    assert cfg.NEW.KEY == 'hello'
+    with pytest.raises(ValueError):
+        cfg.merge_from_list(['TRAINER.LR'])
+
+
+def test_clone_freeze_dump():
+    cfg = em.load_cfg('debug')
+    c2 = cfg.clone()
+    c2.MODEL.TYPE = 'unet'
+    assert cfg.MODEL.TYPE == 'siameseunet'
+    cfg.freeze()
+    with pytest.raises(AttributeError):
+        cfg.MODEL.TYPE = 'x'
+    assert 'siameseunet' in cfg.dump()
+
+
+def test_setup_cfg_with_reference_cli(tmp_path: Path):
+    args = parsers.training_argument_parser().parse_args(
+        ['-c', 'debug', '-p', 'proj', '-o', str(tmp_path), '-d', str(tmp_path), 'TRAINER.EPOCHS', '3'])
+    cfg = em.setup_cfg(args)
+    assert cfg.TRAINER.EPOCHS == 3 and cfg.PATHS.OUTPUT == str(tmp_path) and cfg.NAME == 'debug'
+
+
+def test_relative_base_resolution(tmp_path: Path):
+    (tmp_path / 'sub').mkdir()
+    (tmp_path / 'a.yaml').write_text("X: 1\nM:\n  A: 1\n  B: '2e-3'\n")
+    (tmp_path / 'sub' / 'b.yaml').write_text("_BASE_: '../a.yaml'\nM:\n  A: 5\n")
+    cfg = em.new_config()
+    cfg.merge_from_file(str(tmp_path / 'sub' / 'b.yaml'))
+    assert cfg.X == 1 and cfg.M.A == 5 and cfg.M.B == 2e-3
+
+
+def test_network_surface_on_cpu_is_parameter_identical_to_reference():
+    """Class names / attribute paths / shapes / default init: state_dict keys and shapes as the reference's."""
+    import torch
+    from multimodal_siamese_cd_amd.utils import networks
+    from oracle import siamese_oracle as O
+    from oracle.golden import Fixture
+    fx = Fixture('dtsiamese_t8-16')
+    net = networks.create_network(fx.package_cfg())
+    got = [(k, tuple(p.shape)) for k, p in net.module.named_parameters()]
+    assert got == list(O.param_shapes(fx.model_type, fx.cfg).items())
+    assert all(k.startswith('module.') for k in net.state_dict())
+    with pytest.raises(Exception, match='Unknown network'):
+        c = fx.package_cfg()
+        c.MODEL.TYPE = 'nope'
+        networks.create_network(c)
+    # the HIP path refuses CPU tensors instead of silently falling back
+    x = torch.zeros(1, 5, 32, 32)
+    with pytest.raises(RuntimeError):
+        net(x, x)
+
+
+def test_criterion_registry():
+    from multimodal_siamese_cd_amd.utils import loss_functions
+    assert loss_functions.get_criterion('PowerJaccardLoss') is loss_functions.power_jaccard_loss
+    with pytest.raises(NotImplementedError):
+        loss_functions.get_criterion('SoftDiceLoss')
+    with pytest.raises(Exception, match='unknown loss'):
+        loss_functions.get_criterion('Nope')
