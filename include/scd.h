@@ -122,10 +122,11 @@ typedef struct scd_wgrad {
 /* Number of K-splits the library will use and the slab bytes it needs. */
 int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes);
 int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream);
-/* Sum the slabs and unpack to the parameter layout.
+/* Sum the slabs (deterministic fixed-order two-level reduction; the slabs are scratch and are
+ * overwritten) and unpack to the parameter layout.
  * mode 0: out OIHW [R][c_valid][3][3]  (slab cols (ky*3+kx)*C + c)
  * mode 1: out ConvT [R][C][2][2]       (slab cols (i*2+j)*C + c)                                  */
-int scd_wgrad_finalize(const float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C, int32_t mode,
+int scd_wgrad_finalize(float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C, int32_t mode,
                        int32_t c_valid, float *out, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------

@@ -444,7 +444,16 @@ __global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const float *__re
     const int64_t pend = min(pbeg + BN_CHUNK, npix);
     f4 acc = {0.f, 0.f, 0.f, 0.f};
     if (c < C) {
-        for (int64_t p = pbeg + pl; p < pend; p += npl) {
+        int64_t p = pbeg + pl;
+        if (!wgt) {
+            for (; p + 3 * npl < pend; p += 4 * npl) {
+                f4 v0 = ld4(x + p * ldx + c), v1 = ld4(x + (p + npl) * ldx + c);
+                f4 v2 = ld4(x + (p + 2 * npl) * ldx + c), v3 = ld4(x + (p + 3 * npl) * ldx + c);
+                PIN4(v0, v1, v2, v3);
+                acc += (v0 + v1) + (v2 + v3);
+            }
+        }
+        for (; p < pend; p += npl) {
             f4 v = ld4(x + p * ldx + c);
             if (wgt) {
                 const int64_t img = p / hw, pix = p - img * hw;

@@ -98,23 +98,25 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_f32(IgemmArgs a) 
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
 
-    // Per-thread A-chunk bookkeeping (fixed across the K loop).
-    int a_img[A_PER], a_sy[A_PER], a_sx[A_PER], a_off[A_PER];
-    bool a_ok[A_PER];
+    // Per-thread A-chunk bookkeeping (fixed across the K loop): the source pixel (img, oy*s, ox*s) as a
+    // base pointer; a tap then only adds the wave-uniform offset (dy*ws + dx)*ldc + c0 after a bounds test.
+    const float *a_base[A_PER];
+    int a_sy[A_PER], a_sx[A_PER], a_off[A_PER];
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
         const int ch = tid + i * NT;
         const int row = ch / KC, col = ch % KC;
         const int m = m0 + row;
-        a_ok[i] = (ch < A_CH) && (m < a.M);
-        const uint32_t mm = a_ok[i] ? uint32_t(m) : 0u;
+        const bool ok = (ch < A_CH) && (m < a.M);
+        const uint32_t mm = ok ? uint32_t(m) : 0u;
         const uint32_t img = fdiv(mm, a.div_hw);
         const uint32_t r = mm - img * uint32_t(a.ho * a.wo);
         const uint32_t oy = fdiv(r, a.div_w);
         const uint32_t ox = r - oy * uint32_t(a.wo);
-        a_img[i] = int(img);
-        a_sy[i] = int(oy) * a.stride;
+        // an out-of-range row gets a y coordinate that fails every bounds test
+        a_sy[i] = ok ? int(oy) * a.stride : -(1 << 20);
         a_sx[i] = int(ox) * a.stride;
+        a_base[i] = a.src + (size_t(int(img) * a.hs + a_sy[i] * ok) * a.ws + a_sx[i]) * a.ldc_s + col * 4;
         a_off[i] = row * LS + col * 4;
     }
     int b_row[B_PER], b_off[B_PER];
@@ -134,17 +136,11 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_f32(IgemmArgs a) 
 
     auto load_stage = [&](int t, int c0) {
         const int dyt = tap_at(a.tdy, t), dxt = tap_at(a.tdx, t);
+        const long toff = long(dyt * a.ws + dxt) * a.ldc_s + c0;  // wave-uniform
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
-            const int sy = a_sy[i] + dyt, sx = a_sx[i] + dxt;
-            const bool v = a_ok[i] && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
-            const int col4 = ((tid + i * NT) % KC) * 4;
-            if (v) {
-                const size_t pix = size_t(a_img[i] * a.hs + sy) * a.ws + sx;
-                ra[i] = gload4(a.src + pix * a.ldc_s + c0 + col4);
-            } else {
-                ra[i] = zero4;
-            }
+            const bool v = unsigned(a_sy[i] + dyt) < unsigned(a.hs) && unsigned(a_sx[i] + dxt) < unsigned(a.ws);
+            ra[i] = v ? gload4(a_base[i] + toff) : zero4;
         }
         const int k0 = t * a.c + c0;
 #pragma unroll
@@ -297,7 +293,10 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) 
         a_r[i] = r0 + (ch % AQ) * 4;
         a_ok[i] = a_in[i] && a_r[i] < a.R;
     }
+    // B chunks: fixed column (tap, c) per thread; the pixel m = kb + b_k advances by BK per step, so its
+    // (img, oy, ox) coordinates are stepped incrementally instead of divided out every step.
     int b_k[B_PER], b_dy[B_PER], b_dx[B_PER], b_c[B_PER];
+    int b_img[B_PER], b_oy[B_PER], b_ox[B_PER];
     bool b_in[B_PER], b_ok[B_PER];
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
@@ -310,6 +309,13 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) 
         b_c[i] = j - t * a.C;
         b_dy[i] = tap_at(a.tdy, t);
         b_dx[i] = tap_at(a.tdx, t);
+        const uint32_t mm = uint32_t(min(kbeg + b_k[i], a.M - 1));
+        const uint32_t img = fdiv(mm, a.div_hw);
+        const uint32_t rr = mm - img * uint32_t(a.ho * a.wo);
+        const uint32_t oy = fdiv(rr, a.div_w);
+        b_img[i] = int(img);
+        b_oy[i] = int(oy);
+        b_ox[i] = int(rr - oy * uint32_t(a.wo));
     }
 
     f32x4 ra[A_PER], rb[B_PER];
@@ -322,22 +328,27 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) 
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
-            const int m = kb + b_k[i];
-            bool v = b_ok[i] && m < kend;
-            const uint32_t mm = v ? uint32_t(m) : 0u;
-            const uint32_t img = fdiv(mm, a.div_hw);
-            const uint32_t rr = mm - img * uint32_t(a.ho * a.wo);
-            const uint32_t oy = fdiv(rr, a.div_w);
-            const uint32_t ox = rr - oy * uint32_t(a.wo);
-            const int sy = int(oy) * a.stride + b_dy[i];
-            const int sx = int(ox) * a.stride + b_dx[i];
-            v = v && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
-            if (v) {
-                const size_t pix = size_t(int(img) * a.hs + sy) * a.ws + sx;
-                rb[i] = gload4(a.src + pix * a.ldc_s + b_c[i]);
-            } else {
-                rb[i] = zero4;
+            const int sy = b_oy[i] * a.stride + b_dy[i];
+            const int sx = b_ox[i] * a.stride + b_dx[i];
+            const bool v = b_ok[i] && (kb + b_k[i] < kend) && unsigned(sy) < unsigned(a.hs) &&
+                           unsigned(sx) < unsigned(a.ws);
+            rb[i] = v ? gload4(a.src + (size_t(b_img[i] * a.hs + sy) * a.ws + sx) * a.ldc_s + b_c[i]) : zero4;
+        }
+    };
+    auto advance = [&]() {  // pixel += BK for every B chunk
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            int ox = b_ox[i] + BK, oy = b_oy[i], img = b_img[i];
+            while (ox >= a.wo) {
+                ox -= a.wo;
+                if (++oy == a.ho) {
+                    oy = 0;
+                    ++img;
+                }
             }
+            b_ox[i] = ox;
+            b_oy[i] = oy;
+            b_img[i] = img;
         }
     };
     auto store_stage = [&](int buf) {
@@ -369,21 +380,50 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) 
         __syncthreads();
         for (int s = 0; s < nsteps; ++s) {
             const bool more = s + 1 < nsteps;
-            if (more) load_stage(kbeg + (s + 1) * BK);
+            if (more) {
+                advance();
+                load_stage(kbeg + (s + 1) * BK);
+            }
             const float *S = smem + (s & 1) * STAGE;
+            // Two groups of 4 k-pairs: group 0's fragments are read and waited for, group 1's reads are
+            // issued (sched_barrier keeps them ahead) and land while group 0's MFMAs run.
+            float av0[4][TM], bv0[4][TN], av1[4][TM], bv1[4][TN];
 #pragma unroll
-            for (int kk = 0; kk < BK / 2; ++kk) {
-                float av[TM], bv[TN];
+            for (int u = 0; u < 4; ++u) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = S[a_lane + 2 * kk * BM + i * 32];
+                for (int i = 0; i < TM; ++i) av0[u][i] = S[a_lane + 2 * u * BM + i * 32];
 #pragma unroll
-                for (int j = 0; j < TN; ++j) bv[j] = S[b_lane + 2 * kk * BN + j * 32];
+                for (int j = 0; j < TN; ++j) bv0[u][j] = S[b_lane + 2 * u * BN + j * 32];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(av0[u][i]));
+#pragma unroll
+                for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(bv0[u][j]));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av1[u][i] = S[a_lane + 2 * (4 + u) * BM + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv1[u][j] = S[b_lane + 2 * (4 + u) * BN + j * 32];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-            }
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av0[u][i], bv0[u][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av1[u][i], bv1[u][j], acc[i][j], 0, 0, 0);
             if (more) store_stage((s + 1) & 1);
             __syncthreads();
         }
@@ -404,11 +444,30 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) 
     }
 }
 
-__global__ void wgrad_finalize_kernel(const float *__restrict__ slabs, int nsplit, int R, int ntaps, int C,
-                                      int mode, int c_valid, float *__restrict__ out) {
+// Level 1 of the slab reduction: group g sums slabs [g*per, min((g+1)*per, nsplit)) in a fixed order and
+// writes the result in place into slab g*per (only this thread reads that element of that slab).
+__global__ void wgrad_group_sum(float *__restrict__ slabs, int nsplit, int per, size_t total) {
+    const size_t e = blockIdx.x * size_t(blockDim.x) + threadIdx.x;
+    if (e >= total) return;
+    const int k0 = blockIdx.y * per;
+    const int k1 = min(k0 + per, nsplit);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = k0;
+    for (; k + 3 < k1; k += 4) {
+        s0 += slabs[e + size_t(k) * total];
+        s1 += slabs[e + size_t(k + 1) * total];
+        s2 += slabs[e + size_t(k + 2) * total];
+        s3 += slabs[e + size_t(k + 3) * total];
+    }
+    for (; k < k1; ++k) s0 += slabs[e + size_t(k) * total];
+    slabs[e + size_t(k0) * total] = (s0 + s1) + (s2 + s3);
+}
+
+// Level 2: sum the (group) slabs at stride `gstride` slabs and scatter into the parameter layout.
+__global__ void wgrad_finalize_kernel(const float *__restrict__ slabs, int nsum, int gstride, int R, int ntaps,
+                                      int C, int mode, int c_valid, float *__restrict__ out) {
     const int Ng = ntaps * C;
     const size_t total = size_t(R) * Ng;
-    const size_t stride = total;
     for (size_t e = blockIdx.x * size_t(blockDim.x) + threadIdx.x; e < total; e += size_t(gridDim.x) * blockDim.x) {
         const int r = int(e / Ng);
         const int col = int(e - size_t(r) * Ng);
@@ -416,7 +475,7 @@ __global__ void wgrad_finalize_kernel(const float *__restrict__ slabs, int nspli
         const int c = col - t * C;
         if (c >= c_valid) continue;
         float s = 0.f;
-        for (int k = 0; k < nsplit; ++k) s += slabs[e + k * stride];
+        for (int k = 0; k < nsum; ++k) s += slabs[e + size_t(k) * gstride * total];
         size_t o;
         if (mode == 0)
             o = (size_t(r) * c_valid + c) * ntaps + t;  // OIHW [R][c_valid][3][3], t = ky*3+kx
@@ -540,12 +599,28 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
 
 namespace scd {
 struct WgradTile {
-    int bm, bn;
+    int id, bm, bn, threads;
 };
-static WgradTile wgrad_tile(int R) {
-    if (R >= 128) return {128, 128};
-    if (R >= 64) return {64, 256};
-    return {32, 128};
+// Tile shapes of the wgrad instantiations; per call the one with the least padded MFMA work wins
+// (ties: the larger tile).  E.g. R=64, Ng=576 (9x64): 64x192 is exact where 64x256 computes 33% waste.
+static const WgradTile kWgradTiles[] = {
+    {0, 128, 128, 256},  // wgrad_f32<2,2,2,2>
+    {1, 64, 256, 256},   // wgrad_f32<1,4,2,2>
+    {2, 64, 192, 256},   // wgrad_f32<2,2,1,3>
+    {3, 64, 96, 128},    // wgrad_f32<2,1,1,3>   (first layer: Ng = 9*8 = 72)
+    {4, 32, 128, 256},   // wgrad_f32<1,4,1,1>
+};
+static WgradTile wgrad_tile(int R, int Ng) {
+    WgradTile best = kWgradTiles[0];
+    int64_t best_work = -1;
+    for (const WgradTile &t : kWgradTiles) {
+        const int64_t work = int64_t((R + t.bm - 1) / t.bm) * t.bm * (int64_t((Ng + t.bn - 1) / t.bn) * t.bn);
+        if (best_work < 0 || work < best_work || (work == best_work && t.bm * t.bn > best.bm * best.bn)) {
+            best = t;
+            best_work = work;
+        }
+    }
+    return best;
 }
 static int wgrad_validate(const scd_wgrad_t *d) {
     if (!d) {
@@ -565,19 +640,59 @@ static int wgrad_validate(const scd_wgrad_t *d) {
     }
     return SCD_OK;
 }
+// Workgroups of one wgrad instantiation that the whole chip holds at once (occupancy API x CUs), cached.
+static int wgrad_resident_blocks(const WgradTile &t) {
+    static int cache[8] = {0};
+    if (cache[t.id] > 0) return cache[t.id];
+    int per_cu = 0, cus = 0, dev = 0;
+    const void *fn = nullptr;
+    switch (t.id) {
+        case 0: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 2, 2, 2, 16>); break;
+        case 1: fn = reinterpret_cast<const void *>(&wgrad_f32<1, 4, 2, 2, 16>); break;
+        case 2: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 2, 1, 3, 16>); break;
+        case 3: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 1, 1, 3, 16>); break;
+        default: fn = reinterpret_cast<const void *>(&wgrad_f32<1, 4, 1, 1, 16>); break;
+    }
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, t.threads, 0) != hipSuccess || per_cu < 1 ||
+        cus < 1) {
+        (void)hipGetLastError();
+        return 3 * 256;  // MI355X: 256 CUs, 3 resident 256-thread blocks at ~140 VGPRs
+    }
+    cache[t.id] = per_cu * cus;
+    return cache[t.id];
+}
+
+// Split-K factor: the block count tiles*nsplit is quantised against the chip's resident capacity so the
+// last round is not a handful of lone workgroups (one wave per SIMD cannot keep the MFMA pipe busy):
+// maximise blocks / (rounds * capacity), ties (within 2%) to fewer splits (less slab traffic).
 static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
-    const WgradTile t = wgrad_tile(d->rows.c);
     const int Ng = d->ntaps * d->src.c;
+    const WgradTile t = wgrad_tile(d->rows.c, Ng);
     const int64_t M = pixels(d->rows);
     const int64_t tiles = int64_t((d->rows.c + t.bm - 1) / t.bm) * ((Ng + t.bn - 1) / t.bn);
-    int64_t want = (1024 + tiles - 1) / tiles;
-    const int64_t maxsplit = (M + 511) / 512;  // keep >= 512 pixels per split
-    if (want > maxsplit) want = maxsplit;
-    if (want < 1) want = 1;
-    int64_t kc = (M + want - 1) / want;
-    kc = (kc + 15) / 16 * 16;
-    *kchunk = int(kc);
-    *nsplit = int((M + kc - 1) / kc);
+    const int64_t cap = wgrad_resident_blocks(t);
+    int64_t maxsplit = (M + 255) / 256;  // keep >= 256 pixels per split
+    const int64_t lim = (8 * cap + tiles - 1) / tiles;
+    if (maxsplit > lim) maxsplit = lim;
+    if (maxsplit < 1) maxsplit = 1;
+    int64_t best_kc = (M + 15) / 16 * 16;
+    double best_eff = -1.0;
+    for (int64_t want = 1; want <= maxsplit; ++want) {
+        int64_t kc = (M + want - 1) / want;
+        kc = (kc + 15) / 16 * 16;
+        const int64_t n = (M + kc - 1) / kc;
+        const int64_t blocks = tiles * n;
+        const int64_t rounds = (blocks + cap - 1) / cap;
+        const double eff = double(blocks) / double(rounds * cap);
+        if (eff > best_eff + 0.02) {
+            best_eff = eff;
+            best_kc = kc;
+        }
+    }
+    *kchunk = int(best_kc);
+    *nsplit = int((M + best_kc - 1) / best_kc);
 }
 }  // namespace scd
 
@@ -625,18 +740,20 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
     a.div_w = make_fastdiv(uint32_t(d->rows.w));
     a.div_c = make_fastdiv(uint32_t(d->src.c));
     hipStream_t s = as_stream(stream);
-    const WgradTile t = wgrad_tile(a.R);
+    const WgradTile t = wgrad_tile(a.R, Ng);
     dim3 grid((a.R + t.bm - 1) / t.bm, (Ng + t.bn - 1) / t.bn, ns);
-    if (t.bm == 128)
-        hipLaunchKernelGGL((wgrad_f32<2, 2, 2, 2, 16>), grid, dim3(256), 0, s, a);
-    else if (t.bm == 64)
-        hipLaunchKernelGGL((wgrad_f32<1, 4, 2, 2, 16>), grid, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL((wgrad_f32<1, 4, 1, 1, 16>), grid, dim3(256), 0, s, a);
+    dim3 block(t.threads);
+    switch (t.id) {
+        case 0: hipLaunchKernelGGL((wgrad_f32<2, 2, 2, 2, 16>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((wgrad_f32<1, 4, 2, 2, 16>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((wgrad_f32<2, 2, 1, 3, 16>), grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((wgrad_f32<2, 1, 1, 3, 16>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((wgrad_f32<1, 4, 1, 1, 16>), grid, block, 0, s, a); break;
+    }
     return launch_status("scd_conv_wgrad");
 }
 
-extern "C" int scd_wgrad_finalize(const float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C,
+extern "C" int scd_wgrad_finalize(float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C,
                                   int32_t mode, int32_t c_valid, float *out, scd_stream_t stream) {
     clear_error();
     if (!slabs || !out || nsplit < 1 || R < 1 || ntaps < 1 || C < 1 || (mode != 0 && mode != 1) || c_valid < 1 ||
@@ -645,9 +762,22 @@ extern "C" int scd_wgrad_finalize(const float *slabs, int32_t nsplit, int32_t R,
         return SCD_ERR_ARG;
     }
     const size_t total = size_t(R) * ntaps * C;
-    int blocks = int((total + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), slabs, nsplit, R, ntaps,
-                       C, mode, c_valid, out);
+    const int base_blocks = int((total + 255) / 256);
+    hipStream_t s = as_stream(stream);
+    // enough parallelism for long split lists: G groups of `per` slabs summed first (in place)
+    int G = (2048 + base_blocks - 1) / base_blocks;
+    if (G > (nsplit + 3) / 4) G = (nsplit + 3) / 4;
+    if (G < 1) G = 1;
+    int nsum = nsplit, gstride = 1;
+    if (G > 1) {
+        const int per = (nsplit + G - 1) / G;
+        G = (nsplit + per - 1) / per;
+        hipLaunchKernelGGL(wgrad_group_sum, dim3(base_blocks, G), dim3(256), 0, s, slabs, nsplit, per, total);
+        nsum = G;
+        gstride = per;
+    }
+    const int blocks = base_blocks > 4096 ? 4096 : base_blocks;
+    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, slabs, nsum, gstride, R, ntaps, C, mode,
+                       c_valid, out);
     return launch_status("scd_wgrad_finalize");
 }
