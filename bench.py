@@ -231,9 +231,18 @@ def main():
         summ = timer.summary()
         t_ms = sum(t for _, t in summ.values()) / reps
         achieved = (f3 + fT) / (t_ms * 1e-3) / 1e12
+        traffic = None
+        pmc = sorted(f for f in os.listdir(os.path.join(ROOT, 'profiles')) if f.endswith('_pmc_traffic.json'))
+        if pmc and args.config == 'baseline_siamese' and batch == 32 and size == 256:
+            with open(os.path.join(ROOT, 'profiles', pmc[-1])) as f:
+                tr = json.load(f)
+            traffic = {"bytes_per_step": round(tr['per_step_bytes']['total']),
+                       "by_family": {k: round(v) for k, v in tr['per_step_bytes'].items() if k != 'total'},
+                       "source": f"profiles/{pmc[-1]}: {tr['source']}; L2-miss fabric bytes (Infinity-Cache "
+                                 "hits included, MI355X_MICROARCH.md HBM)"}
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "kernel": "igemm_f32 + wgrad_f32 (all conv launches of one training step: 3x3 fwd/dgrad/wgrad, "
                       "ConvT fwd/dgrad/wgrad)",
             "flop_per_step": f3 + fT,

@@ -1,0 +1,125 @@
+"""World-size-2 data-parallel plumbing on CPU (gloo): multimodal_siamese_cd_amd/parallel.py.
+
+The HIP path has no CPU execution, so the replica here runs the CPU oracle's functional restatement
+(oracle/siamese_oracle.py) wrapped in an nn.Module. What is tested is the distributed plumbing the GPU
+bench/trainer uses, unchanged:
+
+- `init_distributed` from torchrun-style env;
+- `rank_seed` giving disjoint per-rank shards;
+- `wrap_ddp` averaging gradients across ranks (checked against a single process that runs both shards and
+  averages);
+- `allreduce_max` (the bench's max-over-ranks timing) and `barrier`.
+
+It mirrors the reference's DataParallel semantics (utils/networks.py:27): per-replica BatchNorm batch
+statistics, gradients reduced over replicas.
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from multimodal_siamese_cd_amd import parallel
+from oracle import siamese_oracle as orc
+
+CFG = {'TOPOLOGY': [8, 16], 'IN_CHANNELS': 5, 'OUT_CHANNELS': 1, 'S1_BANDS': [0, 1], 'S2_BANDS': [0, 1, 2]}
+HW = 32
+PER_RANK = 2
+
+
+class OracleReplica(torch.nn.Module):
+    """Parameter/buffer container whose forward is the oracle's SiameseUNet (names with '.' -> '__')."""
+
+    def __init__(self, P, B):
+        super().__init__()
+        self._pk = list(P)
+        self._bk = list(B)
+        for k, v in P.items():
+            self.register_parameter(k.replace('.', '__'), torch.nn.Parameter(v.clone()))
+        for k, v in B.items():
+            self.register_buffer(k.replace('.', '__'), v.clone())
+
+    def forward(self, x_t1, x_t2):
+        P = {k: getattr(self, k.replace('.', '__')) for k in self._pk}
+        B = {k: getattr(self, k.replace('.', '__')) for k in self._bk}
+        return orc.forward('siameseunet', P, B, x_t1, x_t2, CFG, training=True)
+
+
+def _model():
+    shapes = orc.param_shapes('siameseunet', CFG)
+    return OracleReplica(orc.deterministic_params(shapes, 5), orc.fresh_buffers(shapes))
+
+
+def _shard(rank):
+    return orc.synthetic_batch(CFG, PER_RANK, HW, parallel.rank_seed(11, rank))
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    r, lr, w = parallel.init_distributed('gloo')
+    assert (r, lr, w) == (rank, rank, world) and parallel.is_distributed()
+    net = parallel.wrap_ddp(_model(), device=None)
+    assert isinstance(net, torch.nn.parallel.DistributedDataParallel)
+    b = _shard(rank)
+    loss = orc.power_jaccard_loss(net(b['x_t1'], b['x_t2']), b['y_change'])
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in net.module.named_parameters()}
+    tmax = parallel.allreduce_max(float(rank) + 0.25, torch.device('cpu'))
+    parallel.barrier()
+    torch.save({'grads': grads, 'loss': loss.item(), 'tmax': tmax},
+               os.path.join(out_dir, f'rank{rank}.pt'))
+    torch.distributed.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def test_rank_seed_disjoint():
+    seeds = {parallel.rank_seed(3, r) for r in range(64)}
+    assert len(seeds) == 64
+    a, b = _shard(0), _shard(1)
+    assert not torch.equal(a['x_t1'], b['x_t1'])
+
+
+def test_single_process_passthrough():
+    net = _model()
+    assert not parallel.is_distributed()
+    assert parallel.wrap_ddp(net) is net
+    assert parallel.allreduce_max(1.5, torch.device('cpu')) == 1.5
+    parallel.barrier()  # no-op
+
+
+@pytest.mark.timeout(300)
+def test_ddp_gradient_average_world2():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+
+    # single-process equivalent: each shard through its own replica (per-replica BN stats), grads averaged
+    ref = None
+    for r in range(world):
+        net = _model()
+        b = _shard(r)
+        loss = orc.power_jaccard_loss(net(b['x_t1'], b['x_t2']), b['y_change'])
+        assert abs(loss.item() - res[r]['loss']) < 1e-6
+        loss.backward()
+        g = {n: p.grad.detach() / world for n, p in net.named_parameters()}
+        ref = g if ref is None else {n: ref[n] + g[n] for n in ref}
+
+    for r in range(world):
+        assert res[r]['tmax'] == pytest.approx(world - 1 + 0.25)
+        for n, g in ref.items():
+            got = res[r]['grads'][n]
+            # pre-BN conv biases have true gradient 0 (float noise ~1e-8): absolute floor
+            assert float((got - g).abs().max()) <= 1e-5 * float(g.abs().max()) + 1e-7, (r, n)
+    # every rank holds the identical averaged gradient
+    for n in ref:
+        assert torch.equal(res[0]['grads'][n], res[1]['grads'][n])
