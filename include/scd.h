@@ -76,7 +76,21 @@ int scd_pack_conv3x3(const float *w, int32_t co, int32_t ci, int32_t ci_pad, int
 int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, float *out, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+ * Conv arithmetic.  Both modes compute an fp32 GEMM with fp32 accumulation:
+ *   SCD_MATH_F32  v_mfma_f32_32x32x2_f32: exact fp32 products (a k-ordered fmaf chain per MFMA).
+ *   SCD_MATH_X3   v_mfma_f32_32x32x16_bf16 on an exact 3-way bf16 split of each fp32 operand
+ *                 (x = h + m + l, each term rounded to nearest), accumulating the six terms
+ *                 hh+hm+mh+mm+hl+lh.  The dropped terms are <= ~2^-26 relative, so the rounding error is
+ *                 of fp32 order, at 6/16 of the matrix-core cycles.  Used when src.c % 16 == 0; other shapes
+ *                 fall back to the fp32 MFMA kernel.
+ * Default: SCD_MATH_X3, or the SCD_CONV_MATH=f32|x3 environment variable at first use.  Returns the
+ * previous mode; SCD_MATH_QUERY only queries.  Process-wide (not per stream).
+ * ------------------------------------------------------------------------------------------- */
+enum scd_conv_math { SCD_MATH_QUERY = -1, SCD_MATH_F32 = 0, SCD_MATH_X3 = 1 };
+int scd_set_conv_math(int32_t mode);
+
+/* ---------------------------------------------------------------------------------------------
+ * Implicit-GEMM convolution on MFMA (arithmetic: scd_set_conv_math).
  *   out[m, o] = bias[o] + sum_{t<ntaps, c<src.c} src[img, oy*stride+dy[t], ox*stride+dx[t], c] * wpk[o][t*src.c + c]
  *   m = (img, oy, ox) over src.n x out_h x out_w; out-of-range source pixels read as 0 (zero padding).
  * store_mode 0: dst[img, oy, ox, o]                            (dst.h == out_h, dst.w == out_w)
@@ -103,7 +117,7 @@ typedef struct scd_igemm {
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Weight gradient (split-K implicit GEMM on fp32 MFMA), deterministic two-stage reduction.
+ * Weight gradient (split-K implicit GEMM on MFMA), deterministic two-stage reduction.
  *   slab[s][r][t*src.c + c] = sum_{m in split s} rows[m, r] * src[img, oy*stride+dy[t], ox*stride+dx[t], c]
  *   m = (img, oy, ox) over rows.n x rows.h x rows.w.
  * Conv2d 3x3: rows = dY, src = X (taps -1..1).  ConvTranspose2d: rows = X, src = dOut (stride 2, taps 0..1).

@@ -1,0 +1,108 @@
+// Shared pieces of the implicit-GEMM conv kernels (fp32 MFMA: conv_f32.hip, split-bf16 MFMA: conv_x3.hip).
+#pragma once
+
+#include "common.h"
+
+namespace scd {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Loads/stores through the global address space (kernel-arg structs otherwise yield flat_* ops).
+__device__ __forceinline__ f32x4 gload4(const float *p) {
+    return *(const __attribute__((address_space(1))) f32x4 *)(p);
+}
+__device__ __forceinline__ void gstore1(float *p, float v) { *(__attribute__((address_space(1))) float *)(p) = v; }
+__device__ __forceinline__ f32x4 lload4(const float *p) { return *reinterpret_cast<const f32x4 *>(p); }
+__device__ __forceinline__ void lstore4(float *p, f32x4 v) { *reinterpret_cast<f32x4 *>(p) = v; }
+
+// Division by a runtime constant: n / d = (umulhi(n, mul) + n) >> shr, valid for n < 2^31.
+struct FastDiv {
+    uint32_t d, mul, shr;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    uint32_t s = 0;
+    while ((1ull << s) < d) ++s;
+    f.shr = s;
+    f.mul = uint32_t(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
+    return (__umulhi(n, f.mul) + n) >> f.shr;
+}
+
+// 9 taps packed as signed 4-bit fields.
+__device__ __forceinline__ int tap_at(uint64_t packed, int t) {
+    int v = int((packed >> (4 * t)) & 15ull);
+    return v >= 8 ? v - 16 : v;
+}
+
+// XCD-aware block order (guide T1, bijective form): the dispatcher deals consecutive workgroup ids round-robin
+// to the 8 XCDs, so id b runs beside ids b+8, b+16, ... under one L2.  Renumbering so that each XCD receives
+// a contiguous range of logical tiles keeps neighbouring pixel tiles (which share halo rows through the
+// 3x3 taps) and the N-tiles of one pixel tile (which share the gathered A rows) under the same L2.
+// Placement only changes speed, never results.
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t nwg) {
+    const uint32_t x = bid & 7u, slot = bid >> 3, q = nwg >> 3, r = nwg & 7u;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
+}
+
+inline int xcd_remap_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("SCD_XCD_REMAP");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v;
+}
+
+inline uint64_t pack_taps(const int8_t *v, int n) {
+    uint64_t p = 0;
+    for (int i = 0; i < n; ++i) p |= uint64_t(uint8_t(v[i]) & 15u) << (4 * i);
+    return p;
+}
+
+// ------------------------------------------------------------------------------------------------
+// igemm
+// ------------------------------------------------------------------------------------------------
+struct IgemmArgs {
+    const float *src;
+    int n_img, hs, ws, c, ldc_s;
+    int ho, wo, stride, ntaps;
+    uint64_t tdy, tdx;
+    const float *w;
+    int n_out, K;
+    const float *bias;
+    float *dst;
+    int ldc_d, dst_h, dst_w, store_mode, cout;
+    int M;
+    int grid_m, grid_n, remap;
+    FastDiv div_hw, div_w;
+};
+
+struct WgradArgs {
+    const float *rows;
+    int ho, wo, R, ldc_r;
+    const float *src;
+    int hs, ws, C, ldc_s;
+    int stride, ntaps;
+    uint64_t tdy, tdx;
+    int Ng, M, kchunk;
+    int grid_r, grid_j, remap;
+    float *slabs;
+    FastDiv div_hw, div_w, div_c;
+};
+
+// Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels
+// (the caller then runs the fp32-MFMA kernel).
+bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s);
+
+// Conv math selection (scd_set_conv_math): SCD_MATH_X3 = split-bf16 MFMA where the shape allows it,
+// SCD_MATH_F32 = fp32 MFMA everywhere.  Initial value from SCD_CONV_MATH=f32|x3 (default x3).
+int conv_math_x3();
+
+}  // namespace scd

@@ -13,68 +13,9 @@
 // MFMA operand trick (fp32, 32x32x2): instruction s of an 8-deep K chunk takes k = 4h + s from lane
 // half h = lane>>5, so every lane reads its 4 k-values for a row with ONE ds_read_b128 from a
 // [row][k] LDS image (row stride BK+4 floats: conflict-free b128 reads).
-#include "common.h"
+#include "conv_common.h"
 
 namespace scd {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// Loads/stores through the global address space (kernel-arg structs otherwise yield flat_* ops).
-__device__ __forceinline__ f32x4 gload4(const float *p) {
-    return *(const __attribute__((address_space(1))) f32x4 *)(p);
-}
-__device__ __forceinline__ void gstore1(float *p, float v) { *(__attribute__((address_space(1))) float *)(p) = v; }
-__device__ __forceinline__ f32x4 lload4(const float *p) { return *reinterpret_cast<const f32x4 *>(p); }
-__device__ __forceinline__ void lstore4(float *p, f32x4 v) { *reinterpret_cast<f32x4 *>(p) = v; }
-
-// Division by a runtime constant: n / d = (umulhi(n, mul) + n) >> shr, valid for n < 2^31.
-struct FastDiv {
-    uint32_t d, mul, shr;
-};
-
-static FastDiv make_fastdiv(uint32_t d) {
-    FastDiv f;
-    f.d = d;
-    uint32_t s = 0;
-    while ((1ull << s) < d) ++s;
-    f.shr = s;
-    f.mul = uint32_t(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-    return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
-    return (__umulhi(n, f.mul) + n) >> f.shr;
-}
-
-// 9 taps packed as signed 4-bit fields.
-__device__ __forceinline__ int tap_at(uint64_t packed, int t) {
-    int v = int((packed >> (4 * t)) & 15ull);
-    return v >= 8 ? v - 16 : v;
-}
-
-static uint64_t pack_taps(const int8_t *v, int n) {
-    uint64_t p = 0;
-    for (int i = 0; i < n; ++i) p |= uint64_t(uint8_t(v[i]) & 15u) << (4 * i);
-    return p;
-}
-
-// ------------------------------------------------------------------------------------------------
-// igemm
-// ------------------------------------------------------------------------------------------------
-struct IgemmArgs {
-    const float *src;
-    int n_img, hs, ws, c, ldc_s;
-    int ho, wo, stride, ntaps;
-    uint64_t tdy, tdx;
-    const float *w;
-    int n_out, K;
-    const float *bias;
-    float *dst;
-    int ldc_d, dst_h, dst_w, store_mode, cout;
-    int M;
-    FastDiv div_hw, div_w;
-};
 
 template <int WAVES_M, int WAVES_N, int TM, int TN, int BK>
 __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_f32(IgemmArgs a) {
@@ -95,8 +36,17 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_f32(IgemmArgs a) 
     const int wid = tid >> 6;
     const int wm = wid % WAVES_M;
     const int wn = wid / WAVES_M;
-    const int m0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    int mt, nt;
+    if (a.remap) {  // logical tiles: N fastest, so the N-tiles of one pixel tile run together on one XCD
+        const uint32_t L = xcd_swizzle(blockIdx.x, uint32_t(a.grid_m * a.grid_n));
+        mt = int(L / uint32_t(a.grid_n));
+        nt = int(L - uint32_t(mt) * uint32_t(a.grid_n));
+    } else {
+        mt = int(blockIdx.x % uint32_t(a.grid_m));
+        nt = int(blockIdx.x / uint32_t(a.grid_m));
+    }
+    const int m0 = mt * BM;
+    const int n0 = nt * BN;
 
     // Per-thread A-chunk bookkeeping (fixed across the K loop): the source pixel (img, oy*s, ox*s) as a
     // base pointer; a tap then only adds the wave-uniform offset (dy*ws + dx)*ldc + c0 after a bounds test.
@@ -247,17 +197,6 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_f32(IgemmArgs a) 
 // ------------------------------------------------------------------------------------------------
 // wgrad
 // ------------------------------------------------------------------------------------------------
-struct WgradArgs {
-    const float *rows;
-    int ho, wo, R, ldc_r;
-    const float *src;
-    int hs, ws, C, ldc_s;
-    int stride, ntaps;
-    uint64_t tdy, tdx;
-    int Ng, M, kchunk;
-    float *slabs;
-    FastDiv div_hw, div_w, div_c;
-};
 
 template <int WAVES_M, int WAVES_N, int TM, int TN, int BK>
 __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) {
@@ -278,9 +217,16 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) 
     const int wid = tid >> 6;
     const int wm = wid % WAVES_M;
     const int wn = wid / WAVES_M;
-    const int r0 = blockIdx.x * BM;
-    const int j0 = blockIdx.y * BN;
-    const int kbeg = blockIdx.z * a.kchunk;
+    // logical block -> (split, column tile, row tile), row tile fastest: the tiles of one pixel split share
+    // their B pixels and run together on one XCD when remapped.
+    const uint32_t per_split = uint32_t(a.grid_r * a.grid_j);
+    const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int split = int(L / per_split);
+    const int rem = int(L - uint32_t(split) * per_split);
+    const int jt = rem / a.grid_r;
+    const int r0 = (rem - jt * a.grid_r) * BM;
+    const int j0 = jt * BN;
+    const int kbeg = split * a.kchunk;
     const int kend = min(a.M, kbeg + a.kchunk);
 
     int a_k[A_PER], a_r[A_PER];
@@ -429,7 +375,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_f32(WgradArgs a) 
         }
     }
 
-    float *slab = a.slabs + size_t(blockIdx.z) * a.R * a.Ng;
+    float *slab = a.slabs + size_t(split) * a.R * a.Ng;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int col = j0 + wn * TN * 32 + j * 32 + (lane & 31);
@@ -491,8 +437,11 @@ __global__ void wgrad_finalize_kernel(const float *__restrict__ slabs, int nsum,
 template <int WM, int WN, int TM, int TN, int BK>
 static void launch_igemm(const IgemmArgs &a, hipStream_t s) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-    dim3 grid((a.M + BM - 1) / BM, (a.n_out + BN - 1) / BN);
-    hipLaunchKernelGGL((igemm_f32<WM, WN, TM, TN, BK>), grid, dim3(64 * WM * WN), 0, s, a);
+    IgemmArgs b = a;
+    b.grid_m = (a.M + BM - 1) / BM;
+    b.grid_n = (a.n_out + BN - 1) / BN;
+    b.remap = xcd_remap_enabled();
+    hipLaunchKernelGGL((igemm_f32<WM, WN, TM, TN, BK>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN), 0, s, b);
 }
 
 template <int WM, int WN, int TM, int TN>
@@ -516,9 +465,31 @@ static int check_taps(int ntaps, const int8_t *dy, const int8_t *dx) {
     return SCD_OK;
 }
 
+static int g_conv_math = -1;
+
+int conv_math_x3() {
+    if (g_conv_math < 0) {
+        const char *e = getenv("SCD_CONV_MATH");
+        g_conv_math = (e && e[0] == 'f') ? SCD_MATH_F32 : SCD_MATH_X3;
+    }
+    return g_conv_math == SCD_MATH_X3;
+}
+
 }  // namespace scd
 
 using namespace scd;
+
+extern "C" int scd_set_conv_math(int32_t mode) {
+    clear_error();
+    const int prev = conv_math_x3() ? SCD_MATH_X3 : SCD_MATH_F32;
+    if (mode == SCD_MATH_F32 || mode == SCD_MATH_X3) {
+        g_conv_math = mode;
+    } else if (mode != SCD_MATH_QUERY) {
+        set_error("scd_set_conv_math: mode %d", mode);
+        return SCD_ERR_ARG;
+    }
+    return prev;
+}
 
 extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
     clear_error();
@@ -588,6 +559,7 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
     a.div_hw = make_fastdiv(uint32_t(d->out_h * d->out_w));
     a.div_w = make_fastdiv(uint32_t(d->out_w));
     hipStream_t s = as_stream(stream);
+    if (conv_math_x3() && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");
     if (d->n_out >= 128)
         launch_igemm_bk<2, 2, 2, 2>(a, s);  // 128 x 128
     else if (d->n_out >= 64)
@@ -741,7 +713,10 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
     a.div_c = make_fastdiv(uint32_t(d->src.c));
     hipStream_t s = as_stream(stream);
     const WgradTile t = wgrad_tile(a.R, Ng);
-    dim3 grid((a.R + t.bm - 1) / t.bm, (Ng + t.bn - 1) / t.bn, ns);
+    a.grid_r = (a.R + t.bm - 1) / t.bm;
+    a.grid_j = (Ng + t.bn - 1) / t.bn;
+    a.remap = xcd_remap_enabled();
+    dim3 grid(a.grid_r * a.grid_j * ns);
     dim3 block(t.threads);
     switch (t.id) {
         case 0: hipLaunchKernelGGL((wgrad_f32<2, 2, 2, 2, 16>), grid, block, 0, s, a); break;

@@ -66,6 +66,7 @@ _SIGS = {
     "scd_pack_nchw": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, NHWC, c_void_p], c_int),
     "scd_pack_conv3x3": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_set_conv_math": ([c_int32], c_int),
     "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
     "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
     "scd_conv_wgrad": ([POINTER(WGRAD), c_void_p, c_size_t, c_void_p], c_int),
@@ -205,6 +206,24 @@ def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:
     _check(lib().scd_pack_convT2x2(w.contiguous().data_ptr(), ci, co, mode, out.data_ptr(), _stream()),
            "scd_pack_convT2x2")
     return out
+
+
+MATH_F32, MATH_X3 = 0, 1
+_MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3}
+
+
+def set_conv_math(mode) -> str:
+    """Select the conv arithmetic ('f32' = fp32 MFMA, 'x3' = exact 3-way split-bf16 MFMA); returns the previous."""
+    m = _MATH_NAMES[mode] if isinstance(mode, str) else int(mode)
+    rc = lib().scd_set_conv_math(m)
+    if rc < 0:
+        _check(rc, "scd_set_conv_math")
+    return {v: k for k, v in _MATH_NAMES.items()}[rc]
+
+
+def conv_math() -> str:
+    rc = lib().scd_set_conv_math(-1)
+    return {v: k for k, v in _MATH_NAMES.items()}[rc]
 
 
 def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,

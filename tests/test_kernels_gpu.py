@@ -1,7 +1,9 @@
 """Per-kernel parity on MI355X: each libscd entry point vs the torch fp32 CPU op it replaces.
 
-Tolerance: max|hip - ref| / max|ref| <= 1e-5 for single ops (fp32 MFMA = exact fp32 fmaf chains; the
-residual is summation order), argmax indices bit-exact.
+Tolerance: max|hip - ref| / max|ref| <= 1e-5 for single ops; argmax indices are bit-exact.
+- fp32 MFMA is exact fp32 fmaf chains, so the residual is summation order only.
+- The split-bf16 x3 conv math drops only terms of <= ~2^-26 relative size.
+Every conv test runs under both conv arithmetics (scd_set_conv_math).
 """
 import numpy as np
 import pytest
@@ -22,6 +24,14 @@ def dev():
     d = torch.device('cuda:0')
     hip.ensure_device(torch.empty(1, device=d))
     return d
+
+
+@pytest.fixture(params=['f32', 'x3'])
+def math(request, dev):
+    from multimodal_siamese_cd_amd import hip
+    prev = hip.set_conv_math(request.param)
+    yield request.param
+    hip.set_conv_math(prev)
 
 
 def rel(a, b):
@@ -49,7 +59,7 @@ CONV_SHAPES = [  # n, h, w, cin, cout
 
 
 @pytest.mark.parametrize('n,h,w,ci,co', CONV_SHAPES)
-def test_conv3x3_forward(dev, n, h, w, ci, co):
+def test_conv3x3_forward(dev, math, n, h, w, ci, co):
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(n * 1000 + ci + co)
     x = torch.randn(n, h, w, ci, generator=g)
@@ -63,7 +73,7 @@ def test_conv3x3_forward(dev, n, h, w, ci, co):
 
 
 @pytest.mark.parametrize('n,h,w,ci,co', CONV_SHAPES)
-def test_conv3x3_data_and_weight_grad(dev, n, h, w, ci, co):
+def test_conv3x3_data_and_weight_grad(dev, math, n, h, w, ci, co):
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(7 + n + ci * co)
     x = torch.randn(n, h, w, ci, generator=g)
@@ -83,7 +93,7 @@ def test_conv3x3_data_and_weight_grad(dev, n, h, w, ci, co):
     assert rel(dw, ref_dw) < TOL
 
 
-def test_conv3x3_channel_padded_input(dev):
+def test_conv3x3_channel_padded_input(dev, math):
     """First layer: 5 real input channels padded to 8 in NHWC (zero channels, zero weights)."""
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(3)
@@ -109,8 +119,34 @@ def test_conv3x3_channel_padded_input(dev):
     assert rel(dw, ref_dw) < TOL
 
 
+@pytest.mark.parametrize('ci,co', [(64, 128), (512, 512), (128, 64)])
+def test_conv_math_accuracy_vs_fp64(dev, ci, co):
+    """Both arithmetics against an fp64 conv on wide-dynamic-range data (magnitudes spread over 1e-3..1e3).
+
+    The x3 split must be as accurate as fp32 MFMA: its error may not exceed 2x the fp32 kernel's error,
+    and both must stay at fp32 rounding level.
+    """
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(ci + 3 * co)
+    n, h, w = 2, 24, 20
+    x = torch.randn(n, h, w, ci, generator=g, dtype=torch.float64) * 10 ** (6 * torch.rand(n, h, w, ci, generator=g, dtype=torch.float64) - 3)
+    wt = torch.randn(co, ci, 3, 3, generator=g, dtype=torch.float64) / (3 * ci ** 0.5)
+    x, wt = x.float(), wt.float()
+    ref = nhwc_t(F.conv2d(nchw(x).double(), wt.double(), None, padding=1))
+    errs = {}
+    for m in ('f32', 'x3'):
+        prev = hip.set_conv_math(m)
+        y = torch.empty(n, h, w, co, device=dev)
+        hip.conv_igemm(hip.nhwc(x.to(dev)), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wt.to(dev), 0), co, None,
+                       hip.nhwc(y))
+        hip.set_conv_math(prev)
+        errs[m] = rel(y, ref)
+    assert errs['f32'] < 1e-5 and errs['x3'] < 1e-5, errs
+    assert errs['x3'] <= 2 * errs['f32'] + 1e-7, errs
+
+
 @pytest.mark.parametrize('n,h,w,c,cs', [(2, 8, 8, 16, 16), (1, 16, 16, 64, 64), (2, 4, 6, 512, 512), (2, 3, 5, 8, 24)])
-def test_convT2x2_forward_into_concat_slice(dev, n, h, w, c, cs):
+def test_convT2x2_forward_into_concat_slice(dev, math, n, h, w, c, cs):
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(c + h)
     x = torch.randn(n, h, w, c, generator=g)
@@ -126,7 +162,7 @@ def test_convT2x2_forward_into_concat_slice(dev, n, h, w, c, cs):
 
 
 @pytest.mark.parametrize('n,h,w,c,cs', [(2, 8, 8, 16, 16), (1, 16, 16, 64, 64), (2, 4, 6, 512, 512)])
-def test_convT2x2_backward(dev, n, h, w, c, cs):
+def test_convT2x2_backward(dev, math, n, h, w, c, cs):
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(11 + c)
     x = torch.randn(n, c, h, w, generator=g, requires_grad=True)

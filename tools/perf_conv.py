@@ -54,8 +54,12 @@ def main():
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--only', default=None)
     ap.add_argument('--layer', default=None, help='run only this layer name (e.g. enc1b)')
+    ap.add_argument('--math', default=None, choices=['f32', 'x3'], help='conv arithmetic (default: library default)')
     args = ap.parse_args()
     hip.load_library()
+    if args.math:
+        hip.set_conv_math(args.math)
+    print(f'conv math: {hip.conv_math()}')
     dev = torch.device('cuda:0')
     tot = {'fwd': [0.0, 0.0], 'dgrad': [0.0, 0.0], 'wgrad': [0.0, 0.0]}
     print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"cin":>5s} {"cout":>5s} | '
@@ -96,7 +100,7 @@ def main():
     allf = sum(v[1] for v in tot.values())
     for k, (t, f) in tot.items():
         if t:
-            print(f'{k:6s} total {t:8.2f} ms  {f / t / 1e9:6.1f} TF/s  ({f / t / 1e9 / PEAK * 100:.1f}% of peak)')
+            print(f'{k:6s} total {t:8.2f} ms  {f / t / 1e9:6.1f} TF/s  ({f / t / 1e9 / PEAK * 100:.1f}% of fp32 peak)')
     print(f'3x3 total {allt:8.2f} ms  {allf / allt / 1e9:6.1f} TF/s  ({allf / allt / 1e9 / PEAK * 100:.1f}% of peak)')
 
 
