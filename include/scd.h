@@ -88,6 +88,9 @@ int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, floa
  * ------------------------------------------------------------------------------------------- */
 enum scd_conv_math { SCD_MATH_QUERY = -1, SCD_MATH_F32 = 0, SCD_MATH_X3 = 1 };
 int scd_set_conv_math(int32_t mode);
+/* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
+ * n % 8 == 0, src and dst 16-byte aligned. */
+int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Implicit-GEMM convolution on MFMA (arithmetic: scd_set_conv_math).
@@ -112,6 +115,10 @@ typedef struct scd_igemm {
     const float *bias;  /* [n_out] (store_mode 0) or [n_out/4] (store_mode 1) or NULL */
     scd_nhwc_t dst;
     int32_t store_mode;
+    /* Optional (SCD_MATH_X3 only): wpk pre-split by scd_split_bf16x3, planes [3][n_out*ntaps*src.c].
+     * The weights are then staged by copy instead of being split in every workgroup.  NULL = split on
+     * the fly.  Must describe the same values as wpk. */
+    const uint16_t *wsplit;
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);

@@ -81,6 +81,9 @@ struct IgemmArgs {
     int ldc_d, dst_h, dst_w, store_mode, cout;
     int M;
     int grid_m, grid_n, remap;
+    const uint16_t *wsplit;  // optional pre-split weight planes [3][n_out*K] (x3 math)
+    int64_t wplane;
+    int dbg;  // ablation flags (SCD_IGEMM_DBG, perf experiments only; 0 in production)
     FastDiv div_hw, div_w;
 };
 
@@ -100,6 +103,9 @@ struct WgradArgs {
 // Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels
 // (the caller then runs the fp32-MFMA kernel).
 bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s);
+// x3 weight-grad instantiations, indexed like kWgradTiles (conv_f32.hip).
+const void *wgrad_x3_fn(int tile_id);
+void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
 
 // Conv math selection (scd_set_conv_math): SCD_MATH_X3 = split-bf16 MFMA where the shape allows it,
 // SCD_MATH_F32 = fp32 MFMA everywhere.  Initial value from SCD_CONV_MATH=f32|x3 (default x3).

@@ -558,6 +558,12 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
     a.M = int(M);
     a.div_hw = make_fastdiv(uint32_t(d->out_h * d->out_w));
     a.div_w = make_fastdiv(uint32_t(d->out_w));
+    a.wsplit = d->wsplit;
+    a.wplane = int64_t(a.n_out) * a.K;
+    if (d->wsplit && !aligned16(d->wsplit)) {
+        set_error("igemm: wsplit must be 16-byte aligned");
+        return SCD_ERR_ALIGN;
+    }
     hipStream_t s = as_stream(stream);
     if (conv_math_x3() && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");
     if (d->n_out >= 128)
@@ -614,26 +620,31 @@ static int wgrad_validate(const scd_wgrad_t *d) {
 }
 // Workgroups of one wgrad instantiation that the whole chip holds at once (occupancy API x CUs), cached.
 static int wgrad_resident_blocks(const WgradTile &t) {
-    static int cache[8] = {0};
-    if (cache[t.id] > 0) return cache[t.id];
+    const int x3 = conv_math_x3();
+    static int cache[2][8] = {{0}};
+    if (cache[x3][t.id] > 0) return cache[x3][t.id];
     int per_cu = 0, cus = 0, dev = 0;
     const void *fn = nullptr;
-    switch (t.id) {
-        case 0: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 2, 2, 2, 16>); break;
-        case 1: fn = reinterpret_cast<const void *>(&wgrad_f32<1, 4, 2, 2, 16>); break;
-        case 2: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 2, 1, 3, 16>); break;
-        case 3: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 1, 1, 3, 16>); break;
-        default: fn = reinterpret_cast<const void *>(&wgrad_f32<1, 4, 1, 1, 16>); break;
+    if (x3) {
+        fn = wgrad_x3_fn(t.id);
+    } else {
+        switch (t.id) {
+            case 0: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 2, 2, 2, 16>); break;
+            case 1: fn = reinterpret_cast<const void *>(&wgrad_f32<1, 4, 2, 2, 16>); break;
+            case 2: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 2, 1, 3, 16>); break;
+            case 3: fn = reinterpret_cast<const void *>(&wgrad_f32<2, 1, 1, 3, 16>); break;
+            default: fn = reinterpret_cast<const void *>(&wgrad_f32<1, 4, 1, 1, 16>); break;
+        }
     }
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, t.threads, 0) != hipSuccess || per_cu < 1 ||
         cus < 1) {
         (void)hipGetLastError();
-        return 3 * 256;  // MI355X: 256 CUs, 3 resident 256-thread blocks at ~140 VGPRs
+        return 2 * 256;  // MI355X: 256 CUs, >= 2 resident 256-thread blocks
     }
-    cache[t.id] = per_cu * cus;
-    return cache[t.id];
+    cache[x3][t.id] = per_cu * cus;
+    return cache[x3][t.id];
 }
 
 // Split-K factor: the block count tiles*nsplit is quantised against the chip's resident capacity so the
@@ -718,6 +729,10 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
     a.remap = xcd_remap_enabled();
     dim3 grid(a.grid_r * a.grid_j * ns);
     dim3 block(t.threads);
+    if (conv_math_x3()) {
+        launch_wgrad_x3(a, t.id, grid, block, s);
+        return launch_status("scd_conv_wgrad");
+    }
     switch (t.id) {
         case 0: hipLaunchKernelGGL((wgrad_f32<2, 2, 2, 2, 16>), grid, block, 0, s, a); break;
         case 1: hipLaunchKernelGGL((wgrad_f32<1, 4, 2, 2, 16>), grid, block, 0, s, a); break;

@@ -52,7 +52,8 @@ __device__ __forceinline__ void split3(const f32x4 v, u32x2 &h, u32x2 &m, u32x2 
     }
 }
 
-template <int WAVES_M, int WAVES_N, int TM, int TN>
+// PRE: B (weights) come pre-split in a.wsplit planes and are staged by copy (8 k per chunk, 3 x 16 B).
+template <int WAVES_M, int WAVES_N, int TM, int TN, bool PRE>
 __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
     constexpr int BK = 16;
     constexpr int NT = 64 * WAVES_M * WAVES_N;
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
     constexpr int ROWS = BM + BN;
     constexpr int KC = BK / 4;            // 4-float chunks per row and stage
     constexpr int A_CH = BM * KC;
-    constexpr int B_CH = BN * KC;
+    constexpr int B_CH = PRE ? BN * 2 : BN * KC;  // PRE: 8-k chunks
     constexpr int A_PER = (A_CH + NT - 1) / NT;
     constexpr int B_PER = (B_CH + NT - 1) / NT;
     constexpr int PLANE = ROWS * 32;      // bytes of one plane: ROWS x 16 bf16
@@ -114,11 +115,19 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
         const int row = ch / KC, col = ch % KC;
         b_in[i] = ch < B_CH;
         b_ok[i] = b_in[i] && (n0 + row < a.n_out);
-        b_row[i] = (n0 + row) * a.K + col * 4;
-        b_off[i] = soff(BM + row, col);
+        if (PRE) {
+            const int r8 = ch >> 1, half = ch & 1;
+            b_ok[i] = b_in[i] && (n0 + r8 < a.n_out);
+            b_row[i] = (n0 + r8) * a.K + half * 8;
+            b_off[i] = (BM + r8) * 32 + (((half ^ ((BM + r8) >> 3)) & 1) << 4);
+        } else {
+            b_row[i] = (n0 + row) * a.K + col * 4;
+            b_off[i] = soff(BM + row, col);
+        }
     }
 
     f32x4 ra[A_PER], rb[B_PER];
+    u32x4 pb[B_PER][3];
     const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
     auto load_stage = [&](int t, int c0) {
@@ -127,11 +136,23 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const bool v = unsigned(a_sy[i] + dyt) < unsigned(a.hs) && unsigned(a_sx[i] + dxt) < unsigned(a.ws);
-            ra[i] = v ? gload4(a_base[i] + toff) : zero4;
+            ra[i] = (v && !(a.dbg & 1)) ? gload4(a_base[i] + toff) : zero4;
         }
         const int k0 = t * a.c + c0;
+        if (a.dbg & 2) return;
+        if (PRE) {
+            const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int i = 0; i < B_PER; ++i) rb[i] = b_ok[i] ? gload4(a.w + size_t(b_row[i]) + k0) : zero4;
+            for (int i = 0; i < B_PER; ++i)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    pb[i][p] = b_ok[i] ? *(const __attribute__((address_space(1))) u32x4 *)(a.wsplit + p * a.wplane +
+                                                                                          size_t(b_row[i]) + k0)
+                                       : z;
+        } else {
+#pragma unroll
+            for (int i = 0; i < B_PER; ++i) rb[i] = b_ok[i] ? gload4(a.w + size_t(b_row[i]) + k0) : zero4;
+        }
     };
     auto store_stage = [&](int buf) {
         unsigned char *S = smem + buf * STAGE;
@@ -139,11 +160,26 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
         for (int i = 0; i < A_PER; ++i)
             if (tid + i * NT < A_CH) {
                 u32x2 h, m, l;
-                split3(ra[i], h, m, l);
+                if (a.dbg & 16) {
+                    h = __builtin_bit_cast(u32x2, ra[i].xy);
+                    m = __builtin_bit_cast(u32x2, ra[i].zw);
+                    l = h;
+                } else {
+                    split3(ra[i], h, m, l);
+                }
                 *reinterpret_cast<u32x2 *>(S + a_off[i]) = h;
                 *reinterpret_cast<u32x2 *>(S + PLANE + a_off[i]) = m;
                 *reinterpret_cast<u32x2 *>(S + 2 * PLANE + a_off[i]) = l;
             }
+        if (PRE) {
+#pragma unroll
+            for (int i = 0; i < B_PER; ++i)
+                if (b_in[i]) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4 *>(S + p * PLANE + b_off[i]) = pb[i][p];
+                }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
             if (b_in[i]) {
@@ -206,8 +242,10 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
         // small terms first: mm, hl, lh, hm, mh, hh
         constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
         constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
+        const int nq = (a.dbg & 8) ? 0 : ((a.dbg & 4) ? 1 : 6);
 #pragma unroll
         for (int q = 0; q < 6; ++q)
+            if (q >= 6 - nq)
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -259,7 +297,13 @@ static void launch_x3(const IgemmArgs &a, hipStream_t s) {
     b.grid_m = (a.M + BM - 1) / BM;
     b.grid_n = (a.n_out + BN - 1) / BN;
     b.remap = xcd_remap_enabled();
-    hipLaunchKernelGGL((igemm_x3<WM, WN, TM, TN>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN), 0, s, b);
+    const char *dbg = getenv("SCD_IGEMM_DBG");
+    b.dbg = dbg ? atoi(dbg) : 0;
+    const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
+    if (a.wsplit)
+        hipLaunchKernelGGL((igemm_x3<WM, WN, TM, TN, true>), grid, block, 0, s, b);
+    else
+        hipLaunchKernelGGL((igemm_x3<WM, WN, TM, TN, false>), grid, block, 0, s, b);
 }
 
 bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
@@ -273,4 +317,265 @@ bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
     return true;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Weight gradient, split-K over pixels (same decomposition as wgrad_f32):
+//   slab[s][r][j] = sum_{m in split s} P[m, r] * Q[src(m, t), c],  j = (t, c)
+// Both MFMA operands need 8 consecutive pixels (k) per lane, but global memory is pixel-major.  The
+// stage is therefore written as it arrives, as [16 px][W ch] bf16 planes, and each fragment is read
+// with two ds_read_b64_tr_b16 (hardware 4x16 transpose).
+// Row stride = 2W bytes padded to = 64 (mod 128), so the 4 rows a 16-lane group reads fall in four
+// different 64-byte bank groups: conflict-free per 32-lane half.
+// ------------------------------------------------------------------------------------------------
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s16x4 lds_tr16(const unsigned char *p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4 *)(reinterpret_cast<const __attribute__((address_space(3))) unsigned char *>(
+            reinterpret_cast<uintptr_t>(p))));
+}
+
+constexpr int tr_stride(int w) { return (2 * w) % 128 == 0 ? 2 * w + 64 : 2 * w; }
+
+template <int WAVES_M, int WAVES_N, int TM, int TN>
+__global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
+    constexpr int BK = 16;
+    constexpr int NT = 64 * WAVES_M * WAVES_N;
+    constexpr int BM = WAVES_M * TM * 32;
+    constexpr int BN = WAVES_N * TN * 32;
+    constexpr int AQ = BM / 4, BQ = BN / 4;
+    constexpr int A_CH = BK * AQ, B_CH = BK * BQ;
+    constexpr int A_PER = (A_CH + NT - 1) / NT;
+    constexpr int B_PER = (B_CH + NT - 1) / NT;
+    constexpr int RSA = tr_stride(BM), RSB = tr_stride(BN);
+    constexpr int PA = BK * RSA, PB = BK * RSB;  // plane bytes
+    constexpr int STAGE = 3 * (PA + PB);
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid % WAVES_M;
+    const int wn = wid / WAVES_M;
+    const uint32_t per_split = uint32_t(a.grid_r * a.grid_j);
+    const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int split = int(L / per_split);
+    const int rem = int(L - uint32_t(split) * per_split);
+    const int jt = rem / a.grid_r;
+    const int r0 = (rem - jt * a.grid_r) * BM;
+    const int j0 = jt * BN;
+    const int kbeg = split * a.kchunk;
+    const int kend = min(a.M, kbeg + a.kchunk);
+
+    int a_k[A_PER], a_r[A_PER], a_off[A_PER];
+    bool a_in[A_PER], a_ok[A_PER];
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+        const int ch = tid + i * NT;
+        a_in[i] = ch < A_CH;
+        a_k[i] = ch / AQ;
+        const int q = ch % AQ;
+        a_r[i] = r0 + q * 4;
+        a_ok[i] = a_in[i] && a_r[i] < a.R;
+        a_off[i] = a_k[i] * RSA + q * 8;
+    }
+    int b_k[B_PER], b_dy[B_PER], b_dx[B_PER], b_c[B_PER], b_off[B_PER];
+    int b_img[B_PER], b_oy[B_PER], b_ox[B_PER];
+    bool b_in[B_PER], b_ok[B_PER];
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+        const int ch = tid + i * NT;
+        b_in[i] = ch < B_CH;
+        b_k[i] = ch / BQ;
+        const int q = ch % BQ;
+        const int j = j0 + q * 4;
+        b_ok[i] = b_in[i] && j < a.Ng;
+        const int t = b_ok[i] ? int(fdiv(uint32_t(j), a.div_c)) : 0;
+        b_c[i] = j - t * a.C;
+        b_dy[i] = tap_at(a.tdy, t);
+        b_dx[i] = tap_at(a.tdx, t);
+        const uint32_t mm = uint32_t(min(kbeg + b_k[i], a.M - 1));
+        const uint32_t img = fdiv(mm, a.div_hw);
+        const uint32_t rr = mm - img * uint32_t(a.ho * a.wo);
+        const uint32_t oy = fdiv(rr, a.div_w);
+        b_img[i] = int(img);
+        b_oy[i] = int(oy);
+        b_ox[i] = int(rr - oy * uint32_t(a.wo));
+        b_off[i] = 3 * PA + b_k[i] * RSB + q * 8;
+    }
+
+    f32x4 ra[A_PER], rb[B_PER];
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    auto load_stage = [&](int kb) {
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            const int m = kb + a_k[i];
+            ra[i] = (a_ok[i] && m < kend) ? gload4(a.rows + size_t(m) * a.ldc_r + a_r[i]) : zero4;
+        }
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            const int sy = b_oy[i] * a.stride + b_dy[i];
+            const int sx = b_ox[i] * a.stride + b_dx[i];
+            const bool v = b_ok[i] && (kb + b_k[i] < kend) && unsigned(sy) < unsigned(a.hs) &&
+                           unsigned(sx) < unsigned(a.ws);
+            rb[i] = v ? gload4(a.src + (size_t(b_img[i] * a.hs + sy) * a.ws + sx) * a.ldc_s + b_c[i]) : zero4;
+        }
+    };
+    auto advance = [&]() {
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            int ox = b_ox[i] + BK, oy = b_oy[i], img = b_img[i];
+            while (ox >= a.wo) {
+                ox -= a.wo;
+                if (++oy == a.ho) {
+                    oy = 0;
+                    ++img;
+                }
+            }
+            b_ox[i] = ox;
+            b_oy[i] = oy;
+            b_img[i] = img;
+        }
+    };
+    auto store_stage = [&](int buf) {
+        unsigned char *S = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i)
+            if (a_in[i]) {
+                u32x2 h, m, l;
+                split3(ra[i], h, m, l);
+                *reinterpret_cast<u32x2 *>(S + a_off[i]) = h;
+                *reinterpret_cast<u32x2 *>(S + PA + a_off[i]) = m;
+                *reinterpret_cast<u32x2 *>(S + 2 * PA + a_off[i]) = l;
+            }
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i)
+            if (b_in[i]) {
+                u32x2 h, m, l;
+                split3(rb[i], h, m, l);
+                *reinterpret_cast<u32x2 *>(S + b_off[i]) = h;
+                *reinterpret_cast<u32x2 *>(S + PB + b_off[i]) = m;
+                *reinterpret_cast<u32x2 *>(S + 2 * PB + b_off[i]) = l;
+            }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // transposed-read addresses: 16-lane group g reads rows k0 = 8*(g>>1) (+4), columns 16*(g&1) + 4*(w&3)
+    const int g = lane >> 4, w = lane & 15;
+    const int trk = 8 * (g >> 1) + (w >> 2);
+    const int trc = 16 * (g & 1) + 4 * (w & 3);
+    int a_rd[TM], b_rd[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a_rd[i] = trk * RSA + (wm * TM * 32 + i * 32 + trc) * 2;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b_rd[j] = 3 * PA + trk * RSB + (wn * TN * 32 + j * 32 + trc) * 2;
+
+    const int nsteps = (kend > kbeg) ? (kend - kbeg + BK - 1) / BK : 0;
+    if (nsteps > 0) {
+        load_stage(kbeg);
+        store_stage(0);
+        __syncthreads();
+        for (int s = 0; s < nsteps; ++s) {
+            const bool more = s + 1 < nsteps;
+            if (more) {
+                advance();
+                load_stage(kbeg + (s + 1) * BK);
+            }
+            const unsigned char *S = smem + (s & 1) * STAGE;
+            bf16x8 av[3][TM], bv[3][TN];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const s16x4 lo = lds_tr16(S + p * PA + a_rd[i]);
+                    const s16x4 hi = lds_tr16(S + p * PA + a_rd[i] + 4 * RSA);
+                    av[p][i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const s16x4 lo = lds_tr16(S + p * PB + b_rd[j]);
+                    const s16x4 hi = lds_tr16(S + p * PB + b_rd[j] + 4 * RSB);
+                    bv[p][j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+                }
+            }
+            constexpr int QA[6] = {1, 0, 2, 0, 1, 0};
+            constexpr int QB[6] = {1, 2, 0, 1, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[QA[q]][i], bv[QB[q]][j], acc[i][j], 0, 0, 0);
+            if (more) store_stage((s + 1) & 1);
+            __syncthreads();
+        }
+    }
+
+    float *slab = a.slabs + size_t(split) * a.R * a.Ng;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = j0 + wn * TN * 32 + j * 32 + (lane & 31);
+        if (col >= a.Ng) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = r0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (row < a.R) gstore1(slab + size_t(row) * a.Ng + col, acc[i][j][r]);
+            }
+    }
+}
+
+const void *wgrad_x3_fn(int tile_id) {
+    switch (tile_id) {
+        case 0: return reinterpret_cast<const void *>(&wgrad_x3<2, 2, 2, 2>);
+        case 1: return reinterpret_cast<const void *>(&wgrad_x3<1, 4, 2, 2>);
+        case 2: return reinterpret_cast<const void *>(&wgrad_x3<2, 2, 1, 3>);
+        case 3: return reinterpret_cast<const void *>(&wgrad_x3<2, 1, 1, 3>);
+        default: return reinterpret_cast<const void *>(&wgrad_x3<1, 4, 1, 1>);
+    }
+}
+
+void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s) {
+    switch (tile_id) {
+        case 0: hipLaunchKernelGGL((wgrad_x3<2, 2, 2, 2>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((wgrad_x3<1, 4, 2, 2>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((wgrad_x3<2, 2, 1, 3>), grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((wgrad_x3<2, 1, 1, 3>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((wgrad_x3<1, 4, 1, 1>), grid, block, 0, s, a); break;
+    }
+}
+
+__global__ void split_bf16x3_kernel(const float *__restrict__ src, int64_t n4, uint16_t *__restrict__ dst, int64_t n) {
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < n4; e += int64_t(gridDim.x) * blockDim.x) {
+        u32x2 h, m, l;
+        split3(gload4(src + 4 * e), h, m, l);
+        *reinterpret_cast<u32x2 *>(dst + 4 * e) = h;
+        *reinterpret_cast<u32x2 *>(dst + n + 4 * e) = m;
+        *reinterpret_cast<u32x2 *>(dst + 2 * n + 4 * e) = l;
+    }
+}
+
 }  // namespace scd
+
+using namespace scd;
+
+extern "C" int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream) {
+    clear_error();
+    if (!src || !dst || n <= 0 || (n & 7) || !aligned16(src) || !aligned16(dst)) {
+        set_error("split_bf16x3: need n %% 8 == 0 and 16-byte aligned src/dst (n=%lld)", (long long)n);
+        return SCD_ERR_ARG;
+    }
+    const int64_t n4 = n / 4;
+    int64_t blocks = (n4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(split_bf16x3_kernel, dim3(unsigned(blocks)), dim3(256), 0, as_stream(stream), src, n4, dst, n);
+    return launch_status("scd_split_bf16x3");
+}

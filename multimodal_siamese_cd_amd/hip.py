@@ -35,6 +35,7 @@ class IGEMM(ctypes.Structure):
         ("bias", c_void_p),
         ("dst", NHWC),
         ("store_mode", c_int32),
+        ("wsplit", c_void_p),
     ]
 
 
@@ -67,6 +68,7 @@ _SIGS = {
     "scd_pack_conv3x3": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_set_conv_math": ([c_int32], c_int),
+    "scd_split_bf16x3": ([c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
     "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
     "scd_conv_wgrad": ([POINTER(WGRAD), c_void_p, c_size_t, c_void_p], c_int),
@@ -197,7 +199,7 @@ def pack_conv3x3(w: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch
     out = torch.empty((co * 9 * ci_pad) if mode == 0 else (ci * 9 * co), device=w.device, dtype=torch.float32)
     _check(lib().scd_pack_conv3x3(w.contiguous().data_ptr(), co, ci, ci_pad, mode, out.data_ptr(), _stream()),
            "scd_pack_conv3x3")
-    return out
+    return _attach_split(out)
 
 
 def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:
@@ -205,7 +207,22 @@ def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:
     out = torch.empty(ci * co * 4, device=w.device, dtype=torch.float32)
     _check(lib().scd_pack_convT2x2(w.contiguous().data_ptr(), ci, co, mode, out.data_ptr(), _stream()),
            "scd_pack_convT2x2")
-    return out
+    return _attach_split(out)
+
+
+def split_bf16x3(src: torch.Tensor) -> torch.Tensor:
+    """Exact 3-way bf16 split of an fp32 tensor: int16 planes [3][numel] (bit patterns of h, m, l)."""
+    n = src.numel()
+    dst = torch.empty(3 * n, dtype=torch.int16, device=src.device)
+    _check(lib().scd_split_bf16x3(src.data_ptr(), n, dst.data_ptr(), _stream()), "scd_split_bf16x3")
+    return dst
+
+
+def _attach_split(wpk: torch.Tensor) -> torch.Tensor:
+    """Under the x3 conv math, pre-split packed weights once so every workgroup stages them by copy."""
+    if wpk.numel() % 8 == 0 and conv_math() == 'x3':
+        wpk._x3 = split_bf16x3(wpk)
+    return wpk
 
 
 MATH_F32, MATH_X3 = 0, 1
@@ -229,7 +246,8 @@ def conv_math() -> str:
 def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
                bias, dst: NHWC, store_mode: int = 0):
     nt, dy, dx = _taps(taps)
-    d = IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode)
+    d = IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
+              _ptr(getattr(wpk, '_x3', None)))
     _check(lib().scd_conv_igemm(ctypes.byref(d), _stream()), "scd_conv_igemm")
 
 

@@ -55,6 +55,36 @@ def test_struct_layout_matches_header(lib):
     assert hip.WGRAD.src.offset == 32 and hip.WGRAD.dx.offset == 81
 
 
+def test_struct_layout_matches_c_compiler(tmp_path):
+    """Compile include/scd.h with the host C compiler and compare every descriptor offset with ctypes."""
+    import shutil
+    import subprocess
+    from multimodal_siamese_cd_amd import hip
+    cc = shutil.which('gcc') or shutil.which('cc')
+    if cc is None:
+        pytest.skip('no host C compiler')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fields = {'scd_nhwc_t': (hip.NHWC, ['data', 'n', 'h', 'w', 'c', 'ldc']),
+              'scd_igemm_t': (hip.IGEMM, [f[0] for f in hip.IGEMM._fields_]),
+              'scd_wgrad_t': (hip.WGRAD, [f[0] for f in hip.WGRAD._fields_])}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "scd.h"', 'int main(void) {']
+    for ctype, (_, names) in fields.items():
+        lines.append(f'printf("{ctype} size %zu\\n", sizeof({ctype}));')
+        for nm in names:
+            lines.append(f'printf("{ctype} {nm} %zu\\n", offsetof({ctype}, {nm}));')
+    lines += ['return 0;', '}']
+    src = tmp_path / 'layout.c'
+    src.write_text('\n'.join(lines))
+    exe = tmp_path / 'layout'
+    subprocess.run([cc, '-I', os.path.join(root, 'include'), str(src), '-o', str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split('\n')
+    got = {(a, b): int(c) for a, b, c in (ln.split() for ln in out if ln)}
+    for ctype, (cls, names) in fields.items():
+        assert got[(ctype, 'size')] == ctypes.sizeof(cls), ctype
+        for nm in names:
+            assert got[(ctype, nm)] == getattr(cls, nm).offset, (ctype, nm)
+
+
 def test_product_path_refuses_cpu_tensors(lib):
     import torch
     from multimodal_siamese_cd_amd import engine

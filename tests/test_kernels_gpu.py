@@ -134,14 +134,46 @@ def test_conv_math_accuracy_vs_fp64(dev, ci, co):
     x, wt = x.float(), wt.float()
     ref = nhwc_t(F.conv2d(nchw(x).double(), wt.double(), None, padding=1))
     errs = {}
-    for m in ('f32', 'x3'):
-        prev = hip.set_conv_math(m)
+    for m in ('f32', 'x3', 'x3-onthefly'):
+        prev = hip.set_conv_math(m.split('-')[0])
         y = torch.empty(n, h, w, co, device=dev)
-        hip.conv_igemm(hip.nhwc(x.to(dev)), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wt.to(dev), 0), co, None,
-                       hip.nhwc(y))
+        wpk = hip.pack_conv3x3(wt.to(dev), 0)
+        if m == 'x3-onthefly':  # weights split inside every workgroup instead of pre-split planes
+            del wpk._x3
+        hip.conv_igemm(hip.nhwc(x.to(dev)), h, w, 1, hip.TAPS_3X3, wpk, co, None, hip.nhwc(y))
         hip.set_conv_math(prev)
         errs[m] = rel(y, ref)
-    assert errs['f32'] < 1e-5 and errs['x3'] < 1e-5, errs
+    assert max(errs.values()) < 1e-5, errs
+    assert errs['x3'] <= 2 * errs['f32'] + 1e-7, errs
+    assert errs['x3-onthefly'] <= 2 * errs['f32'] + 1e-7, errs
+
+
+@pytest.mark.parametrize('ci,co', [(64, 64), (128, 256), (8, 64)])
+def test_wgrad_math_accuracy_vs_fp64(dev, ci, co):
+    """Weight gradient under both arithmetics against fp64, on wide-dynamic-range data.
+
+    Pixels are the K dimension here (long sums), so this also exercises the split-K slab reduction.
+    """
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(5 * ci + co)
+    n, h, w = 4, 40, 36
+    x = (torch.randn(n, h, w, ci, generator=g, dtype=torch.float64)
+         * 10 ** (4 * torch.rand(n, h, w, ci, generator=g, dtype=torch.float64) - 2)).float()
+    dy = (torch.randn(n, h, w, co, generator=g, dtype=torch.float64)
+          * 10 ** (4 * torch.rand(n, h, w, co, generator=g, dtype=torch.float64) - 2)).float()
+    ref = torch.nn.grad.conv2d_weight(nchw(x).double(), (co, ci, 3, 3), nchw(dy).double(), padding=1)
+    errs = {}
+    for m in ('f32', 'x3'):
+        prev = hip.set_conv_math(m)
+        xd, dyd = x.to(dev), dy.to(dev)
+        d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dyd), hip.nhwc(xd), 1, hip.TAPS_3X3)
+        slabs = torch.empty(nbytes // 4, device=dev)
+        hip.conv_wgrad(d, slabs)
+        dw = torch.empty(co, ci, 3, 3, device=dev)
+        hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
+        hip.set_conv_math(prev)
+        errs[m] = rel(dw, ref)
+    assert max(errs.values()) < 1e-5, errs
     assert errs['x3'] <= 2 * errs['f32'] + 1e-7, errs
 
 
