@@ -8,9 +8,12 @@ on synthetic 256x256 SAR(2)+optical(3) pairs generated on the device (weak scali
 own batch).  Rank 0 prints ONE JSON line; `value` is pairs/s of the whole job (all ranks' pairs / max rank time).
 
 Measurement extras (rank 0, after the timed region):
-  roofline      the MFMA conv kernels (igemm_f32 + wgrad_f32, every conv launch of one step) bracketed by
-                HIP events on the launch stream: algorithmic conv FLOPs per step / summed kernel time vs the
-                gfx950 fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
+  roofline      the MFMA conv kernels (every conv launch of one step) bracketed by HIP events on the launch
+                stream: algorithmic conv FLOPs per step / summed kernel time.  The peak is each launch's own
+                matrix-core ceiling, combined as flops / sum(flops_i / peak_i):
+                  - fp32 MFMA: 157.3 TFLOP/s;
+                  - split-bf16 x3: bf16 dense 2516.6 / 6 products = 419.4 fp32-equivalent TFLOP/s
+                    (MI355X_MICROARCH.md).
   cpu_baseline  the CPU oracle (oracle/siamese_oracle.py, torch fp32 on host cores) running the same training
                 step on a bounded sample (bs=2, 256x256).
 """
@@ -31,6 +34,8 @@ from multimodal_siamese_cd_amd import engine, hip, parallel  # noqa: E402
 from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_functions, networks  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3
+BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # dense, MI355X_MICROARCH.md (1/16 ratio)
+X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6           # six bf16 products per fp32 multiply-add
 METRIC = "image-pairs/sec training step, 256×256 SAR+optical Siamese U-Net, 1/2/4/8 MI355X"
 
 
@@ -68,28 +73,32 @@ class KernelTimer:
         self.active = False
         self._igemm = hip.conv_igemm
         self._wgrad = hip.conv_wgrad
+        self.math = hip.conv_math()
 
     def install(self):
         timer = self
 
-        def igemm(*a, **k):
+        def igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k):
             if not timer.active:
-                return timer._igemm(*a, **k)
+                return timer._igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            r = timer._igemm(*a, **k)
+            r = timer._igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k)
             e.record()
-            timer.events.append(('igemm', s, e))
+            flops = 2.0 * src.n * out_h * out_w * n_out * len(taps[0]) * src.c
+            x3 = timer.math == 'x3' and src.c % 16 == 0  # the library's x3 eligibility rule (conv_x3.hip)
+            timer.events.append(('igemm', s, e, flops, x3))
             return r
 
-        def wgrad(*a, **k):
+        def wgrad(d, slabs):
             if not timer.active:
-                return timer._wgrad(*a, **k)
+                return timer._wgrad(d, slabs)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            r = timer._wgrad(*a, **k)
+            r = timer._wgrad(d, slabs)
             e.record()
-            timer.events.append(('wgrad', s, e))
+            flops = 2.0 * d.rows.n * d.rows.h * d.rows.w * d.rows.c * d.ntaps * d.src.c
+            timer.events.append(('wgrad', s, e, flops, timer.math == 'x3'))
             return r
 
         hip.conv_igemm = igemm
@@ -98,10 +107,17 @@ class KernelTimer:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, s, e in self.events:
+        for name, s, e, _, _ in self.events:
             n, t = out.get(name, (0, 0.0))
             out[name] = (n + 1, t + s.elapsed_time(e))
         return out
+
+    def peak(self):
+        """Harmonic flop-weighted matrix-core peak of the timed launches (TFLOP/s)."""
+        f = sum(ev[3] for ev in self.events)
+        t = sum(ev[3] / ((X3_PEAK_TFLOPS if ev[4] else FP32_MFMA_PEAK_TFLOPS) * 1e12) for ev in self.events)
+        x3_share = sum(ev[3] for ev in self.events if ev[4]) / f
+        return f / t / 1e12, x3_share
 
 
 def cpu_baseline(cfg, steps: int = 2, batch: int = 2, size: int = 256):
@@ -240,10 +256,15 @@ def main():
                        "by_family": {k: round(v) for k, v in tr['per_step_bytes'].items() if k != 'total'},
                        "source": f"profiles/{pmc[-1]}: {tr['source']}; L2-miss fabric bytes (Infinity-Cache "
                                  "hits included, MI355X_MICROARCH.md HBM)"}
+        peak, x3_share = timer.peak()
         result["roofline"] = {
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-            "kernel": "igemm_f32 + wgrad_f32 (all conv launches of one training step: 3x3 fwd/dgrad/wgrad, "
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "peak_basis": f"conv math {timer.math}: {x3_share:.3f} of executed conv FLOPs on split-bf16 x3 "
+                          f"(peak {X3_PEAK_TFLOPS:.1f} = bf16 dense {BF16_MFMA_PEAK_TFLOPS:.1f} / 6 products), the rest "
+                          f"on fp32 MFMA ({FP32_MFMA_PEAK_TFLOPS}); combined flop-weighted harmonically",
+            "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "kernel": "igemm + wgrad (all conv launches of one training step: 3x3 fwd/dgrad/wgrad, "
                       "ConvT fwd/dgrad/wgrad)",
             "flop_per_step": f3 + fT,
             "kernel_ms_per_step": round(t_ms, 3),

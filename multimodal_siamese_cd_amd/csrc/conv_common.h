@@ -60,6 +60,16 @@ inline int xcd_remap_enabled() {
     return v;
 }
 
+// Halo-tiled igemm for 3x3 convs (x3 math); SCD_HALO=0 disables it (A/B experiments).
+inline int halo_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("SCD_HALO");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v;
+}
+
 inline uint64_t pack_taps(const int8_t *v, int n) {
     uint64_t p = 0;
     for (int i = 0; i < n; ++i) p |= uint64_t(uint8_t(v[i]) & 15u) << (4 * i);

@@ -306,8 +306,253 @@ static void launch_x3(const IgemmArgs &a, hipStream_t s) {
         hipLaunchKernelGGL((igemm_x3<WM, WN, TM, TN, false>), grid, block, 0, s, b);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Halo-tiled 3x3 igemm (stride 1, "same" padding).  A block owns a TR x TW patch of output pixels of one
+// image and BN output channels.  For every 16-channel chunk it stages the (TR+2) x (TW+2) input halo
+// once, split into its three bf16 planes, and serves all 9 taps from LDS by shifting the row index.  The
+// per-tap path above re-loads and re-splits every input element 9 times.
+// B (pre-split weight planes) is streamed per (chunk, tap), double-buffered.  A is single-buffered: the
+// next chunk's halo is loaded into registers at tap 0 and written behind an extra barrier after tap 8.
+// ------------------------------------------------------------------------------------------------
+template <int WAVES_M, int WAVES_N, int TM, int TN, int TW>
+__global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_halo_x3(IgemmArgs a) {
+    constexpr int NT = 64 * WAVES_M * WAVES_N;
+    constexpr int BM = WAVES_M * TM * 32;
+    constexpr int BN = WAVES_N * TN * 32;
+    constexpr int TR = BM / TW;
+    constexpr int HWD = TW + 2;
+    constexpr int HR = (TR + 2) * HWD;
+    constexpr int A_CH = HR * 4;
+    constexpr int A_PER = (A_CH + NT - 1) / NT;
+    constexpr int B_CH = BN * 2;
+    constexpr int B_PER = (B_CH + NT - 1) / NT;
+    constexpr int PA = HR * 32;
+    constexpr int PB = BN * 32;
+    constexpr int A_BYTES = 3 * PA;
+    constexpr int B_STAGE = 3 * PB;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[A_BYTES + 2 * B_STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid % WAVES_M;
+    const int wn = wid / WAVES_M;
+    int mt, nt;
+    if (a.remap) {
+        const uint32_t L = xcd_swizzle(blockIdx.x, uint32_t(a.grid_m * a.grid_n));
+        mt = int(L / uint32_t(a.grid_n));
+        nt = int(L - uint32_t(mt) * uint32_t(a.grid_n));
+    } else {
+        mt = int(blockIdx.x % uint32_t(a.grid_m));
+        nt = int(blockIdx.x / uint32_t(a.grid_m));
+    }
+    const int tiles_x = a.wo / TW, tiles_y = a.ho / TR;
+    const int img = mt / (tiles_x * tiles_y);
+    const int trem = mt - img * tiles_x * tiles_y;
+    const int ty = trem / tiles_x;
+    const int y0 = ty * TR, x0 = (trem - ty * tiles_x) * TW;
+    const int n0 = nt * BN;
+
+    auto soff = [](int row, int col) { return row * 32 + ((((col >> 1) ^ (row >> 3)) & 1) << 4) + ((col & 1) << 3); };
+
+    const float *a_ptr[A_PER];
+    int a_off[A_PER];
+    bool a_ok[A_PER], a_in[A_PER];
+#pragma unroll
+    for (int i = 0; i < A_PER; ++i) {
+        const int e = tid + i * NT;
+        a_in[i] = e < A_CH;
+        const int hp = a_in[i] ? (e >> 2) : 0, col = e & 3;
+        const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
+        const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
+        a_ok[i] = a_in[i] && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+        a_ptr[i] = a.src + (a_ok[i] ? (size_t(img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4 : 0);
+        a_off[i] = soff(hp, col);
+    }
+    int b_row[B_PER], b_off[B_PER];
+    bool b_ok[B_PER], b_in[B_PER];
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+        const int e = tid + i * NT;
+        const int r8 = e >> 1, half = e & 1;
+        b_in[i] = e < B_CH;
+        b_ok[i] = b_in[i] && (n0 + r8 < a.n_out);
+        b_row[i] = (n0 + r8) * a.K + half * 8;
+        b_off[i] = r8 * 32 + (((half ^ (r8 >> 3)) & 1) << 4);
+    }
+
+    f32x4 ra[A_PER];
+    u32x4 pb[B_PER][3];
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    auto load_A = [&](int cc) {
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) ra[i] = a_ok[i] ? gload4(a_ptr[i] + cc * 16) : zero4;
+    };
+    auto load_B = [&](int cc, int t) {
+        const int k0 = t * a.c + cc * 16;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                pb[i][p] = b_ok[i] ? *(const __attribute__((address_space(1))) u32x4 *)(a.wsplit + p * a.wplane +
+                                                                                      size_t(b_row[i]) + k0)
+                                   : z;
+    };
+    auto store_A = [&]() {
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i)
+            if (a_in[i]) {
+                u32x2 h, m, l;
+                split3(ra[i], h, m, l);
+                *reinterpret_cast<u32x2 *>(smem + a_off[i]) = h;
+                *reinterpret_cast<u32x2 *>(smem + PA + a_off[i]) = m;
+                *reinterpret_cast<u32x2 *>(smem + 2 * PA + a_off[i]) = l;
+            }
+    };
+    auto store_B = [&](int buf) {
+        unsigned char *S = smem + A_BYTES + buf * B_STAGE;
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i)
+            if (b_in[i]) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4 *>(S + p * PB + b_off[i]) = pb[i][p];
+            }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int h = lane >> 5;
+    int a_hr[TM], b_rd[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int p = wm * TM * 32 + i * 32 + (lane & 31);
+        a_hr[i] = (p / TW + 1) * HWD + (p % TW) + 1;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int row = wn * TN * 32 + j * 32 + (lane & 31);
+        b_rd[j] = row * 32 + (((h ^ (row >> 3)) & 1) << 4);
+    }
+
+    const int nc = a.c / 16;
+    const int nsteps = nc * a.ntaps;
+    load_A(0);
+    load_B(0, 0);
+    store_A();
+    store_B(0);
+    __syncthreads();
+    int cc = 0, t = 0;
+    for (int s = 0; s < nsteps; ++s) {
+        int t1 = t + 1, cc1 = cc;
+        if (t1 == a.ntaps) {
+            t1 = 0;
+            cc1 = cc + 1;
+        }
+        const bool more = s + 1 < nsteps;
+        if (t == 0 && cc + 1 < nc) load_A(cc + 1);
+        if (more) load_B(cc1, t1);
+        const unsigned char *SB = smem + A_BYTES + (s & 1) * B_STAGE;
+        const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
+        bf16x8 av[3][TM], bv[3][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int hr = a_hr[i] + toff;
+            const int ad = hr * 32 + (((h ^ (hr >> 3)) & 1) << 4);
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                av[p][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(smem + p * PA + ad));
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bv[p][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(SB + p * PB + b_rd[j]));
+        constexpr int QA[6] = {1, 0, 2, 0, 1, 0};
+        constexpr int QB[6] = {1, 2, 0, 1, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[QA[q]][i], bv[QB[q]][j], acc[i][j], 0, 0, 0);
+        if (more) {
+            if (t1 == 0) {  // every wave is done with chunk cc's halo: overwrite it with chunk cc+1
+                __syncthreads();
+                store_A();
+            }
+            store_B((s + 1) & 1);
+        }
+        __syncthreads();
+        t = t1;
+        cc = cc1;
+    }
+
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
+        if (n >= a.n_out) continue;
+        const float bias = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int p = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+                gstore1(a.dst + pix * a.ldc_d + n, acc[i][j][r] + bias);
+            }
+    }
+}
+
+template <int WM, int WN, int TM, int TN>
+static bool launch_halo(const IgemmArgs &a, hipStream_t s) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    int tw = 0;
+    for (int cand : {64, 32, 16})
+        if (a.wo % cand == 0 && a.ho % (BM / cand) == 0) {
+            tw = cand;
+            break;
+        }
+    if (!tw) return false;
+    IgemmArgs b = a;
+    b.grid_m = a.n_img * (a.ho / (BM / tw)) * (a.wo / tw);
+    b.grid_n = (a.n_out + BN - 1) / BN;
+    b.remap = xcd_remap_enabled();
+    const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
+    if (tw == 64)
+        hipLaunchKernelGGL((igemm_halo_x3<WM, WN, TM, TN, 64>), grid, block, 0, s, b);
+    else if (tw == 32)
+        hipLaunchKernelGGL((igemm_halo_x3<WM, WN, TM, TN, 32>), grid, block, 0, s, b);
+    else
+        hipLaunchKernelGGL((igemm_halo_x3<WM, WN, TM, TN, 16>), grid, block, 0, s, b);
+    return true;
+}
+
+// 3x3 / stride 1 / same-size convs with pre-split weights take the halo path.
+static bool halo_eligible(const IgemmArgs &a) {
+    if (!a.wsplit || a.store_mode != 0 || a.stride != 1 || a.ntaps != 9 || a.ho != a.hs || a.wo != a.ws) return false;
+    for (int t = 0; t < 9; ++t) {
+        const int dy = int((a.tdy >> (4 * t)) & 15ull), dx = int((a.tdx >> (4 * t)) & 15ull);
+        const int sdy = dy >= 8 ? dy - 16 : dy, sdx = dx >= 8 ? dx - 16 : dx;
+        if (sdy < -1 || sdy > 1 || sdx < -1 || sdx > 1) return false;
+    }
+    return halo_enabled();
+}
+
 bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
     if (a.c % 16) return false;
+    if (halo_eligible(a)) {
+        if (a.n_out >= 128 && launch_halo<2, 2, 2, 2>(a, s)) return true;
+        if (a.n_out >= 64 && a.n_out < 128 && launch_halo<4, 1, 2, 2>(a, s)) return true;
+        if (a.n_out < 64 && launch_halo<4, 1, 2, 1>(a, s)) return true;
+    }
     if (a.n_out >= 128)
         launch_x3<2, 2, 2, 2>(a, s);  // 128 x 128
     else if (a.n_out >= 64)
