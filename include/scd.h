@@ -119,9 +119,17 @@ typedef struct scd_igemm {
      * The weights are then staged by copy instead of being split in every workgroup.  NULL = split on
      * the fly.  Must describe the same values as wpk. */
     const uint16_t *wsplit;
+    /* Optional fused BatchNorm statistics of the stored output (bias included): per output tile of
+     * `tile_pixels` pixels (one image's rows) and channel, {mean, M2} -> stat_rec[tile][n_out][2], tiles in
+     * image-major order.  Only when scd_igemm_stat_tiles() reports > 0 tiles for this descriptor; NULL = off.
+     * replaces: the batch-statistics pass of aten::native_batch_norm (networks.py:393,396). */
+    float *stat_rec;
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);
+/* Number of statistic tiles scd_conv_igemm would write for `d` (0: no fused statistics for this shape or
+ * arithmetic, use scd_bn_train_stats); *tile_pixels receives the pixels per tile. */
+int scd_igemm_stat_tiles(const scd_igemm_t *d, int32_t *tile_pixels);
 
 /* ---------------------------------------------------------------------------------------------
  * Weight gradient (split-K implicit GEMM on MFMA), deterministic two-stage reduction.
@@ -166,6 +174,13 @@ int scd_bn_train_stats(scd_nhwc_t y, int32_t nseg, const float *gamma, const flo
                        float momentum, int32_t update_running, float *running_mean, float *running_var,
                        float *save_mean, float *save_invstd, float *scale, float *shift, void *ws,
                        size_t ws_bytes, scd_stream_t stream);
+/* Same outputs as scd_bn_train_stats, from the conv-fused tile records of scd_conv_igemm (stat_rec):
+ * ntiles tiles of tile_pixels pixels each, image-major, split evenly into nseg segments. */
+size_t scd_bn_tile_stats_workspace_bytes(int32_t ntiles, int32_t c, int32_t nseg);
+int scd_bn_stats_from_tiles(const float *tile_rec, int32_t ntiles, int32_t tile_pixels, int32_t c, int32_t nseg,
+                            const float *gamma, const float *beta, float eps, float momentum, int32_t update_running,
+                            float *running_mean, float *running_var, float *save_mean, float *save_invstd,
+                            float *scale, float *shift, void *ws, size_t ws_bytes, scd_stream_t stream);
 /* Eval: scale/shift [C] from running statistics. */
 int scd_bn_eval_coeffs(int32_t c, const float *gamma, const float *beta, const float *running_mean,
                        const float *running_var, float eps, float *scale, float *shift, scd_stream_t stream);

@@ -4,7 +4,7 @@
 // reference's `Conv2d -> BatchNorm2d -> ReLU(inplace)` pairs (utils/networks.py:392-397).
 //
 // Reductions are two-stage and deterministic:
-//   partial  : one workgroup per (segment, 4096-pixel chunk, channel group); every thread owns one channel
+//   partial  : one workgroup per (segment, pixel chunk, channel group); every thread owns one channel
 //              quad (float4) and walks pixels with 4 independent 16-byte loads in flight; forward stats use
 //              shifted sums (shift = the chunk's first value of the channel) turned into (n, mean, M2) and
 //              Chan-merged in LDS, so there is no E[x^2]-E[x]^2 cancellation.  Records are written
@@ -15,26 +15,35 @@
 namespace scd {
 
 constexpr int BN_THREADS = 256;
-constexpr int BN_CHUNK = 4096;  // pixels per reduction chunk
+constexpr int BN_CHUNK_MAX = 4096;  // pixels per reduction chunk (large maps)
+constexpr int BN_CHUNK_MIN = 64;
+constexpr int BN_TARGET_BLOCKS = 2048;  // 8 workgroups per CU
 
 struct BnGeom {
     int64_t pseg;  // pixels per segment
+    int chunk;     // pixels per chunk
     int ncps;      // chunks per segment
     int nrec;      // nseg * ncps
     int qpb;       // channel quads per block (power of two)
     int cgroups;   // channel groups (grid.y)
 };
 
+// The chunk shrinks (power of two, >= 64 px) until the grid fills the chip: deep 16x16..64x64 maps
+// otherwise launch a few dozen workgroups that each walk thousands of pixels serially.
 static BnGeom bn_geom(const scd_nhwc_t &y, int nseg) {
     BnGeom g;
     g.pseg = pixels(y) / nseg;
-    g.ncps = int((g.pseg + BN_CHUNK - 1) / BN_CHUNK);
-    g.nrec = nseg * g.ncps;
     const int cq = y.c / 4;
     int q = 1;
     while (q * 2 <= cq && q * 2 <= 64) q *= 2;
     g.qpb = q;
     g.cgroups = (cq + q - 1) / q;
+    int chunk = BN_CHUNK_MAX;
+    while (chunk > BN_CHUNK_MIN && int64_t(nseg) * ((g.pseg + chunk - 1) / chunk) * g.cgroups < BN_TARGET_BLOCKS)
+        chunk /= 2;
+    g.chunk = chunk;
+    g.ncps = int((g.pseg + chunk - 1) / chunk);
+    g.nrec = nseg * g.ncps;
     return g;
 }
 
@@ -71,12 +80,12 @@ struct Chunk {
     int64_t beg, end;
     int seg;
 };
-__device__ __forceinline__ Chunk chunk_of(int64_t pseg, int ncps) {
+__device__ __forceinline__ Chunk chunk_of(int64_t pseg, int ncps, int chunk) {
     Chunk c;
     c.seg = blockIdx.x / ncps;
     const int k = blockIdx.x % ncps;
-    c.beg = c.seg * pseg + int64_t(k) * BN_CHUNK;
-    c.end = min(c.beg + BN_CHUNK, (c.seg + 1) * pseg);
+    c.beg = c.seg * pseg + int64_t(k) * chunk;
+    c.end = min(c.beg + chunk, (c.seg + 1) * pseg);
     return c;
 }
 
@@ -84,13 +93,13 @@ __device__ __forceinline__ Chunk chunk_of(int64_t pseg, int ncps) {
 // forward statistics
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const float *__restrict__ y, int ldc, int C,
-                                                               int64_t pseg, int ncps, int nrec, int qpb,
+                                                               int64_t pseg, int ncps, int chunk, int nrec, int qpb,
                                                                float *__restrict__ rec) {
     __shared__ Welford4 sh[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
     const int c = (blockIdx.y * qpb + q) * 4;
-    const Chunk ch = chunk_of(pseg, ncps);
+    const Chunk ch = chunk_of(pseg, ncps, chunk);
     Welford4 w;
     w.n = 0.f;
     w.mean = f4{0.f, 0.f, 0.f, 0.f};
@@ -217,6 +226,33 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_finalize(const float *__r
     }
 }
 
+// Conv-fused statistics: tile records trec[tile][C] = {mean, M2} of tile_px pixels each (scd_conv_igemm
+// stat_rec) are Chan-merged in fixed order over groups of `group` consecutive tiles of one segment into the
+// chunk records rec[c][g] = {n, mean, M2} that bn_stats_finalize merges in double.
+__global__ __launch_bounds__(BN_THREADS) void bn_tile_merge(const float *__restrict__ trec, int C, int tiles_per_seg,
+                                                            int group, int ncps, int nrec, float tile_px,
+                                                            float *__restrict__ rec) {
+    const int c = blockIdx.y * BN_THREADS + threadIdx.x;
+    if (c >= C) return;
+    const int g = blockIdx.x;
+    const int seg = g / ncps, k = g - (g / ncps) * ncps;
+    const int t0 = seg * tiles_per_seg + k * group;
+    const int t1 = min(t0 + group, (seg + 1) * tiles_per_seg);
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    for (int t = t0; t < t1; ++t) {
+        const float2 r = *reinterpret_cast<const float2 *>(trec + (size_t(t) * C + c) * 2);
+        const float nn = n + tile_px;
+        const float d = r.x - mean;
+        mean += d * (tile_px / nn);
+        m2 += r.y + d * d * (n * tile_px / nn);
+        n = nn;
+    }
+    float *o = rec + (size_t(c) * nrec + g) * 3;
+    o[0] = n;
+    o[1] = mean;
+    o[2] = m2;
+}
+
 __global__ void bn_eval_coeffs_kernel(int C, const float *gamma, const float *beta, const float *rm, const float *rv,
                                       float eps, float *scale, float *shift) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -259,14 +295,14 @@ __device__ __forceinline__ f4 relu_mask(f4 y, f4 sc, f4 sf, f4 g) {
 // per (chunk) record {sum dz, sum dz*xhat}, rec[c][chunk][2]
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__restrict__ y, int ldy,
                                                              const float *__restrict__ da, int ldda, int C,
-                                                             int64_t pseg, int ncps, int nrec, int qpb,
+                                                             int64_t pseg, int ncps, int chunk, int nrec, int qpb,
                                                              const float *smean, const float *sinv, const float *scale,
                                                              const float *shift, float *__restrict__ rec) {
     __shared__ f4 sh1[BN_THREADS], sh2[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
     const int c = (blockIdx.y * qpb + q) * 4;
-    const Chunk ch = chunk_of(pseg, ncps);
+    const Chunk ch = chunk_of(pseg, ncps, chunk);
     f4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
     if (c < C) {
         const int o = ch.seg * C + c;
@@ -356,7 +392,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__res
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restrict__ y, int ldy,
                                                            const float *__restrict__ da, int ldda,
                                                            float *__restrict__ dy, int lddy, int C, int64_t pseg,
-                                                           int ncps, int nrec, int qpb, const float *smean,
+                                                           int ncps, int chunk, int nrec, int qpb, const float *smean,
                                                            const float *sinv, const float *gamma, const float *scale,
                                                            const float *shift, const float *coef,
                                                            float *__restrict__ brec) {
@@ -364,7 +400,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
     const int c = (blockIdx.y * qpb + q) * 4;
-    const Chunk ch = chunk_of(pseg, ncps);
+    const Chunk ch = chunk_of(pseg, ncps, chunk);
     f4 acc = {0.f, 0.f, 0.f, 0.f};
     if (c < C) {
         const int o = ch.seg * C + c;
@@ -433,15 +469,15 @@ __global__ __launch_bounds__(BN_THREADS) void sum_records(const float *__restric
 // Per-chunk channel sums (ConvTranspose2d bias grad) and weighted sums (1x1 head weight grad):
 //   rec[c][chunk] = sum_p w(p) * x[p][c],  w(p) = 1 or gout[img][o][pix]
 __global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const float *__restrict__ x, int ldx, int C,
-                                                               int64_t npix, int nrec, int qpb,
+                                                               int64_t npix, int chunk, int nrec, int qpb,
                                                                const float *__restrict__ wgt, int hw, int n_out,
                                                                int o, float *__restrict__ rec) {
     __shared__ f4 sh[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
     const int c = (blockIdx.y * qpb + q) * 4;
-    const int64_t pbeg = int64_t(blockIdx.x) * BN_CHUNK;
-    const int64_t pend = min(pbeg + BN_CHUNK, npix);
+    const int64_t pbeg = int64_t(blockIdx.x) * chunk;
+    const int64_t pend = min(pbeg + chunk, npix);
     f4 acc = {0.f, 0.f, 0.f, 0.f};
     if (c < C) {
         int64_t p = pbeg + pl;
@@ -486,6 +522,11 @@ static int bn_check(const scd_nhwc_t &y, int nseg) {
 }
 
 // Shared with misc_f32.hip (1x1 head weight grad).
+size_t weighted_channel_sum_bytes(const scd_nhwc_t &x) {
+    const BnGeom g = bn_geom(x, 1);
+    return size_t(g.nrec) * x.c * sizeof(float);
+}
+
 int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o, float *out, void *ws,
                          size_t ws_bytes, hipStream_t s);
 
@@ -498,7 +539,7 @@ int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o
     }
     float *rec = static_cast<float *>(ws);
     hipLaunchKernelGGL(chan_sum_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(x.data), x.ldc, x.c, pixels(x), g.nrec, g.qpb, wgt, x.h * x.w, n_out,
+                       static_cast<const float *>(x.data), x.ldc, x.c, pixels(x), g.chunk, g.nrec, g.qpb, wgt, x.h * x.w, n_out,
                        o, rec);
     hipLaunchKernelGGL(sum_records, dim3(x.c), dim3(BN_THREADS), 0, s, rec, g.nrec, out);
     return SCD_OK;
@@ -536,11 +577,51 @@ extern "C" int scd_bn_train_stats(scd_nhwc_t y, int32_t nseg, const float *gamma
     hipStream_t s = as_stream(stream);
     float *rec = static_cast<float *>(ws);
     hipLaunchKernelGGL(bn_stats_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, y.c, g.pseg, g.ncps, g.nrec, g.qpb, rec);
+                       static_cast<const float *>(y.data), y.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, rec);
     hipLaunchKernelGGL(bn_stats_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, gamma,
                        beta, eps, momentum, update_running, running_mean, running_var, save_mean, save_invstd, scale,
                        shift);
     return launch_status("scd_bn_train_stats");
+}
+
+static void tile_groups(int ntiles, int nseg, int *tiles_per_seg, int *group, int *ncps) {
+    *tiles_per_seg = ntiles / nseg;
+    *group = *tiles_per_seg / 256 > 1 ? *tiles_per_seg / 256 : 1;
+    *ncps = (*tiles_per_seg + *group - 1) / *group;
+}
+
+extern "C" size_t scd_bn_tile_stats_workspace_bytes(int32_t ntiles, int32_t c, int32_t nseg) {
+    if (nseg < 1 || ntiles < 1 || c < 1) return 0;
+    int tps, group, ncps;
+    tile_groups(ntiles, nseg, &tps, &group, &ncps);
+    return size_t(nseg) * ncps * c * 3 * sizeof(float) + 256;
+}
+
+extern "C" int scd_bn_stats_from_tiles(const float *tile_rec, int32_t ntiles, int32_t tile_pixels, int32_t c,
+                                       int32_t nseg, const float *gamma, const float *beta, float eps, float momentum,
+                                       int32_t update_running, float *running_mean, float *running_var,
+                                       float *save_mean, float *save_invstd, float *scale, float *shift, void *ws,
+                                       size_t ws_bytes, scd_stream_t stream) {
+    clear_error();
+    if (!tile_rec || ntiles < 1 || tile_pixels < 1 || c < 1 || nseg < 1 || ntiles % nseg || !save_mean ||
+        !save_invstd || !scale || !shift || (update_running && (!running_mean || !running_var))) {
+        set_error("bn_stats_from_tiles: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    if (!ws || ws_bytes < scd_bn_tile_stats_workspace_bytes(ntiles, c, nseg)) {
+        set_error("bn_stats_from_tiles: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    int tps, group, ncps;
+    tile_groups(ntiles, nseg, &tps, &group, &ncps);
+    const int nrec = nseg * ncps;
+    float *rec = static_cast<float *>(ws);
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(bn_tile_merge, dim3(nrec, (c + BN_THREADS - 1) / BN_THREADS), dim3(BN_THREADS), 0, s, tile_rec,
+                       c, tps, group, ncps, nrec, float(tile_pixels), rec);
+    hipLaunchKernelGGL(bn_stats_finalize, dim3(c), dim3(BN_THREADS), 0, s, rec, c, nseg, ncps, nrec, gamma, beta, eps,
+                       momentum, update_running, running_mean, running_var, save_mean, save_invstd, scale, shift);
+    return launch_status("scd_bn_stats_from_tiles");
 }
 
 extern "C" int scd_bn_eval_coeffs(int32_t c, const float *gamma, const float *beta, const float *running_mean,
@@ -599,12 +680,12 @@ extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, c
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL(bn_bwd_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        static_cast<const float *>(y.data), y.ldc, static_cast<const float *>(da.data), da.ldc, y.c,
-                       g.pseg, g.ncps, g.nrec, g.qpb, save_mean, save_invstd, scale, shift, rec);
+                       g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean, save_invstd, scale, shift, rec);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
                        coef, dgamma, dbeta);
     hipLaunchKernelGGL(bn_bwd_apply, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        static_cast<const float *>(y.data), y.ldc, static_cast<const float *>(da.data), da.ldc,
-                       static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.nrec, g.qpb, save_mean,
+                       static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean,
                        save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
     return launch_status("scd_bn_relu_backward");

@@ -54,6 +54,25 @@ inline int launch_status(const char *what) {
         if (_rc != SCD_OK) return _rc; \
     } while (0)
 
+// Division by a runtime constant: n / d = (umulhi(n, mul) + n) >> shr, valid for n < 2^31.
+struct FastDiv {
+    uint32_t d, mul, shr;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    uint32_t s = 0;
+    while ((1ull << s) < d) ++s;
+    f.shr = s;
+    f.mul = uint32_t(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
+    return (__umulhi(n, f.mul) + n) >> f.shr;
+}
+
 // Device-side NHWC element pointer helpers.
 struct View {
     float *p;

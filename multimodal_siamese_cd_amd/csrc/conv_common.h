@@ -16,25 +16,6 @@ __device__ __forceinline__ void gstore1(float *p, float v) { *(__attribute__((ad
 __device__ __forceinline__ f32x4 lload4(const float *p) { return *reinterpret_cast<const f32x4 *>(p); }
 __device__ __forceinline__ void lstore4(float *p, f32x4 v) { *reinterpret_cast<f32x4 *>(p) = v; }
 
-// Division by a runtime constant: n / d = (umulhi(n, mul) + n) >> shr, valid for n < 2^31.
-struct FastDiv {
-    uint32_t d, mul, shr;
-};
-
-inline FastDiv make_fastdiv(uint32_t d) {
-    FastDiv f;
-    f.d = d;
-    uint32_t s = 0;
-    while ((1ull << s) < d) ++s;
-    f.shr = s;
-    f.mul = uint32_t(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-    return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
-    return (__umulhi(n, f.mul) + n) >> f.shr;
-}
-
 // 9 taps packed as signed 4-bit fields.
 __device__ __forceinline__ int tap_at(uint64_t packed, int t) {
     int v = int((packed >> (4 * t)) & 15ull);
@@ -93,6 +74,7 @@ struct IgemmArgs {
     int grid_m, grid_n, remap;
     const uint16_t *wsplit;  // optional pre-split weight planes [3][n_out*K] (x3 math)
     int64_t wplane;
+    float *stat_rec;  // optional fused BN statistics [tile][n_out][2] (halo path)
     int dbg;  // ablation flags (SCD_IGEMM_DBG, perf experiments only; 0 in production)
     FastDiv div_hw, div_w;
 };
@@ -113,6 +95,8 @@ struct WgradArgs {
 // Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels
 // (the caller then runs the fp32-MFMA kernel).
 bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s);
+// Tiles (and pixels per tile) of the halo path for `a`, or 0 when `a` does not take it.
+int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels);
 // x3 weight-grad instantiations, indexed like kWgradTiles (conv_f32.hip).
 const void *wgrad_x3_fn(int tile_id);
 void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);

@@ -491,8 +491,9 @@ extern "C" int scd_set_conv_math(int32_t mode) {
     return prev;
 }
 
-extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
-    clear_error();
+namespace scd {
+// Validate a descriptor and fill the kernel arguments.
+static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     if (!d) {
         set_error("scd_conv_igemm: null descriptor");
         return SCD_ERR_ARG;
@@ -532,7 +533,6 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
         set_error("igemm: store_mode %d", d->store_mode);
         return SCD_ERR_ARG;
     }
-    IgemmArgs a;
     a.src = static_cast<const float *>(d->src.data);
     a.n_img = d->src.n;
     a.hs = d->src.h;
@@ -560,9 +560,36 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
     a.div_w = make_fastdiv(uint32_t(d->out_w));
     a.wsplit = d->wsplit;
     a.wplane = int64_t(a.n_out) * a.K;
+    a.stat_rec = d->stat_rec;
+    a.dbg = 0;
     if (d->wsplit && !aligned16(d->wsplit)) {
         set_error("igemm: wsplit must be 16-byte aligned");
         return SCD_ERR_ALIGN;
+    }
+    return SCD_OK;
+}
+}  // namespace scd
+
+extern "C" int scd_igemm_stat_tiles(const scd_igemm_t *d, int32_t *tile_pixels) {
+    clear_error();
+    IgemmArgs a;
+    if (igemm_prepare(d, a) != SCD_OK || d->store_mode != 0) return 0;
+    int tp = 0;
+    const int n = halo_stat_tiles(a, &tp);
+    if (tile_pixels) *tile_pixels = tp;
+    return n;
+}
+
+extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
+    clear_error();
+    IgemmArgs a;
+    SCD_TRY(igemm_prepare(d, a));
+    if (d->stat_rec) {
+        int tp = 0;
+        if (halo_stat_tiles(a, &tp) == 0) {
+            set_error("igemm: fused statistics requested for a shape without them (check scd_igemm_stat_tiles)");
+            return SCD_ERR_ARG;
+        }
     }
     hipStream_t s = as_stream(stream);
     if (conv_math_x3() && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");

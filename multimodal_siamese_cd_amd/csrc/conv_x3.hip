@@ -509,18 +509,68 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_halo_x3(IgemmArgs
                 gstore1(a.dst + pix * a.ldc_d + n, acc[i][j][r] + bias);
             }
     }
+
+    // Fused BatchNorm statistics of this tile (BM pixels of one image) per channel: two passes over the
+    // stored values (mean, then M2 about it), lane halves combined by shuffle, waves through LDS.
+    if (a.stat_rec) {
+        float *red = reinterpret_cast<float *>(smem);  // [WAVES_M][BN]; the main loop ended on a barrier
+        float bias_j[TN], mean_j[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int nl = wn * TN * 32 + j * 32 + (lane & 31);
+            bias_j[j] = (a.bias && n0 + nl < a.n_out) ? a.bias[n0 + nl] : 0.f;
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sum += acc[i][j][r] + bias_j[j];
+            sum += __shfl_xor(sum, 32);
+            if (lane < 32) red[wm * BN + nl] = sum;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int nl = wn * TN * 32 + j * 32 + (lane & 31);
+            float t = 0.f;
+#pragma unroll
+            for (int w = 0; w < WAVES_M; ++w) t += red[w * BN + nl];
+            mean_j[j] = t * (1.f / float(BM));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int nl = wn * TN * 32 + j * 32 + (lane & 31);
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float d = (acc[i][j][r] + bias_j[j]) - mean_j[j];
+                    q = fmaf(d, d, q);
+                }
+            q += __shfl_xor(q, 32);
+            if (lane < 32) red[wm * BN + nl] = q;
+        }
+        __syncthreads();
+        if (wm == 0 && lane < 32) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int nl = wn * TN * 32 + j * 32 + lane;
+                if (n0 + nl >= a.n_out) continue;
+                float m2 = 0.f;
+#pragma unroll
+                for (int w = 0; w < WAVES_M; ++w) m2 += red[w * BN + nl];
+                float *rec = a.stat_rec + (size_t(mt) * a.n_out + n0 + nl) * 2;
+                rec[0] = mean_j[j];
+                rec[1] = m2;
+            }
+        }
+    }
 }
 
 template <int WM, int WN, int TM, int TN>
-static bool launch_halo(const IgemmArgs &a, hipStream_t s) {
+static void launch_halo(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-    int tw = 0;
-    for (int cand : {64, 32, 16})
-        if (a.wo % cand == 0 && a.ho % (BM / cand) == 0) {
-            tw = cand;
-            break;
-        }
-    if (!tw) return false;
     IgemmArgs b = a;
     b.grid_m = a.n_img * (a.ho / (BM / tw)) * (a.wo / tw);
     b.grid_n = (a.n_out + BN - 1) / BN;
@@ -532,7 +582,6 @@ static bool launch_halo(const IgemmArgs &a, hipStream_t s) {
         hipLaunchKernelGGL((igemm_halo_x3<WM, WN, TM, TN, 32>), grid, block, 0, s, b);
     else
         hipLaunchKernelGGL((igemm_halo_x3<WM, WN, TM, TN, 16>), grid, block, 0, s, b);
-    return true;
 }
 
 // 3x3 / stride 1 / same-size convs with pre-split weights take the halo path.
@@ -546,12 +595,35 @@ static bool halo_eligible(const IgemmArgs &a) {
     return halo_enabled();
 }
 
+// Halo configuration of `a`: 0 = not eligible, 1 = <2,2,2,2> (128 px x 128), 2 = <4,1,2,2> (256 x 64),
+// 3 = <4,1,2,1> (256 x 32); *bm = pixels per tile, *tw = tile width (tile = bm/tw rows of one image).
+static int halo_pick(const IgemmArgs &a, int *bm, int *tw) {
+    if (a.c % 16 || !halo_eligible(a)) return 0;
+    const int cfg = a.n_out >= 128 ? 1 : (a.n_out >= 64 ? 2 : 3);
+    *bm = cfg == 1 ? 128 : 256;
+    for (int cand : {64, 32, 16})
+        if (a.wo % cand == 0 && a.ho % (*bm / cand) == 0) {
+            *tw = cand;
+            return cfg;
+        }
+    return 0;
+}
+
+int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels) {
+    int bm = 0, tw = 0;
+    if (!conv_math_x3() || !halo_pick(a, &bm, &tw)) return 0;
+    *tile_pixels = bm;
+    return a.n_img * (a.ho * a.wo / bm);
+}
+
 bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
     if (a.c % 16) return false;
-    if (halo_eligible(a)) {
-        if (a.n_out >= 128 && launch_halo<2, 2, 2, 2>(a, s)) return true;
-        if (a.n_out >= 64 && a.n_out < 128 && launch_halo<4, 1, 2, 2>(a, s)) return true;
-        if (a.n_out < 64 && launch_halo<4, 1, 2, 1>(a, s)) return true;
+    int bm = 0, tw = 0;
+    switch (halo_pick(a, &bm, &tw)) {
+        case 1: launch_halo<2, 2, 2, 2>(a, tw, s); return true;
+        case 2: launch_halo<4, 1, 2, 2>(a, tw, s); return true;
+        case 3: launch_halo<4, 1, 2, 1>(a, tw, s); return true;
+        default: break;
     }
     if (a.n_out >= 128)
         launch_x3<2, 2, 2, 2>(a, s);  // 128 x 128

@@ -22,11 +22,15 @@ void set_error(const char *fmt, ...) {
 }
 void clear_error() { g_err.clear(); }
 
-constexpr int RED_CHUNK = 4096;  // pixels per reduction chunk (matches bn_f32.hip)
-
 // bn_f32.hip: sum_p w(p) x[p][c] over all pixels (w = 1 or gout[img][o][pix]).
 int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o, float *out, void *ws,
                          size_t ws_bytes, hipStream_t s);
+size_t weighted_channel_sum_bytes(const scd_nhwc_t &x);
+
+// Row-decomposed grid: x covers the quads of one row (256 per block), y walks rows (grid-stride past 65535).
+static dim3 row_grid(int row_quads, int64_t rows) {
+    return dim3(unsigned((row_quads + 255) / 256), unsigned(rows < 65535 ? rows : 65535));
+}
 
 static int grid_for(int64_t total, int cap = 4096) {
     int64_t b = (total + 255) / 256;
@@ -91,16 +95,20 @@ __device__ __forceinline__ void pool_pick(float v, int k, float &mx, int &idx) {
     }
 }
 
+// Row-decomposed elementwise grids: grid.y walks image rows (img, y), grid.x the channel quads of a row,
+// so the per-element index math is 32-bit (one FastDiv by the quads per pixel) instead of 64-bit div/mod.
 __global__ void maxpool2_fwd_kernel(const float *__restrict__ x, int hx, int wx, int ldx, float *__restrict__ y,
-                                   int hy, int wy, int ldy, uint8_t *__restrict__ idx, int C, int64_t total) {
+                                   int hy, int wy, int ldy, uint8_t *__restrict__ idx, int C, int rows,
+                                   FastDiv div_cq) {
     const int cq = C / 4;
-    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
-        const int c = int(e % cq) * 4;
-        const int64_t p = e / cq;  // output pixel
-        const int ox = int(p % wy);
-        const int oy = int((p / wy) % hy);
-        const int64_t img = p / (int64_t(wy) * hy);
-        const float *base = x + ((img * hx + 2 * oy) * wx + 2 * ox) * ldx + c;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= wy * cq) return;
+    const int ox = int(fdiv(uint32_t(e), div_cq));
+    const int c = (e - ox * cq) * 4;
+    for (int row = blockIdx.y; row < rows; row += gridDim.y) {
+        const int img = row / hy, oy = row - img * hy;
+        const int64_t p = int64_t(row) * wy + ox;  // output pixel
+        const float *base = x + ((int64_t(img) * hx + 2 * oy) * wx + 2 * ox) * ldx + c;
         const float4 v0 = *reinterpret_cast<const float4 *>(base);
         const float4 v1 = *reinterpret_cast<const float4 *>(base + ldx);
         const float4 v2 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx);
@@ -128,19 +136,20 @@ __global__ void maxpool2_fwd_kernel(const float *__restrict__ x, int hx, int wx,
 __global__ void feature_grad_kernel(const float *__restrict__ gy, int hy, int wy, int ldgy,
                                     const uint8_t *__restrict__ idx, const float *__restrict__ gs, int gsn, int ldgs,
                                     int skip_mode, float *__restrict__ gx, int hx, int wx, int ldgx, int C,
-                                    int accumulate, int64_t total) {
+                                    int accumulate, int rows, FastDiv div_cq) {
     const int cq = C / 4;
-    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
-        const int c = int(e % cq) * 4;
-        const int64_t p = e / cq;
-        const int x = int(p % wx);
-        const int yy = int((p / wx) % hx);
-        const int64_t img = p / (int64_t(wx) * hx);
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= wx * cq) return;
+    const int x = int(fdiv(uint32_t(e), div_cq));
+    const int c = (e - x * cq) * 4;
+    for (int row = blockIdx.y; row < rows; row += gridDim.y) {
+        const int img = row / hx, yy = row - img * hx;
+        const int64_t p = int64_t(row) * wx + x;
         float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
         if (gy) {
             const int oy = yy >> 1, ox = x >> 1;
             if (oy < hy && ox < wy) {
-                const int64_t q = (img * hy + oy) * wy + ox;
+                const int64_t q = (int64_t(img) * hy + oy) * wy + ox;
                 const uint32_t pk = *reinterpret_cast<const uint32_t *>(idx + q * C + c);
                 const float4 g = *reinterpret_cast<const float4 *>(gy + q * ldgy + c);
                 const uint32_t want = uint32_t((yy & 1) * 2 + (x & 1));
@@ -151,9 +160,9 @@ __global__ void feature_grad_kernel(const float *__restrict__ gy, int hy, int wy
             }
         }
         if (gs) {
-            const int64_t simg = img % gsn;
+            const int simg = img % gsn;
             const float sg = (skip_mode == 1 && img < gsn) ? -1.f : 1.f;
-            const float4 s = *reinterpret_cast<const float4 *>(gs + ((simg * hx + yy) * wx + x) * ldgs + c);
+            const float4 s = *reinterpret_cast<const float4 *>(gs + ((int64_t(simg) * hx + yy) * wx + x) * ldgs + c);
             r.x += sg * s.x;
             r.y += sg * s.y;
             r.z += sg * s.z;
@@ -172,11 +181,14 @@ __global__ void feature_grad_kernel(const float *__restrict__ gy, int hy, int wy
 }
 
 __global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float *__restrict__ d, int ldd, int C,
-                                    int64_t half_pixels, int64_t total) {
+                                    int w, int64_t half_pixels, int rows, FastDiv div_cq) {
     const int cq = C / 4;
-    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
-        const int c = int(e % cq) * 4;
-        const int64_t p = e / cq;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= w * cq) return;
+    const int x = int(fdiv(uint32_t(e), div_cq));
+    const int c = (e - x * cq) * 4;
+    for (int row = blockIdx.y; row < rows; row += gridDim.y) {
+        const int64_t p = int64_t(row) * w + x;
         const float4 v1 = *reinterpret_cast<const float4 *>(a + p * lda + c);
         const float4 v2 = *reinterpret_cast<const float4 *>(a + (p + half_pixels) * lda + c);
         *reinterpret_cast<float4 *>(d + p * ldd + c) = make_float4(v2.x - v1.x, v2.y - v1.y, v2.z - v1.z, v2.w - v1.w);
@@ -426,10 +438,10 @@ extern "C" int scd_maxpool2_fwd(scd_nhwc_t x, scd_nhwc_t y, uint8_t *idx, scd_st
         set_error("maxpool2_fwd: y must be (n, h/2, w/2, c); idx 4-byte aligned");
         return SCD_ERR_ARG;
     }
-    const int64_t total = pixels(y) * (y.c / 4);
-    hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+    const int64_t rows = int64_t(y.n) * y.h;
+    hipLaunchKernelGGL(maxpool2_fwd_kernel, row_grid(y.w * (y.c / 4), rows), dim3(256), 0, as_stream(stream),
                        static_cast<const float *>(x.data), x.h, x.w, x.ldc, static_cast<float *>(y.data), y.h, y.w,
-                       y.ldc, idx, y.c, total);
+                       y.ldc, idx, y.c, int(rows), make_fastdiv(uint32_t(y.c / 4)));
     return launch_status("scd_maxpool2_fwd");
 }
 
@@ -452,11 +464,12 @@ extern "C" int scd_feature_grad(scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gs
             return SCD_ERR_ARG;
         }
     }
-    const int64_t total = pixels(gx) * (gx.c / 4);
-    hipLaunchKernelGGL(feature_grad_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+    const int64_t rows = int64_t(gx.n) * gx.h;
+    hipLaunchKernelGGL(feature_grad_kernel, row_grid(gx.w * (gx.c / 4), rows), dim3(256), 0, as_stream(stream),
                        static_cast<const float *>(gy.data), gy.h, gy.w, gy.ldc, idx,
                        static_cast<const float *>(gskip.data), gskip.n > 0 ? gskip.n : 1, gskip.ldc, skip_mode,
-                       static_cast<float *>(gx.data), gx.h, gx.w, gx.ldc, gx.c, accumulate, total);
+                       static_cast<float *>(gx.data), gx.h, gx.w, gx.ldc, gx.c, accumulate, int(rows),
+                       make_fastdiv(uint32_t(gx.c / 4)));
     return launch_status("scd_feature_grad");
 }
 
@@ -468,10 +481,10 @@ extern "C" int scd_siamese_diff(scd_nhwc_t a, scd_nhwc_t d, scd_stream_t stream)
         set_error("siamese_diff: a must be (2n, h, w, c) of d");
         return SCD_ERR_ARG;
     }
-    const int64_t total = pixels(d) * (d.c / 4);
-    hipLaunchKernelGGL(siamese_diff_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(a.data), a.ldc, static_cast<float *>(d.data), d.ldc, d.c, pixels(d),
-                       total);
+    const int64_t rows = int64_t(d.n) * d.h;
+    hipLaunchKernelGGL(siamese_diff_kernel, row_grid(d.w * (d.c / 4), rows), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(a.data), a.ldc, static_cast<float *>(d.data), d.ldc, d.c, d.w,
+                       pixels(d), int(rows), make_fastdiv(uint32_t(d.c / 4)));
     return launch_status("scd_siamese_diff");
 }
 
@@ -495,8 +508,7 @@ extern "C" int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int
 }
 
 extern "C" size_t scd_conv1x1_workspace_bytes(scd_nhwc_t x, int32_t n_out) {
-    const int64_t nchunk = (pixels(x) + RED_CHUNK - 1) / RED_CHUNK;
-    return size_t(nchunk) * x.c * sizeof(float) + size_t(1024) * n_out * sizeof(float) + 256;
+    return weighted_channel_sum_bytes(x) + size_t(1024) * n_out * sizeof(float) + 256;
 }
 
 extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, int32_t n_out, scd_nhwc_t gx,
@@ -525,14 +537,13 @@ extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, 
         hipLaunchKernelGGL(conv1x1_bwd_dx_kernel, dim3(grid_for(total)), dim3(256), 0, s, gout, n_out, hw, w,
                            static_cast<float *>(gx.data), gx.ldc, x.c, accumulate, total);
     }
-    const int nchunk = int((npix + RED_CHUNK - 1) / RED_CHUNK);
     float *rec = static_cast<float *>(ws);
-    const size_t wbytes = size_t(nchunk) * x.c * sizeof(float);
+    const size_t wbytes = weighted_channel_sum_bytes(x);
     if (gw)
         for (int o = 0; o < n_out; ++o)  // stream-ordered reuse of the record buffer
             SCD_TRY(weighted_channel_sum(x, gout, n_out, o, gw + size_t(o) * x.c, ws, wbytes, s));
     if (gb) {
-        float *brec = rec + size_t(nchunk) * x.c;
+        float *brec = rec + wbytes / sizeof(float);
         const int nb = 1024;
         hipLaunchKernelGGL(conv1x1_bwd_db_partial, dim3(nb, n_out), dim3(256), 0, s, gout, n_out, hw, npix, brec);
         hipLaunchKernelGGL(sum_rows_block, dim3(n_out), dim3(256), 0, s, brec, nb, gb);

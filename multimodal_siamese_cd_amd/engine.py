@@ -51,19 +51,32 @@ class _BNSaved:
     nseg: int
 
 
-def _bn_forward(y: torch.Tensor, bn: torch.nn.BatchNorm2d, nseg: int, training: bool) -> _BNSaved:
-    """Batch statistics (train) or running statistics (eval) -> per-segment scale/shift."""
+def _bn_uses_batch_stats(bn: torch.nn.BatchNorm2d, training: bool) -> bool:
+    return training or not bn.track_running_stats or bn.running_mean is None
+
+
+def _bn_forward(y: torch.Tensor, bn: torch.nn.BatchNorm2d, nseg: int, training: bool, tiles=None) -> _BNSaved:
+    """Batch statistics (train) or running statistics (eval) -> per-segment scale/shift.
+
+    `tiles` = (tile records, ntiles, pixels per tile) from the conv that produced y (fused statistics);
+    without it the statistics are a separate pass over y.
+    """
     n, h, w, c = y.shape
-    use_batch = training or not bn.track_running_stats or bn.running_mean is None
-    if use_batch:
+    if _bn_uses_batch_stats(bn, training):
         smean, sinv, scale, shift = (_empty((nseg * c,), y) for _ in range(4))
-        ws = _ws(hip.bn_workspace_bytes(n, h, w, c, nseg), y)
         update = training and bn.track_running_stats and bn.running_mean is not None
         mom = bn.momentum if bn.momentum is not None else 0.1
         if update and bn.momentum is None:
             raise NotImplementedError("BatchNorm2d(momentum=None) cumulative averaging is not supported")
-        hip.bn_train_stats(nhwc(y), nseg, bn.weight, bn.bias, bn.eps, mom, update, bn.running_mean,
-                           bn.running_var, smean, sinv, scale, shift, ws)
+        if tiles is not None:
+            rec, ntiles, tpx = tiles
+            ws = _ws(hip.bn_tile_stats_workspace_bytes(ntiles, c, nseg), y)
+            hip.bn_stats_from_tiles(rec, ntiles, tpx, c, nseg, bn.weight, bn.bias, bn.eps, mom, update,
+                                    bn.running_mean, bn.running_var, smean, sinv, scale, shift, ws)
+        else:
+            ws = _ws(hip.bn_workspace_bytes(n, h, w, c, nseg), y)
+            hip.bn_train_stats(nhwc(y), nseg, bn.weight, bn.bias, bn.eps, mom, update, bn.running_mean,
+                               bn.running_var, smean, sinv, scale, shift, ws)
         if update:
             bn.num_batches_tracked.add_(nseg)
         return _BNSaved(smean, sinv, scale, shift, nseg)
@@ -87,18 +100,35 @@ def _conv3x3(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int) -> torch.Tens
     return y
 
 
+def _conv3x3_stats(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int, want: bool):
+    """Conv 3x3 forward; with `want`, also the fused per-tile BatchNorm statistics when the conv provides them."""
+    n, h, w, _ = x.shape
+    y = _empty((n, h, w, n_out), x)
+    tiles = None
+    if want:
+        ntiles, tpx = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(y))
+        if ntiles:
+            rec = _empty((ntiles * n_out * 2,), x)
+            tiles = (rec, ntiles, tpx)
+    hip.conv_igemm(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, bias, nhwc(y),
+                   stat_rec=None if tiles is None else tiles[0])
+    return y, tiles
+
+
 def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool):
     s = dc.conv
     conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
     cin = x.shape[3]
     if conv0.in_channels > cin:
         raise ValueError(f"DoubleConv expects {conv0.in_channels} input channels, got {cin}")
-    y0 = _conv3x3(x, hip.pack_conv3x3(conv0.weight.detach(), 0, ci_pad=cin), conv0.bias, conv0.out_channels)
-    st0 = _bn_forward(y0, bn0, nseg, training)
+    y0, t0 = _conv3x3_stats(x, hip.pack_conv3x3(conv0.weight.detach(), 0, ci_pad=cin), conv0.bias,
+                            conv0.out_channels, _bn_uses_batch_stats(bn0, training))
+    st0 = _bn_forward(y0, bn0, nseg, training, t0)
     a0 = torch.empty_like(y0)
     hip.bn_relu_apply(nhwc(y0), st0.nseg, st0.scale, st0.shift, nhwc(a0))
-    y1 = _conv3x3(a0, hip.pack_conv3x3(conv1.weight.detach(), 0), conv1.bias, conv1.out_channels)
-    st1 = _bn_forward(y1, bn1, nseg, training)
+    y1, t1 = _conv3x3_stats(a0, hip.pack_conv3x3(conv1.weight.detach(), 0), conv1.bias, conv1.out_channels,
+                            _bn_uses_batch_stats(bn1, training))
+    st1 = _bn_forward(y1, bn1, nseg, training, t1)
     a1 = torch.empty_like(y1)
     hip.bn_relu_apply(nhwc(y1), st1.nseg, st1.scale, st1.shift, nhwc(a1))
     saved = (x, y0, a0, st0, y1, st1) if save else None

@@ -36,6 +36,7 @@ class IGEMM(ctypes.Structure):
         ("dst", NHWC),
         ("store_mode", c_int32),
         ("wsplit", c_void_p),
+        ("stat_rec", c_void_p),
     ]
 
 
@@ -70,6 +71,7 @@ _SIGS = {
     "scd_set_conv_math": ([c_int32], c_int),
     "scd_split_bf16x3": ([c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
+    "scd_igemm_stat_tiles": ([POINTER(IGEMM), POINTER(c_int32)], c_int),
     "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
     "scd_conv_wgrad": ([POINTER(WGRAD), c_void_p, c_size_t, c_void_p], c_int),
     "scd_wgrad_finalize": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
@@ -77,6 +79,12 @@ _SIGS = {
     "scd_bn_train_stats": (
         [NHWC, c_int32, c_void_p, c_void_p, c_float, c_float, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+        c_int,
+    ),
+    "scd_bn_tile_stats_workspace_bytes": ([c_int32, c_int32, c_int32], c_size_t),
+    "scd_bn_stats_from_tiles": (
+        [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_float, c_float, c_int32, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
         c_int,
     ),
     "scd_bn_eval_coeffs": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p], c_int),
@@ -243,12 +251,25 @@ def conv_math() -> str:
     return {v: k for k, v in _MATH_NAMES.items()}[rc]
 
 
-def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
-               bias, dst: NHWC, store_mode: int = 0):
+def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None):
     nt, dy, dx = _taps(taps)
-    d = IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
-              _ptr(getattr(wpk, '_x3', None)))
+    return IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
+                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec))
+
+
+def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
+               bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None):
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec)
     _check(lib().scd_conv_igemm(ctypes.byref(d), _stream()), "scd_conv_igemm")
+
+
+def igemm_stat_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
+                     dst: NHWC) -> tuple[int, int]:
+    """(tiles, pixels per tile) of the conv-fused BatchNorm statistics for this conv, (0, 0) if unavailable."""
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0)
+    tp = c_int32(0)
+    n = lib().scd_igemm_stat_tiles(ctypes.byref(d), ctypes.byref(tp))
+    return (n, tp.value) if n > 0 else (0, 0)
 
 
 def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps):
@@ -279,6 +300,21 @@ def bn_train_stats(y: NHWC, nseg, gamma, beta, eps, momentum, update, rmean, rva
                                  smean.data_ptr(), sinv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(),
                                  ws.numel(), _stream()),
         "scd_bn_train_stats")
+
+
+def bn_tile_stats_workspace_bytes(ntiles, c, nseg) -> int:
+    return lib().scd_bn_tile_stats_workspace_bytes(ntiles, c, nseg)
+
+
+def bn_stats_from_tiles(tile_rec, ntiles, tile_px, c, nseg, gamma, beta, eps, momentum, update, rmean, rvar, smean,
+                        sinv, scale, shift, ws):
+    _check(
+        lib().scd_bn_stats_from_tiles(tile_rec.data_ptr(), ntiles, tile_px, c, nseg, _ptr(gamma), _ptr(beta), eps,
+                                      momentum, int(update), _ptr(rmean), _ptr(rvar), smean.data_ptr(),
+                                      sinv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(), ws.numel(),
+                                      _stream()),
+        "scd_bn_stats_from_tiles",
+    )
 
 
 def bn_eval_coeffs(c, gamma, beta, rmean, rvar, eps, scale, shift):

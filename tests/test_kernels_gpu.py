@@ -222,6 +222,46 @@ def test_convT2x2_backward(dev, math, n, h, w, c, cs):
     assert rel(gb, b.grad) < TOL
 
 
+@pytest.mark.parametrize('n,h,w,ci,co,nseg', [(4, 32, 32, 64, 128, 2), (4, 16, 16, 32, 64, 2), (2, 64, 64, 16, 32, 1),
+                                              (2, 16, 16, 512, 512, 1)])
+def test_conv_fused_bn_stats(dev, n, h, w, ci, co, nseg):
+    """Conv-fused per-tile BatchNorm statistics (x3 halo path) == the separate statistics pass on the same y."""
+    from multimodal_siamese_cd_amd import hip
+    prev = hip.set_conv_math('x3')
+    try:
+        g = torch.Generator().manual_seed(ci * co + n)
+        x = torch.randn(n, h, w, ci, generator=g).to(dev)
+        wt = (torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)).to(dev)
+        b = (torch.randn(co, generator=g) + 3.0).to(dev)  # offset: M2 about a non-zero mean
+        wpk = hip.pack_conv3x3(wt, 0)
+        y = torch.empty(n, h, w, co, device=dev)
+        ntiles, tpx = hip.igemm_stat_tiles(hip.nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y))
+        assert ntiles > 0 and ntiles * tpx == n * h * w
+        rec = torch.empty(ntiles * co * 2, device=dev)
+        hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, b, hip.nhwc(y), stat_rec=rec)
+        gamma = torch.rand(co, device=dev) + 0.5
+        beta = torch.randn(co, device=dev)
+        outs = []
+        for fused in (False, True):
+            rm, rv = torch.zeros(co, device=dev), torch.ones(co, device=dev)
+            o = [torch.empty(nseg * co, device=dev) for _ in range(4)]
+            if fused:
+                ws = torch.empty(hip.bn_tile_stats_workspace_bytes(ntiles, co, nseg), dtype=torch.uint8, device=dev)
+                hip.bn_stats_from_tiles(rec, ntiles, tpx, co, nseg, gamma, beta, 1e-5, 0.1, True, rm, rv, *o, ws)
+            else:
+                ws = torch.empty(hip.bn_workspace_bytes(n, h, w, co, nseg), dtype=torch.uint8, device=dev)
+                hip.bn_train_stats(hip.nhwc(y), nseg, gamma, beta, 1e-5, 0.1, True, rm, rv, *o, ws)
+            outs.append(o + [rm, rv])
+        for a, b_ in zip(*outs):
+            assert rel(a, b_) < 2e-6
+        # and against the definition on the host
+        yc = y.double().cpu().reshape(nseg, -1, co)
+        assert rel(outs[1][0].reshape(nseg, co), yc.mean(1)) < 2e-6
+        assert rel(outs[1][1].reshape(nseg, co), 1 / torch.sqrt(yc.var(1, unbiased=False) + 1e-5)) < 2e-6
+    finally:
+        hip.set_conv_math(prev)
+
+
 @pytest.mark.parametrize('n,h,w,c,nseg', [(4, 16, 16, 8, 2), (2, 33, 17, 64, 2), (2, 64, 64, 16, 1), (6, 8, 8, 512, 2)])
 def test_batchnorm_relu_train_forward_backward(dev, n, h, w, c, nseg):
     from multimodal_siamese_cd_amd import hip

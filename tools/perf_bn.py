@@ -1,0 +1,63 @@
+"""Per-layer timing of the BatchNorm / elementwise kernels of the bench workload (SiameseUNet 256^2, bs=32).
+
+    python tools/perf_bn.py [--batch 32] [--reps 5]
+
+For every conv output of one training step, times scd_bn_train_stats, scd_bn_relu_apply and
+scd_bn_relu_backward with HIP events.  Prints the achieved HBM rate from the algorithmic bytes:
+4, 8 and 20 B/elem respectively (the backward reads y and da twice and writes dy).
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from multimodal_siamese_cd_amd import hip  # noqa: E402
+from perf_conv import layers, timeit  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--reps', type=int, default=5)
+    args = ap.parse_args()
+    hip.load_library()
+    dev = torch.device('cuda:0')
+    tot = {'stats': 0.0, 'apply': 0.0, 'bwd': 0.0}
+    byt = {'stats': 0.0, 'apply': 0.0, 'bwd': 0.0}
+    print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"c":>5s} | {"stats ms":>8s} {"TB/s":>5s} | {"apply ms":>8s} {"TB/s":>5s} | '
+          f'{"bwd ms":>8s} {"TB/s":>5s}')
+    for name, n, s, _, co in layers(args.batch):
+        nseg = 2 if name.startswith('enc') else 1
+        y = torch.randn(n, s, s, co, device=dev)
+        da = torch.randn(n, s, s, co, device=dev)
+        a = torch.empty_like(y)
+        dy = torch.empty_like(y)
+        gamma = torch.rand(co, device=dev) + 0.5
+        beta = torch.randn(co, device=dev)
+        rm, rv = torch.zeros(co, device=dev), torch.ones(co, device=dev)
+        sm, si = torch.empty(nseg * co, device=dev), torch.empty(nseg * co, device=dev)
+        sc, sh = torch.empty(nseg * co, device=dev), torch.empty(nseg * co, device=dev)
+        dg, db, dbias = torch.empty(co, device=dev), torch.empty(co, device=dev), torch.empty(co, device=dev)
+        ws = torch.empty(hip.bn_workspace_bytes(n, s, s, co, nseg), dtype=torch.uint8, device=dev)
+        Y, A, DA, DY = hip.nhwc(y), hip.nhwc(a), hip.nhwc(da), hip.nhwc(dy)
+        el = y.numel()
+        t_s = timeit(lambda: hip.bn_train_stats(Y, nseg, gamma, beta, 1e-5, 0.1, False, rm, rv, sm, si, sc, sh, ws),
+                     args.reps)
+        t_a = timeit(lambda: hip.bn_relu_apply(Y, nseg, sc, sh, A), args.reps)
+        t_b = timeit(lambda: hip.bn_relu_backward(Y, DA, nseg, sm, si, gamma, sc, sh, dg, db, dbias, DY, ws),
+                     args.reps)
+        cells = []
+        for k, t, b in (('stats', t_s, 4), ('apply', t_a, 8), ('bwd', t_b, 20)):
+            tot[k] += t
+            byt[k] += b * el
+            cells.append(f'{t:8.3f} {b * el / t / 1e9:5.2f}')
+        print(f'{name:8s} {n:3d} {s:4d} {co:5d} | ' + ' | '.join(cells), flush=True)
+    for k in tot:
+        print(f'{k:6s} total {tot[k]:8.2f} ms  {byt[k] / tot[k] / 1e9:5.2f} TB/s')
+
+
+if __name__ == '__main__':
+    main()
