@@ -88,6 +88,7 @@ struct WgradArgs {
     uint64_t tdy, tdx;
     int Ng, M, kchunk;
     int grid_r, grid_j, remap;
+    uint32_t rows_bytes, src_bytes;  // extents of rows/src for the buffer-load range check (< 2 GiB)
     float *slabs;
     FastDiv div_hw, div_w, div_c;
 };

@@ -749,6 +749,15 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
     a.div_hw = make_fastdiv(uint32_t(d->rows.h * d->rows.w));
     a.div_w = make_fastdiv(uint32_t(d->rows.w));
     a.div_c = make_fastdiv(uint32_t(d->src.c));
+    // byte extents for the x3 kernel's buffer loads (32-bit offsets)
+    const int64_t rb = (pixels(d->rows) - 1) * d->rows.ldc * 4 + int64_t(d->rows.c) * 4;
+    const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * 4 + int64_t(d->src.c) * 4;
+    if (rb >= (int64_t(1) << 31) || sb >= (int64_t(1) << 31)) {
+        set_error("wgrad: operands above 2 GiB are not supported (32-bit buffer offsets)");
+        return SCD_ERR_ARG;
+    }
+    a.rows_bytes = uint32_t(rb);
+    a.src_bytes = uint32_t(sb);
     hipStream_t s = as_stream(stream);
     const WgradTile t = wgrad_tile(a.R, Ng);
     a.grid_r = (a.R + t.bm - 1) / t.bm;

@@ -645,6 +645,17 @@ bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
+// Raw buffer loads: 32-bit byte offsets with the hardware range check, so an out-of-range offset
+// (kOOB) returns zeros with no branch, no exec-mask juggling and no zero-fill moves.
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, int(bytes), 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 __device__ __forceinline__ s16x4 lds_tr16(const unsigned char *p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (__attribute__((address_space(3))) s16x4 *)(reinterpret_cast<const __attribute__((address_space(3))) unsigned char *>(
@@ -652,6 +663,20 @@ __device__ __forceinline__ s16x4 lds_tr16(const unsigned char *p) {
 }
 
 constexpr int tr_stride(int w) { return (2 * w) % 128 == 0 ? 2 * w + 64 : 2 * w; }
+
+// [16 px][W ch] bf16 plane addressing for the transposed reads.  W % 128 == 0: unpadded 2W-byte rows with the
+// 64-byte segments of each 256-byte bank row XOR-permuted by (k & 3), so the 4 rows a 16-lane group reads
+// land in 4 different segments (conflict-free, and 25% less LDS than padding -> one more workgroup per CU).
+// Other widths: rows padded to tr_stride.
+template <int W>
+struct TrPlane {
+    static constexpr bool XOR = (W % 128) == 0;
+    static constexpr int RS = XOR ? 2 * W : tr_stride(W);
+    static constexpr int BYTES = 16 * RS;
+    __device__ static __forceinline__ int off(int k, int colbyte) {
+        return XOR ? k * RS + (colbyte ^ ((k & 3) << 6)) : k * RS + colbyte;
+    }
+};
 
 template <int WAVES_M, int WAVES_N, int TM, int TN>
 __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
@@ -663,8 +688,10 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
     constexpr int A_CH = BK * AQ, B_CH = BK * BQ;
     constexpr int A_PER = (A_CH + NT - 1) / NT;
     constexpr int B_PER = (B_CH + NT - 1) / NT;
-    constexpr int RSA = tr_stride(BM), RSB = tr_stride(BN);
-    constexpr int PA = BK * RSA, PB = BK * RSB;  // plane bytes
+    constexpr bool A_FULL = A_CH % NT == 0, B_FULL = B_CH % NT == 0;
+    using LA = TrPlane<BM>;
+    using LB = TrPlane<BN>;
+    constexpr int PA = LA::BYTES, PB = LB::BYTES;  // plane bytes
     constexpr int STAGE = 3 * (PA + PB);
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
 
@@ -693,7 +720,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
         const int q = ch % AQ;
         a_r[i] = r0 + q * 4;
         a_ok[i] = a_in[i] && a_r[i] < a.R;
-        a_off[i] = a_k[i] * RSA + q * 8;
+        a_off[i] = LA::off(a_k[i], q * 8);
     }
     int b_k[B_PER], b_dy[B_PER], b_dx[B_PER], b_c[B_PER], b_off[B_PER];
     int b_img[B_PER], b_oy[B_PER], b_ox[B_PER];
@@ -717,16 +744,17 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
         b_img[i] = int(img);
         b_oy[i] = int(oy);
         b_ox[i] = int(rr - oy * uint32_t(a.wo));
-        b_off[i] = 3 * PA + b_k[i] * RSB + q * 8;
+        b_off[i] = 3 * PA + LB::off(b_k[i], q * 8);
     }
 
     f32x4 ra[A_PER], rb[B_PER];
-    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
+    const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
     auto load_stage = [&](int kb) {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int m = kb + a_k[i];
-            ra[i] = (a_ok[i] && m < kend) ? gload4(a.rows + size_t(m) * a.ldc_r + a_r[i]) : zero4;
+            ra[i] = bload4(rs_rows, (a_ok[i] && m < kend) ? uint32_t(m * a.ldc_r + a_r[i]) * 4u : kOOB);
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
@@ -734,30 +762,33 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
             const int sx = b_ox[i] * a.stride + b_dx[i];
             const bool v = b_ok[i] && (kb + b_k[i] < kend) && unsigned(sy) < unsigned(a.hs) &&
                            unsigned(sx) < unsigned(a.ws);
-            rb[i] = v ? gload4(a.src + (size_t(b_img[i] * a.hs + sy) * a.ws + sx) * a.ldc_s + b_c[i]) : zero4;
+            rb[i] = bload4(rs_src, v ? uint32_t(((b_img[i] * a.hs + sy) * a.ws + sx) * a.ldc_s + b_c[i]) * 4u : kOOB);
         }
     };
     auto advance = [&]() {
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
-            int ox = b_ox[i] + BK, oy = b_oy[i], img = b_img[i];
-            while (ox >= a.wo) {
-                ox -= a.wo;
-                if (++oy == a.ho) {
-                    oy = 0;
-                    ++img;
+            b_ox[i] += BK;
+            if (b_ox[i] >= a.wo) {  // row wrap (rare: once per wo/16 steps)
+                int ox = b_ox[i], oy = b_oy[i], img = b_img[i];
+                while (ox >= a.wo) {
+                    ox -= a.wo;
+                    if (++oy == a.ho) {
+                        oy = 0;
+                        ++img;
+                    }
                 }
+                b_ox[i] = ox;
+                b_oy[i] = oy;
+                b_img[i] = img;
             }
-            b_ox[i] = ox;
-            b_oy[i] = oy;
-            b_img[i] = img;
         }
     };
     auto store_stage = [&](int buf) {
         unsigned char *S = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i)
-            if (a_in[i]) {
+            if (A_FULL || a_in[i]) {
                 u32x2 h, m, l;
                 split3(ra[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(S + a_off[i]) = h;
@@ -766,7 +797,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
             }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
-            if (b_in[i]) {
+            if (B_FULL || b_in[i]) {
                 u32x2 h, m, l;
                 split3(rb[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(S + b_off[i]) = h;
@@ -787,11 +818,17 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
     const int g = lane >> 4, w = lane & 15;
     const int trk = 8 * (g >> 1) + (w >> 2);
     const int trc = 16 * (g & 1) + 4 * (w & 3);
-    int a_rd[TM], b_rd[TN];
+    int a_rd[TM], a_rd4[TM], b_rd[TN], b_rd4[TN];  // rows trk and trk + 4
 #pragma unroll
-    for (int i = 0; i < TM; ++i) a_rd[i] = trk * RSA + (wm * TM * 32 + i * 32 + trc) * 2;
+    for (int i = 0; i < TM; ++i) {
+        a_rd[i] = LA::off(trk, (wm * TM * 32 + i * 32 + trc) * 2);
+        a_rd4[i] = LA::off(trk + 4, (wm * TM * 32 + i * 32 + trc) * 2);
+    }
 #pragma unroll
-    for (int j = 0; j < TN; ++j) b_rd[j] = 3 * PA + trk * RSB + (wn * TN * 32 + j * 32 + trc) * 2;
+    for (int j = 0; j < TN; ++j) {
+        b_rd[j] = 3 * PA + LB::off(trk, (wn * TN * 32 + j * 32 + trc) * 2);
+        b_rd4[j] = 3 * PA + LB::off(trk + 4, (wn * TN * 32 + j * 32 + trc) * 2);
+    }
 
     const int nsteps = (kend > kbeg) ? (kend - kbeg + BK - 1) / BK : 0;
     if (nsteps > 0) {
@@ -811,13 +848,13 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
                     const s16x4 lo = lds_tr16(S + p * PA + a_rd[i]);
-                    const s16x4 hi = lds_tr16(S + p * PA + a_rd[i] + 4 * RSA);
+                    const s16x4 hi = lds_tr16(S + p * PA + a_rd4[i]);
                     av[p][i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
                 }
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     const s16x4 lo = lds_tr16(S + p * PB + b_rd[j]);
-                    const s16x4 hi = lds_tr16(S + p * PB + b_rd[j] + 4 * RSB);
+                    const s16x4 hi = lds_tr16(S + p * PB + b_rd4[j]);
                     bv[p][j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
                 }
             }
