@@ -52,6 +52,20 @@ __device__ __forceinline__ void split3(const f32x4 v, u32x2 &h, u32x2 &m, u32x2 
     }
 }
 
+// Raw buffer loads: 32-bit byte offsets with the hardware range check, so an out-of-range offset
+// (kOOB) returns zeros with no branch, no exec-mask juggling and no zero-fill moves.
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, int(bytes), 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ u32x4 bload4u(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 // PRE: B (weights) come pre-split in a.wsplit planes and are staged by copy (8 k per chunk, 3 x 16 B).
 template <int WAVES_M, int WAVES_N, int TM, int TN, bool PRE>
 __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
@@ -315,7 +329,7 @@ static void launch_x3(const IgemmArgs &a, hipStream_t s) {
 // next chunk's halo is loaded into registers at tap 0 and written behind an extra barrier after tap 8.
 // ------------------------------------------------------------------------------------------------
 template <int WAVES_M, int WAVES_N, int TM, int TN, int TW>
-__global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_halo_x3(IgemmArgs a) {
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(IgemmArgs a) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int BM = WAVES_M * TM * 32;
     constexpr int BN = WAVES_N * TN * 32;
@@ -355,9 +369,9 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_halo_x3(IgemmArgs
 
     auto soff = [](int row, int col) { return row * 32 + ((((col >> 1) ^ (row >> 3)) & 1) << 4) + ((col & 1) << 3); };
 
-    const float *a_ptr[A_PER];
+    uint32_t a_boff[A_PER];  // byte offset of the chunk's source (kOOB when outside the image: reads 0)
     int a_off[A_PER];
-    bool a_ok[A_PER], a_in[A_PER];
+    bool a_in[A_PER];
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
         const int e = tid + i * NT;
@@ -365,39 +379,38 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_halo_x3(IgemmArgs
         const int hp = a_in[i] ? (e >> 2) : 0, col = e & 3;
         const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
         const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
-        a_ok[i] = a_in[i] && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
-        a_ptr[i] = a.src + (a_ok[i] ? (size_t(img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4 : 0);
+        const bool ok = a_in[i] && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+        a_boff[i] = ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * 4u : kOOB;
         a_off[i] = soff(hp, col);
     }
-    int b_row[B_PER], b_off[B_PER];
-    bool b_ok[B_PER], b_in[B_PER];
+    uint32_t b_boff[B_PER];  // byte offset into plane 0 of the pre-split weights (kOOB past n_out)
+    int b_off[B_PER];
+    bool b_in[B_PER];
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
         const int e = tid + i * NT;
         const int r8 = e >> 1, half = e & 1;
         b_in[i] = e < B_CH;
-        b_ok[i] = b_in[i] && (n0 + r8 < a.n_out);
-        b_row[i] = (n0 + r8) * a.K + half * 8;
+        b_boff[i] = (b_in[i] && n0 + r8 < a.n_out) ? uint32_t((n0 + r8) * a.K + half * 8) * 2u : kOOB;
         b_off[i] = r8 * 32 + (((half ^ (r8 >> 3)) & 1) << 4);
     }
 
     f32x4 ra[A_PER];
     u32x4 pb[B_PER][3];
-    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
+    const uint32_t wplane_b = uint32_t(a.wplane) * 2u;
+    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, 3u * wplane_b);
     auto load_A = [&](int cc) {
 #pragma unroll
-        for (int i = 0; i < A_PER; ++i) ra[i] = a_ok[i] ? gload4(a_ptr[i] + cc * 16) : zero4;
+        for (int i = 0; i < A_PER; ++i) ra[i] = bload4(rs_src, a_boff[i] == kOOB ? kOOB : a_boff[i] + cc * 64u);
     };
     auto load_B = [&](int cc, int t) {
-        const int k0 = t * a.c + cc * 16;
-        const u32x4 z = {0u, 0u, 0u, 0u};
+        const uint32_t k0b = uint32_t(t * a.c + cc * 16) * 2u;
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-                pb[i][p] = b_ok[i] ? *(const __attribute__((address_space(1))) u32x4 *)(a.wsplit + p * a.wplane +
-                                                                                      size_t(b_row[i]) + k0)
-                                   : z;
+                pb[i][p] = bload4u(rs_w, b_boff[i] == kOOB ? kOOB : b_boff[i] + p * wplane_b + k0b);
     };
     auto store_A = [&]() {
 #pragma unroll
@@ -456,8 +469,10 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_halo_x3(IgemmArgs
             cc1 = cc + 1;
         }
         const bool more = s + 1 < nsteps;
-        if (t == 0 && cc + 1 < nc) load_A(cc + 1);
+        // vmcnt retires in order, so each step's wait for its weights also drains any older halo load: the
+        // next chunk's halo is therefore fetched during the last tap of this chunk, right before it is stored.
         if (more) load_B(cc1, t1);
+        if (more && t1 == 0) load_A(cc1);
         const unsigned char *SB = smem + A_BYTES + (s & 1) * B_STAGE;
         const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
         bf16x8 av[3][TM], bv[3][TN];
@@ -586,7 +601,9 @@ static void launch_halo(const IgemmArgs &a, int tw, hipStream_t s) {
 
 // 3x3 / stride 1 / same-size convs with pre-split weights take the halo path.
 static bool halo_eligible(const IgemmArgs &a) {
-    if (!a.wsplit || a.store_mode != 0 || a.stride != 1 || a.ntaps != 9 || a.ho != a.hs || a.wo != a.ws) return false;
+    if (!a.wsplit || !a.src_bytes || a.store_mode != 0 || a.stride != 1 || a.ntaps != 9 || a.ho != a.hs ||
+        a.wo != a.ws || 3 * a.wplane * 2 >= (int64_t(1) << 31))
+        return false;
     for (int t = 0; t < 9; ++t) {
         const int dy = int((a.tdy >> (4 * t)) & 15ull), dx = int((a.tdx >> (4 * t)) & 15ull);
         const int sdy = dy >= 8 ? dy - 16 : dy, sdx = dx >= 8 ? dx - 16 : dx;
@@ -645,16 +662,6 @@ bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
-// Raw buffer loads: 32-bit byte offsets with the hardware range check, so an out-of-range offset
-// (kOOB) returns zeros with no branch, no exec-mask juggling and no zero-fill moves.
-constexpr uint32_t kOOB = 0x80000000u;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, int(bytes), 0x00020000);
-}
-__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
 
 __device__ __forceinline__ s16x4 lds_tr16(const unsigned char *p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
