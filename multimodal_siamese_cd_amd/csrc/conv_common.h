@@ -90,6 +90,7 @@ struct WgradArgs {
     int Ng, M, kchunk;
     int grid_r, grid_j, remap;
     uint32_t rows_bytes, src_bytes;  // extents of rows/src for the buffer-load range check (< 2 GiB)
+    int n_img_w;                     // images (halo wgrad: split-K over 2x16 patches of all images)
     float *slabs;
     FastDiv div_hw, div_w, div_c;
 };
@@ -102,6 +103,9 @@ int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels);
 // x3 weight-grad instantiations, indexed like kWgradTiles (conv_f32.hip).
 const void *wgrad_x3_fn(int tile_id);
 void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
+// Halo weight grad (3x3 / stride 1 / same size, R and C multiples of 64, maps in 2x16 patches).
+const void *wgrad_halo_fn();
+void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
 
 // Conv math selection (scd_set_conv_math): SCD_MATH_X3 = split-bf16 MFMA where the shape allows it,
 // SCD_MATH_F32 = fp32 MFMA everywhere.  Initial value from SCD_CONV_MATH=f32|x3 (default x3).

@@ -681,21 +681,20 @@ static int wgrad_resident_blocks(const WgradTile &t) {
 // Split-K factor: the block count tiles*nsplit is quantised against the chip's resident capacity so the
 // last round is not a handful of lone workgroups (one wave per SIMD cannot keep the MFMA pipe busy):
 // maximise blocks / (rounds * capacity), ties (within 2%) to fewer splits (less slab traffic).
-static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
-    const int Ng = d->ntaps * d->src.c;
-    const WgradTile t = wgrad_tile(d->rows.c, Ng);
-    const int64_t M = pixels(d->rows);
-    const int64_t tiles = int64_t((d->rows.c + t.bm - 1) / t.bm) * ((Ng + t.bn - 1) / t.bn);
-    const int64_t cap = wgrad_resident_blocks(t);
-    int64_t maxsplit = (M + 255) / 256;  // keep >= 256 pixels per split
+// Split factor over K units (pixels, or 2x16 patches for the halo kernel): the block count tiles*nsplit is
+// quantised against the chip's resident capacity so the last round is not a handful of lone workgroups.
+// Maximise blocks / (rounds * capacity); ties (within 2%) go to fewer splits (less slab traffic).
+static void split_units(int64_t M, int64_t tiles, int64_t cap, int64_t min_units, int64_t gran, int *nsplit,
+                        int *kchunk) {
+    int64_t maxsplit = (M + min_units - 1) / min_units;
     const int64_t lim = (8 * cap + tiles - 1) / tiles;
     if (maxsplit > lim) maxsplit = lim;
     if (maxsplit < 1) maxsplit = 1;
-    int64_t best_kc = (M + 15) / 16 * 16;
+    int64_t best_kc = (M + gran - 1) / gran * gran;
     double best_eff = -1.0;
     for (int64_t want = 1; want <= maxsplit; ++want) {
         int64_t kc = (M + want - 1) / want;
-        kc = (kc + 15) / 16 * 16;
+        kc = (kc + gran - 1) / gran * gran;
         const int64_t n = (M + kc - 1) / kc;
         const int64_t blocks = tiles * n;
         const int64_t rounds = (blocks + cap - 1) / cap;
@@ -707,6 +706,44 @@ static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
     }
     *kchunk = int(best_kc);
     *nsplit = int((M + best_kc - 1) / best_kc);
+}
+
+// Halo weight grad eligibility: x3 math, 3x3 taps in standard order, stride 1, same-size maps,
+// R and C multiples of 64, maps tiled by 2x16 patches.
+static bool wgrad_halo_ok(const scd_wgrad_t *d) {
+    if (!conv_math_x3() || d->stride != 1 || d->ntaps != 9) return false;
+    for (int t = 0; t < 9; ++t)
+        if (d->dy[t] != t / 3 - 1 || d->dx[t] != t % 3 - 1) return false;
+    return d->rows.h == d->src.h && d->rows.w == d->src.w && d->rows.c % 64 == 0 && d->src.c % 64 == 0 &&
+           d->rows.h % 2 == 0 && d->rows.w % 16 == 0 && halo_enabled();
+}
+
+static int wgrad_halo_resident() {
+    static int cache = 0;
+    if (cache > 0) return cache;
+    int per_cu = 0, cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_halo_fn(), 256, 0) != hipSuccess || per_cu < 1 ||
+        cus < 1) {
+        (void)hipGetLastError();
+        return 2 * 256;
+    }
+    cache = per_cu * cus;
+    return cache;
+}
+
+static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
+    if (wgrad_halo_ok(d)) {
+        const int64_t patches = pixels(d->rows) / 32;
+        const int64_t tiles = int64_t(d->rows.c / 64) * (d->src.c / 64);
+        split_units(patches, tiles, wgrad_halo_resident(), 8, 1, nsplit, kchunk);
+        return;
+    }
+    const int Ng = d->ntaps * d->src.c;
+    const WgradTile t = wgrad_tile(d->rows.c, Ng);
+    const int64_t tiles = int64_t((d->rows.c + t.bm - 1) / t.bm) * ((Ng + t.bn - 1) / t.bn);
+    split_units(pixels(d->rows), tiles, wgrad_resident_blocks(t), 256, 16, nsplit, kchunk);
 }
 }  // namespace scd
 
@@ -763,6 +800,14 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
     a.rows_bytes = uint32_t(rb);
     a.src_bytes = uint32_t(sb);
     hipStream_t s = as_stream(stream);
+    if (wgrad_halo_ok(d)) {
+        a.n_img_w = d->rows.n;
+        a.grid_r = a.R / 64;
+        a.grid_j = a.C / 64;
+        a.remap = xcd_remap_enabled();
+        launch_wgrad_halo_x3(a, dim3(a.grid_r * a.grid_j * ns), s);
+        return launch_status("scd_conv_wgrad");
+    }
     const WgradTile t = wgrad_tile(a.R, Ng);
     a.grid_r = (a.R + t.bm - 1) / t.bm;
     a.grid_j = (Ng + t.bn - 1) / t.bn;

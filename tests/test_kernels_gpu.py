@@ -156,7 +156,7 @@ def test_wgrad_math_accuracy_vs_fp64(dev, ci, co):
     """
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(5 * ci + co)
-    n, h, w = 4, 40, 36
+    n, h, w = 4, 40, 48  # 2x16 patches: the x3 halo weight-grad path for C, R multiples of 64
     x = (torch.randn(n, h, w, ci, generator=g, dtype=torch.float64)
          * 10 ** (4 * torch.rand(n, h, w, ci, generator=g, dtype=torch.float64) - 2)).float()
     dy = (torch.randn(n, h, w, co, generator=g, dtype=torch.float64)
