@@ -13,7 +13,7 @@ import json
 import os
 from collections import defaultdict
 
-FAMILIES = {'igemm_f32': 'igemm', 'wgrad_f32': 'wgrad'}
+FAMILIES = {'igemm': 'igemm', 'wgrad_': 'wgrad'}  # substring -> family (igemm_f32/_x3/_halo_x3, wgrad_f32/_x3/_halo_x3)
 
 
 def load(path, counter):
@@ -22,10 +22,14 @@ def load(path, counter):
     for r in csv.DictReader(open(path)):
         if r['Counter_Name'] != counter:
             continue
+        name = r['Kernel_Name']
+        if 'wgrad_finalize' in name or 'wgrad_group_sum' in name:
+            continue
         for key, fam in FAMILIES.items():
-            if key in r['Kernel_Name']:
+            if key in name:
                 out[fam] += float(r['Counter_Value'])
                 n[fam] += 1
+                break
     return out, n
 
 
