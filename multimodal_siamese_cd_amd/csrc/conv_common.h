@@ -76,7 +76,6 @@ struct IgemmArgs {
     int64_t wplane;
     float *stat_rec;  // optional fused BN statistics [tile][n_out][2] (halo path)
     uint32_t src_bytes;  // byte extent of src for buffer loads (0 = above 2 GiB: no halo path)
-    int dbg;  // ablation flags (SCD_IGEMM_DBG, perf experiments only; 0 in production)
     FastDiv div_hw, div_w;
 };
 

@@ -561,7 +561,6 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     a.wsplit = d->wsplit;
     a.wplane = int64_t(a.n_out) * a.K;
     a.stat_rec = d->stat_rec;
-    a.dbg = 0;
     {
         const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * 4 + int64_t(d->src.c) * 4;
         a.src_bytes = sb < (int64_t(1) << 31) ? uint32_t(sb) : 0u;

@@ -150,10 +150,9 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const bool v = unsigned(a_sy[i] + dyt) < unsigned(a.hs) && unsigned(a_sx[i] + dxt) < unsigned(a.ws);
-            ra[i] = (v && !(a.dbg & 1)) ? gload4(a_base[i] + toff) : zero4;
+            ra[i] = v ? gload4(a_base[i] + toff) : zero4;
         }
         const int k0 = t * a.c + c0;
-        if (a.dbg & 2) return;
         if (PRE) {
             const u32x4 z = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -174,13 +173,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
         for (int i = 0; i < A_PER; ++i)
             if (tid + i * NT < A_CH) {
                 u32x2 h, m, l;
-                if (a.dbg & 16) {
-                    h = __builtin_bit_cast(u32x2, ra[i].xy);
-                    m = __builtin_bit_cast(u32x2, ra[i].zw);
-                    l = h;
-                } else {
-                    split3(ra[i], h, m, l);
-                }
+                split3(ra[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(S + a_off[i]) = h;
                 *reinterpret_cast<u32x2 *>(S + PLANE + a_off[i]) = m;
                 *reinterpret_cast<u32x2 *>(S + 2 * PLANE + a_off[i]) = l;
@@ -256,10 +249,8 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
         // small terms first: mm, hl, lh, hm, mh, hh
         constexpr int PA[6] = {1, 0, 2, 0, 1, 0};
         constexpr int PB[6] = {1, 2, 0, 1, 0, 0};
-        const int nq = (a.dbg & 8) ? 0 : ((a.dbg & 4) ? 1 : 6);
 #pragma unroll
         for (int q = 0; q < 6; ++q)
-            if (q >= 6 - nq)
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -311,8 +302,6 @@ static void launch_x3(const IgemmArgs &a, hipStream_t s) {
     b.grid_m = (a.M + BM - 1) / BM;
     b.grid_n = (a.n_out + BN - 1) / BN;
     b.remap = xcd_remap_enabled();
-    const char *dbg = getenv("SCD_IGEMM_DBG");
-    b.dbg = dbg ? atoi(dbg) : 0;
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
     if (a.wsplit)
         hipLaunchKernelGGL((igemm_x3<WM, WN, TM, TN, true>), grid, block, 0, s, b);
