@@ -91,6 +91,11 @@ int scd_set_conv_math(int32_t mode);
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);
+/* The same split of a packed weight matrix w [n_out][K] (K % 16 == 0) in MFMA-fragment order, the layout
+ * scd_igemm_t.wsplit expects: dst[p][nb][ks][lane][8] holds rows n = 32nb + (lane & 31) and
+ * k = 16ks + 8(lane >> 5) + j (zero for n >= n_out), so one wave's B fragment is one 1 KB load. */
+size_t scd_split_frag_bytes(int32_t n_out, int32_t K);
+int scd_split_bf16x3_frag(const float *w, int32_t n_out, int32_t K, uint16_t *dst, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Implicit-GEMM convolution on MFMA (arithmetic: scd_set_conv_math).
@@ -115,7 +120,7 @@ typedef struct scd_igemm {
     const float *bias;  /* [n_out] (store_mode 0) or [n_out/4] (store_mode 1) or NULL */
     scd_nhwc_t dst;
     int32_t store_mode;
-    /* Optional (SCD_MATH_X3 only): wpk pre-split by scd_split_bf16x3, planes [3][n_out*ntaps*src.c].
+    /* Optional (SCD_MATH_X3 only): wpk pre-split by scd_split_bf16x3_frag (fragment order).
      * The weights are then staged by copy instead of being split in every workgroup.  NULL = split on
      * the fly.  Must describe the same values as wpk. */
     const uint16_t *wsplit;

@@ -559,7 +559,7 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     a.div_hw = make_fastdiv(uint32_t(d->out_h * d->out_w));
     a.div_w = make_fastdiv(uint32_t(d->out_w));
     a.wsplit = d->wsplit;
-    a.wplane = int64_t(a.n_out) * a.K;
+    a.wplane = int64_t((a.n_out + 31) / 32) * 32 * a.K;  // fragment-major pre-split plane (rows padded to 32)
     a.stat_rec = d->stat_rec;
     {
         const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * 4 + int64_t(d->src.c) * 4;

@@ -129,10 +129,11 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
         const int row = ch / KC, col = ch % KC;
         b_in[i] = ch < B_CH;
         b_ok[i] = b_in[i] && (n0 + row < a.n_out);
-        if (PRE) {
+        if (PRE) {  // fragment-major pre-split weights: the 16-byte piece (n, 8 k) sits in lane (n&31) + 32*half
             const int r8 = ch >> 1, half = ch & 1;
-            b_ok[i] = b_in[i] && (n0 + r8 < a.n_out);
-            b_row[i] = (n0 + r8) * a.K + half * 8;
+            const int n = n0 + r8;
+            b_ok[i] = b_in[i] && (n < a.n_out);
+            b_row[i] = ((n >> 5) * (a.K / 16)) * 512 + ((n & 31) + 32 * half) * 8;
             b_off[i] = (BM + r8) * 32 + (((half ^ ((BM + r8) >> 3)) & 1) << 4);
         } else {
             b_row[i] = (n0 + row) * a.K + col * 4;
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
                     pb[i][p] = b_ok[i] ? *(const __attribute__((address_space(1))) u32x4 *)(a.wsplit + p * a.wplane +
-                                                                                          size_t(b_row[i]) + k0)
+                                                                                          size_t(b_row[i]) + (k0 / 16) * 512)
                                        : z;
         } else {
 #pragma unroll
@@ -318,7 +319,7 @@ static void launch_x3(const IgemmArgs &a, hipStream_t s) {
 // next chunk's halo is loaded into registers at tap 0 and written behind an extra barrier after tap 8.
 // ------------------------------------------------------------------------------------------------
 template <int WAVES_M, int WAVES_N, int TM, int TN, int TW>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(IgemmArgs a) {
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 2) void igemm_halo_x3(IgemmArgs a) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int BM = WAVES_M * TM * 32;
     constexpr int BN = WAVES_N * TN * 32;
@@ -327,13 +328,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(Igemm
     constexpr int HR = (TR + 2) * HWD;
     constexpr int A_CH = HR * 4;
     constexpr int A_PER = (A_CH + NT - 1) / NT;
-    constexpr int B_CH = BN * 2;
-    constexpr int B_PER = (B_CH + NT - 1) / NT;
     constexpr int PA = HR * 32;
-    constexpr int PB = BN * 32;
-    constexpr int A_BYTES = 3 * PA;
-    constexpr int B_STAGE = 3 * PB;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[A_BYTES + 2 * B_STAGE];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[3 * PA > 2 * WAVES_M * BN * 4 ? 3 * PA : 2 * WAVES_M * BN * 4];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -364,51 +360,39 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(Igemm
 
     uint32_t a_boff[A_PER];  // byte offset of the chunk's source (kOOB when outside the image: reads 0)
     int a_off[A_PER];
-    bool a_in[A_PER];
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
         const int e = tid + i * NT;
-        a_in[i] = e < A_CH;
-        const int hp = a_in[i] ? (e >> 2) : 0, col = e & 3;
+        const bool in = e < A_CH;
+        const int hp = in ? (e >> 2) : 0, col = e & 3;
         const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
         const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
-        const bool ok = a_in[i] && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+        const bool ok = in && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
         a_boff[i] = ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * 4u : kOOB;
-        a_off[i] = soff(hp, col);
+        a_off[i] = in ? soff(hp, col) : -1;
     }
-    uint32_t b_boff[B_PER];  // byte offset into plane 0 of the pre-split weights (kOOB past n_out)
-    int b_off[B_PER];
-    bool b_in[B_PER];
+    // B fragments straight from the fragment-major pre-split weights into registers: fragment (plane p,
+    // 32-row block nb, k step ks) of this wave's tile j is 1 KB at ((p*NB + nb)*KS + ks)*1024 + lane*16.
+    const int KS = a.K / 16, NB = (a.n_out + 31) / 32;
+    const uint32_t wplane_b = uint32_t(a.wplane) * 2u;
+    uint32_t b_base[TN];
 #pragma unroll
-    for (int i = 0; i < B_PER; ++i) {
-        const int e = tid + i * NT;
-        const int r8 = e >> 1, half = e & 1;
-        b_in[i] = e < B_CH;
-        b_boff[i] = (b_in[i] && n0 + r8 < a.n_out) ? uint32_t((n0 + r8) * a.K + half * 8) * 2u : kOOB;
-        b_off[i] = r8 * 32 + (((half ^ (r8 >> 3)) & 1) << 4);
+    for (int j = 0; j < TN; ++j) {
+        const int nb = (n0 >> 5) + wn * TN + j;
+        b_base[j] = nb < NB ? uint32_t(nb * KS) * 1024u + uint32_t(lane) * 16u : kOOB;
     }
 
     f32x4 ra[A_PER];
-    u32x4 pb[B_PER][3];
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
-    const uint32_t wplane_b = uint32_t(a.wplane) * 2u;
     const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, 3u * wplane_b);
     auto load_A = [&](int cc) {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) ra[i] = bload4(rs_src, a_boff[i] == kOOB ? kOOB : a_boff[i] + cc * 64u);
     };
-    auto load_B = [&](int cc, int t) {
-        const uint32_t k0b = uint32_t(t * a.c + cc * 16) * 2u;
-#pragma unroll
-        for (int i = 0; i < B_PER; ++i)
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                pb[i][p] = bload4u(rs_w, b_boff[i] == kOOB ? kOOB : b_boff[i] + p * wplane_b + k0b);
-    };
     auto store_A = [&]() {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i)
-            if (a_in[i]) {
+            if ((A_CH % NT == 0) || a_off[i] >= 0) {
                 u32x2 h, m, l;
                 split3(ra[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(smem + a_off[i]) = h;
@@ -416,14 +400,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(Igemm
                 *reinterpret_cast<u32x2 *>(smem + 2 * PA + a_off[i]) = l;
             }
     };
-    auto store_B = [&](int buf) {
-        unsigned char *S = smem + A_BYTES + buf * B_STAGE;
+    auto load_B = [&](int cc, int t, u32x4 (&bq)[3][TN]) {
+        const uint32_t ko = uint32_t(t * (a.c / 16) + cc) * 1024u;
 #pragma unroll
-        for (int i = 0; i < B_PER; ++i)
-            if (b_in[i]) {
+        for (int p = 0; p < 3; ++p)
 #pragma unroll
-                for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4 *>(S + p * PB + b_off[i]) = pb[i][p];
-            }
+            for (int j = 0; j < TN; ++j)
+                bq[p][j] = bload4u(rs_w, b_base[j] == kOOB ? kOOB : b_base[j] + ko + uint32_t(p) * wplane_b);
     };
 
     f32x16 acc[TM][TN];
@@ -435,38 +418,31 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(Igemm
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int h = lane >> 5;
-    int a_hr[TM], b_rd[TN];
+    int a_hr[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int p = wm * TM * 32 + i * 32 + (lane & 31);
         a_hr[i] = (p / TW + 1) * HWD + (p % TW) + 1;
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int row = wn * TN * 32 + j * 32 + (lane & 31);
-        b_rd[j] = row * 32 + (((h ^ (row >> 3)) & 1) << 4);
-    }
 
     const int nc = a.c / 16;
     const int nsteps = nc * a.ntaps;
+    u32x4 bq0[3][TN], bq1[3][TN];
     load_A(0);
-    load_B(0, 0);
+    load_B(0, 0, bq0);
     store_A();
-    store_B(0);
     __syncthreads();
-    int cc = 0, t = 0;
-    for (int s = 0; s < nsteps; ++s) {
+    int cc = 0, t = 0, s = 0;
+    // one step: B(s) in `cur`, B(s+1) prefetched into `nxt` while the MFMAs run; barriers only at chunk ends
+    auto step = [&](u32x4 (&cur)[3][TN], u32x4 (&nxt)[3][TN]) {
         int t1 = t + 1, cc1 = cc;
         if (t1 == a.ntaps) {
             t1 = 0;
             cc1 = cc + 1;
         }
         const bool more = s + 1 < nsteps;
-        // vmcnt retires in order, so each step's wait for its weights also drains any older halo load: the
-        // next chunk's halo is therefore fetched during the last tap of this chunk, right before it is stored.
-        if (more) load_B(cc1, t1);
+        if (more) load_B(cc1, t1, nxt);
         if (more && t1 == 0) load_A(cc1);
-        const unsigned char *SB = smem + A_BYTES + (s & 1) * B_STAGE;
         const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
         bf16x8 av[3][TM], bv[3][TN];
 #pragma unroll
@@ -480,8 +456,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(Igemm
 #pragma unroll
         for (int p = 0; p < 3; ++p)
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                bv[p][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(SB + p * PB + b_rd[j]));
+            for (int j = 0; j < TN; ++j) bv[p][j] = __builtin_bit_cast(bf16x8, cur[p][j]);
         constexpr int QA[6] = {1, 0, 2, 0, 1, 0};
         constexpr int QB[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
@@ -491,17 +466,21 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(Igemm
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[QA[q]][i], bv[QB[q]][j], acc[i][j], 0, 0, 0);
-        if (more) {
-            if (t1 == 0) {  // every wave is done with chunk cc's halo: overwrite it with chunk cc+1
-                __syncthreads();
-                store_A();
-            }
-            store_B((s + 1) & 1);
+        if (more && t1 == 0) {  // chunk end: every wave is done with this halo; overwrite it with the next one
+            __syncthreads();
+            store_A();
+            __syncthreads();
         }
-        __syncthreads();
         t = t1;
         cc = cc1;
+        ++s;
+    };
+    while (s + 1 < nsteps) {
+        step(bq0, bq1);
+        step(bq1, bq0);
     }
+    if (s < nsteps) step(bq0, bq1);
+    __syncthreads();  // the epilogue reuses smem for the statistics reduction
 
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -1130,6 +1109,33 @@ void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hip
     }
 }
 
+// Fragment-major pre-split weights: dst[p][nb][ks][lane][8] (bf16 bits of term p), the B-operand fragment of
+// rows n = 32*nb + (lane & 31), k = 16*ks + 8*(lane >> 5) + j of a [n_out][K] fp32 matrix (zero for n >= n_out).
+// One wave's fragment for (p, nb, ks) is 1 KB contiguous: a single coalesced load straight into registers.
+__global__ void split_frag_kernel(const float *__restrict__ w, int n_out, int K, int NB, uint16_t *__restrict__ dst) {
+    const int KS = K / 16;
+    const int64_t total = int64_t(NB) * KS * 64;
+    const int64_t plane = total * 8;
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        const int lane = int(e & 63);
+        const int64_t fk = e >> 6;  // nb * KS + ks
+        const int nb = int(fk / KS), ks = int(fk - int64_t(nb) * KS);
+        const int n = nb * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
+        f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+        if (n < n_out) {
+            v0 = gload4(w + size_t(n) * K + k0);
+            v1 = gload4(w + size_t(n) * K + k0 + 4);
+        }
+        u32x2 h0, m0, l0, h1, m1, l1;
+        split3(v0, h0, m0, l0);
+        split3(v1, h1, m1, l1);
+        uint16_t *o = dst + e * 8;
+        *reinterpret_cast<u32x4 *>(o) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+        *reinterpret_cast<u32x4 *>(o + plane) = u32x4{m0[0], m0[1], m1[0], m1[1]};
+        *reinterpret_cast<u32x4 *>(o + 2 * plane) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+    }
+}
+
 __global__ void split_bf16x3_kernel(const float *__restrict__ src, int64_t n4, uint16_t *__restrict__ dst, int64_t n) {
     for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < n4; e += int64_t(gridDim.x) * blockDim.x) {
         u32x2 h, m, l;
@@ -1143,6 +1149,25 @@ __global__ void split_bf16x3_kernel(const float *__restrict__ src, int64_t n4, u
 }  // namespace scd
 
 using namespace scd;
+
+extern "C" size_t scd_split_frag_bytes(int32_t n_out, int32_t K) {
+    if (n_out < 1 || K < 16 || K % 16) return 0;
+    return size_t(3) * ((n_out + 31) / 32) * 32 * size_t(K) * sizeof(uint16_t);
+}
+
+extern "C" int scd_split_bf16x3_frag(const float *w, int32_t n_out, int32_t K, uint16_t *dst, scd_stream_t stream) {
+    clear_error();
+    if (!w || !dst || n_out < 1 || K < 16 || K % 16 || !aligned16(w) || !aligned16(dst)) {
+        set_error("split_bf16x3_frag: need K %% 16 == 0 and 16-byte aligned w/dst (n_out=%d K=%d)", n_out, K);
+        return SCD_ERR_ARG;
+    }
+    const int NB = (n_out + 31) / 32;
+    const int64_t total = int64_t(NB) * (K / 16) * 64;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(split_frag_kernel, dim3(unsigned(blocks)), dim3(256), 0, as_stream(stream), w, n_out, K, NB, dst);
+    return launch_status("scd_split_bf16x3_frag");
+}
 
 extern "C" int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream) {
     clear_error();

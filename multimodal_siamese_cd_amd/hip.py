@@ -12,7 +12,7 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_int8, c_int32, c_int64, 
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libscd.so")
+LIB_PATH = os.environ.get("SCD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libscd.so")
 
 
 class NHWC(ctypes.Structure):
@@ -70,6 +70,8 @@ _SIGS = {
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_set_conv_math": ([c_int32], c_int),
     "scd_split_bf16x3": ([c_void_p, c_int64, c_void_p, c_void_p], c_int),
+    "scd_split_frag_bytes": ([c_int32, c_int32], c_size_t),
+    "scd_split_bf16x3_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
     "scd_igemm_stat_tiles": ([POINTER(IGEMM), POINTER(c_int32)], c_int),
     "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
@@ -207,7 +209,7 @@ def pack_conv3x3(w: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch
     out = torch.empty((co * 9 * ci_pad) if mode == 0 else (ci * 9 * co), device=w.device, dtype=torch.float32)
     _check(lib().scd_pack_conv3x3(w.contiguous().data_ptr(), co, ci, ci_pad, mode, out.data_ptr(), _stream()),
            "scd_pack_conv3x3")
-    return _attach_split(out)
+    return _attach_split(out, co, 9 * ci_pad) if mode == 0 else _attach_split(out, ci, 9 * co)
 
 
 def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:
@@ -215,7 +217,7 @@ def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:
     out = torch.empty(ci * co * 4, device=w.device, dtype=torch.float32)
     _check(lib().scd_pack_convT2x2(w.contiguous().data_ptr(), ci, co, mode, out.data_ptr(), _stream()),
            "scd_pack_convT2x2")
-    return _attach_split(out)
+    return _attach_split(out, 4 * co, ci) if mode == 0 else _attach_split(out, ci, 4 * co)
 
 
 def split_bf16x3(src: torch.Tensor) -> torch.Tensor:
@@ -226,10 +228,18 @@ def split_bf16x3(src: torch.Tensor) -> torch.Tensor:
     return dst
 
 
-def _attach_split(wpk: torch.Tensor) -> torch.Tensor:
+def split_bf16x3_frag(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
+    """Fragment-major exact 3-way bf16 split of a packed [n_out][K] fp32 weight matrix (see scd.h)."""
+    nbytes = lib().scd_split_frag_bytes(n_out, K)
+    dst = torch.empty(nbytes // 2, dtype=torch.int16, device=wpk.device)
+    _check(lib().scd_split_bf16x3_frag(wpk.data_ptr(), n_out, K, dst.data_ptr(), _stream()), "scd_split_bf16x3_frag")
+    return dst
+
+
+def _attach_split(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
     """Under the x3 conv math, pre-split packed weights once so every workgroup stages them by copy."""
-    if wpk.numel() % 8 == 0 and conv_math() == 'x3':
-        wpk._x3 = split_bf16x3(wpk)
+    if K % 16 == 0 and conv_math() == 'x3':
+        wpk._x3 = split_bf16x3_frag(wpk, n_out, K)
     return wpk
 
 
