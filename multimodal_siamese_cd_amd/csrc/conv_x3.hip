@@ -319,7 +319,7 @@ static void launch_x3(const IgemmArgs &a, hipStream_t s) {
 // next chunk's halo is loaded into registers at tap 0 and written behind an extra barrier after tap 8.
 // ------------------------------------------------------------------------------------------------
 template <int WAVES_M, int WAVES_N, int TM, int TN, int TW>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 2) void igemm_halo_x3(IgemmArgs a) {
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 3) void igemm_halo_x3(IgemmArgs a) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int BM = WAVES_M * TM * 32;
     constexpr int BN = WAVES_N * TN * 32;
@@ -427,21 +427,22 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 2) void igemm_halo_x3(Igemm
 
     const int nc = a.c / 16;
     const int nsteps = nc * a.ntaps;
-    u32x4 bq0[3][TN], bq1[3][TN];
+    u32x4 bq[3][TN];
     load_A(0);
-    load_B(0, 0, bq0);
+    load_B(0, 0, bq);
     store_A();
     __syncthreads();
-    int cc = 0, t = 0, s = 0;
-    // one step: B(s) in `cur`, B(s+1) prefetched into `nxt` while the MFMAs run; barriers only at chunk ends
-    auto step = [&](u32x4 (&cur)[3][TN], u32x4 (&nxt)[3][TN]) {
+    int cc = 0, t = 0;
+    // B(s) in registers; B(s+1) is loaded into the same registers once the step's MFMAs are issued (they
+    // still execute for several hundred cycles, hiding most of the latency).  One B register set keeps the
+    // kernel at 3 waves per SIMD.  Barriers only at 16-channel chunk ends (halo rewrite).
+    for (int s = 0; s < nsteps; ++s) {
         int t1 = t + 1, cc1 = cc;
         if (t1 == a.ntaps) {
             t1 = 0;
             cc1 = cc + 1;
         }
         const bool more = s + 1 < nsteps;
-        if (more) load_B(cc1, t1, nxt);
         if (more && t1 == 0) load_A(cc1);
         const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
         bf16x8 av[3][TM], bv[3][TN];
@@ -456,7 +457,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 2) void igemm_halo_x3(Igemm
 #pragma unroll
         for (int p = 0; p < 3; ++p)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bv[p][j] = __builtin_bit_cast(bf16x8, cur[p][j]);
+            for (int j = 0; j < TN; ++j) bv[p][j] = __builtin_bit_cast(bf16x8, bq[p][j]);
         constexpr int QA[6] = {1, 0, 2, 0, 1, 0};
         constexpr int QB[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
@@ -466,6 +467,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 2) void igemm_halo_x3(Igemm
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[QA[q]][i], bv[QB[q]][j], acc[i][j], 0, 0, 0);
+        if (more) load_B(cc1, t1, bq);
         if (more && t1 == 0) {  // chunk end: every wave is done with this halo; overwrite it with the next one
             __syncthreads();
             store_A();
@@ -473,13 +475,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 2) void igemm_halo_x3(Igemm
         }
         t = t1;
         cc = cc1;
-        ++s;
-    };
-    while (s + 1 < nsteps) {
-        step(bq0, bq1);
-        step(bq1, bq0);
     }
-    if (s < nsteps) step(bq0, bq1);
     __syncthreads();  // the epilogue reuses smem for the statistics reduction
 
 #pragma unroll
