@@ -39,6 +39,13 @@ def pad8(c: int) -> int:
     return (c + 7) // 8 * 8
 
 
+def pad_in(c: int) -> int:
+    """Input channel padding: the MFMA K granule -- 16 under the split-bf16 arithmetic (so the input layer
+    takes the halo x3 path with fused BatchNorm statistics), 8 under fp32 MFMA."""
+    g = 16 if hip.conv_math() == 'x3' else 8
+    return (c + g - 1) // g * g
+
+
 # ------------------------------------------------------------------------------------------------
 # BatchNorm + ReLU
 # ------------------------------------------------------------------------------------------------
@@ -181,26 +188,26 @@ def _dc_backward(g_out: torch.Tensor, saved, dc, need_dx: bool):
 # Input packing
 # ------------------------------------------------------------------------------------------------
 def pack_pair(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:
-    """Siamese input: [2B, H, W, pad8(C)] NHWC with t1 images first (one shared-encoder batch)."""
+    """Siamese input: [2B, H, W, pad_in(C)] NHWC with t1 images first (one shared-encoder batch)."""
     hip.ensure_device(x_t1)
     if x_t1.requires_grad or x_t2.requires_grad:
         raise NotImplementedError("input gradients are not computed by the HIP path")
     b, c, h, w = x_t1.shape
     c_count = c - c_begin if c_count is None else c_count
-    out = torch.empty((2 * b, h, w, pad8(c_count)), device=x_t1.device, dtype=_F32)
+    out = torch.empty((2 * b, h, w, pad_in(c_count)), device=x_t1.device, dtype=_F32)
     hip.pack_nchw(x_t1.float(), c_begin, c_count, out[:b])
     hip.pack_nchw(x_t2.float(), c_begin, c_count, out[b:])
     return out
 
 
 def pack_stream(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:
-    """Early-fusion input cat((t1[bands], t2[bands]), dim=1) as [B, H, W, pad8(2*nb)] NHWC."""
+    """Early-fusion input cat((t1[bands], t2[bands]), dim=1) as [B, H, W, pad_in(2*nb)] NHWC."""
     hip.ensure_device(x_t1)
     if x_t1.requires_grad or x_t2.requires_grad:
         raise NotImplementedError("input gradients are not computed by the HIP path")
     b, c, h, w = x_t1.shape
     c_count = c - c_begin if c_count is None else c_count
-    cp = pad8(2 * c_count)
+    cp = pad_in(2 * c_count)
     out = torch.empty((b, h, w, cp), device=x_t1.device, dtype=_F32)
     # t1 bands -> channels [0, nb) (zero-padding the rest), then t2 bands -> [nb, 2nb)
     hip.pack_nchw(x_t1.float(), c_begin, c_count, out, 0, cp)  # t1 bands -> [0, nb), zero-pad to cp
