@@ -88,6 +88,11 @@ int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, floa
  * ------------------------------------------------------------------------------------------- */
 enum scd_conv_math { SCD_MATH_QUERY = -1, SCD_MATH_F32 = 0, SCD_MATH_X3 = 1 };
 int scd_set_conv_math(int32_t mode);
+/* Tile selection of the 16x16x32-MFMA halo conv kernel (SCD_MATH_X3, 3x3 / stride 1, C % 32 == 0):
+ * 0 = off (32x32x16 halo kernel), 1 = automatic, 2 + id = force tile id (0: 128 px x 128 ch, 1: 128 x 64,
+ * 2: 64 x 128).  Returns the previous mode; -1 only queries.  Process-wide; results are identical up to
+ * summation order. */
+int scd_set_halo16(int32_t mode);
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);

@@ -20,51 +20,9 @@
 // LDS image: per stage and per operand, three planes (h, m, l) of [row][16 bf16] with 32-byte rows.  The
 // 16-byte half of a row is XOR-swizzled with row bit 3, which makes the ds_read_b128 operand reads
 // conflict-free; see the bank analysis in DESIGN.md.
-#include "conv_common.h"
+#include "x3_common.h"
 
 namespace scd {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-    const f32x2 v = {a, b};
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));  // v_cvt_pk_bf16_f32 (RNE)
-}
-__device__ __forceinline__ float bf16_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
-__device__ __forceinline__ float bf16_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
-
-// Split four consecutive fp32 values into their h, m, l bf16 terms (4 bf16 = 8 bytes each).
-__device__ __forceinline__ void split3(const f32x4 v, u32x2 &h, u32x2 &m, u32x2 &l) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        const float x0 = v[2 * p], x1 = v[2 * p + 1];
-        const uint32_t ph = cvt_pk_bf16(x0, x1);
-        const float r0 = x0 - bf16_lo(ph), r1 = x1 - bf16_hi(ph);
-        const uint32_t pm = cvt_pk_bf16(r0, r1);
-        const float s0 = r0 - bf16_lo(pm), s1 = r1 - bf16_hi(pm);
-        h[p] = ph;
-        m[p] = pm;
-        l[p] = cvt_pk_bf16(s0, s1);
-    }
-}
-
-// Raw buffer loads: 32-bit byte offsets with the hardware range check, so an out-of-range offset
-// (kOOB) returns zeros with no branch, no exec-mask juggling and no zero-fill moves.
-constexpr uint32_t kOOB = 0x80000000u;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, int(bytes), 0x00020000);
-}
-__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-__device__ __forceinline__ u32x4 bload4u(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
 
 // PRE: B (weights) come pre-split in a.wsplit planes and are staged by copy (8 k per chunk, 3 x 16 B).
 template <int WAVES_M, int WAVES_N, int TM, int TN, bool PRE>
@@ -602,7 +560,8 @@ static int halo_pick(const IgemmArgs &a, int *bm, int *tw) {
 
 int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels) {
     int bm = 0, tw = 0;
-    if (!conv_math_x3() || !halo_pick(a, &bm, &tw)) return 0;
+    if (!conv_math_x3()) return 0;
+    if (!halo16_pick(a, halo_eligible(a), &bm, &tw) && !halo_pick(a, &bm, &tw)) return 0;
     *tile_pixels = bm;
     return a.n_img * (a.ho * a.wo / bm);
 }
@@ -610,6 +569,10 @@ int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels) {
 bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
     if (a.c % 16) return false;
     int bm = 0, tw = 0;
+    if (const int c16 = halo16_pick(a, halo_eligible(a), &bm, &tw)) {
+        launch_halo16(a, c16, tw, s);
+        return true;
+    }
     switch (halo_pick(a, &bm, &tw)) {
         case 1: launch_halo<2, 2, 2, 2>(a, tw, s); return true;
         case 2: launch_halo<4, 1, 2, 2>(a, tw, s); return true;

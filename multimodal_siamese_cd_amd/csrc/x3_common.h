@@ -1,0 +1,51 @@
+// Shared pieces of the split-bf16 ("x3") conv kernels (conv_x3.hip, conv_halo16.hip): operand types, the
+// exact three-way bf16 split and raw buffer loads.
+#pragma once
+
+#include "conv_common.h"
+
+namespace scd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+    const f32x2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));  // v_cvt_pk_bf16_f32 (RNE)
+}
+__device__ __forceinline__ float bf16_lo(uint32_t p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t p) { return __builtin_bit_cast(float, p & 0xffff0000u); }
+
+// Split four consecutive fp32 values into their h, m, l bf16 terms (4 bf16 = 8 bytes each).
+__device__ __forceinline__ void split3(const f32x4 v, u32x2 &h, u32x2 &m, u32x2 &l) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const float x0 = v[2 * p], x1 = v[2 * p + 1];
+        const uint32_t ph = cvt_pk_bf16(x0, x1);
+        const float r0 = x0 - bf16_lo(ph), r1 = x1 - bf16_hi(ph);
+        const uint32_t pm = cvt_pk_bf16(r0, r1);
+        const float s0 = r0 - bf16_lo(pm), s1 = r1 - bf16_hi(pm);
+        h[p] = ph;
+        m[p] = pm;
+        l[p] = cvt_pk_bf16(s0, s1);
+    }
+}
+
+// Raw buffer loads: 32-bit byte offsets with the hardware range check, so an out-of-range offset
+// (kOOB) returns zeros with no branch, no exec-mask juggling and no zero-fill moves.
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, int(bytes), 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ u32x4 bload4u(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+}  // namespace scd

@@ -69,6 +69,7 @@ _SIGS = {
     "scd_pack_conv3x3": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_set_conv_math": ([c_int32], c_int),
+    "scd_set_halo16": ([c_int32], c_int),
     "scd_split_bf16x3": ([c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "scd_split_frag_bytes": ([c_int32, c_int32], c_size_t),
     "scd_split_bf16x3_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
@@ -254,6 +255,14 @@ def set_conv_math(mode) -> str:
     if rc < 0:
         _check(rc, "scd_set_conv_math")
     return {v: k for k, v in _MATH_NAMES.items()}[rc]
+
+
+def set_halo16(mode: int) -> int:
+    """Tile selection of the 16x16x32-MFMA halo conv kernel (see scd.h); returns the previous mode."""
+    rc = lib().scd_set_halo16(int(mode))
+    if rc < 0:
+        _check(rc, "scd_set_halo16")
+    return rc
 
 
 def conv_math() -> str:

@@ -262,6 +262,56 @@ def test_conv_fused_bn_stats(dev, n, h, w, ci, co, nseg):
         hip.set_conv_math(prev)
 
 
+HALO16_SHAPES = [  # n, h, w, cin, cout: tile widths 64 / 32 / 16, ragged n_out, 512-channel layers
+    (2, 32, 64, 64, 128),
+    (2, 16, 32, 128, 128),
+    (1, 16, 16, 32, 256),
+    (2, 8, 64, 96, 136),
+    (2, 16, 16, 512, 512),
+]
+
+
+@pytest.mark.parametrize('cfg', [0, 1, 2])
+@pytest.mark.parametrize('n,h,w,ci,co', HALO16_SHAPES)
+def test_conv_halo16_tiles(dev, cfg, n, h, w, ci, co):
+    """16x16x32-MFMA halo kernel, every tile config forced: forward (+ bias, fused BN tile statistics) and
+    data-grad against torch fp32, statistics against the separate pass."""
+    from multimodal_siamese_cd_amd import hip
+    prev_m = hip.set_conv_math('x3')
+    prev_h = hip.set_halo16(2 + cfg)
+    try:
+        g = torch.Generator().manual_seed(11 * cfg + ci + co)
+        x = torch.randn(n, h, w, ci, generator=g)
+        wt = torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)
+        b = torch.randn(co, generator=g) + 2.0
+        ref = nhwc_t(F.conv2d(nchw(x), wt, b, padding=1))
+        xd, wd, bd = x.to(dev), wt.to(dev), b.to(dev)
+        wpk = hip.pack_conv3x3(wd, 0)
+        y = torch.empty(n, h, w, co, device=dev)
+        ntiles, tpx = hip.igemm_stat_tiles(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y))
+        assert ntiles * tpx == n * h * w and tpx == (128 if cfg < 2 else 64)
+        rec = torch.empty(ntiles * co * 2, device=dev)
+        hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, bd, hip.nhwc(y), stat_rec=rec)
+        assert rel(y, ref) < TOL
+        # per-tile (mean, M2) records against the host definition on the kernel's own output
+        tw = next(c for c in (64, 32, 16) if w % c == 0 and h % (tpx // c) == 0)
+        tr = tpx // tw
+        yy = y.double().cpu().reshape(n, h // tr, tr, w // tw, tw, co).permute(0, 1, 3, 2, 4, 5).reshape(-1, tpx, co)
+        r = rec.double().cpu().reshape(ntiles, co, 2)
+        assert rel(r[..., 0], yy.mean(1)) < 2e-6
+        assert rel(r[..., 1], ((yy - yy.mean(1, keepdim=True)) ** 2).sum(1)) < 2e-5
+        # data-grad (n_out = ci)
+        if ci % 4 == 0:
+            dy = torch.randn(n, h, w, co, generator=g)
+            ref_dx = nhwc_t(torch.nn.grad.conv2d_input((n, ci, h, w), wt, nchw(dy), padding=1))
+            dx = torch.empty(n, h, w, ci, device=dev)
+            hip.conv_igemm(hip.nhwc(dy.to(dev)), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wd, 1), ci, None, hip.nhwc(dx))
+            assert rel(dx, ref_dx) < TOL
+    finally:
+        hip.set_halo16(prev_h)
+        hip.set_conv_math(prev_m)
+
+
 @pytest.mark.parametrize('n,h,w,c,nseg', [(4, 16, 16, 8, 2), (2, 33, 17, 64, 2), (2, 64, 64, 16, 1), (6, 8, 8, 512, 2)])
 def test_batchnorm_relu_train_forward_backward(dev, n, h, w, c, nseg):
     from multimodal_siamese_cd_amd import hip

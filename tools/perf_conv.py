@@ -55,13 +55,16 @@ def main():
     ap.add_argument('--only', default=None)
     ap.add_argument('--layer', default=None, help='run only this layer name (e.g. enc1b)')
     ap.add_argument('--math', default=None, choices=['f32', 'x3'], help='conv arithmetic (default: library default)')
+    ap.add_argument('--halo16', default=None,
+                    help='comma-separated scd_set_halo16 modes, interleaved per layer (e.g. 0,1,3)')
     args = ap.parse_args()
     hip.load_library()
     if args.math:
         hip.set_conv_math(args.math)
     print(f'conv math: {hip.conv_math()}')
     dev = torch.device('cuda:0')
-    tot = {'fwd': [0.0, 0.0], 'dgrad': [0.0, 0.0], 'wgrad': [0.0, 0.0]}
+    modes = [None] if args.halo16 is None else [int(m) for m in args.halo16.split(',')]
+    tots = {m: {'fwd': [0.0, 0.0], 'dgrad': [0.0, 0.0], 'wgrad': [0.0, 0.0]} for m in modes}
     print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"cin":>5s} {"cout":>5s} | '
           f'{"fwd ms":>8s} {"TF/s":>6s} | {"dgrad ms":>8s} {"TF/s":>6s} | {"wgrad ms":>8s} {"TF/s":>6s}')
     for name, n, s, ci, co in layers(args.batch):
@@ -75,34 +78,41 @@ def main():
         wf = hip.pack_conv3x3(w, 0)
         wb = hip.pack_conv3x3(w, 1)
         flops = 2.0 * n * s * s * co * 9 * ci
-        res = {}
-        if args.only in (None, 'fwd'):
-            res['fwd'] = timeit(lambda: hip.conv_igemm(hip.nhwc(x), s, s, 1, hip.TAPS_3X3, wf, co, None,
-                                                       hip.nhwc(y)), args.reps)
-        if args.only in (None, 'dgrad') and not name.startswith('enc0a'):
-            res['dgrad'] = timeit(lambda: hip.conv_igemm(hip.nhwc(dy), s, s, 1, hip.TAPS_3X3, wb, ci, None,
-                                                         hip.nhwc(dx)), args.reps)
-        if args.only in (None, 'wgrad'):
-            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dy), hip.nhwc(x), 1, hip.TAPS_3X3)
-            slabs = torch.empty(nbytes // 4, device=dev)
-            res['wgrad'] = timeit(lambda: hip.conv_wgrad(d, slabs), args.reps)
-        cells = []
-        for k in ('fwd', 'dgrad', 'wgrad'):
-            if k in res:
-                t = res[k]
-                tot[k][0] += t
-                tot[k][1] += flops
-                cells.append(f'{t:8.3f} {flops / t / 1e9:6.1f}')
-            else:
-                cells.append(f'{"-":>8s} {"-":>6s}')
-        print(f'{name:8s} {n:3d} {s:4d} {ci:5d} {co:5d} | ' + ' | '.join(cells), flush=True)
-    allt = sum(v[0] for v in tot.values())
-    allf = sum(v[1] for v in tot.values())
-    for k, (t, f) in tot.items():
-        if t:
-            print(f'{k:6s} total {t:8.2f} ms  {f / t / 1e9:6.1f} TF/s  ({f / t / 1e9 / PEAK * 100:.1f}% of fp32 peak)')
-    print(f'3x3 total {allt:8.2f} ms  {allf / allt / 1e9:6.1f} TF/s  ({allf / allt / 1e9 / PEAK * 100:.1f}% of peak)')
-
+        for mode in modes:
+            if mode is not None:
+                hip.set_halo16(mode)
+            tot = tots[mode]
+            res = {}
+            if args.only in (None, 'fwd'):
+                res['fwd'] = timeit(lambda: hip.conv_igemm(hip.nhwc(x), s, s, 1, hip.TAPS_3X3, wf, co, None,
+                                                           hip.nhwc(y)), args.reps)
+            if args.only in (None, 'dgrad') and not name.startswith('enc0a'):
+                res['dgrad'] = timeit(lambda: hip.conv_igemm(hip.nhwc(dy), s, s, 1, hip.TAPS_3X3, wb, ci, None,
+                                                             hip.nhwc(dx)), args.reps)
+            if args.only in (None, 'wgrad'):
+                d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dy), hip.nhwc(x), 1, hip.TAPS_3X3)
+                slabs = torch.empty(nbytes // 4, device=dev)
+                res['wgrad'] = timeit(lambda: hip.conv_wgrad(d, slabs), args.reps)
+            cells = []
+            for k in ('fwd', 'dgrad', 'wgrad'):
+                if k in res:
+                    t = res[k]
+                    tot[k][0] += t
+                    tot[k][1] += flops
+                    cells.append(f'{t:8.3f} {flops / t / 1e9:6.1f}')
+                else:
+                    cells.append(f'{"-":>8s} {"-":>6s}')
+            tag = name if mode is None else f'{name}/{mode}'
+            print(f'{tag:8s} {n:3d} {s:4d} {ci:5d} {co:5d} | ' + ' | '.join(cells), flush=True)
+    for mode, tot in tots.items():
+        if mode is not None:
+            print(f'-- halo16 mode {mode}')
+        allt = sum(v[0] for v in tot.values())
+        allf = sum(v[1] for v in tot.values())
+        for k, (t, f) in tot.items():
+            if t:
+                print(f'{k:6s} total {t:8.2f} ms  {f / t / 1e9:6.1f} TF/s  ({f / t / 1e9 / PEAK * 100:.1f}% of fp32 peak)')
+        print(f'3x3 total {allt:8.2f} ms  {allf / allt / 1e9:6.1f} TF/s  ({allf / allt / 1e9 / PEAK * 100:.1f}% of peak)')
 
 if __name__ == '__main__':
     main()
