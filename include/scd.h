@@ -93,6 +93,9 @@ int scd_set_conv_math(int32_t mode);
  * 2: 64 x 128).  Returns the previous mode; -1 only queries.  Process-wide; results are identical up to
  * summation order. */
 int scd_set_halo16(int32_t mode);
+/* Halo weight-grad kernel selection (SCD_MATH_X3, 3x3 / stride 1, R and C multiples of 64): 0 = 32x32x16
+ * MFMA kernel, 1 = 16x16x32 MFMA kernel (default).  Returns the previous mode; -1 only queries. */
+int scd_set_wgrad16(int32_t mode);
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);

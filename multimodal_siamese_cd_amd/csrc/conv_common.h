@@ -102,6 +102,10 @@ int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels);
 // 16x16x32-MFMA halo igemm (conv_halo16.hip): 0 when `a` does not take it, else its config; launcher.
 int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw);
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
+// 16x16x32-MFMA halo weight grad (conv_halo16.hip), selected by wgrad16_mode() (scd_set_wgrad16).
+int wgrad16_mode();
+const void *wgrad_halo16_fn();
+void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
 // x3 weight-grad instantiations, indexed like kWgradTiles (conv_f32.hip).
 const void *wgrad_x3_fn(int tile_id);
 void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);

@@ -718,7 +718,8 @@ static bool wgrad_halo_ok(const scd_wgrad_t *d) {
 }
 
 static int wgrad_halo_resident() {
-    static int cache = 0;
+    static int caches[2] = {0, 0};  // per halo weight-grad kernel (scd_set_wgrad16)
+    int &cache = caches[wgrad16_mode() ? 1 : 0];
     if (cache > 0) return cache;
     int per_cu = 0, cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

@@ -344,9 +344,231 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Halo weight gradient on v_mfma_f32_16x16x32_bf16 (3x3 / stride 1 / same size, R and C multiples of 64).
+//   dW[r][t][c] = sum_p dY[p][r] * X[p + off_t][c]
+// Same decomposition as wgrad_halo_x3 (conv_x3.hip): a block owns 64 rows r x 64 channels c x 9 taps and
+// walks a range of 2x16-pixel patches (split-K); per patch the dY patch (32 px x 64 r) and the X halo
+// (4 x 18 px x 64 c) are staged once, split into bf16 planes, and every tap is a shifted read.
+// One MFMA consumes the whole 32-pixel patch as its k.  k = 8g + j of lane group g is pixel
+// (g >> 1, 4(g & 1) + (j & 3) + 8(j >> 2)): each 32-lane half of a transposed read then touches 8
+// consecutive staged rows, which the 160-byte row stride spreads over the 8 distinct 32-byte bank slots
+// (conflict-free for every tap shift).
+// Roles: A = X (rows = channels c), B = dY (columns = r), so a lane's result is 4 consecutive c of one r:
+// one 16-byte slab store per tile.
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int kW16RS = 160;
+
+template <int T, int CB, int PB, int HW_>
+__device__ __forceinline__ void w16_read_x(s16x4 (&f)[6], uint32_t xbase) {
+    constexpr int toff = (T / 3) * HW_ + (T % 3);  // (1 + dy) * HW_ + (1 + dx)
+    tr_read<0 * PB + toff * kW16RS + CB * 32>(f[0], xbase);
+    tr_read<0 * PB + (toff + 8) * kW16RS + CB * 32>(f[1], xbase);
+    tr_read<1 * PB + toff * kW16RS + CB * 32>(f[2], xbase);
+    tr_read<1 * PB + (toff + 8) * kW16RS + CB * 32>(f[3], xbase);
+    tr_read<2 * PB + toff * kW16RS + CB * 32>(f[4], xbase);
+    tr_read<2 * PB + (toff + 8) * kW16RS + CB * 32>(f[5], xbase);
+}
+
+// One half tap (tap T, channel block CB): wait for its X fragments, then six split products x 2 r-blocks.
+template <int T, int CB, int WAIT>
+__device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f)[6]) {
+    bf16x8 x0 = cat8(f[0], f[1]), x1 = cat8(f[2], f[3]), x2 = cat8(f[4], f[5]);
+    lds_wait<WAIT>(x0, x1, x2);
+    if (T == 0 && CB == 0) {
+        lds_wait<WAIT>(dv[0][0], dv[1][0], dv[2][0]);
+        lds_wait<WAIT>(dv[0][1], dv[1][1], dv[2][1]);
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
+        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[2][rb], acc[T][CB][rb], 0, 0, 0);
+        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
+        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
+        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
+        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
+    }
+}
+
+// Half taps H = 2T + CB, one ahead: compute H from buffer H & 1, then refill that buffer with H + 2.
+template <int H, int PB, int HW_>
+__device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f0)[6], s16x4 (&f1)[6],
+                                          uint32_t xbase) {
+    if constexpr (H < 18) {
+        s16x4 (&f)[6] = (H & 1) ? f1 : f0;
+        w16_half<H / 2, H % 2, (H == 17 ? 0 : 6)>(acc, dv, f);
+        if constexpr (H + 2 < 18) w16_read_x<(H + 2) / 2, (H + 2) % 2, PB, HW_>(f, xbase);
+        w16_chain<H + 1, PB, HW_>(acc, dv, f0, f1, xbase);
+    }
+}
+}  // namespace
+
+__global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
+    constexpr int PH = 2, PW = 16, P = PH * PW;
+    constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
+    constexpr int RS = kW16RS;
+    constexpr int PA = P * RS, PB = HP * RS;            // plane bytes
+    constexpr int A_CH = P * 16, B_CH = HP * 16;        // 4-channel pieces
+    constexpr int A_PER = A_CH / 256, B_PER = (B_CH + 255) / 256;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[3 * PA + 3 * PB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wi = wid >> 1, wj = wid & 1;
+    const uint32_t per_split = uint32_t(a.grid_r * a.grid_j);
+    const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int split = int(L / per_split);
+    const int rem = int(L - uint32_t(split) * per_split);
+    const int ct = rem / a.grid_r;
+    const int r0 = (rem - ct * a.grid_r) * 64, c0 = ct * 64;
+    const int pw_n = a.wo / PW, ph_n = a.ho / PH, pimg = pw_n * ph_n;
+    const int npatch = a.n_img_w * pimg;
+    const int pbeg = split * a.kchunk, pend = min(npatch, pbeg + a.kchunk);
+
+    const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
+    const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
+
+    f32x4 ra[A_PER], rb[B_PER];
+    auto load_patch = [&](int pi) {
+        const int img = pi / pimg, pr = pi - img * pimg;
+        const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            const int e = tid + i * 256, q = e >> 4, cq = e & 15;
+            const int py = q >> 4, px = q & 15;
+            const uint32_t off = uint32_t(((img * a.ho + y0 + py) * a.wo + x0 + px) * a.ldc_r + r0 + cq * 4) * 4u;
+            ra[i] = bload4(rs_rows, off);
+        }
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            const int e = tid + i * 256, hp = e >> 4, cq = e & 15;
+            const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
+            const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
+            const bool v = e < B_CH && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+            rb[i] = bload4(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + cq * 4) * 4u : kOOB);
+        }
+    };
+    auto store_patch = [&]() {
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            u32x2 h, m, l;
+            split3(ra[i], h, m, l);
+            const int e = tid + i * 256;
+            const int o = (e >> 4) * RS + (e & 15) * 8;
+            *reinterpret_cast<u32x2 *>(smem + o) = h;
+            *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
+            *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
+        }
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i)
+            if (tid + i * 256 < B_CH) {
+                u32x2 h, m, l;
+                split3(rb[i], h, m, l);
+                const int e = tid + i * 256;
+                const int o = 3 * PA + (e >> 4) * RS + (e & 15) * 8;
+                *reinterpret_cast<u32x2 *>(smem + o) = h;
+                *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
+                *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
+            }
+    };
+
+    f32x4 acc[9][2][2];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // transposed-read lane roles: 16-lane group g supplies patch pixels (g >> 1, 4(g & 1) + (w16 >> 2)) (+8
+    // for the second read of a fragment) and channel columns 4(w16 & 3)..+3 of a 16-channel block
+    const int g = lane >> 4, w16 = lane & 15;
+    const int py = g >> 1, pxq = 4 * (g & 1) + (w16 >> 2);
+    const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RS + (32 * wi + 4 * (w16 & 3)) * 2;
+    const uint32_t xbase = lds_addr(smem) + 3 * PA + (py * HW_ + pxq) * RS + (32 * wj + 4 * (w16 & 3)) * 2;
+
+    if (pbeg < pend) {
+        load_patch(pbeg);
+        store_patch();
+        __syncthreads();
+        for (int pi = pbeg; pi < pend; ++pi) {
+            const bool more = pi + 1 < pend;
+            if (more) load_patch(pi + 1);
+            s16x4 fa[12];
+            tr_read<0 * PA + 0>(fa[0], dbase);
+            tr_read<0 * PA + 8 * RS>(fa[1], dbase);
+            tr_read<0 * PA + 32>(fa[2], dbase);
+            tr_read<0 * PA + 8 * RS + 32>(fa[3], dbase);
+            tr_read<1 * PA + 0>(fa[4], dbase);
+            tr_read<1 * PA + 8 * RS>(fa[5], dbase);
+            tr_read<1 * PA + 32>(fa[6], dbase);
+            tr_read<1 * PA + 8 * RS + 32>(fa[7], dbase);
+            tr_read<2 * PA + 0>(fa[8], dbase);
+            tr_read<2 * PA + 8 * RS>(fa[9], dbase);
+            tr_read<2 * PA + 32>(fa[10], dbase);
+            tr_read<2 * PA + 8 * RS + 32>(fa[11], dbase);
+            bf16x8 dv[3][2];
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int r = 0; r < 2; ++r) dv[p][r] = cat8(fa[4 * p + 2 * r], fa[4 * p + 2 * r + 1]);
+            s16x4 f0[6], f1[6];
+            w16_read_x<0, 0, PB, HW_>(f0, xbase);
+            w16_read_x<0, 1, PB, HW_>(f1, xbase);
+            w16_chain<0, PB, HW_>(acc, dv, f0, f1, xbase);
+            if (more) {
+                __syncthreads();  // every wave is done with this patch
+                store_patch();
+                __syncthreads();
+            }
+        }
+    }
+
+    // acc[t][cb][rb][q]: r = r0 + 32wi + 16rb + (lane & 15), c = c0 + 32wj + 16cb + 4g + q
+    float *slab = a.slabs + size_t(split) * a.R * a.Ng;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int row = r0 + 32 * wi + 16 * r + w16;
+                const int col = c0 + 32 * wj + 16 * cb + 4 * g;
+                gstore4(slab + size_t(row) * a.Ng + t * a.C + col, acc[t][cb][r]);
+            }
+}
+
+// 0 = the 32x32x16 halo weight-grad kernel, 1 = this one (scd_set_wgrad16; initial value from SCD_WGRAD16).
+int g_wgrad16 = -1;
+int wgrad16_mode() {
+    if (g_wgrad16 < 0) {
+        const char *e = getenv("SCD_WGRAD16");
+        g_wgrad16 = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_wgrad16;
+}
+const void *wgrad_halo16_fn() { return reinterpret_cast<const void *>(&wgrad_halo16_x3); }
+void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
+    hipLaunchKernelGGL(wgrad_halo16_x3, grid, dim3(256), 0, s, a);
+}
+
 }  // namespace scd
 
 using namespace scd;
+
+extern "C" int scd_set_wgrad16(int32_t mode) {
+    clear_error();
+    const int prev = wgrad16_mode();
+    if (mode == 0 || mode == 1) {
+        g_wgrad16 = mode;
+    } else if (mode != -1) {
+        set_error("scd_set_wgrad16: mode %d", mode);
+        return SCD_ERR_ARG;
+    }
+    return prev;
+}
+
 
 extern "C" int scd_set_halo16(int32_t mode) {
     clear_error();

@@ -597,33 +597,6 @@ bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
 // Row stride = 2W bytes padded to = 64 (mod 128), so the 4 rows a 16-lane group reads fall in four
 // different 64-byte bank groups: conflict-free per 32-lane half.
 // ------------------------------------------------------------------------------------------------
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-
-
-__device__ __forceinline__ s16x4 lds_tr16(const unsigned char *p) {
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4 *)(reinterpret_cast<const __attribute__((address_space(3))) unsigned char *>(
-            reinterpret_cast<uintptr_t>(p))));
-}
-
-constexpr int tr_stride(int w) { return (2 * w) % 128 == 0 ? 2 * w + 64 : 2 * w; }
-
-// ds_read_b64_tr_b16 with an immediate offset (hipcc does not fold offsets into the builtin, which then
-// needs one address VGPR per distinct read).  Inline asm is invisible to the compiler's LDS counters: every
-// use is preceded by lds_wait<N>() on the fragments it consumes.
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return uint32_t(uintptr_t((const __attribute__((address_space(3))) unsigned char *)(p)));
-}
-template <int OFF>
-__device__ __forceinline__ void tr_read(s16x4 &dst, uint32_t vaddr) {
-    static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(dst) : "v"(vaddr), "i"(OFF) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void lds_wait(bf16x8 &a, bf16x8 &b, bf16x8 &c) {
-    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N));
-}
-
 // [16 px][W ch] bf16 plane addressing for the transposed reads.  W % 128 == 0: unpadded 2W-byte rows with the
 // 64-byte segments of each 256-byte bank row XOR-permuted by (k & 3), so the 4 rows a 16-lane group reads
 // land in 4 different segments (conflict-free, and 25% less LDS than padding -> one more workgroup per CU).
@@ -858,9 +831,6 @@ __device__ __forceinline__ void halo_read_b(s16x4 (&f)[6], uint32_t bbase) {
     tr_read<2 * PB + (hr + 4) * RS>(f[5], bbase);
 }
 
-__device__ __forceinline__ bf16x8 cat8(s16x4 lo, s16x4 hi) {
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
 
 // One tap: wait for its fragments (older reads retire first), then the six split products.
 template <int T, int WAIT>
@@ -1042,10 +1012,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_x3(WgradArgs a) {
         }
 }
 
-const void *wgrad_halo_fn() { return reinterpret_cast<const void *>(&wgrad_halo_x3); }
+const void *wgrad_halo_fn() {
+    return wgrad16_mode() ? wgrad_halo16_fn() : reinterpret_cast<const void *>(&wgrad_halo_x3);
+}
 
 void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL(wgrad_halo_x3, grid, dim3(256), 0, s, a);
+    if (wgrad16_mode())
+        launch_wgrad_halo16_x3(a, grid, s);
+    else
+        hipLaunchKernelGGL(wgrad_halo_x3, grid, dim3(256), 0, s, a);
 }
 
 const void *wgrad_x3_fn(int tile_id) {

@@ -48,4 +48,36 @@ __device__ __forceinline__ u32x4 bload4u(__amdgpu_buffer_rsrc_t r, uint32_t off)
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+
+__device__ __forceinline__ s16x4 lds_tr16(const unsigned char *p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4 *)(reinterpret_cast<const __attribute__((address_space(3))) unsigned char *>(
+            reinterpret_cast<uintptr_t>(p))));
+}
+
+constexpr int tr_stride(int w) { return (2 * w) % 128 == 0 ? 2 * w + 64 : 2 * w; }
+
+// ds_read_b64_tr_b16 with an immediate offset (hipcc does not fold offsets into the builtin, which then
+// needs one address VGPR per distinct read).  Inline asm is invisible to the compiler's LDS counters: every
+// use is preceded by lds_wait<N>() on the fragments it consumes.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return uint32_t(uintptr_t((const __attribute__((address_space(3))) unsigned char *)(p)));
+}
+template <int OFF>
+__device__ __forceinline__ void tr_read(s16x4 &dst, uint32_t vaddr) {
+    static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(dst) : "v"(vaddr), "i"(OFF) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lds_wait(bf16x8 &a, bf16x8 &b, bf16x8 &c) {
+    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N));
+}
+
+__device__ __forceinline__ bf16x8 cat8(s16x4 lo, s16x4 hi) {
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 }  // namespace scd

@@ -70,6 +70,7 @@ _SIGS = {
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_set_conv_math": ([c_int32], c_int),
     "scd_set_halo16": ([c_int32], c_int),
+    "scd_set_wgrad16": ([c_int32], c_int),
     "scd_split_bf16x3": ([c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "scd_split_frag_bytes": ([c_int32, c_int32], c_size_t),
     "scd_split_bf16x3_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
@@ -262,6 +263,14 @@ def set_halo16(mode: int) -> int:
     rc = lib().scd_set_halo16(int(mode))
     if rc < 0:
         _check(rc, "scd_set_halo16")
+    return rc
+
+
+def set_wgrad16(mode: int) -> int:
+    """Halo weight-grad kernel selection (0 = 32x32x16 MFMA, 1 = 16x16x32 MFMA); returns the previous mode."""
+    rc = lib().scd_set_wgrad16(int(mode))
+    if rc < 0:
+        _check(rc, "scd_set_wgrad16")
     return rc
 
 

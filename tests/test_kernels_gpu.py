@@ -312,6 +312,31 @@ def test_conv_halo16_tiles(dev, cfg, n, h, w, ci, co):
         hip.set_conv_math(prev_m)
 
 
+@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('n,h,w,ci,co', [(2, 4, 32, 64, 64), (3, 6, 16, 128, 192), (1, 32, 64, 64, 128),
+                                         (2, 16, 16, 512, 512)])
+def test_wgrad_halo_variants(dev, variant, n, h, w, ci, co):
+    """Both halo weight-grad kernels (32x32x16 and 16x16x32 MFMA) against torch fp32, incl. split-K slabs."""
+    from multimodal_siamese_cd_amd import hip
+    prev_m = hip.set_conv_math('x3')
+    prev_w = hip.set_wgrad16(variant)
+    try:
+        g = torch.Generator().manual_seed(5 * variant + ci + co + h)
+        x = torch.randn(n, h, w, ci, generator=g)
+        dy = torch.randn(n, h, w, co, generator=g)
+        wt = torch.empty(co, ci, 3, 3)
+        ref_dw = torch.nn.grad.conv2d_weight(nchw(x), wt.shape, nchw(dy), padding=1)
+        d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dy.to(dev)), hip.nhwc(x.to(dev)), 1, hip.TAPS_3X3)
+        slabs = torch.empty(nbytes // 4, device=dev)
+        hip.conv_wgrad(d, slabs)
+        dw = torch.empty(co, ci, 3, 3, device=dev)
+        hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
+        assert rel(dw, ref_dw) < TOL
+    finally:
+        hip.set_wgrad16(prev_w)
+        hip.set_conv_math(prev_m)
+
+
 @pytest.mark.parametrize('n,h,w,c,nseg', [(4, 16, 16, 8, 2), (2, 33, 17, 64, 2), (2, 64, 64, 16, 1), (6, 8, 8, 512, 2)])
 def test_batchnorm_relu_train_forward_backward(dev, n, h, w, c, nseg):
     from multimodal_siamese_cd_amd import hip

@@ -1,0 +1,84 @@
+"""A/B of library variants on the bench training step, interleaved in ONE process (guide rule 24).
+
+    python tools/ab_step.py --variants "h16=1,w16=0" "h16=1,w16=1" [--rounds 6 --steps 8]
+
+A variant is a comma list of knob=value with knobs:
+  h16   scd_set_halo16 mode        w16   scd_set_wgrad16 mode
+  fuse  engine BN-apply fusion into the consuming conv (multimodal_siamese_cd_amd.engine.FUSE_INPUT_BN)
+Prints per-variant median / min ms per step over the rounds.
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from multimodal_siamese_cd_amd import engine, hip  # noqa: E402
+from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_functions, networks  # noqa: E402
+
+
+def apply(variant: str):
+    for kv in filter(None, variant.split(',')):
+        k, v = kv.split('=')
+        if k == 'h16':
+            hip.set_halo16(int(v))
+        elif k == 'w16':
+            hip.set_wgrad16(int(v))
+        elif k == 'fuse':
+            engine.set_options(fuse_input_bn=bool(int(v)))
+        else:
+            raise SystemExit(f'unknown knob {k}')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--variants', nargs='+', required=True)
+    ap.add_argument('--rounds', type=int, default=6)
+    ap.add_argument('--steps', type=int, default=8)
+    ap.add_argument('--config', default='baseline_siamese')
+    ap.add_argument('--batch', type=int, default=None)
+    args = ap.parse_args()
+    hip.load_library()
+    dev = torch.device('cuda:0')
+    cfg = experiment_manager.load_cfg(args.config)
+    batch = args.batch or int(cfg.TRAINER.BATCH_SIZE)
+    torch.manual_seed(cfg.SEED)
+    net = networks.create_network(cfg).to(dev).train()
+    opt = torch.optim.AdamW(net.parameters(), lr=float(cfg.TRAINER.LR), weight_decay=0.01, fused=True)
+    crit = loss_functions.get_criterion(cfg.MODEL.LOSS_TYPE)
+    gen = torch.Generator(device=dev).manual_seed(7)
+    b = datasets.synthetic_batch(cfg, batch, dev, gen)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = crit(net(b['x_t1'], b['x_t2']), b['y_change'])
+        loss.backward()
+        opt.step()
+
+    times = {v: [] for v in args.variants}
+    for v in args.variants:  # warm every variant (allocator, occupancy caches, clocks)
+        apply(v)
+        for _ in range(3):
+            step()
+    torch.cuda.synchronize()
+    for r in range(args.rounds):
+        for v in args.variants:
+            apply(v)
+            step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            times[v].append(1000.0 * (time.perf_counter() - t0) / args.steps)
+    for v, ts in times.items():
+        print(f'{v:30s} median {statistics.median(ts):8.3f} ms  min {min(ts):8.3f} ms  '
+              f'({batch / statistics.median(ts) * 1000:.1f} pairs/s)  rounds {["%.2f" % t for t in ts]}', flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -55,15 +55,16 @@ def main():
     ap.add_argument('--only', default=None)
     ap.add_argument('--layer', default=None, help='run only this layer name (e.g. enc1b)')
     ap.add_argument('--math', default=None, choices=['f32', 'x3'], help='conv arithmetic (default: library default)')
-    ap.add_argument('--halo16', default=None,
-                    help='comma-separated scd_set_halo16 modes, interleaved per layer (e.g. 0,1,3)')
+    ap.add_argument('--variants', default=None,
+                    help='comma-separated kernel variants H/W (scd_set_halo16 mode / scd_set_wgrad16 mode), '
+                         'interleaved per layer, e.g. 0/0,1/1')
     args = ap.parse_args()
     hip.load_library()
     if args.math:
         hip.set_conv_math(args.math)
     print(f'conv math: {hip.conv_math()}')
     dev = torch.device('cuda:0')
-    modes = [None] if args.halo16 is None else [int(m) for m in args.halo16.split(',')]
+    modes = [None] if args.variants is None else args.variants.split(',')
     tots = {m: {'fwd': [0.0, 0.0], 'dgrad': [0.0, 0.0], 'wgrad': [0.0, 0.0]} for m in modes}
     print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"cin":>5s} {"cout":>5s} | '
           f'{"fwd ms":>8s} {"TF/s":>6s} | {"dgrad ms":>8s} {"TF/s":>6s} | {"wgrad ms":>8s} {"TF/s":>6s}')
@@ -80,7 +81,9 @@ def main():
         flops = 2.0 * n * s * s * co * 9 * ci
         for mode in modes:
             if mode is not None:
-                hip.set_halo16(mode)
+                hv, wv = mode.split('/')
+                hip.set_halo16(int(hv))
+                hip.set_wgrad16(int(wv))
             tot = tots[mode]
             res = {}
             if args.only in (None, 'fwd'):
@@ -106,7 +109,7 @@ def main():
             print(f'{tag:8s} {n:3d} {s:4d} {ci:5d} {co:5d} | ' + ' | '.join(cells), flush=True)
     for mode, tot in tots.items():
         if mode is not None:
-            print(f'-- halo16 mode {mode}')
+            print(f'-- variant (halo16/wgrad16) {mode}')
         allt = sum(v[0] for v in tot.values())
         allf = sum(v[1] for v in tot.values())
         for k, (t, f) in tot.items():
