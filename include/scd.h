@@ -137,9 +137,19 @@ typedef struct scd_igemm {
      * image-major order.  Only when scd_igemm_stat_tiles() reports > 0 tiles for this descriptor; NULL = off.
      * replaces: the batch-statistics pass of aten::native_batch_norm (networks.py:393,396). */
     float *stat_rec;
+    /* Optional fused input transform: the BatchNorm-apply + ReLU of the layer that produced src
+     * (networks.py:393-394,396-397), so its activation never goes to memory.  Every in-range source
+     * element of image img, channel c is read as max(s * in_scale[g*src.c + c] + in_shift[g*src.c + c], 0),
+     * g = img / (src.n / in_nseg); the zero padding stays zero.  NULL = off.  Only for descriptors where
+     * scd_igemm_input_bn_supported() returns 1 (16-byte aligned coefficient arrays). */
+    const float *in_scale;
+    const float *in_shift;
+    int32_t in_nseg;
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);
+/* 1 if the kernel scd_conv_igemm would run for `d` applies the in_scale/in_shift input transform, else 0. */
+int scd_igemm_input_bn_supported(const scd_igemm_t *d);
 /* Number of statistic tiles scd_conv_igemm would write for `d` (0: no fused statistics for this shape or
  * arithmetic, use scd_bn_train_stats); *tile_pixels receives the pixels per tile. */
 int scd_igemm_stat_tiles(const scd_igemm_t *d, int32_t *tile_pixels);
@@ -159,11 +169,19 @@ typedef struct scd_wgrad {
     int32_t stride;
     int32_t ntaps;
     int8_t dy[9], dx[9];
+    /* Optional fused transform of src (as scd_igemm_t.in_scale): src elements of image img, channel c
+     * are read as max(s * src_scale[g*src.c + c] + src_shift[g*src.c + c], 0), g = img / (src.n / src_nseg).
+     * NULL = off.  Only where scd_wgrad_src_bn_supported() returns 1. */
+    const float *src_scale;
+    const float *src_shift;
+    int32_t src_nseg;
 } scd_wgrad_t;
 
 /* Number of K-splits the library will use and the slab bytes it needs. */
 int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes);
 int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream);
+/* 1 if the weight-grad kernel scd_conv_wgrad would run for `d` applies the src_scale/src_shift transform. */
+int scd_wgrad_src_bn_supported(const scd_wgrad_t *d);
 /* Sum the slabs (deterministic fixed-order two-level reduction; the slabs are scratch and are
  * overwritten) and unpack to the parameter layout.
  * mode 0: out OIHW [R][c_valid][3][3]  (slab cols (ky*3+kx)*C + c)

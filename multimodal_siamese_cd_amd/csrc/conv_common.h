@@ -77,6 +77,8 @@ struct IgemmArgs {
     float *stat_rec;  // optional fused BN statistics [tile][n_out][2] (halo path)
     uint32_t src_bytes;  // byte extent of src for buffer loads (0 = above 2 GiB: no halo path)
     FastDiv div_hw, div_w;
+    const float *in_scale, *in_shift;  // optional fused input BN-apply + ReLU (halo16 path only)
+    int in_seg_imgs;                   // images per coefficient segment
 };
 
 struct WgradArgs {
@@ -92,6 +94,8 @@ struct WgradArgs {
     int n_img_w;                     // images (halo wgrad: split-K over 2x16 patches of all images)
     float *slabs;
     FastDiv div_hw, div_w, div_c;
+    const float *src_scale, *src_shift;  // optional fused src BN-apply + ReLU (halo16 weight grad only)
+    int src_seg_imgs;
 };
 
 // Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels
@@ -101,6 +105,8 @@ bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s);
 int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels);
 // 16x16x32-MFMA halo igemm (conv_halo16.hip): 0 when `a` does not take it, else its config; launcher.
 int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw);
+// Whether launch_igemm_x3 would run the halo16 kernel for `a` (the only one with the input transform).
+bool igemm_takes_halo16(const IgemmArgs &a);
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
 // 16x16x32-MFMA halo weight grad (conv_halo16.hip), selected by wgrad16_mode() (scd_set_wgrad16).
 int wgrad16_mode();

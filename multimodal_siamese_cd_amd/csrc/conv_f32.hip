@@ -561,6 +561,18 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     a.wsplit = d->wsplit;
     a.wplane = int64_t((a.n_out + 31) / 32) * 32 * a.K;  // fragment-major pre-split plane (rows padded to 32)
     a.stat_rec = d->stat_rec;
+    a.in_scale = d->in_scale;
+    a.in_shift = d->in_shift;
+    a.in_seg_imgs = d->src.n;
+    if (d->in_scale || d->in_shift) {
+        if (!d->in_scale || !d->in_shift || d->in_nseg < 1 || d->src.n % d->in_nseg || !aligned16(d->in_scale) ||
+            !aligned16(d->in_shift)) {
+            set_error("igemm: input transform needs both 16-byte aligned coefficient arrays and in_nseg | src.n "
+                      "(in_nseg=%d, n=%d)", d->in_nseg, d->src.n);
+            return SCD_ERR_ARG;
+        }
+        a.in_seg_imgs = d->src.n / d->in_nseg;
+    }
     {
         const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * 4 + int64_t(d->src.c) * 4;
         a.src_bytes = sb < (int64_t(1) << 31) ? uint32_t(sb) : 0u;
@@ -583,6 +595,13 @@ extern "C" int scd_igemm_stat_tiles(const scd_igemm_t *d, int32_t *tile_pixels) 
     return n;
 }
 
+extern "C" int scd_igemm_input_bn_supported(const scd_igemm_t *d) {
+    clear_error();
+    IgemmArgs a;
+    if (igemm_prepare(d, a) != SCD_OK) return 0;
+    return igemm_takes_halo16(a) ? 1 : 0;
+}
+
 extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
     clear_error();
     IgemmArgs a;
@@ -595,6 +614,11 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
         }
     }
     hipStream_t s = as_stream(stream);
+    if (a.in_scale && !igemm_takes_halo16(a)) {
+        set_error("igemm: the fused input transform is not supported for this shape/arithmetic "
+                  "(check scd_igemm_input_bn_supported)");
+        return SCD_ERR_ARG;
+    }
     if (conv_math_x3() && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");
     if (d->n_out >= 128)
         launch_igemm_bk<2, 2, 2, 2>(a, s);  // 128 x 128
@@ -747,6 +771,16 @@ static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
 }
 }  // namespace scd
 
+namespace scd {
+static bool wgrad_src_bn_ok(const scd_wgrad_t *d) { return wgrad_halo_ok(d) && wgrad16_mode(); }
+}  // namespace scd
+
+extern "C" int scd_wgrad_src_bn_supported(const scd_wgrad_t *d) {
+    clear_error();
+    if (wgrad_validate(d) != SCD_OK) return 0;
+    return wgrad_src_bn_ok(d) ? 1 : 0;
+}
+
 extern "C" int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
@@ -799,6 +833,18 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
     }
     a.rows_bytes = uint32_t(rb);
     a.src_bytes = uint32_t(sb);
+    a.src_scale = d->src_scale;
+    a.src_shift = d->src_shift;
+    a.src_seg_imgs = d->src.n;
+    if (d->src_scale || d->src_shift) {
+        if (!d->src_scale || !d->src_shift || d->src_nseg < 1 || d->src.n % d->src_nseg ||
+            !aligned16(d->src_scale) || !aligned16(d->src_shift) || !wgrad_src_bn_ok(d)) {
+            set_error("wgrad: src transform needs both 16-byte aligned coefficient arrays, src_nseg | src.n and a "
+                      "supported shape (check scd_wgrad_src_bn_supported)");
+            return SCD_ERR_ARG;
+        }
+        a.src_seg_imgs = d->src.n / d->src_nseg;
+    }
     hipStream_t s = as_stream(stream);
     if (wgrad_halo_ok(d)) {
         a.n_img_w = d->rows.n;

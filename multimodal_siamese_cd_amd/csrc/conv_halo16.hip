@@ -38,7 +38,10 @@ __device__ __forceinline__ float row16_sum(float x) {
 __device__ __forceinline__ void gstore4(float *p, f32x4 v) { *(__attribute__((address_space(1))) f32x4 *)(p) = v; }
 
 // WAVES_M x WAVES_N waves; a wave computes TM*16 pixels x TN*16 channels (TM x TN MFMA tiles).
-template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC>
+// IN_BN: the source is a conv output y of the previous layer; its BatchNorm-apply + ReLU,
+// max(fma(y, scale, shift), 0) with the exact expression of bn_relu_apply_kernel, is applied while the halo
+// is staged (in-range pixels only: the zero padding belongs to the activation).
+template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int WPX = TM * 16, WCH = TN * 16;
@@ -107,17 +110,30 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     }
 
     f32x4 ra[A_PER];
+    f32x4 in_sc, in_sh;  // IN_BN coefficients of this thread's 4 channels (col = tid & 7 for every piece)
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
     const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, 3u * wplane_b);
     auto load_A = [&](int cc) {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) ra[i] = bload4(rs_src, a_boff[i] == kOOB ? kOOB : a_boff[i] + cc * 128u);
+        if constexpr (IN_BN) {
+            const int ch = (img / a.in_seg_imgs) * a.c + cc * 32 + (tid & 7) * 4;
+            in_sc = gload4(a.in_scale + ch);
+            in_sh = gload4(a.in_shift + ch);
+        }
     };
     auto store_A = [&]() {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i)
             if ((A_CH % NT == 0) || a_off[i] >= 0) {
                 u32x2 h, m, l;
+                if constexpr (IN_BN) {
+                    f32x4 v;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        v[q] = a_boff[i] == kOOB ? 0.f : fmaxf(fmaf(ra[i][q], in_sc[q], in_sh[q]), 0.f);
+                    ra[i] = v;
+                }
                 split3(ra[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(smem + a_off[i]) = h;
                 *reinterpret_cast<u32x2 *>(smem + PA + a_off[i]) = m;
@@ -283,8 +299,8 @@ int halo16_mode() {
     return g_halo16;
 }
 
-template <int WM, int WN, int TM, int TN, int OCC>
-void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
+template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN>
+void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     IgemmArgs b = a;
     b.grid_m = a.n_img * (a.ho / (BM / tw)) * (a.wo / tw);
@@ -296,11 +312,19 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
     }
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
     if (tw == 64)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN>), grid, block, 0, s, b);
     else if (tw == 32)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN>), grid, block, 0, s, b);
     else
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN>), grid, block, 0, s, b);
+}
+
+template <int WM, int WN, int TM, int TN, int OCC>
+void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
+    if (a.in_scale)
+        launch16b<WM, WN, TM, TN, OCC, true>(a, tw, s);
+    else
+        launch16b<WM, WN, TM, TN, OCC, false>(a, tw, s);
 }
 
 // Tile configurations: id -> (pixels, channels) per block.
@@ -430,8 +454,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
 
     f32x4 ra[A_PER], rb[B_PER];
+    f32x4 x_sc, x_sh;      // src transform coefficients of this thread's 4 channels (cq = tid & 15)
+    uint32_t x_valid = 0;  // bit i: halo piece i is inside the image (the padding stays zero)
     auto load_patch = [&](int pi) {
         const int img = pi / pimg, pr = pi - img * pimg;
+        if (a.src_scale) {
+            const int ch = (img / a.src_seg_imgs) * a.C + c0 + (tid & 15) * 4;
+            x_sc = gload4(a.src_scale + ch);
+            x_sh = gload4(a.src_shift + ch);
+        }
+        x_valid = 0;
         const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
@@ -446,6 +478,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
             const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
             const bool v = e < B_CH && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+            x_valid |= uint32_t(v) << i;
             rb[i] = bload4(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + cq * 4) * 4u : kOOB);
         }
     };
@@ -464,6 +497,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
         for (int i = 0; i < B_PER; ++i)
             if (tid + i * 256 < B_CH) {
                 u32x2 h, m, l;
+                if (a.src_scale) {
+                    const bool v = (x_valid >> i) & 1u;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                }
                 split3(rb[i], h, m, l);
                 const int e = tid + i * 256;
                 const int o = 3 * PA + (e >> 4) * RS + (e & 15) * 8;

@@ -558,6 +558,11 @@ static int halo_pick(const IgemmArgs &a, int *bm, int *tw) {
     return 0;
 }
 
+bool igemm_takes_halo16(const IgemmArgs &a) {
+    int bm = 0, tw = 0;
+    return conv_math_x3() && a.c % 16 == 0 && halo16_pick(a, halo_eligible(a), &bm, &tw) != 0;
+}
+
 int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels) {
     int bm = 0, tw = 0;
     if (!conv_math_x3()) return 0;

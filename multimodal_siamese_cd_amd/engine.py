@@ -26,6 +26,20 @@ from .hip import TAPS_1, TAPS_2X2, TAPS_3X3, nhwc
 
 _F32 = torch.float32
 
+# Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
+_OPTS = {'fuse_input_bn': True}
+
+
+def set_options(**kw) -> dict:
+    """fuse_input_bn: apply a DoubleConv's first BatchNorm + ReLU inside the second conv's operand staging
+    (forward and weight-grad) instead of materialising the activation.  Returns the previous options."""
+    prev = dict(_OPTS)
+    for k, v in kw.items():
+        if k not in _OPTS:
+            raise KeyError(k)
+        _OPTS[k] = v
+    return prev
+
 
 def _empty(shape, like: torch.Tensor, dtype=_F32):
     return torch.empty(shape, device=like.device, dtype=dtype)
@@ -107,10 +121,11 @@ def _conv3x3(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int) -> torch.Tens
     return y
 
 
-def _conv3x3_stats(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int, want: bool):
-    """Conv 3x3 forward; with `want`, also the fused per-tile BatchNorm statistics when the conv provides them."""
+def _conv3x3_stats(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int, want: bool, in_bn=None, y=None):
+    """Conv 3x3 forward; with `want`, also the fused per-tile BatchNorm statistics when the conv provides them.
+    `in_bn` = (scale, shift, nseg): x is the previous conv's output, read through its BatchNorm + ReLU."""
     n, h, w, _ = x.shape
-    y = _empty((n, h, w, n_out), x)
+    y = _empty((n, h, w, n_out), x) if y is None else y
     tiles = None
     if want:
         ntiles, tpx = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(y))
@@ -118,8 +133,19 @@ def _conv3x3_stats(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int, want: b
             rec = _empty((ntiles * n_out * 2,), x)
             tiles = (rec, ntiles, tpx)
     hip.conv_igemm(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, bias, nhwc(y),
-                   stat_rec=None if tiles is None else tiles[0])
+                   stat_rec=None if tiles is None else tiles[0], in_bn=in_bn)
     return y, tiles
+
+
+def _can_fuse_input_bn(y0: torch.Tensor, wpk1: torch.Tensor, y1: torch.Tensor, st: '_BNSaved', save: bool) -> bool:
+    """Whether conv1 (and, when training, its weight grad) can read y0 through BN0 + ReLU directly."""
+    if not _OPTS['fuse_input_bn']:
+        return False
+    n, h, w, _ = y0.shape
+    bn = (st.scale, st.shift, st.nseg)
+    if not hip.igemm_input_bn_supported(nhwc(y0), h, w, 1, TAPS_3X3, wpk1, y1.shape[3], nhwc(y1), bn):
+        return False
+    return not save or hip.wgrad_src_bn_supported(nhwc(y1), nhwc(y0), 1, TAPS_3X3, bn)
 
 
 def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool):
@@ -131,10 +157,17 @@ def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool):
     y0, t0 = _conv3x3_stats(x, hip.pack_conv3x3(conv0.weight.detach(), 0, ci_pad=cin), conv0.bias,
                             conv0.out_channels, _bn_uses_batch_stats(bn0, training))
     st0 = _bn_forward(y0, bn0, nseg, training, t0)
-    a0 = torch.empty_like(y0)
-    hip.bn_relu_apply(nhwc(y0), st0.nseg, st0.scale, st0.shift, nhwc(a0))
-    y1, t1 = _conv3x3_stats(a0, hip.pack_conv3x3(conv1.weight.detach(), 0), conv1.bias, conv1.out_channels,
-                            _bn_uses_batch_stats(bn1, training))
+    wpk1 = hip.pack_conv3x3(conv1.weight.detach(), 0)
+    n, h, w, _ = y0.shape
+    y1 = _empty((n, h, w, conv1.out_channels), y0)
+    if _can_fuse_input_bn(y0, wpk1, y1, st0, save):
+        a0 = None  # never materialised: conv1 and its weight grad apply BN0 + ReLU while staging y0
+        y1, t1 = _conv3x3_stats(y0, wpk1, conv1.bias, conv1.out_channels, _bn_uses_batch_stats(bn1, training),
+                                in_bn=(st0.scale, st0.shift, st0.nseg), y=y1)
+    else:
+        a0 = torch.empty_like(y0)
+        hip.bn_relu_apply(nhwc(y0), st0.nseg, st0.scale, st0.shift, nhwc(a0))
+        y1, t1 = _conv3x3_stats(a0, wpk1, conv1.bias, conv1.out_channels, _bn_uses_batch_stats(bn1, training), y=y1)
     st1 = _bn_forward(y1, bn1, nseg, training, t1)
     a1 = torch.empty_like(y1)
     hip.bn_relu_apply(nhwc(y1), st1.nseg, st1.scale, st1.shift, nhwc(a1))
@@ -142,8 +175,8 @@ def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool):
     return a1, saved
 
 
-def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3)
+def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, src_bn=None) -> torch.Tensor:
+    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3, src_bn)
     slabs = _empty((nbytes // 4,), dy)
     hip.conv_wgrad(d, slabs)
     gw = torch.empty_like(weight)
@@ -172,7 +205,10 @@ def _dc_backward(g_out: torch.Tensor, saved, dc, need_dx: bool):
     if st1.smean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported (call net.train())")
     dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None)
-    gw1 = _wgrad3x3(dy1, a0, conv1.weight)
+    if a0 is None:  # fused forward: the weight grad reads y0 through BN0 + ReLU as well
+        gw1 = _wgrad3x3(dy1, y0, conv1.weight, (st0.scale, st0.shift, st0.nseg))
+    else:
+        gw1 = _wgrad3x3(dy1, a0, conv1.weight)
     ga0 = _conv3x3(dy1, hip.pack_conv3x3(conv1.weight.detach(), 1), None, conv1.in_channels)
     dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None)
     gw0 = _wgrad3x3(dy0, x, conv0.weight)

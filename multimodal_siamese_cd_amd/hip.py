@@ -37,6 +37,9 @@ class IGEMM(ctypes.Structure):
         ("store_mode", c_int32),
         ("wsplit", c_void_p),
         ("stat_rec", c_void_p),
+        ("in_scale", c_void_p),
+        ("in_shift", c_void_p),
+        ("in_nseg", c_int32),
     ]
 
 
@@ -48,6 +51,9 @@ class WGRAD(ctypes.Structure):
         ("ntaps", c_int32),
         ("dy", c_int8 * 9),
         ("dx", c_int8 * 9),
+        ("src_scale", c_void_p),
+        ("src_shift", c_void_p),
+        ("src_nseg", c_int32),
     ]
 
 
@@ -75,6 +81,8 @@ _SIGS = {
     "scd_split_frag_bytes": ([c_int32, c_int32], c_size_t),
     "scd_split_bf16x3_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
+    "scd_igemm_input_bn_supported": ([POINTER(IGEMM)], c_int),
+    "scd_wgrad_src_bn_supported": ([POINTER(WGRAD)], c_int),
     "scd_igemm_stat_tiles": ([POINTER(IGEMM), POINTER(c_int32)], c_int),
     "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
     "scd_conv_wgrad": ([POINTER(WGRAD), c_void_p, c_size_t, c_void_p], c_int),
@@ -279,16 +287,24 @@ def conv_math() -> str:
     return {v: k for k, v in _MATH_NAMES.items()}[rc]
 
 
-def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None):
+def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None, in_bn=None):
     nt, dy, dx = _taps(taps)
+    sc, sh, nseg = in_bn if in_bn is not None else (None, None, 0)
     return IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
-                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec))
+                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg)
 
 
 def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
-               bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None):
-    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec)
+               bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None, in_bn=None):
+    """`in_bn` = (scale, shift, nseg): read src through the producing layer's BatchNorm-apply + ReLU."""
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec, in_bn)
     _check(lib().scd_conv_igemm(ctypes.byref(d), _stream()), "scd_conv_igemm")
+
+
+def igemm_input_bn_supported(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
+                             dst: NHWC, in_bn) -> bool:
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0, None, in_bn)
+    return lib().scd_igemm_input_bn_supported(ctypes.byref(d)) == 1
 
 
 def igemm_stat_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
@@ -300,13 +316,22 @@ def igemm_stat_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: 
     return (n, tp.value) if n > 0 else (0, 0)
 
 
-def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps):
+def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None):
+    """`src_bn` = (scale, shift, nseg): read src through its BatchNorm-apply + ReLU (see scd_wgrad_t)."""
     nt, dy, dx = _taps(taps)
-    d = WGRAD(rows, src, stride, nt, dy, dx)
+    sc, sh, nseg = src_bn if src_bn is not None else (None, None, 0)
+    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg)
     ns = c_int32(0)
     nb = c_size_t(0)
     _check(lib().scd_wgrad_plan(ctypes.byref(d), ctypes.byref(ns), ctypes.byref(nb)), "scd_wgrad_plan")
     return d, ns.value, nb.value
+
+
+def wgrad_src_bn_supported(rows: NHWC, src: NHWC, stride: int, taps, src_bn) -> bool:
+    nt, dy, dx = _taps(taps)
+    sc, sh, nseg = src_bn
+    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg)
+    return lib().scd_wgrad_src_bn_supported(ctypes.byref(d)) == 1
 
 
 def conv_wgrad(d: WGRAD, slabs: torch.Tensor):

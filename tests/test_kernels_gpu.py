@@ -312,6 +312,49 @@ def test_conv_halo16_tiles(dev, cfg, n, h, w, ci, co):
         hip.set_conv_math(prev_m)
 
 
+@pytest.mark.parametrize('n,h,w,ci,co,nseg', [(4, 16, 32, 64, 128, 2), (2, 8, 64, 128, 64, 1), (4, 8, 16, 64, 64, 2)])
+def test_fused_input_bn(dev, n, h, w, ci, co, nseg):
+    """Conv forward and weight grad reading y through BN-apply + ReLU (in_bn / src_bn) are bit-identical to the
+    same kernels on the materialised activation (bn_relu_apply), per-segment coefficients included."""
+    from multimodal_siamese_cd_amd import hip
+    prev_m = hip.set_conv_math('x3')
+    try:
+        g = torch.Generator().manual_seed(n * h + ci)
+        y = torch.randn(n, h, w, ci, generator=g).to(dev)
+        sc = (torch.rand(nseg * ci, generator=g) * 2 - 0.5).to(dev)  # some negative scales
+        sh = torch.randn(nseg * ci, generator=g).to(dev)
+        a = torch.empty_like(y)
+        hip.bn_relu_apply(hip.nhwc(y), nseg, sc, sh, hip.nhwc(a))
+        wt = (torch.randn(co, ci, 3, 3, generator=g) / (3 * ci ** 0.5)).to(dev)
+        b = torch.randn(co, generator=g).to(dev)
+        wpk = hip.pack_conv3x3(wt, 0)
+        out_ref, out = torch.empty(n, h, w, co, device=dev), torch.empty(n, h, w, co, device=dev)
+        bn = (sc, sh, nseg)
+        assert hip.igemm_input_bn_supported(hip.nhwc(y), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(out), bn)
+        hip.conv_igemm(hip.nhwc(a), h, w, 1, hip.TAPS_3X3, wpk, co, b, hip.nhwc(out_ref))
+        hip.conv_igemm(hip.nhwc(y), h, w, 1, hip.TAPS_3X3, wpk, co, b, hip.nhwc(out), in_bn=bn)
+        assert torch.equal(out, out_ref)
+        dy = torch.randn(n, h, w, co, generator=g).to(dev)
+        dws = []
+        for src, sbn in ((a, None), (y, bn)):
+            if sbn is not None:
+                assert hip.wgrad_src_bn_supported(hip.nhwc(dy), hip.nhwc(y), 1, hip.TAPS_3X3, sbn)
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dy), hip.nhwc(src), 1, hip.TAPS_3X3, sbn)
+            slabs = torch.empty(nbytes // 4, device=dev)
+            hip.conv_wgrad(d, slabs)
+            dw = torch.empty(co, ci, 3, 3, device=dev)
+            hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
+            dws.append(dw)
+        assert torch.equal(dws[0], dws[1])
+        # not offered where the kernel cannot apply it: fp32 arithmetic -> the call is rejected, not ignored
+        hip.set_conv_math('f32')
+        assert not hip.igemm_input_bn_supported(hip.nhwc(y), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(out), bn)
+        with pytest.raises(RuntimeError):
+            hip.conv_igemm(hip.nhwc(y), h, w, 1, hip.TAPS_3X3, wpk, co, b, hip.nhwc(out), in_bn=bn)
+    finally:
+        hip.set_conv_math(prev_m)
+
+
 @pytest.mark.parametrize('variant', [0, 1])
 @pytest.mark.parametrize('n,h,w,ci,co', [(2, 4, 32, 64, 64), (3, 6, 16, 128, 192), (1, 32, 64, 64, 128),
                                          (2, 16, 16, 512, 512)])

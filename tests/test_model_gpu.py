@@ -179,3 +179,68 @@ def test_state_dict_interchanges_with_reference_keys(dev):
     keys = set(net.state_dict())
     want = {'module.' + k for k in fx.params0} | {'module.' + k for k in fx.prefixed('r1/')}
     assert keys == want
+
+
+def test_fused_input_bn_model_step(dev):
+    """A topology whose DoubleConvs take the fused BN0 path (channels multiple of 32): fused and materialised
+    runs are bit-identical, and both match the CPU oracle (logits, loss, gradients)."""
+    from multimodal_siamese_cd_amd import engine, hip
+    from multimodal_siamese_cd_amd.utils import experiment_manager, loss_functions, networks
+    from oracle import siamese_oracle as O
+    if hip.conv_math() != 'x3':
+        pytest.skip('fusion only under the x3 arithmetic')
+    ocfg = dict(TOPOLOGY=[32, 64], IN_CHANNELS=5, OUT_CHANNELS=1, S1_BANDS=[0, 1], S2_BANDS=[2, 1, 0])
+    shapes = O.param_shapes('siameseunet', ocfg)
+    P = O.deterministic_params(shapes, 7)
+    b = O.synthetic_batch(ocfg, 2, 64, 8)
+    cfg = experiment_manager.new_config()
+    cfg.MODEL.TYPE, cfg.MODEL.IN_CHANNELS, cfg.MODEL.OUT_CHANNELS = 'siameseunet', 5, 1
+    cfg.MODEL.TOPOLOGY = [32, 64]
+    cfg.DATALOADER.S1_BANDS, cfg.DATALOADER.S2_BANDS = [0, 1], [2, 1, 0]
+    crit = loss_functions.get_criterion('PowerJaccardLoss')
+    runs = []
+    for fuse in (True, False):
+        prev = engine.set_options(fuse_input_bn=fuse)
+        try:
+            net = networks.create_network(cfg)
+            with torch.no_grad():
+                for k, p in net.module.named_parameters():
+                    p.copy_(P[k])
+            net.to(dev).train()
+            out = net(b['x_t1'].to(dev), b['x_t2'].to(dev))
+            loss = crit(out, b['y_change'].to(dev))
+            loss.backward()
+            runs.append((out.detach().cpu(), loss.item(),
+                         {k: p.grad.detach().cpu() for k, p in net.module.named_parameters()}))
+        finally:
+            engine.set_options(**prev)
+    (o1, l1, g1), (o0, l0, g0) = runs
+    assert torch.equal(o1, o0) and l1 == l0
+    for k in g1:
+        assert torch.equal(g1[k], g0[k]), k
+    # against the CPU oracle
+    Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    ref = O.forward('siameseunet', Pr, O.fresh_buffers(shapes), b['x_t1'], b['x_t2'], ocfg, True)
+    lref = O.power_jaccard_loss(ref, b['y_change'])
+    lref.backward()
+    check_logits(o1, ref.detach().numpy())
+    assert abs(l1 - lref.item()) < 1e-5
+    bad = []
+    for k, v in Pr.items():
+        if _pre_bn_bias(k):
+            continue
+        e = rel_err(g1[k].numpy(), v.grad.numpy())
+        print(f'{k:60s} rel err {e:.2e}')
+        if not e < GRAD_TOL:
+            bad.append((k, e))
+    if bad:
+        O.RECORD = []
+        try:
+            with torch.no_grad():
+                O.forward('siameseunet', P, O.fresh_buffers(shapes), b['x_t1'], b['x_t2'], ocfg, True)
+            kinks = [(k, float(z.abs().min())) for k, z in O.RECORD
+                     if float(z.abs().min()) < 1e-6 * float(z.abs().max())]
+        finally:
+            O.RECORD = None
+        print('kink-ambiguous pre-activations in the reference forward:', kinks)
+        assert kinks and all(e < KINK_TOL for _, e in bad), (bad, kinks)
