@@ -41,7 +41,10 @@ __device__ __forceinline__ void gstore4(float *p, f32x4 v) { *(__attribute__((ad
 // IN_BN: the source is a conv output y of the previous layer; its BatchNorm-apply + ReLU,
 // max(fma(y, scale, shift), 0) with the exact expression of bn_relu_apply_kernel, is applied while the halo
 // is staged (in-range pixels only: the zero padding belongs to the activation).
-template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN>
+// DB: double-buffered halo.  The next chunk's halo is written into the other buffer in the middle of the
+// current chunk (its loads were issued at the chunk's first tap), so a chunk end costs one barrier and the
+// split/store work overlaps the MFMAs instead of stalling between two barriers.
+template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int WPX = TM * 16, WCH = TN * 16;
@@ -53,7 +56,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     constexpr int A_PER = (A_CH + NT - 1) / NT;
     constexpr int PA = HR * 64;
     constexpr int RED = 2 * WAVES_M * BN * 4;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[3 * PA > RED ? 3 * PA : RED];
+    constexpr int NBUF = DB ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * 3 * PA > RED ? NBUF * 3 * PA : RED];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -122,7 +126,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             in_sh = gload4(a.in_shift + ch);
         }
     };
-    auto store_A = [&]() {
+    auto store_A = [&](int buf) {
+        unsigned char *const sb = smem + buf * (3 * PA);
 #pragma unroll
         for (int i = 0; i < A_PER; ++i)
             if ((A_CH % NT == 0) || a_off[i] >= 0) {
@@ -135,9 +140,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                     ra[i] = v;
                 }
                 split3(ra[i], h, m, l);
-                *reinterpret_cast<u32x2 *>(smem + a_off[i]) = h;
-                *reinterpret_cast<u32x2 *>(smem + PA + a_off[i]) = m;
-                *reinterpret_cast<u32x2 *>(smem + 2 * PA + a_off[i]) = l;
+                *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
+                *reinterpret_cast<u32x2 *>(sb + PA + a_off[i]) = m;
+                *reinterpret_cast<u32x2 *>(sb + 2 * PA + a_off[i]) = l;
             }
     };
     const int cpk = a.c / 32;
@@ -164,10 +169,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     }
 
     const int nsteps = cpk * a.ntaps;
+    constexpr int T_STORE = 4;  // DB: tap at which the prefetched halo is written to the other buffer
     u32x4 wq[3][TN];
     load_A(0);
     load_W(0, 0, wq);
-    store_A();
+    store_A(0);
     __syncthreads();
     int cc = 0, t = 0;
     for (int s = 0; s < nsteps; ++s) {
@@ -177,7 +183,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             cc1 = cc + 1;
         }
         const bool more = s + 1 < nsteps;
-        if (more && t1 == 0) load_A(cc1);
+        if constexpr (DB) {
+            if (t == 0 && cc + 1 < cpk) load_A(cc + 1);
+        } else {
+            if (more && t1 == 0) load_A(cc1);
+        }
+        const unsigned char *const sbuf = smem + (DB ? (cc & 1) * (3 * PA) : 0);
         const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
         bf16x8 xv[3][TM], wv[3][TN];
 #pragma unroll
@@ -186,7 +197,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             const int ad = hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-                xv[p][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(smem + p * PA + ad));
+                xv[p][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(sbuf + p * PA + ad));
         }
 #pragma unroll
         for (int p = 0; p < 3; ++p)
@@ -202,10 +213,16 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                 for (int i = 0; i < TM; ++i)
                     acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[QW[q]][j], xv[QX[q]][i], acc[j][i], 0, 0, 0);
         if (more) load_W(cc1, t1, wq);
-        if (more && t1 == 0) {  // chunk end: every wave is done with this halo; overwrite it with the next one
-            __syncthreads();
-            store_A();
-            __syncthreads();
+        if constexpr (DB) {
+            // the other buffer was last read in the previous chunk, which every wave has left (barrier below)
+            if (t == T_STORE && cc + 1 < cpk) store_A((cc + 1) & 1);
+            if (more && t1 == 0) __syncthreads();  // chunk end: the next halo is complete
+        } else {
+            if (more && t1 == 0) {  // chunk end: every wave is done with this halo; overwrite it with the next one
+                __syncthreads();
+                store_A(0);
+                __syncthreads();
+            }
         }
         t = t1;
         cc = cc1;
@@ -299,7 +316,7 @@ int halo16_mode() {
     return g_halo16;
 }
 
-template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN>
+template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN, bool DB>
 void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     IgemmArgs b = a;
@@ -312,19 +329,35 @@ void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     }
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
     if (tw == 64)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN, DB>), grid, block, 0, s, b);
     else if (tw == 32)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN, DB>), grid, block, 0, s, b);
     else
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN, DB>), grid, block, 0, s, b);
+}
+
+// Double buffering where two halo buffers of every resident block still fit the CU's 160 KB of LDS.
+int halo16_db() {
+    const char *e = getenv("SCD_HALO16_DB");  // experiment switch
+    return e ? atoi(e) : 1;
+}
+
+template <int WM, int WN, int TM, int TN, int OCC, bool DB>
+void launch16c(const IgemmArgs &a, int tw, hipStream_t s) {
+    if (a.in_scale)
+        launch16b<WM, WN, TM, TN, OCC, true, DB>(a, tw, s);
+    else
+        launch16b<WM, WN, TM, TN, OCC, false, DB>(a, tw, s);
 }
 
 template <int WM, int WN, int TM, int TN, int OCC>
 void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
-    if (a.in_scale)
-        launch16b<WM, WN, TM, TN, OCC, true>(a, tw, s);
+    constexpr int BM = WM * TM * 16;
+    const int hr = (BM / tw + 2) * (tw + 2);
+    if (tw != 64 && halo16_db() && OCC * 2 * 3 * hr * 64 <= 160 * 1024)
+        launch16c<WM, WN, TM, TN, OCC, true>(a, tw, s);
     else
-        launch16b<WM, WN, TM, TN, OCC, false>(a, tw, s);
+        launch16c<WM, WN, TM, TN, OCC, false>(a, tw, s);
 }
 
 // Tile configurations: id -> (pixels, channels) per block.
@@ -352,7 +385,9 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
         return 0;
     if (id < 0 || id > 2) return 0;
     *bm = kCfg[id].bm;
-    for (int cand : {64, 32, 16})
+    const char *twe = getenv("SCD_HALO16_TW");  // preferred tile width (hip.halo16_tile_width_pref mirrors it)
+    const int pref = twe ? atoi(twe) : 16;  // 16: smallest halo per pixel (180 rows for 128 px)
+    for (int cand : {pref, 64, 32, 16})
         if (a.wo % cand == 0 && a.ho % (*bm / cand) == 0 && *bm / cand >= 1 && *bm % cand == 0) {
             *tw = cand;
             return 1 + id;

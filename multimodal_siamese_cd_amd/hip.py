@@ -274,6 +274,11 @@ def set_halo16(mode: int) -> int:
     return rc
 
 
+def halo16_tile_width_pref() -> int:
+    """The tile width the 16x16x32 halo kernel tries first (mirrors halo16_pick in conv_halo16.hip)."""
+    return int(os.environ.get('SCD_HALO16_TW', '16'))
+
+
 def set_wgrad16(mode: int) -> int:
     """Halo weight-grad kernel selection (0 = 32x32x16 MFMA, 1 = 16x16x32 MFMA); returns the previous mode."""
     rc = lib().scd_set_wgrad16(int(mode))

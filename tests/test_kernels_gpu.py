@@ -294,7 +294,8 @@ def test_conv_halo16_tiles(dev, cfg, n, h, w, ci, co):
         hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, bd, hip.nhwc(y), stat_rec=rec)
         assert rel(y, ref) < TOL
         # per-tile (mean, M2) records against the host definition on the kernel's own output
-        tw = next(c for c in (64, 32, 16) if w % c == 0 and h % (tpx // c) == 0)
+        tw = next(c for c in (hip.halo16_tile_width_pref(), 64, 32, 16)
+                  if w % c == 0 and tpx % c == 0 and h % (tpx // c) == 0)
         tr = tpx // tw
         yy = y.double().cpu().reshape(n, h // tr, tr, w // tw, tw, co).permute(0, 1, 3, 2, 4, 5).reshape(-1, tpx, co)
         r = rec.double().cpu().reshape(ntiles, co, 2)

@@ -4,7 +4,8 @@
 
 A variant is a comma list of knob=value with knobs:
   h16   scd_set_halo16 mode        w16   scd_set_wgrad16 mode
-  fuse  engine BN-apply fusion into the consuming conv (multimodal_siamese_cd_amd.engine.FUSE_INPUT_BN)
+  fuse  engine BN-apply fusion into the consuming conv (engine.set_options(fuse_input_bn=...))
+  SCD_* library environment switches read at launch (e.g. SCD_HALO16_TW=64)
 Prints per-variant median / min ms per step over the rounds.
 """
 import argparse
@@ -22,6 +23,8 @@ from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_f
 
 
 def apply(variant: str):
+    for k in [k for k in os.environ if k.startswith('SCD_')]:
+        del os.environ[k]
     for kv in filter(None, variant.split(',')):
         k, v = kv.split('=')
         if k == 'h16':
@@ -30,6 +33,8 @@ def apply(variant: str):
             hip.set_wgrad16(int(v))
         elif k == 'fuse':
             engine.set_options(fuse_input_bn=bool(int(v)))
+        elif k.startswith('SCD_'):  # library environment switch (read at launch)
+            os.environ[k] = v
         else:
             raise SystemExit(f'unknown knob {k}')
 

@@ -56,8 +56,9 @@ def main():
     ap.add_argument('--layer', default=None, help='run only this layer name (e.g. enc1b)')
     ap.add_argument('--math', default=None, choices=['f32', 'x3'], help='conv arithmetic (default: library default)')
     ap.add_argument('--variants', default=None,
-                    help='comma-separated kernel variants H/W (scd_set_halo16 mode / scd_set_wgrad16 mode), '
-                         'interleaved per layer, e.g. 0/0,1/1')
+                    help='comma-separated variants, interleaved per layer; a variant is "+"-joined settings '
+                         'h16=<scd_set_halo16 mode>, w16=<scd_set_wgrad16 mode> or ENVVAR=value (read by the '
+                         'library at launch), e.g. h16=1+SCD_HALO16_DB=0,h16=1')
     args = ap.parse_args()
     hip.load_library()
     if args.math:
@@ -65,6 +66,7 @@ def main():
     print(f'conv math: {hip.conv_math()}')
     dev = torch.device('cuda:0')
     modes = [None] if args.variants is None else args.variants.split(',')
+    env_set = set()
     tots = {m: {'fwd': [0.0, 0.0], 'dgrad': [0.0, 0.0], 'wgrad': [0.0, 0.0]} for m in modes}
     print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"cin":>5s} {"cout":>5s} | '
           f'{"fwd ms":>8s} {"TF/s":>6s} | {"dgrad ms":>8s} {"TF/s":>6s} | {"wgrad ms":>8s} {"TF/s":>6s}')
@@ -81,10 +83,19 @@ def main():
         flops = 2.0 * n * s * s * co * 9 * ci
         for mode in modes:
             if mode is not None:
-                hv, wv = mode.split('/')
-                hip.set_halo16(int(hv))
-                hip.set_wgrad16(int(wv))
+                for kv in mode.split('+'):
+                    k, v = kv.split('=')
+                    if k == 'h16':
+                        hip.set_halo16(int(v))
+                    elif k == 'w16':
+                        hip.set_wgrad16(int(v))
+                    else:
+                        os.environ[k] = v
+                        env_set.add(k)
             tot = tots[mode]
+            if mode is not None:  # settings not named by this variant go back to their defaults
+                for k in env_set - {kv.split('=')[0] for kv in mode.split('+')}:
+                    os.environ.pop(k, None)
             res = {}
             if args.only in (None, 'fwd'):
                 res['fwd'] = timeit(lambda: hip.conv_igemm(hip.nhwc(x), s, s, 1, hip.TAPS_3X3, wf, co, None,
@@ -109,7 +120,7 @@ def main():
             print(f'{tag:8s} {n:3d} {s:4d} {ci:5d} {co:5d} | ' + ' | '.join(cells), flush=True)
     for mode, tot in tots.items():
         if mode is not None:
-            print(f'-- variant (halo16/wgrad16) {mode}')
+            print(f'-- variant {mode}')
         allt = sum(v[0] for v in tot.values())
         allf = sum(v[1] for v in tot.values())
         for k, (t, f) in tot.items():
