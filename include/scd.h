@@ -117,6 +117,19 @@ int scd_split_bf16x3_frag(const float *w, int32_t n_out, int32_t K, uint16_t *ds
  *           of aten::convolution_backward.  `cat([x2, x1], 1)` (networks.py:449) is zero-copy: dst may
  *           be a channel slice of the concat buffer.
  * ------------------------------------------------------------------------------------------- */
+/* Fused BatchNorm + ReLU backward partial sums in the conv epilogue (for a data-grad conv whose output g
+ * is dL/da of the layer a = relu(BN(y))): per output tile and channel c
+ *   {sum dz, sum dz * xhat},  dz = g if fma(y, scale, shift) > 0 else 0,  xhat = (y - save_mean) * save_invstd
+ * (coefficients of the tile's segment g = img / (n / nseg)) -> rec[c][tile][2], the records
+ * scd_bn_relu_backward_tiles() consumes in place of its own partial pass over (y, g).
+ * replaces: the reductions of native_batch_norm_backward (networks.py:393,396). */
+typedef struct scd_bn_bwd_tiles {
+    scd_nhwc_t y;  /* the BatchNorm input; same n, h, w as the conv output, c = n_out */
+    int32_t nseg;
+    const float *save_mean, *save_invstd, *scale, *shift;  /* [nseg][c] from the forward */
+    float *rec;                                             /* [c][tiles][2] */
+} scd_bn_bwd_tiles_t;
+
 typedef struct scd_igemm {
     scd_nhwc_t src;
     int32_t out_h, out_w;
@@ -145,9 +158,14 @@ typedef struct scd_igemm {
     const float *in_scale;
     const float *in_shift;
     int32_t in_nseg;
+    /* Optional fused BatchNorm backward partial sums of the stored output (see scd_bn_bwd_tiles_t); only
+     * where scd_igemm_bn_bwd_tiles() reports > 0 tiles.  NULL = off. */
+    const scd_bn_bwd_tiles_t *bn_bwd;
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);
+/* Tiles (and *tile_pixels) of the fused BatchNorm-backward partial sums for `d`, 0 if not available. */
+int scd_igemm_bn_bwd_tiles(const scd_igemm_t *d, int32_t *tile_pixels);
 /* 1 if the kernel scd_conv_igemm would run for `d` applies the in_scale/in_shift input transform, else 0. */
 int scd_igemm_input_bn_supported(const scd_igemm_t *d);
 /* Number of statistic tiles scd_conv_igemm would write for `d` (0: no fused statistics for this shape or
@@ -227,6 +245,13 @@ int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float 
                          const float *save_invstd, const float *gamma, const float *scale, const float *shift,
                          float *dgamma, float *dbeta, float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes,
                          scd_stream_t stream);
+
+/* scd_bn_relu_backward with the partial sums taken from conv-epilogue tile records (scd_bn_bwd_tiles_t.rec,
+ * ntiles tiles, image-major, split evenly into nseg segments) instead of a pass over (y, da). */
+int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
+                               const float *save_invstd, const float *gamma, const float *scale, const float *shift,
+                               const float *tile_rec, int32_t ntiles, float *dgamma, float *dbeta,
+                               float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes, scd_stream_t stream);
 
 /* out[c] = sum over all pixels of x[., c] (ConvTranspose2d bias grad, networks.py:433); workspace as
  * scd_bn_workspace_bytes(n, h, w, c, 1).  replaces: the bias-grad reduction of convolution_backward. */

@@ -691,6 +691,40 @@ extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, c
     return launch_status("scd_bn_relu_backward");
 }
 
+extern "C" int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
+                                          const float *save_invstd, const float *gamma, const float *scale,
+                                          const float *shift, const float *tile_rec, int32_t ntiles, float *dgamma,
+                                          float *dbeta, float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes,
+                                          scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(bn_check(y, nseg));
+    SCD_TRY(check_view(da, "bn_bwd.da"));
+    SCD_TRY(check_view(dy, "bn_bwd.dy"));
+    if (da.n != y.n || da.h != y.h || da.w != y.w || da.c != y.c || dy.n != y.n || dy.h != y.h || dy.w != y.w ||
+        dy.c != y.c || !save_mean || !save_invstd || !scale || !shift || !tile_rec || ntiles < nseg ||
+        ntiles % nseg || pixels(y) % ntiles) {
+        set_error("bn_relu_backward_tiles: shape mismatch / null / %d tiles not divisible into %d segments", ntiles,
+                  nseg);
+        return SCD_ERR_ARG;
+    }
+    if (!ws || ws_bytes < scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg)) {
+        set_error("bn_relu_backward_tiles: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    const BnGeom g = bn_geom(y, nseg);
+    float *brec = static_cast<float *>(ws);
+    float *coef = brec + size_t(g.nrec) * y.c;
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, tile_rec, y.c, nseg, ntiles / nseg, ntiles,
+                       g.pseg, coef, dgamma, dbeta);
+    hipLaunchKernelGGL(bn_bwd_apply, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       static_cast<const float *>(y.data), y.ldc, static_cast<const float *>(da.data), da.ldc,
+                       static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean,
+                       save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr);
+    if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
+    return launch_status("scd_bn_relu_backward_tiles");
+}
+
 extern "C" int scd_channel_sum(scd_nhwc_t x, float *out, void *ws, size_t ws_bytes, scd_stream_t stream) {
     clear_error();
     SCD_TRY(check_view(x, "channel_sum.x"));

@@ -79,6 +79,11 @@ struct IgemmArgs {
     FastDiv div_hw, div_w;
     const float *in_scale, *in_shift;  // optional fused input BN-apply + ReLU (halo16 path only)
     int in_seg_imgs;                   // images per coefficient segment
+    // optional fused BatchNorm-backward partial sums of the output (halo16 path only)
+    const float *bb_y;
+    int bb_ldy, bb_seg_imgs, bb_ntiles;
+    const float *bb_mean, *bb_inv, *bb_scale, *bb_shift;
+    float *bb_rec;
 };
 
 struct WgradArgs {

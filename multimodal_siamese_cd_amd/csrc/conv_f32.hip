@@ -573,6 +573,26 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
         }
         a.in_seg_imgs = d->src.n / d->in_nseg;
     }
+    a.bb_y = nullptr;
+    a.bb_rec = nullptr;
+    if (const scd_bn_bwd_tiles_t *b = d->bn_bwd) {
+        if (!b->y.data || !b->rec || !b->save_mean || !b->save_invstd || !b->scale || !b->shift || b->nseg < 1 ||
+            b->y.n != d->dst.n || b->y.h != d->dst.h || b->y.w != d->dst.w || b->y.c != d->n_out ||
+            d->dst.n % b->nseg || b->y.ldc % 4 || (reinterpret_cast<uintptr_t>(b->y.data) & 15) ||
+            !aligned16(b->save_mean) || !aligned16(b->save_invstd) || !aligned16(b->scale) || !aligned16(b->shift)) {
+            set_error("igemm: bn_bwd needs y shaped like dst (c = n_out, 16-byte aligned, ldc %% 4 == 0), all "
+                      "coefficient arrays 16-byte aligned and nseg | n");
+            return SCD_ERR_ARG;
+        }
+        a.bb_y = static_cast<const float *>(b->y.data);
+        a.bb_ldy = b->y.ldc;
+        a.bb_seg_imgs = d->dst.n / b->nseg;
+        a.bb_mean = b->save_mean;
+        a.bb_inv = b->save_invstd;
+        a.bb_scale = b->scale;
+        a.bb_shift = b->shift;
+        a.bb_rec = b->rec;
+    }
     {
         const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * 4 + int64_t(d->src.c) * 4;
         a.src_bytes = sb < (int64_t(1) << 31) ? uint32_t(sb) : 0u;
@@ -589,6 +609,16 @@ extern "C" int scd_igemm_stat_tiles(const scd_igemm_t *d, int32_t *tile_pixels) 
     clear_error();
     IgemmArgs a;
     if (igemm_prepare(d, a) != SCD_OK || d->store_mode != 0) return 0;
+    int tp = 0;
+    const int n = halo_stat_tiles(a, &tp);
+    if (tile_pixels) *tile_pixels = tp;
+    return n;
+}
+
+extern "C" int scd_igemm_bn_bwd_tiles(const scd_igemm_t *d, int32_t *tile_pixels) {
+    clear_error();
+    IgemmArgs a;
+    if (igemm_prepare(d, a) != SCD_OK || d->store_mode != 0 || !igemm_takes_halo16(a)) return 0;
     int tp = 0;
     const int n = halo_stat_tiles(a, &tp);
     if (tile_pixels) *tile_pixels = tp;
@@ -614,6 +644,14 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
         }
     }
     hipStream_t s = as_stream(stream);
+    if (a.bb_rec) {
+        int tp = 0;
+        if (!igemm_takes_halo16(a) || d->stat_rec || (a.bb_ntiles = halo_stat_tiles(a, &tp)) == 0) {
+            set_error("igemm: fused BatchNorm-backward sums are not supported for this descriptor "
+                      "(check scd_igemm_bn_bwd_tiles)");
+            return SCD_ERR_ARG;
+        }
+    }
     if (a.in_scale && !igemm_takes_halo16(a)) {
         set_error("igemm: the fused input transform is not supported for this shape/arithmetic "
                   "(check scd_igemm_input_bn_supported)");

@@ -295,6 +295,56 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             rec[1] = m2;
         }
     }
+
+    // Fused BatchNorm + ReLU backward partial sums of the stored g over this tile (exclusive with stat_rec):
+    // {sum dz, sum dz * xhat} with the expressions of bn_bwd_partial (bn_f32.hip) -> bb_rec[c][tile][2].
+    if (a.bb_rec) {
+        float *red1 = reinterpret_cast<float *>(smem);  // [WAVES_M][BN]
+        float *red2 = red1 + WAVES_M * BN;
+        const int co = (img / a.bb_seg_imgs) * a.n_out;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WCH + j * 16 + 4 * g;
+            const bool nok = n < a.n_out;
+            const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+            const f32x4 mu = nok ? gload4(a.bb_mean + co + n) : z4, iv = nok ? gload4(a.bb_inv + co + n) : z4;
+            const f32x4 sc = nok ? gload4(a.bb_scale + co + n) : z4, sf = nok ? gload4(a.bb_shift + co + n) : z4;
+            f32x4 s1 = z4, s2 = z4;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int p = wm * WPX + i * 16 + l16;
+                const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+                const f32x4 y4 = nok ? gload4(a.bb_y + pix * a.bb_ldy + n) : z4;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float dz = fmaf(y4[r], sc[r], sf[r]) > 0.f ? acc[j][i][r] : 0.f;
+                    s1[r] += dz;
+                    s2[r] += dz * ((y4[r] - mu[r]) * iv[r]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float t1 = row16_sum(s1[r]), t2 = row16_sum(s2[r]);
+                if (l16 == 0) {
+                    red1[wm * BN + wn * WCH + j * 16 + 4 * g + r] = t1;
+                    red2[wm * BN + wn * WCH + j * 16 + 4 * g + r] = t2;
+                }
+            }
+        }
+        __syncthreads();
+        for (int nl = tid; nl < BN; nl += NT) {
+            if (n0 + nl >= a.n_out) continue;
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < WAVES_M; ++w) {
+                t1 += red1[w * BN + nl];
+                t2 += red2[w * BN + nl];
+            }
+            float *rec = a.bb_rec + (size_t(n0 + nl) * a.bb_ntiles + mt) * 2;
+            rec[0] = t1;
+            rec[1] = t2;
+        }
+    }
 }
 
 namespace {

@@ -27,12 +27,14 @@ from .hip import TAPS_1, TAPS_2X2, TAPS_3X3, nhwc
 _F32 = torch.float32
 
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
-_OPTS = {'fuse_input_bn': True}
+_OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True}
 
 
 def set_options(**kw) -> dict:
     """fuse_input_bn: apply a DoubleConv's first BatchNorm + ReLU inside the second conv's operand staging
-    (forward and weight-grad) instead of materialising the activation.  Returns the previous options."""
+    (forward and weight-grad) instead of materialising the activation.
+    fuse_bn_bwd: compute the first BatchNorm's backward partial sums in the epilogue of the data-grad conv that
+    produces its incoming gradient, instead of a separate pass.  Returns the previous options."""
     prev = dict(_OPTS)
     for k, v in kw.items():
         if k not in _OPTS:
@@ -184,7 +186,8 @@ def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, src_bn=No
     return gw
 
 
-def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool):
+def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None):
+    """`tiles` = (records, ntiles) of the partial sums from the conv epilogue that produced g."""
     c = y.shape[3]
     dy = torch.empty_like(y)
     dgamma = _empty((c,), y)
@@ -192,9 +195,29 @@ def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool):
     dbias = _empty((c,), y) if conv_bias_grad else None
     n, h, w, _ = y.shape
     ws = _ws(hip.bn_workspace_bytes(n, h, w, c, st.nseg), y)
-    hip.bn_relu_backward(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift, dgamma, dbeta,
-                         dbias, nhwc(dy), ws)
+    if tiles is not None:
+        hip.bn_relu_backward_tiles(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift,
+                                   tiles[0], tiles[1], dgamma, dbeta, dbias, nhwc(dy), ws)
+    else:
+        hip.bn_relu_backward(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift, dgamma,
+                             dbeta, dbias, nhwc(dy), ws)
     return dy, dgamma, dbeta, dbias
+
+
+def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Tensor, st0: _BNSaved):
+    """Data-grad conv producing dL/da0, with BN0's backward partial sums fused into its epilogue when the kernel
+    offers them.  Returns (ga0, tiles or None)."""
+    n, h, w, _ = dy1.shape
+    ga0 = _empty((n, h, w, n_out), dy1)
+    if _OPTS['fuse_bn_bwd'] and st0.smean is not None:
+        ntiles, _ = hip.igemm_bn_bwd_tiles(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(ga0))
+        if ntiles and ntiles % st0.nseg == 0:
+            rec = _empty((n_out * ntiles * 2,), dy1)
+            hip.conv_igemm(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, None, nhwc(ga0),
+                           bn_bwd=(y0, st0.nseg, st0.smean, st0.sinv, st0.scale, st0.shift, rec))
+            return ga0, (rec, ntiles)
+    hip.conv_igemm(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, None, nhwc(ga0))
+    return ga0, None
 
 
 def _dc_backward(g_out: torch.Tensor, saved, dc, need_dx: bool):
@@ -209,8 +232,8 @@ def _dc_backward(g_out: torch.Tensor, saved, dc, need_dx: bool):
         gw1 = _wgrad3x3(dy1, y0, conv1.weight, (st0.scale, st0.shift, st0.nseg))
     else:
         gw1 = _wgrad3x3(dy1, a0, conv1.weight)
-    ga0 = _conv3x3(dy1, hip.pack_conv3x3(conv1.weight.detach(), 1), None, conv1.in_channels)
-    dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None)
+    ga0, tiles0 = _dgrad_bn_bwd(dy1, hip.pack_conv3x3(conv1.weight.detach(), 1), conv1.in_channels, y0, st0)
+    dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0)
     gw0 = _wgrad3x3(dy0, x, conv0.weight)
     gx = None
     if need_dx:

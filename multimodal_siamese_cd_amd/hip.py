@@ -21,6 +21,13 @@ class NHWC(ctypes.Structure):
     _fields_ = [("data", c_void_p), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32), ("ldc", c_int32)]
 
 
+class BNBWD(ctypes.Structure):
+    """scd_bn_bwd_tiles_t: fused BatchNorm-backward partial sums in a data-grad conv epilogue."""
+
+    _fields_ = [("y", NHWC), ("nseg", c_int32), ("save_mean", c_void_p), ("save_invstd", c_void_p),
+                ("scale", c_void_p), ("shift", c_void_p), ("rec", c_void_p)]
+
+
 class IGEMM(ctypes.Structure):
     _fields_ = [
         ("src", NHWC),
@@ -40,6 +47,7 @@ class IGEMM(ctypes.Structure):
         ("in_scale", c_void_p),
         ("in_shift", c_void_p),
         ("in_nseg", c_int32),
+        ("bn_bwd", POINTER(BNBWD)),
     ]
 
 
@@ -82,6 +90,7 @@ _SIGS = {
     "scd_split_bf16x3_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
     "scd_igemm_input_bn_supported": ([POINTER(IGEMM)], c_int),
+    "scd_igemm_bn_bwd_tiles": ([POINTER(IGEMM), POINTER(c_int32)], c_int),
     "scd_wgrad_src_bn_supported": ([POINTER(WGRAD)], c_int),
     "scd_igemm_stat_tiles": ([POINTER(IGEMM), POINTER(c_int32)], c_int),
     "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
@@ -104,6 +113,11 @@ _SIGS = {
     "scd_bn_relu_backward": (
         [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC,
          c_void_p, c_size_t, c_void_p],
+        c_int,
+    ),
+    "scd_bn_relu_backward_tiles": (
+        [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+         c_void_p, c_void_p, NHWC, c_void_p, c_size_t, c_void_p],
         c_int,
     ),
     "scd_channel_sum": ([NHWC, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
@@ -292,18 +306,34 @@ def conv_math() -> str:
     return {v: k for k, v in _MATH_NAMES.items()}[rc]
 
 
-def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None, in_bn=None):
+def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None, in_bn=None,
+                bn_bwd=None):
     nt, dy, dx = _taps(taps)
     sc, sh, nseg = in_bn if in_bn is not None else (None, None, 0)
+    bb = None
+    if bn_bwd is not None:  # (y, nseg, save_mean, save_invstd, scale, shift, rec)
+        y, bseg, mu, iv, bsc, bsh, rec = bn_bwd
+        bb = ctypes.pointer(BNBWD(nhwc(y), bseg, _ptr(mu), _ptr(iv), _ptr(bsc), _ptr(bsh), _ptr(rec)))
     return IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
-                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg)
+                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg, bb)
 
 
 def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
-               bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None, in_bn=None):
-    """`in_bn` = (scale, shift, nseg): read src through the producing layer's BatchNorm-apply + ReLU."""
-    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec, in_bn)
+               bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None, in_bn=None, bn_bwd=None):
+    """`in_bn` = (scale, shift, nseg): read src through the producing layer's BatchNorm-apply + ReLU.
+    `bn_bwd` = (y, nseg, save_mean, save_invstd, scale, shift, rec): also emit the BatchNorm-backward partial
+    sums of the stored output into rec (see scd_bn_bwd_tiles_t)."""
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec, in_bn, bn_bwd)
     _check(lib().scd_conv_igemm(ctypes.byref(d), _stream()), "scd_conv_igemm")
+
+
+def igemm_bn_bwd_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
+                       dst: NHWC) -> tuple[int, int]:
+    """(tiles, pixels per tile) of the fused BatchNorm-backward partial sums for this conv, (0, 0) if unavailable."""
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0)
+    tp = c_int32(0)
+    n = lib().scd_igemm_bn_bwd_tiles(ctypes.byref(d), ctypes.byref(tp))
+    return (n, tp.value) if n > 0 else (0, 0)
 
 
 def igemm_input_bn_supported(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
@@ -390,6 +420,16 @@ def bn_relu_backward(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, 
                                    shift.data_ptr(), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), dy, ws.data_ptr(),
                                    ws.numel(), _stream()),
         "scd_bn_relu_backward")
+
+
+def bn_relu_backward_tiles(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, tile_rec, ntiles, dgamma, dbeta,
+                           dbias, dy: NHWC, ws):
+    """bn_relu_backward with the partial sums from conv-epilogue tile records (conv_igemm(..., bn_bwd=...))."""
+    _check(
+        lib().scd_bn_relu_backward_tiles(y, da, nseg, smean.data_ptr(), sinv.data_ptr(), _ptr(gamma), scale.data_ptr(),
+                                         shift.data_ptr(), tile_rec.data_ptr(), ntiles, _ptr(dgamma), _ptr(dbeta),
+                                         _ptr(dbias), dy, ws.data_ptr(), ws.numel(), _stream()),
+        "scd_bn_relu_backward_tiles")
 
 
 def channel_sum(x: NHWC, out: torch.Tensor, ws: torch.Tensor):

@@ -356,6 +356,51 @@ def test_fused_input_bn(dev, n, h, w, ci, co, nseg):
         hip.set_conv_math(prev_m)
 
 
+@pytest.mark.parametrize('n,h,w,ci,co,nseg', [(4, 16, 32, 128, 64, 2), (2, 32, 16, 64, 128, 1), (4, 8, 16, 256, 96, 2)])
+def test_fused_bn_backward_partials(dev, n, h, w, ci, co, nseg):
+    """Data-grad conv with BatchNorm-backward partial sums in its epilogue + bn_relu_backward_tiles == the conv
+    followed by bn_relu_backward's own partial pass (dy, dgamma, dbeta, conv-bias grad)."""
+    from multimodal_siamese_cd_amd import hip
+    prev_m = hip.set_conv_math('x3')
+    try:
+        g = torch.Generator().manual_seed(n + ci + co)
+        dy1 = torch.randn(n, h, w, ci, generator=g).to(dev)  # gradient of the next conv's output (ci channels)
+        wt = (torch.randn(ci, co, 3, 3, generator=g) / (3 * ci ** 0.5)).to(dev)  # next conv: co -> ci
+        wb = hip.pack_conv3x3(wt, 1)
+        y0 = torch.randn(n, h, w, co, generator=g).to(dev)  # BN input (conv output of this layer)
+        gamma = (torch.rand(co, generator=g) + 0.5).to(dev)
+        beta = torch.randn(co, generator=g).to(dev)
+        smean, sinv, scale, shift = (torch.empty(nseg * co, device=dev) for _ in range(4))
+        ws = torch.empty(hip.bn_workspace_bytes(n, h, w, co, nseg), dtype=torch.uint8, device=dev)
+        hip.bn_train_stats(hip.nhwc(y0), nseg, gamma, beta, 1e-5, 0.1, False, None, None, smean, sinv, scale, shift, ws)
+        ga_ref = torch.empty(n, h, w, co, device=dev)
+        hip.conv_igemm(hip.nhwc(dy1), h, w, 1, hip.TAPS_3X3, wb, co, None, hip.nhwc(ga_ref))
+        ga = torch.empty(n, h, w, co, device=dev)
+        ntiles, tpx = hip.igemm_bn_bwd_tiles(hip.nhwc(dy1), h, w, 1, hip.TAPS_3X3, wb, co, hip.nhwc(ga))
+        assert ntiles > 0 and ntiles * tpx == n * h * w
+        rec = torch.empty(co * ntiles * 2, device=dev)
+        hip.conv_igemm(hip.nhwc(dy1), h, w, 1, hip.TAPS_3X3, wb, co, None, hip.nhwc(ga),
+                       bn_bwd=(y0, nseg, smean, sinv, scale, shift, rec))
+        assert torch.equal(ga, ga_ref)  # the epilogue sums do not touch the stored output
+        outs = []
+        for fused in (False, True):
+            o = [torch.empty(n, h, w, co, device=dev)] + [torch.empty(co, device=dev) for _ in range(3)]
+            if fused:
+                hip.bn_relu_backward_tiles(hip.nhwc(y0), hip.nhwc(ga), nseg, smean, sinv, gamma, scale, shift, rec,
+                                           ntiles, o[1], o[2], o[3], hip.nhwc(o[0]), ws)
+            else:
+                hip.bn_relu_backward(hip.nhwc(y0), hip.nhwc(ga_ref), nseg, smean, sinv, gamma, scale, shift, o[1], o[2],
+                                     o[3], hip.nhwc(o[0]), ws)
+            outs.append(o)
+        for a, b in zip(outs[0][:3], outs[1][:3]):  # dy, dgamma, dbeta
+            assert rel(a, b) < 2e-6
+        # conv-bias grad sum(dy): exactly 0 in real arithmetic (BatchNorm removes the mean), rounding noise here
+        scale_dy = outs[0][0].abs().max().item()
+        assert outs[0][3].abs().max().item() < 1e-3 * scale_dy and outs[1][3].abs().max().item() < 1e-3 * scale_dy
+    finally:
+        hip.set_conv_math(prev_m)
+
+
 @pytest.mark.parametrize('variant', [0, 1])
 @pytest.mark.parametrize('n,h,w,ci,co', [(2, 4, 32, 64, 64), (3, 6, 16, 128, 192), (1, 32, 64, 64, 128),
                                          (2, 16, 16, 512, 512)])

@@ -200,7 +200,7 @@ def test_fused_input_bn_model_step(dev):
     crit = loss_functions.get_criterion('PowerJaccardLoss')
     runs = []
     for fuse in (True, False):
-        prev = engine.set_options(fuse_input_bn=fuse)
+        prev = engine.set_options(fuse_input_bn=fuse, fuse_bn_bwd=False)
         try:
             net = networks.create_network(cfg)
             with torch.no_grad():
@@ -218,6 +218,21 @@ def test_fused_input_bn_model_step(dev):
     assert torch.equal(o1, o0) and l1 == l0
     for k in g1:
         assert torch.equal(g1[k], g0[k]), k
+    # fused BatchNorm-backward partial sums: same result up to summation order
+    prev = engine.set_options(fuse_input_bn=True, fuse_bn_bwd=True)
+    try:
+        net = networks.create_network(cfg)
+        with torch.no_grad():
+            for k, p in net.module.named_parameters():
+                p.copy_(P[k])
+        net.to(dev).train()
+        loss = crit(net(b['x_t1'].to(dev), b['x_t2'].to(dev)), b['y_change'].to(dev))
+        loss.backward()
+        for k, p in net.module.named_parameters():
+            if not _pre_bn_bias(k):
+                assert rel_err(p.grad.cpu().numpy(), g1[k].numpy()) < 1e-4, k
+    finally:
+        engine.set_options(**prev)
     # against the CPU oracle
     Pr = {k: v.clone().requires_grad_(True) for k, v in P.items()}
     ref = O.forward('siameseunet', Pr, O.fresh_buffers(shapes), b['x_t1'], b['x_t2'], ocfg, True)
