@@ -262,6 +262,11 @@ int scd_channel_sum(scd_nhwc_t x, float *out, void *ws, size_t ws_bytes, scd_str
  * NaN propagates, as aten::max_pool2d_with_indices).  replaces: nn.MaxPool2d(2) (networks.py:420).
  * ------------------------------------------------------------------------------------------- */
 int scd_maxpool2_fwd(scd_nhwc_t x, scd_nhwc_t y, uint8_t *idx, scd_stream_t stream);
+/* The same on max(fma(x, scale[g][c], shift[g][c]), 0), g = img / (n / nseg): the encoder level's
+ * BatchNorm-apply + ReLU (networks.py:396-397) fused into the next level's MaxPool2d (networks.py:420), so the
+ * activation is not materialised.  Bit-identical to pooling the output of scd_bn_relu_apply. */
+int scd_bn_relu_maxpool2_fwd(scd_nhwc_t x, int32_t nseg, const float *scale, const float *shift, scd_nhwc_t y,
+                             uint8_t *idx, scd_stream_t stream);
 
 /* Gradient into an encoder feature map (both Siamese branches):
  *   gx[img] = maxpool_bwd(gy, idx)[img]   (if gy.data != NULL)
@@ -275,6 +280,11 @@ int scd_feature_grad(scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip, int32_
 /* d[b] = a[half + b] - a[b], half = d.n (a.n == 2*d.n): f_t2 - f_t1 (networks.py:147-150).  d may be the
  * skip slice [0:C) of the decoder concat buffer (networks.py:449). */
 int scd_siamese_diff(scd_nhwc_t a, scd_nhwc_t d, scd_stream_t stream);
+/* d = relu(bn_t2(a[n + b])) - relu(bn_t1(a[b])), coefficients [2][c] (t1 segment 0, t2 segment 1): the
+ * feature difference (networks.py:147-150) of the encoder's BatchNorm + ReLU outputs without materialising
+ * them.  d may be a channel slice of the decoder's concat buffer (networks.py:449). */
+int scd_bn_relu_siamese_diff(scd_nhwc_t a, const float *scale, const float *shift, scd_nhwc_t d,
+                             scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * OutConv 1x1 head (networks.py:454-461): out NCHW [n][n_out][h][w] = b + x . w   (n_out <= 4)

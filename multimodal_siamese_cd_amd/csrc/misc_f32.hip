@@ -97,9 +97,19 @@ __device__ __forceinline__ void pool_pick(float v, int k, float &mx, int &idx) {
 
 // Row-decomposed elementwise grids: grid.y walks image rows (img, y), grid.x the channel quads of a row,
 // so the per-element index math is 32-bit (one FastDiv by the quads per pixel) instead of 64-bit div/mod.
+// BN: the input is a conv output read through its BatchNorm-apply + ReLU, max(fma(x, sc, sh), 0) with the
+// coefficients of the image's segment (the expression of bn_relu_apply_kernel, so results are bit-identical
+// to pooling the materialised activation).
+__device__ __forceinline__ float4 bn_relu_f4(float4 v, float4 sc, float4 sh) {
+    return make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
+                       fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
+}
+
+template <bool BN>
 __global__ void maxpool2_fwd_kernel(const float *__restrict__ x, int hx, int wx, int ldx, float *__restrict__ y,
                                    int hy, int wy, int ldy, uint8_t *__restrict__ idx, int C, int rows,
-                                   FastDiv div_cq) {
+                                   FastDiv div_cq, const float *__restrict__ bsc, const float *__restrict__ bsh,
+                                   int seg_imgs) {
     const int cq = C / 4;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= wy * cq) return;
@@ -109,10 +119,18 @@ __global__ void maxpool2_fwd_kernel(const float *__restrict__ x, int hx, int wx,
         const int img = row / hy, oy = row - img * hy;
         const int64_t p = int64_t(row) * wy + ox;  // output pixel
         const float *base = x + ((int64_t(img) * hx + 2 * oy) * wx + 2 * ox) * ldx + c;
-        const float4 v0 = *reinterpret_cast<const float4 *>(base);
-        const float4 v1 = *reinterpret_cast<const float4 *>(base + ldx);
-        const float4 v2 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx);
-        const float4 v3 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx + ldx);
+        float4 v0 = *reinterpret_cast<const float4 *>(base);
+        float4 v1 = *reinterpret_cast<const float4 *>(base + ldx);
+        float4 v2 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx);
+        float4 v3 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx + ldx);
+        if constexpr (BN) {
+            const int o = (img / seg_imgs) * C + c;
+            const float4 sc = *reinterpret_cast<const float4 *>(bsc + o), sh = *reinterpret_cast<const float4 *>(bsh + o);
+            v0 = bn_relu_f4(v0, sc, sh);
+            v1 = bn_relu_f4(v1, sc, sh);
+            v2 = bn_relu_f4(v2, sc, sh);
+            v3 = bn_relu_f4(v3, sc, sh);
+        }
         const float a0[4] = {v0.x, v0.y, v0.z, v0.w}, a1[4] = {v1.x, v1.y, v1.z, v1.w};
         const float a2[4] = {v2.x, v2.y, v2.z, v2.w}, a3[4] = {v3.x, v3.y, v3.z, v3.w};
         float o[4];
@@ -180,8 +198,10 @@ __global__ void feature_grad_kernel(const float *__restrict__ gy, int hy, int wy
     }
 }
 
+template <bool BN>
 __global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float *__restrict__ d, int ldd, int C,
-                                    int w, int64_t half_pixels, int rows, FastDiv div_cq) {
+                                    int w, int64_t half_pixels, int rows, FastDiv div_cq,
+                                    const float *__restrict__ bsc, const float *__restrict__ bsh) {
     const int cq = C / 4;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= w * cq) return;
@@ -189,8 +209,13 @@ __global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float 
     const int c = (e - x * cq) * 4;
     for (int row = blockIdx.y; row < rows; row += gridDim.y) {
         const int64_t p = int64_t(row) * w + x;
-        const float4 v1 = *reinterpret_cast<const float4 *>(a + p * lda + c);
-        const float4 v2 = *reinterpret_cast<const float4 *>(a + (p + half_pixels) * lda + c);
+        float4 v1 = *reinterpret_cast<const float4 *>(a + p * lda + c);
+        float4 v2 = *reinterpret_cast<const float4 *>(a + (p + half_pixels) * lda + c);
+        if constexpr (BN) {  // branch t1 = coefficient segment 0, t2 = segment 1
+            v1 = bn_relu_f4(v1, *reinterpret_cast<const float4 *>(bsc + c), *reinterpret_cast<const float4 *>(bsh + c));
+            v2 = bn_relu_f4(v2, *reinterpret_cast<const float4 *>(bsc + C + c),
+                            *reinterpret_cast<const float4 *>(bsh + C + c));
+        }
         *reinterpret_cast<float4 *>(d + p * ldd + c) = make_float4(v2.x - v1.x, v2.y - v1.y, v2.z - v1.z, v2.w - v1.w);
     }
 }
@@ -439,10 +464,27 @@ extern "C" int scd_maxpool2_fwd(scd_nhwc_t x, scd_nhwc_t y, uint8_t *idx, scd_st
         return SCD_ERR_ARG;
     }
     const int64_t rows = int64_t(y.n) * y.h;
-    hipLaunchKernelGGL(maxpool2_fwd_kernel, row_grid(y.w * (y.c / 4), rows), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<false>, row_grid(y.w * (y.c / 4), rows), dim3(256), 0, as_stream(stream),
                        static_cast<const float *>(x.data), x.h, x.w, x.ldc, static_cast<float *>(y.data), y.h, y.w,
-                       y.ldc, idx, y.c, int(rows), make_fastdiv(uint32_t(y.c / 4)));
+                       y.ldc, idx, y.c, int(rows), make_fastdiv(uint32_t(y.c / 4)), nullptr, nullptr, 1);
     return launch_status("scd_maxpool2_fwd");
+}
+
+extern "C" int scd_bn_relu_maxpool2_fwd(scd_nhwc_t x, int32_t nseg, const float *scale, const float *shift,
+                                        scd_nhwc_t y, uint8_t *idx, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(x, "bn_relu_maxpool.x"));
+    SCD_TRY(check_view(y, "bn_relu_maxpool.y"));
+    if (!idx || !scale || !shift || nseg < 1 || x.n % nseg || y.n != x.n || y.c != x.c || y.h != x.h / 2 ||
+        y.w != x.w / 2 || y.h < 1 || y.w < 1 || !aligned16(scale) || !aligned16(shift)) {
+        set_error("bn_relu_maxpool2_fwd: y must be (n, h/2, w/2, c) with idx, nseg | n, aligned coefficients");
+        return SCD_ERR_ARG;
+    }
+    const int64_t rows = int64_t(y.n) * y.h;
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<true>, row_grid(y.w * (y.c / 4), rows), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(x.data), x.h, x.w, x.ldc, static_cast<float *>(y.data), y.h, y.w,
+                       y.ldc, idx, y.c, int(rows), make_fastdiv(uint32_t(y.c / 4)), scale, shift, x.n / nseg);
+    return launch_status("scd_bn_relu_maxpool2_fwd");
 }
 
 extern "C" int scd_feature_grad(scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip, int32_t skip_mode,
@@ -482,10 +524,27 @@ extern "C" int scd_siamese_diff(scd_nhwc_t a, scd_nhwc_t d, scd_stream_t stream)
         return SCD_ERR_ARG;
     }
     const int64_t rows = int64_t(d.n) * d.h;
-    hipLaunchKernelGGL(siamese_diff_kernel, row_grid(d.w * (d.c / 4), rows), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(siamese_diff_kernel<false>, row_grid(d.w * (d.c / 4), rows), dim3(256), 0, as_stream(stream),
                        static_cast<const float *>(a.data), a.ldc, static_cast<float *>(d.data), d.ldc, d.c, d.w,
-                       pixels(d), int(rows), make_fastdiv(uint32_t(d.c / 4)));
+                       pixels(d), int(rows), make_fastdiv(uint32_t(d.c / 4)), nullptr, nullptr);
     return launch_status("scd_siamese_diff");
+}
+
+extern "C" int scd_bn_relu_siamese_diff(scd_nhwc_t a, const float *scale, const float *shift, scd_nhwc_t d,
+                                        scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(a, "bn_relu_diff.a"));
+    SCD_TRY(check_view(d, "bn_relu_diff.d"));
+    if (a.n != 2 * d.n || a.h != d.h || a.w != d.w || a.c != d.c || !scale || !shift || !aligned16(scale) ||
+        !aligned16(shift)) {
+        set_error("bn_relu_siamese_diff: a must be (2n, h, w, c) of d, aligned coefficients [2][c]");
+        return SCD_ERR_ARG;
+    }
+    const int64_t rows = int64_t(d.n) * d.h;
+    hipLaunchKernelGGL(siamese_diff_kernel<true>, row_grid(d.w * (d.c / 4), rows), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(a.data), a.ldc, static_cast<float *>(d.data), d.ldc, d.c, d.w,
+                       pixels(d), int(rows), make_fastdiv(uint32_t(d.c / 4)), scale, shift);
+    return launch_status("scd_bn_relu_siamese_diff");
 }
 
 extern "C" int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int32_t n_out, float *out,

@@ -27,14 +27,20 @@ from .hip import TAPS_1, TAPS_2X2, TAPS_3X3, nhwc
 _F32 = torch.float32
 
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
-_OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True}
+_OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True}
+
+
+def option(name: str):
+    return _OPTS[name]
 
 
 def set_options(**kw) -> dict:
     """fuse_input_bn: apply a DoubleConv's first BatchNorm + ReLU inside the second conv's operand staging
     (forward and weight-grad) instead of materialising the activation.
     fuse_bn_bwd: compute the first BatchNorm's backward partial sums in the epilogue of the data-grad conv that
-    produces its incoming gradient, instead of a separate pass.  Returns the previous options."""
+    produces its incoming gradient, instead of a separate pass.
+    fuse_siamese_encoder: Siamese streams run SiameseEncoderFn (BN1 + ReLU fused into the next MaxPool and the
+    feature difference, differences written into the decoder's concat buffers).  Returns the previous options."""
     prev = dict(_OPTS)
     for k, v in kw.items():
         if k not in _OPTS:
@@ -150,7 +156,9 @@ def _can_fuse_input_bn(y0: torch.Tensor, wpk1: torch.Tensor, y1: torch.Tensor, s
     return not save or hip.wgrad_src_bn_supported(nhwc(y1), nhwc(y0), 1, TAPS_3X3, bn)
 
 
-def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool):
+def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool, materialize: bool = True):
+    """(a1, saved, y1, st1); with materialize=False the output activation a1 = relu(BN1(y1)) is left to the
+    consumers (None is returned for it)."""
     s = dc.conv
     conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
     cin = x.shape[3]
@@ -171,10 +179,12 @@ def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool):
         hip.bn_relu_apply(nhwc(y0), st0.nseg, st0.scale, st0.shift, nhwc(a0))
         y1, t1 = _conv3x3_stats(a0, wpk1, conv1.bias, conv1.out_channels, _bn_uses_batch_stats(bn1, training), y=y1)
     st1 = _bn_forward(y1, bn1, nseg, training, t1)
-    a1 = torch.empty_like(y1)
-    hip.bn_relu_apply(nhwc(y1), st1.nseg, st1.scale, st1.shift, nhwc(a1))
+    a1 = None
+    if materialize:
+        a1 = torch.empty_like(y1)
+        hip.bn_relu_apply(nhwc(y1), st1.nseg, st1.scale, st1.shift, nhwc(a1))
     saved = (x, y0, a0, st0, y1, st1) if save else None
-    return a1, saved
+    return a1, saved, y1, st1
 
 
 def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, src_bn=None) -> torch.Tensor:
@@ -303,7 +313,7 @@ class EncoderFn(torch.autograd.Function):
                 cur = _empty((n, h // 2, w // 2, c), prev)
                 idx = _empty((n, h // 2, w // 2, c), prev, dtype=torch.uint8)
                 hip.maxpool2_fwd(nhwc(prev), nhwc(cur), idx)
-            a, sv = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save)
+            a, sv, _, _ = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save)
             feats.append(a)
             saved.append((idx, sv))
         if meta.save:
@@ -340,6 +350,88 @@ def run_encoder(inc, encoder, x: torch.Tensor, nseg: int, training: bool) -> lis
     save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
     meta = _Meta(blocks=blocks, nseg=nseg, training=training, save=save)
     return list(EncoderFn.apply(x, meta, *params))
+
+
+# ------------------------------------------------------------------------------------------------
+# Siamese encoder with the feature difference fused in (SiameseUNet / WhateverNet streams)
+# ------------------------------------------------------------------------------------------------
+def _two_seg(st: _BNSaved):
+    """Per-branch [2][C] coefficients (eval mode has one set for both branches)."""
+    if st.nseg == 2:
+        return st.scale, st.shift
+    return torch.cat([st.scale, st.scale]), torch.cat([st.shift, st.shift])
+
+
+class SiameseEncoderFn(torch.autograd.Function):
+    """InConv + Encoder on the 2B-image pair batch, returning f_t2 - f_t1 per level (networks.py:141-150).
+
+    Each level's output activation relu(BN1(y1)) is never materialised: the next level's MaxPool2d and the
+    difference read y1 through BN1 + ReLU.  A level's difference is written into channels [0, C) of the
+    decoder's concat buffer when `meta.extra[level]` names its ConvT channels (zero-copy cat, networks.py:449).
+    Backward: one pass per level forms dL/da1 = maxpool_bwd(g_pool) -/+ g_diff (t1/t2)."""
+
+    @staticmethod
+    def forward(ctx, x, meta, *params):
+        ctx.set_materialize_grads(False)
+        blocks = meta.blocks
+        diffs, saved, bufs = [], [], []
+        cur = x
+        prev = None  # (y1, st1) of the previous level
+        for level, dc in enumerate(blocks):
+            idx = None
+            if level > 0:
+                y1p, st1p = prev
+                n, h, w, c = y1p.shape
+                cur = _empty((n, h // 2, w // 2, c), y1p)
+                idx = _empty((n, h // 2, w // 2, c), y1p, dtype=torch.uint8)
+                hip.bn_relu_maxpool2_fwd(nhwc(y1p), st1p.nseg, st1p.scale, st1p.shift, nhwc(cur), idx)
+            _, sv, y1, st1 = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save, materialize=False)
+            n2, h, w, c = y1.shape
+            extra = meta.extra.get(level, 0)
+            buf = _empty((n2 // 2, h, w, c + extra), y1)
+            d = buf[..., :c] if extra else buf
+            sc, sh = _two_seg(st1)
+            hip.bn_relu_siamese_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c))
+            diffs.append(d)
+            bufs.append(buf if extra else None)
+            saved.append((idx, sv))
+            prev = (y1, st1)
+        meta.cat_buffers = bufs
+        if meta.save:
+            ctx.meta = meta
+            ctx.saved = saved
+        return tuple(diffs)
+
+    @staticmethod
+    def backward(ctx, *g_diffs):
+        meta, saved = ctx.meta, ctx.saved
+        blocks = meta.blocks
+        L = len(blocks) - 1
+        grads = [None] * (8 * len(blocks))
+        g_pool = None
+        for level in range(L, -1, -1):
+            idx_next = saved[level + 1][0] if level < L else None
+            sv = saved[level][1]
+            y1 = sv[4]
+            ga = torch.empty_like(y1)
+            gd = g_diffs[level]
+            hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL, idx_next if g_pool is not None else None,
+                             nhwc(gd) if gd is not None else hip._NULL, 1, nhwc(ga))
+            gx, pg = _dc_backward(ga, sv, blocks[level], need_dx=level > 0)
+            grads[8 * level:8 * level + 8] = pg
+            g_pool = gx
+        ctx.saved = None
+        return (None, None, *grads)
+
+
+def run_siamese_encoder(inc, encoder, x: torch.Tensor, training: bool, extra: dict | None = None):
+    """Feature differences per level (level 0 first) and the concat buffers they live in (None where plain)."""
+    blocks = encoder_blocks(inc, encoder)
+    params = [p for dc in blocks for p in dc_params(dc)]
+    save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+    meta = _Meta(blocks=blocks, nseg=2, training=training, save=save, extra=extra or {})
+    diffs = list(SiameseEncoderFn.apply(x, meta, *params))
+    return diffs, meta.cat_buffers
 
 
 # ------------------------------------------------------------------------------------------------
@@ -390,11 +482,16 @@ class DecoderFn(torch.autograd.Function):
                 raise NotImplementedError(
                     f"Up: non-zero F.pad (skip {h}x{w} vs upsampled {2 * hc}x{2 * wc}) is not supported yet; "
                     "use tile sizes divisible by 2**len(TOPOLOGY)")
-            cat = _empty((b, h, w, cs + cto), skip)
-            hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
+            buf = meta.cat_buffers[k] if meta.cat_buffers is not None else None
+            if (buf is not None and buf.data_ptr() == skip.data_ptr() and tuple(buf.shape) == (b, h, w, cs + cto)
+                    and skip.stride(2) == cs + cto):
+                cat = buf  # the encoder wrote the skip into channels [0, cs) already (zero-copy cat)
+            else:
+                cat = _empty((b, h, w, cs + cto), skip)
+                hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
             wT = hip.pack_convT2x2(convT.weight.detach(), 0)
             hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto), store_mode=1)
-            a, sv = _dc_forward(cat, up.conv, 1, meta.training, meta.save)
+            a, sv, _, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save)
             saved.append((cur, cat, cs, sv))
             cur = a
         if meta.save:
@@ -440,12 +537,20 @@ class DecoderFn(torch.autograd.Function):
         return (None, g, *g_skips, *grads)
 
 
-def run_decoder(decoder, features: list, training: bool) -> torch.Tensor:
-    """`features` in the reference's order: [deepest, ..., level 0] (Encoder.forward's reversed list)."""
+def decoder_cat_channels(decoder, n_levels: int) -> dict:
+    """{encoder level: ConvT output channels of the Up that takes that level's skip}: the concat buffer extent
+    an encoder level can write its skip into (run_siamese_encoder `extra`)."""
+    ups = list(decoder.up_seq.values())
+    return {n_levels - 2 - k: up.up.out_channels for k, up in enumerate(ups)}
+
+
+def run_decoder(decoder, features: list, training: bool, cat_buffers: list | None = None) -> torch.Tensor:
+    """`features` in the reference's order: [deepest, ..., level 0] (Encoder.forward's reversed list).
+    `cat_buffers`: per Up (same order as decoder.up_seq), the concat buffer its skip already lives in, or None."""
     ups = list(decoder.up_seq.values())
     params = [p for up in ups for p in up_params(up)]
     save = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or any(f.requires_grad for f in features))
-    meta = _Meta(ups=ups, training=training, save=save)
+    meta = _Meta(ups=ups, training=training, save=save, cat_buffers=cat_buffers)
     return DecoderFn.apply(meta, features[0], *features[1:1 + len(ups)], *params)
 
 

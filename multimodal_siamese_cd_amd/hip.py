@@ -122,6 +122,8 @@ _SIGS = {
     ),
     "scd_channel_sum": ([NHWC, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
     "scd_maxpool2_fwd": ([NHWC, NHWC, c_void_p, c_void_p], c_int),
+    "scd_bn_relu_maxpool2_fwd": ([NHWC, c_int32, c_void_p, c_void_p, NHWC, c_void_p, c_void_p], c_int),
+    "scd_bn_relu_siamese_diff": ([NHWC, c_void_p, c_void_p, NHWC, c_void_p], c_int),
     "scd_feature_grad": ([NHWC, c_void_p, NHWC, c_int32, NHWC, c_int32, c_void_p], c_int),
     "scd_siamese_diff": ([NHWC, NHWC, c_void_p], c_int),
     "scd_conv1x1_fwd": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p], c_int),
@@ -438,6 +440,18 @@ def channel_sum(x: NHWC, out: torch.Tensor, ws: torch.Tensor):
 
 def maxpool2_fwd(x: NHWC, y: NHWC, idx: torch.Tensor):
     _check(lib().scd_maxpool2_fwd(x, y, idx.data_ptr(), _stream()), "scd_maxpool2_fwd")
+
+
+def bn_relu_maxpool2_fwd(x: NHWC, nseg: int, scale, shift, y: NHWC, idx: torch.Tensor):
+    """MaxPool2d(2) of max(fma(x, scale, shift), 0) per segment (BatchNorm-apply + ReLU fused into the pool)."""
+    _check(lib().scd_bn_relu_maxpool2_fwd(x, nseg, scale.data_ptr(), shift.data_ptr(), y, idx.data_ptr(), _stream()),
+           "scd_bn_relu_maxpool2_fwd")
+
+
+def bn_relu_siamese_diff(a: NHWC, scale, shift, d: NHWC):
+    """d = relu(bn_t2(a[n:])) - relu(bn_t1(a[:n])) with per-branch coefficients [2][C]."""
+    _check(lib().scd_bn_relu_siamese_diff(a, scale.data_ptr(), shift.data_ptr(), d, _stream()),
+           "scd_bn_relu_siamese_diff")
 
 
 def feature_grad(gy: NHWC, idx, gskip: NHWC, skip_mode: int, gx: NHWC, accumulate: bool = False):

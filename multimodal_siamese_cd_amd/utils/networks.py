@@ -91,10 +91,17 @@ def _band_counts(cfg):
 
 def _stream(inc, encoder, decoder, x, nseg, training, siamese):
     """inc + encoder (+ Siamese diff) + decoder of one stream; returns (decoder output, features)."""
+    if siamese and engine.option('fuse_siamese_encoder'):  # networks.py:141-150, fused (engine.SiameseEncoderFn)
+        n_levels = len(encoder.down_seq) + 1
+        diffs, bufs = engine.run_siamese_encoder(inc, encoder, x, training,
+                                                 engine.decoder_cat_channels(decoder, n_levels))
+        feats = diffs[::-1]  # Encoder.forward returns the reversed list (networks.py:342)
+        ups_bufs = [bufs[n_levels - 2 - k] for k in range(len(decoder.up_seq))]
+        return engine.run_decoder(decoder, feats, training, ups_bufs), feats
     feats = engine.run_encoder(inc, encoder, x, nseg, training)
     if siamese:
         feats = [engine.siamese_diff(f) for f in feats]
-    feats = feats[::-1]  # Encoder.forward returns the reversed list (networks.py:342)
+    feats = feats[::-1]
     return engine.run_decoder(decoder, feats, training), feats
 
 

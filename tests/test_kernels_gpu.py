@@ -515,6 +515,30 @@ def test_maxpool_forward_indices_and_feature_grad(dev, n, h, w, c):
     assert torch.allclose(gx.cpu(), want, atol=1e-6)
 
 
+@pytest.mark.parametrize('n,h,w,c,nseg', [(4, 16, 16, 64, 2), (2, 7, 9, 32, 1), (4, 32, 32, 128, 2)])
+def test_bn_relu_fused_pool_and_diff(dev, n, h, w, c, nseg):
+    """MaxPool2d and the Siamese difference reading y through BN-apply + ReLU == the same ops on the
+    materialised activation (bit-identical, argmax bytes included)."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * c + h)
+    y = torch.randn(n, h, w, c, generator=g).to(dev)
+    sc = (torch.rand(nseg * c, generator=g) * 2 - 0.5).to(dev)
+    sh = torch.randn(nseg * c, generator=g).to(dev)
+    a = torch.empty_like(y)
+    hip.bn_relu_apply(hip.nhwc(y), nseg, sc, sh, hip.nhwc(a))
+    p_ref, p = (torch.empty(n, h // 2, w // 2, c, device=dev) for _ in range(2))
+    i_ref, i = (torch.empty(n, h // 2, w // 2, c, device=dev, dtype=torch.uint8) for _ in range(2))
+    hip.maxpool2_fwd(hip.nhwc(a), hip.nhwc(p_ref), i_ref)
+    hip.bn_relu_maxpool2_fwd(hip.nhwc(y), nseg, sc, sh, hip.nhwc(p), i)
+    assert torch.equal(p, p_ref) and torch.equal(i, i_ref)
+    sc2, sh2 = (sc, sh) if nseg == 2 else (torch.cat([sc, sc]), torch.cat([sh, sh]))
+    d_ref = torch.empty(n // 2, h, w, c, device=dev)
+    hip.siamese_diff(hip.nhwc(a), hip.nhwc(d_ref))
+    buf = torch.full((n // 2, h, w, c + 8), 7.0, device=dev)  # write into a concat slice; the rest untouched
+    hip.bn_relu_siamese_diff(hip.nhwc(y), sc2, sh2, hip.nhwc(buf, 0, c))
+    assert torch.equal(buf[..., :c], d_ref) and bool((buf[..., c:] == 7.0).all())
+
+
 def test_siamese_diff(dev):
     from multimodal_siamese_cd_amd import hip
     a = torch.randn(6, 5, 7, 16)

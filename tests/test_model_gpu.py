@@ -259,3 +259,30 @@ def test_fused_input_bn_model_step(dev):
             O.RECORD = None
         print('kink-ambiguous pre-activations in the reference forward:', kinks)
         assert kinks and all(e < KINK_TOL for _, e in bad), (bad, kinks)
+
+
+@pytest.mark.parametrize('name', ['siamese_t8-16', 'whatevernet_t8-16'])
+def test_fused_siamese_encoder_matches_unfused(dev, name):
+    """SiameseEncoderFn (BN + ReLU fused into pool / difference, zero-copy concat) vs the plain encoder +
+    SiameseDiffFn path: logits bit-identical, gradients equal up to summation order."""
+    from multimodal_siamese_cd_amd import engine, trainers
+    fx = Fixture(name)
+    res = []
+    for fused in (True, False):
+        prev = engine.set_options(fuse_siamese_encoder=fused)
+        try:
+            cfg, net = _build(fx, dev)
+            net.train()
+            batch = {k: v.to(dev) for k, v in fx.batch().items()}
+            out = net(batch['x_t1'], batch['x_t2'])
+            loss = trainers.step_loss(cfg, out, batch)
+            loss.backward()
+            res.append(([o.detach().cpu() for o in _outs(out)],
+                        {k: p.grad.cpu() for k, p in net.module.named_parameters() if p.grad is not None}))
+        finally:
+            engine.set_options(**prev)
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b)
+    for k in res[0][1]:
+        if not _pre_bn_bias(k):
+            assert rel_err(res[0][1][k].numpy(), res[1][1][k].numpy()) < 1e-5, k

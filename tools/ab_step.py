@@ -6,6 +6,7 @@ A variant is a comma list of knob=value with knobs:
   h16   scd_set_halo16 mode        w16   scd_set_wgrad16 mode
   fuse  engine BN-apply fusion into the consuming conv (engine.set_options(fuse_input_bn=...))
   fuse_bb  BN-backward partial sums in the data-grad epilogue (engine.set_options(fuse_bn_bwd=...))
+  fuse_enc  fused Siamese encoder (engine.set_options(fuse_siamese_encoder=...))
   SCD_* library environment switches read at launch (e.g. SCD_HALO16_TW=64)
 Prints per-variant median / min ms per step over the rounds.
 """
@@ -36,6 +37,8 @@ def apply(variant: str):
             engine.set_options(fuse_input_bn=bool(int(v)))
         elif k == 'fuse_bb':
             engine.set_options(fuse_bn_bwd=bool(int(v)))
+        elif k == 'fuse_enc':
+            engine.set_options(fuse_siamese_encoder=bool(int(v)))
         elif k.startswith('SCD_'):  # library environment switch (read at launch)
             os.environ[k] = v
         else:
