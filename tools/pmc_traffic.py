@@ -33,12 +33,35 @@ def load(path, counter):
     return out, n
 
 
+def per_kernel(path, counter, out):
+    """All kernels of the pass: dispatches, counter total (KiB) and KiB per dispatch, largest first."""
+    tot = defaultdict(float)
+    n = defaultdict(int)
+    for r in csv.DictReader(open(path)):
+        if r['Counter_Name'] != counter:
+            continue
+        name = r['Kernel_Name'].split('(')[0]
+        tot[name] += float(r['Counter_Value'])
+        n[name] += 1
+    with open(out, 'w', newline='') as f:
+        w = csv.writer(f)
+        w.writerow(['kernel', 'dispatches', f'{counter}_KiB_total', 'KiB_per_dispatch'])
+        for k in sorted(tot, key=lambda k: -tot[k]):
+            w.writerow([k, n[k], f'{tot[k]:.1f}', f'{tot[k] / n[k]:.1f}'])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('dir')
     ap.add_argument('--steps', type=int, required=True, help='training steps covered by the pass')
     ap.add_argument('--out', default=None)
+    ap.add_argument('--summaries', default=None,
+                    help='prefix for per-kernel CSVs: <prefix>_pmc_fetch_summary.csv / _pmc_write_summary.csv')
     args = ap.parse_args()
+    if args.summaries:
+        for counter, tag in (('FETCH_SIZE', 'fetch'), ('WRITE_SIZE', 'write')):
+            per_kernel(os.path.join(args.dir, tag, 'run_counter_collection.csv'), counter,
+                       f'{args.summaries}_pmc_{tag}_summary.csv')
     fetch, nf = load(os.path.join(args.dir, 'fetch', 'run_counter_collection.csv'), 'FETCH_SIZE')
     write, nw = load(os.path.join(args.dir, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE')
     res = {'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over bench.py, '
