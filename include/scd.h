@@ -309,6 +309,26 @@ int scd_pjaccard_fwd(const float *logits, const float *target, int64_t n, float 
 int scd_pjaccard_bwd(const float *logits, const float *target, int64_t n, const float *sums,
                      const float *gloss, float *glogits, float *gtarget, scd_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Eval path
+ * ------------------------------------------------------------------------------------------- */
+/* dst[n, y, x, :] = src[n, y + oy, x + ox, :] where that source pixel exists, else 0 (same n and c).
+ * replaces: F.pad(x1, (dX//2, dX - dX//2, dY//2, dY - dY//2)) of Up.forward (networks.py:437-443) when the skip
+ * is larger than the upsampled map (oy = -dY//2, ox = -dX//2, dst = the concat buffer's up slice), and the
+ * crop of its backward (oy = +dY//2, ox = +dX//2, dst = the ConvT output gradient). */
+int scd_window_copy(scd_nhwc_t src, scd_nhwc_t dst, int32_t oy, int32_t ox, scd_stream_t stream);
+
+/* Confusion counts of MultiThresholdMetric.add_sample (utils/metrics.py:22-31) over n flat elements, for
+ * n_thr <= 16 thresholds:
+ *   p = from_logits ? 1 / (1 + exp(-pred)) : pred      (utils/evaluation.py:25 folded in)
+ *   positive(k) = round(p - thr[k] + 0.5) != 0          (fp32, round half to even; NaN counts as positive)
+ *   label = truth != 0
+ * counts (device int64[1 + 2*n_thr]) = {#label, then per k: #(label & positive(k)), #positive(k)}.  The
+ * reference's TP/TN/FP/FN follow exactly from these and n.  Workspace from the query (0 = bad arguments). */
+size_t scd_threshold_counts_workspace_bytes(int64_t n, int32_t n_thr);
+int scd_threshold_counts(const float *pred, const float *truth, int64_t n, const float *thresholds, int32_t n_thr,
+                         int32_t from_logits, int64_t *counts, void *ws, size_t ws_bytes, scd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -478,10 +478,9 @@ class DecoderFn(torch.autograd.Function):
             _, hc, wc, cu = cur.shape
             convT = up.up
             cto = convT.out_channels
-            if (h, w) != (2 * hc, 2 * wc):
-                raise NotImplementedError(
-                    f"Up: non-zero F.pad (skip {h}x{w} vs upsampled {2 * hc}x{2 * wc}) is not supported yet; "
-                    "use tile sizes divisible by 2**len(TOPOLOGY)")
+            pad_y, pad_x = h - 2 * hc, w - 2 * wc  # networks.py:437-443 (diffY, diffX)
+            if pad_y < 0 or pad_x < 0:
+                raise ValueError(f"Up: upsampled map {2 * hc}x{2 * wc} is larger than the skip {h}x{w}")
             buf = meta.cat_buffers[k] if meta.cat_buffers is not None else None
             if (buf is not None and buf.data_ptr() == skip.data_ptr() and tuple(buf.shape) == (b, h, w, cs + cto)
                     and skip.stride(2) == cs + cto):
@@ -490,7 +489,14 @@ class DecoderFn(torch.autograd.Function):
                 cat = _empty((b, h, w, cs + cto), skip)
                 hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
             wT = hip.pack_convT2x2(convT.weight.detach(), 0)
-            hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto), store_mode=1)
+            if pad_y or pad_x:
+                # ConvT into its own map, then F.pad's zero border and placement in one window copy
+                upm = _empty((b, 2 * hc, 2 * wc, cto), skip)
+                hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(upm), store_mode=1)
+                hip.window_copy(nhwc(upm), nhwc(cat, cs, cto), -(pad_y // 2), -(pad_x // 2))
+            else:
+                hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto),
+                               store_mode=1)
             a, sv, _, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save)
             saved.append((cur, cat, cs, sv))
             cur = a
@@ -517,7 +523,14 @@ class DecoderFn(torch.autograd.Function):
             convT = up.up
             cto = convT.out_channels
             b, hc, wc, cu = cur.shape
-            g_up = nhwc(g_cat, cs, cto)
+            bb, hh, ww, _ = g_cat.shape
+            if (hh, ww) != (2 * hc, 2 * wc):  # backward of F.pad: crop the ConvT's window out of g_cat
+                g_up_t = _empty((b, 2 * hc, 2 * wc, cto), g_cat)
+                hip.window_copy(nhwc(g_cat, cs, cto), nhwc(g_up_t), (hh - 2 * hc) // 2, (ww - 2 * wc) // 2)
+                g_up = nhwc(g_up_t)
+                hh, ww = 2 * hc, 2 * wc
+            else:
+                g_up = nhwc(g_cat, cs, cto)
             # ConvT data grad: 4-tap stride-2 gather of g_cat's up half
             g_cur = torch.empty_like(cur)
             hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, hip.pack_convT2x2(convT.weight.detach(), 1), cu, None,
@@ -529,7 +542,6 @@ class DecoderFn(torch.autograd.Function):
             gwT = torch.empty_like(convT.weight)
             hip.wgrad_finalize(slabs, nsplit, cu, 4, cto, 1, cto, gwT)
             gbT = _empty((cto,), cur)
-            bb, hh, ww, _ = g_cat.shape
             hip.channel_sum(g_up, gbT, _ws(hip.bn_workspace_bytes(bb, hh, ww, cto, 1), cur))
             grads[10 * k:10 * k + 10] = [gwT, gbT] + pg
             g = g_cur

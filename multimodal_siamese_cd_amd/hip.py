@@ -135,6 +135,10 @@ _SIGS = {
     "scd_pjaccard_workspace_bytes": ([c_int64], c_size_t),
     "scd_pjaccard_fwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
     "scd_pjaccard_bwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "scd_window_copy": ([NHWC, NHWC, c_int32, c_int32, c_void_p], c_int),
+    "scd_threshold_counts_workspace_bytes": ([c_int64, c_int32], c_size_t),
+    "scd_threshold_counts": (
+        [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -487,3 +491,26 @@ def pjaccard_fwd(logits, target, sums, loss, ws):
 def pjaccard_bwd(logits, target, sums, gloss, glogits, gtarget=None):
     _check(lib().scd_pjaccard_bwd(logits.data_ptr(), target.data_ptr(), logits.numel(), sums.data_ptr(),
                                   _ptr(gloss), glogits.data_ptr(), _ptr(gtarget), _stream()), "scd_pjaccard_bwd")
+
+
+def window_copy(src: NHWC, dst: NHWC, oy: int, ox: int):
+    """dst[n, y, x] = src[n, y + oy, x + ox] where it exists, else 0 (Up's F.pad and its backward crop)."""
+    _check(lib().scd_window_copy(src, dst, oy, ox, _stream()), "scd_window_copy")
+
+
+THRESHOLD_MAX = 16  # thresholds per scd_threshold_counts launch
+
+
+def threshold_counts_workspace_bytes(n: int, n_thr: int) -> int:
+    return lib().scd_threshold_counts_workspace_bytes(n, n_thr)
+
+
+def threshold_counts(pred: torch.Tensor, truth: torch.Tensor, thresholds: torch.Tensor, from_logits: bool,
+                     counts: torch.Tensor, ws: torch.Tensor):
+    """counts (int64[1 + 2T]) = {#label, per threshold: TP, #positive} of utils/metrics.py:22-31."""
+    n = pred.numel()
+    if truth.numel() != n or counts.numel() != 1 + 2 * thresholds.numel() or counts.dtype != torch.int64:
+        raise ValueError("threshold_counts: pred/truth sizes or counts buffer mismatch")
+    _check(lib().scd_threshold_counts(pred.data_ptr(), truth.data_ptr(), n, thresholds.data_ptr(), thresholds.numel(),
+                                      int(from_logits), counts.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
+           "scd_threshold_counts")

@@ -18,7 +18,18 @@ import numpy as np
 import torch
 
 from . import hip, parallel, trainers
-from .utils import datasets, experiment_manager, networks, parsers
+from .utils import datasets, evaluation, experiment_manager, networks, parsers
+
+
+def _evaluate(net, cfg, device, run_types, epoch_float, step, rank):
+    """evaluation.model_evaluation on rank 0 (the reference evaluates its single DataParallel process,
+    train_supervised.py:84-113), on the unwrapped module so no DDP collective is involved; back to train mode."""
+    if rank != 0 or not cfg.get('EVALUATE', True):
+        return
+    module = net.module if isinstance(net, torch.nn.parallel.DistributedDataParallel) else net
+    for rt in run_types:
+        evaluation.model_evaluation(module, cfg, device, rt, epoch_float, step)
+    net.train()
 
 
 def run_training(cfg, device, max_steps: int | None = None):
@@ -47,12 +58,20 @@ def run_training(cfg, device, max_steps: int | None = None):
             optimizer.step()
             losses.append(loss.detach())
             global_step += 1
+            epoch_float = global_step / steps_per_epoch
+            if cfg.DEBUG:
+                _evaluate(net, cfg, device, ('test',), epoch_float, global_step, rank)
+                break
             if global_step % int(cfg.LOG_FREQ) == 0 and rank == 0:
                 t = timeit.default_timer() - start
-                print(f'step {global_step} epoch {global_step / steps_per_epoch:.2f} '
+                print(f'step {global_step} epoch {epoch_float:.2f} '
                       f'loss {torch.stack(losses).mean().item():.5f} time {t:.1f}s', flush=True)
-            if cfg.DEBUG or (max_steps is not None and global_step >= max_steps):
+                _evaluate(net, cfg, device, ('training', 'validation'), epoch_float, global_step, rank)
+            if max_steps is not None and global_step >= max_steps:
                 break
+        if not cfg.DEBUG:  # evaluation at the end of an epoch (train_supervised.py:107-110)
+            _evaluate(net, cfg, device, ('training', 'validation', 'test'), global_step / steps_per_epoch,
+                      global_step, rank)
         if rank == 0:
             print(f'epoch {epoch}: mean loss {torch.stack(losses).mean().item():.5f}', flush=True)
             if epoch in list(cfg.SAVE_CHECKPOINTS) and not cfg.DEBUG:

@@ -23,20 +23,22 @@ def _channels(cfg) -> int:
     return n1 + n2
 
 
-def synthetic_batch(cfg, batch_size: int, device, generator: torch.Generator, size: int | None = None,
+def synthetic_batch(cfg, batch_size: int, device, generator: torch.Generator, size=None,
                     change_rate: float = 0.05, sem_rate: float = 0.2):
-    """One batch of item dicts stacked along dim 0, generated on `device`."""
+    """One batch of item dicts stacked along dim 0, generated on `device`.  `size`: int or (H, W); default
+    AUGMENTATION.CROP_SIZE (training crops); eval AOIs may be any size (networks.py:437-443 pads)."""
     c = cfg.MODEL.IN_CHANNELS if 'IN_CHANNELS' in cfg.MODEL else _channels(cfg)
     s = size or cfg.AUGMENTATION.CROP_SIZE
+    h, w = (s, s) if isinstance(s, int) else tuple(s)
     kw = dict(device=device, generator=generator)
     b = {
-        'x_t1': torch.rand((batch_size, c, s, s), **kw),
-        'x_t2': torch.rand((batch_size, c, s, s), **kw),
-        'y_change': (torch.rand((batch_size, 1, s, s), **kw) < change_rate).float(),
+        'x_t1': torch.rand((batch_size, c, h, w), **kw),
+        'x_t2': torch.rand((batch_size, c, h, w), **kw),
+        'y_change': (torch.rand((batch_size, 1, h, w), **kw) < change_rate).float(),
     }
     if cfg.DATALOADER.get('INCLUDE_BUILDING_LABELS', False) or cfg.MODEL.TYPE == 'dtsiameseunet':
-        b['y_sem_t1'] = (torch.rand((batch_size, 1, s, s), **kw) < sem_rate).float()
-        b['y_sem_t2'] = (torch.rand((batch_size, 1, s, s), **kw) < sem_rate).float()
+        b['y_sem_t1'] = (torch.rand((batch_size, 1, h, w), **kw) < sem_rate).float()
+        b['y_sem_t2'] = (torch.rand((batch_size, 1, h, w), **kw) < sem_rate).float()
     frac = float(cfg.DATALOADER.get('LABELED_FRACTION', 1.0))
     n_lab = max(1, int(round(frac * batch_size))) if frac > 0 else 0
     b['is_labeled'] = torch.arange(batch_size, device=device) < n_lab
@@ -46,9 +48,11 @@ def synthetic_batch(cfg, batch_size: int, device, generator: torch.Generator, si
 class SyntheticCDDataset(Dataset):
     """Per-item synthetic dataset (CPU tensors), deterministic in (seed, index)."""
 
-    def __init__(self, cfg, run_type: str = 'training', length: int | None = None, seed: int | None = None):
+    def __init__(self, cfg, run_type: str = 'training', length: int | None = None, seed: int | None = None,
+                 size=None):
         self.cfg = cfg
         self.run_type = run_type
+        self.size = size
         self.length = length if length is not None else int(cfg.TRAINER.get('STEPS_PER_EPOCH', 100)) * int(
             cfg.TRAINER.BATCH_SIZE)
         self.seed = int(cfg.SEED if seed is None else seed)
@@ -58,7 +62,7 @@ class SyntheticCDDataset(Dataset):
 
     def __getitem__(self, index):
         g = torch.Generator().manual_seed(self.seed * 1_000_003 + index)
-        item = synthetic_batch(self.cfg, 1, 'cpu', g)
+        item = synthetic_batch(self.cfg, 1, 'cpu', g, size=self.size)
         out = {k: v[0] for k, v in item.items()}
         out['is_labeled'] = bool(index % 2 == 0) if self.cfg.DATALOADER.get('INCLUDE_UNLABELED', False) else True
         out['aoi_id'] = f'synthetic_{index:06d}'

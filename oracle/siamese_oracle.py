@@ -302,13 +302,14 @@ def synthetic_batch(cfg, batch, hw, seed, labeled=None):
 
     rng = np.random.default_rng(seed)
     c = cfg['IN_CHANNELS']
+    h, w = (hw, hw) if isinstance(hw, int) else tuple(hw)
     f = lambda *s: torch.from_numpy(rng.random(s, dtype=np.float32))
     out = {
-        'x_t1': f(batch, c, hw, hw),
-        'x_t2': f(batch, c, hw, hw),
-        'y_change': (f(batch, 1, hw, hw) > 0.9).float(),
-        'y_sem_t1': (f(batch, 1, hw, hw) > 0.8).float(),
-        'y_sem_t2': (f(batch, 1, hw, hw) > 0.8).float(),
+        'x_t1': f(batch, c, h, w),
+        'x_t2': f(batch, c, h, w),
+        'y_change': (f(batch, 1, h, w) > 0.9).float(),
+        'y_sem_t1': (f(batch, 1, h, w) > 0.8).float(),
+        'y_sem_t2': (f(batch, 1, h, w) > 0.8).float(),
     }
     out['is_labeled'] = torch.tensor(labeled if labeled is not None else [True] * batch)
     return out

@@ -38,6 +38,9 @@ CONFIGS = [
     ('dualstream_t8-16', 'dualstreamunet', [8, 16], 5, [0, 1], [2, 1, 0], 2, 32, None),
     ('dtsiamese_t8-16', 'dtsiameseunet', [8, 16], 5, [0, 1], [2, 1, 0], 2, 32, None),
     ('whatevernet_t8-16', 'whatevernet', [8, 16], 5, [0, 1], [2, 1, 0], 2, 32, [True, False]),
+    # tiles not divisible by 2**levels: MaxPool floors and Up zero-pads the upsampled map (networks.py:437-443)
+    ('siamese_t8-16-32_odd', 'siameseunet', [8, 16, 32], 5, [0, 1], [2, 1, 0], 2, (37, 45), None),
+    ('dualstream_t8-16_odd', 'dualstreamunet', [8, 16], 5, [0, 1], [2, 1, 0], 1, (27, 30), None),
 ]
 LR = 1e-3
 WD = 0.01
@@ -79,6 +82,10 @@ def main():
     ap.add_argument('--only', default=None)
     args = ap.parse_args()
     networks, loss_functions = import_reference(args.ref)
+    if args.only in (None, 'metrics'):
+        make_metrics_fixture()
+        if args.only == 'metrics':
+            return
     pj = loss_functions.get_criterion('PowerJaccardLoss')
     torch.set_num_threads(min(8, os.cpu_count() or 1))
 
@@ -147,6 +154,47 @@ def main():
         path = os.path.join(HERE, f'{name}.npz')
         np.savez_compressed(path, **rec)
         print(f'{name}: loss0={losses[0]:.6f} losses={losses} -> {os.path.getsize(path) / 1024:.0f} KiB')
+
+
+def make_metrics_fixture():
+    """utils/metrics.py MultiThresholdMetric (metrics.py:5-59) over three add_sample calls.
+
+    Probabilities include exact threshold values, their fp32 neighbours, 0, 1 and NaN, so the
+    round(p - t + 0.5) decision (metrics.py:26) is pinned at its ties; one label is NaN (bool() -> True)."""
+    from utils import metrics
+    rng = np.random.default_rng(SEED + 100)
+    thr = torch.linspace(0, 1, 11)
+    m = metrics.MultiThresholdMetric(thr)
+    m5 = metrics.MultiThresholdMetric(torch.linspace(0.5, 1, 1))  # utils/evaluation.py:12
+    rec = {'thresholds': thr.numpy()}
+    for i, (b, h, w) in enumerate([(2, 16, 24), (1, 37, 45), (3, 8, 8)]):
+        p = rng.random((b, 1, h, w), dtype=np.float32)
+        flat = p.reshape(-1)
+        ties = np.concatenate([thr.numpy(), np.nextafter(thr.numpy(), 2), np.nextafter(thr.numpy(), -1),
+                               np.float32([0, 1, 0.5, np.nan])]).astype(np.float32)
+        flat[:ties.size] = np.clip(ties, 0, 1) if i else ties
+        y = (rng.random((b, 1, h, w)) > 0.6).astype(np.float32)
+        if i == 0:
+            y.reshape(-1)[-1] = np.nan
+        rec[f'y_pred/{i}'] = p
+        rec[f'y_true/{i}'] = y
+        m.add_sample(torch.from_numpy(y), torch.from_numpy(p))
+        m5.add_sample(torch.from_numpy(y), torch.from_numpy(p))
+    for k in ('TP', 'TN', 'FP', 'FN'):
+        rec[k] = getattr(m, k).numpy()
+        rec['eval_' + k] = getattr(m5, k).numpy()
+    rec['precision'] = m.precision.numpy()
+    rec['recall'] = m.recall.numpy()
+    rec['f1'] = m.compute_f1().numpy()
+    fpr, fnr = m.compute_basic_metrics()
+    rec['fpr'] = fpr.numpy()
+    rec['fnr'] = fnr.numpy()
+    rec['eval_f1'] = m5.compute_f1().numpy()
+    rec['meta'] = np.array(json.dumps(dict(name='metrics', generator='reference utils/metrics.py (CPU, torch '
+                                           + torch.__version__ + ')')))
+    path = os.path.join(HERE, 'metrics_mt.npz')
+    np.savez_compressed(path, **rec)
+    print(f'metrics: f1={rec["f1"]} -> {os.path.getsize(path) / 1024:.0f} KiB')
 
 
 def _ref_step_loss(mtype, out, batch, pj):
