@@ -1,6 +1,6 @@
 """Throughput benchmark of the Siamese U-Net training step on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config baseline_siamese] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config baseline_siamese] [--batch B] [--math x3|bf16|f32]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 One step = zero_grad -> SiameseUNet forward (HIP) -> power_jaccard_loss -> backward (HIP) -> AdamW step,
@@ -13,7 +13,9 @@ Measurement extras (rank 0, after the timed region):
                 matrix-core ceiling, combined as flops / sum(flops_i / peak_i):
                   - fp32 MFMA: 157.3 TFLOP/s;
                   - split-bf16 x3: bf16 dense 2516.6 / 6 products = 419.4 fp32-equivalent TFLOP/s
-                    (MI355X_MICROARCH.md).
+                    (MI355X_MICROARCH.md);
+                  - bf16 (--math bf16, or a config with MODEL.PRECISION: bf16): bf16 dense 2516.6 TFLOP/s.
+                The arithmetic of every launch comes from the library (scd_igemm_arith / scd_wgrad_arith).
   cpu_baseline  the CPU oracle (oracle/siamese_oracle.py, torch fp32 on host cores) running the same training
                 step on a bounded sample (bs=2, 256x256).
 """
@@ -36,6 +38,7 @@ from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_f
 FP32_MFMA_PEAK_TFLOPS = 157.3
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # dense, MI355X_MICROARCH.md (1/16 ratio)
 X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6           # six bf16 products per fp32 multiply-add
+PEAKS = {'f32': FP32_MFMA_PEAK_TFLOPS, 'x3': X3_PEAK_TFLOPS, 'bf16': BF16_MFMA_PEAK_TFLOPS}
 METRIC = "image-pairs/sec training step, 256×256 SAR+optical Siamese U-Net, 1/2/4/8 MI355X"
 
 
@@ -73,7 +76,6 @@ class KernelTimer:
         self.active = False
         self._igemm = hip.conv_igemm
         self._wgrad = hip.conv_wgrad
-        self.math = hip.conv_math()
 
     def install(self):
         timer = self
@@ -81,24 +83,26 @@ class KernelTimer:
         def igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k):
             if not timer.active:
                 return timer._igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k)
+            arith = hip.igemm_arith(src, out_h, out_w, stride, taps, wpk, n_out, a[1] if len(a) > 1 else k['dst'],
+                                    a[2] if len(a) > 2 else k.get('store_mode', 0))
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             r = timer._igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k)
             e.record()
             flops = 2.0 * src.n * out_h * out_w * n_out * len(taps[0]) * src.c
-            x3 = timer.math == 'x3' and src.c % 16 == 0  # the library's x3 eligibility rule (conv_x3.hip)
-            timer.events.append(('igemm', s, e, flops, x3))
+            timer.events.append(('igemm', s, e, flops, arith))
             return r
 
         def wgrad(d, slabs):
             if not timer.active:
                 return timer._wgrad(d, slabs)
+            arith = hip.wgrad_arith(d)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             r = timer._wgrad(d, slabs)
             e.record()
             flops = 2.0 * d.rows.n * d.rows.h * d.rows.w * d.rows.c * d.ntaps * d.src.c
-            timer.events.append(('wgrad', s, e, flops, timer.math == 'x3'))
+            timer.events.append(('wgrad', s, e, flops, arith))
             return r
 
         hip.conv_igemm = igemm
@@ -113,11 +117,14 @@ class KernelTimer:
         return out
 
     def peak(self):
-        """Harmonic flop-weighted matrix-core peak of the timed launches (TFLOP/s)."""
+        """Harmonic flop-weighted matrix-core peak of the timed launches (TFLOP/s) and each arithmetic's share."""
         f = sum(ev[3] for ev in self.events)
-        t = sum(ev[3] / ((X3_PEAK_TFLOPS if ev[4] else FP32_MFMA_PEAK_TFLOPS) * 1e12) for ev in self.events)
-        x3_share = sum(ev[3] for ev in self.events if ev[4]) / f
-        return f / t / 1e12, x3_share
+        t = sum(ev[3] / (PEAKS[ev[4]] * 1e12) for ev in self.events)
+        share = {m: round(sum(ev[3] for ev in self.events if ev[4] == m) / f, 4) for m in PEAKS}
+        return f / t / 1e12, {m: v for m, v in share.items() if v > 0}
+
+    def launched_flops(self, reps):
+        return sum(ev[3] for ev in self.events) / reps
 
 
 def cpu_baseline(cfg, steps: int = 2, batch: int = 2, size: int = 256):
@@ -128,7 +135,8 @@ def cpu_baseline(cfg, steps: int = 2, batch: int = 2, size: int = 256):
     torch.set_num_threads(threads)
     ocfg = dict(TOPOLOGY=list(cfg.MODEL.TOPOLOGY), IN_CHANNELS=cfg.MODEL.IN_CHANNELS, OUT_CHANNELS=1,
                 S1_BANDS=list(cfg.DATALOADER.S1_BANDS), S2_BANDS=list(cfg.DATALOADER.S2_BANDS))
-    shapes = O.param_shapes('siameseunet', ocfg)
+    mtype = cfg.MODEL.TYPE
+    shapes = O.param_shapes(mtype, ocfg)
     P = {k: v.requires_grad_(True) for k, v in O.deterministic_params(shapes, 7).items()}
     B = O.fresh_buffers(shapes)
     b = O.synthetic_batch(ocfg, batch, size, 8)
@@ -136,8 +144,8 @@ def cpu_baseline(cfg, steps: int = 2, batch: int = 2, size: int = 256):
 
     def step():
         opt.zero_grad()
-        out = O.forward('siameseunet', P, B, b['x_t1'], b['x_t2'], ocfg, True)
-        loss = O.power_jaccard_loss(out, b['y_change'])
+        out = O.forward(mtype, P, B, b['x_t1'], b['x_t2'], ocfg, True)
+        loss = O.step_loss(mtype, out, b, 0.5)
         loss.backward()
         opt.step()
 
@@ -147,7 +155,7 @@ def cpu_baseline(cfg, steps: int = 2, batch: int = 2, size: int = 256):
         step()
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 4), "unit": "image-pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} timed training steps (after 1 warm-up) of the CPU oracle, bs={batch}, "
+            "sample": f"{steps} timed training steps (after 1 warm-up) of the CPU oracle ({mtype}), bs={batch}, "
                       f"{size}x{size}, {cfg.MODEL.IN_CHANNELS}-ch, TOPOLOGY {list(cfg.MODEL.TOPOLOGY)}, fp32, "
                       f"torch {torch.__version__} with {threads} threads ({dt:.1f} s)"}
 
@@ -162,6 +170,8 @@ def main():
     ap.add_argument('--size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'bf16'],
+                    help='conv arithmetic (default: from the config, engine.conv_math_for: MODEL.PRECISION fp32 -> x3)')
     args = ap.parse_args()
 
     rank, local_rank, world = parallel.init_distributed()
@@ -170,6 +180,9 @@ def main():
     hip.load_library()
 
     cfg = experiment_manager.load_cfg(args.config)
+    math = args.math or engine.conv_math_for(cfg)
+    hip.set_conv_math(math)
+    dtype = 'bf16' if math == 'bf16' else 'f32'
     batch = args.batch or int(cfg.TRAINER.BATCH_SIZE)
     size = args.size or int(cfg.AUGMENTATION.CROP_SIZE)
     torch.manual_seed(cfg.SEED)
@@ -223,18 +236,21 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": dtype,
         "data": "synthetic (on-device U[0,1) pairs, Bernoulli(0.05) change masks; random-init weights)",
-        "config": {"workload": f"{args.config}: siameseunet TOPOLOGY {list(cfg.MODEL.TOPOLOGY)}, "
-                               f"{cfg.MODEL.IN_CHANNELS}-ch SAR+optical, {size}x{size}, bs={batch}/GPU, fp32, "
-                               f"train step incl. AdamW",
+        "config": {"workload": f"{args.config}: {cfg.MODEL.TYPE} TOPOLOGY {list(cfg.MODEL.TOPOLOGY)}, "
+                               f"{cfg.MODEL.IN_CHANNELS}-ch SAR+optical, {size}x{size}, bs={batch}/GPU, "
+                               f"conv math {math}, train step incl. AdamW",
                    "global_batch": batch * world, "tile": size, "parallelism": f"dp{world}",
                    "topology": list(cfg.MODEL.TOPOLOGY)},
         "loss_first_last": [round(first_loss, 6), round(last_loss, 6)],
-        "step_roofline": {"formula": "3x3-stack train FLOP/pair x pairs/s/GPU / fp32 MFMA peak",
-                          "gflop_per_pair_3x3": round(f3 / batch / 1e9, 2),
-                          "frac": round(f3 / batch * (value / world) / (FP32_MFMA_PEAK_TFLOPS * 1e12), 4)},
     }
+    if cfg.MODEL.TYPE == 'siameseunet':  # SURVEY 8(d) formula (273.3 GF/pair at 256^2, 5-ch)
+        dpeak = BF16_MFMA_PEAK_TFLOPS if dtype == 'bf16' else FP32_MFMA_PEAK_TFLOPS
+        result["step_roofline"] = {
+            "formula": f"3x3-stack train FLOP/pair x pairs/s/GPU / {dtype} MFMA peak ({dpeak})",
+            "gflop_per_pair_3x3": round(f3 / batch / 1e9, 2),
+            "frac": round(f3 / batch * (value / world) / (dpeak * 1e12), 4)}
 
     if rank == 0 and not args.no_kernel_timing:
         timer = KernelTimer()
@@ -246,27 +262,30 @@ def main():
         timer.active = False
         summ = timer.summary()
         t_ms = sum(t for _, t in summ.values()) / reps
-        achieved = (f3 + fT) / (t_ms * 1e-3) / 1e12
+        # algorithmic conv FLOPs for the Siamese U-Net; other models: the launched conv FLOPs
+        flop_step = f3 + fT if cfg.MODEL.TYPE == 'siameseunet' else timer.launched_flops(reps)
+        achieved = flop_step / (t_ms * 1e-3) / 1e12
         traffic = None
         pmc = sorted(f for f in os.listdir(os.path.join(ROOT, 'profiles')) if f.endswith('_pmc_traffic.json'))
-        if pmc and args.config == 'baseline_siamese' and batch == 32 and size == 256:
+        if pmc and args.config == 'baseline_siamese' and batch == 32 and size == 256 and math == 'x3':
             with open(os.path.join(ROOT, 'profiles', pmc[-1])) as f:
                 tr = json.load(f)
             traffic = {"bytes_per_step": round(tr['per_step_bytes']['total']),
                        "by_family": {k: round(v) for k, v in tr['per_step_bytes'].items() if k != 'total'},
                        "source": f"profiles/{pmc[-1]}: {tr['source']}; L2-miss fabric bytes (Infinity-Cache "
                                  "hits included, MI355X_MICROARCH.md HBM)"}
-        peak, x3_share = timer.peak()
+        peak, shares = timer.peak()
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
-            "peak_basis": f"conv math {timer.math}: {x3_share:.3f} of executed conv FLOPs on split-bf16 x3 "
-                          f"(peak {X3_PEAK_TFLOPS:.1f} = bf16 dense {BF16_MFMA_PEAK_TFLOPS:.1f} / 6 products), the rest "
-                          f"on fp32 MFMA ({FP32_MFMA_PEAK_TFLOPS}); combined flop-weighted harmonically",
+            "peak_basis": f"conv math {math}: share of executed conv FLOPs per arithmetic {shares} (peaks: x3 "
+                          f"{X3_PEAK_TFLOPS:.1f} = bf16 dense {BF16_MFMA_PEAK_TFLOPS:.1f} / 6 products, bf16 "
+                          f"{BF16_MFMA_PEAK_TFLOPS:.1f}, fp32 MFMA {FP32_MFMA_PEAK_TFLOPS}); combined flop-weighted "
+                          "harmonically",
             "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
             "kernel": "igemm + wgrad (all conv launches of one training step: 3x3 fwd/dgrad/wgrad, "
                       "ConvT fwd/dgrad/wgrad)",
-            "flop_per_step": f3 + fT,
+            "flop_per_step": flop_step,
             "kernel_ms_per_step": round(t_ms, 3),
             "launches_per_step": {k: v[0] // reps for k, v in summ.items()},
             "ms_per_family": {k: round(v[1] / reps, 3) for k, v in summ.items()},

@@ -83,11 +83,20 @@ int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, floa
  *                 hh+hm+mh+mm+hl+lh.  The dropped terms are <= ~2^-26 relative, so the rounding error is
  *                 of fp32 order, at 6/16 of the matrix-core cycles.  Used when src.c % 16 == 0; other shapes
  *                 fall back to the fp32 MFMA kernel.
- * Default: SCD_MATH_X3, or the SCD_CONV_MATH=f32|x3 environment variable at first use.  Returns the
+ *   SCD_MATH_BF16 bf16 operands (each fp32 operand rounded to nearest bf16, the h term of the split), one
+ *                 v_mfma_f32_16x16x32_bf16 product per k step, fp32 accumulation: the arithmetic of a bf16
+ *                 autocast conv (BASELINE configs baseline_dualstream / siamese_mmcr, dtype bf16).  Applies to
+ *                 the 16x16x32 halo kernels (3x3 stride-1 fwd / data-grad / weight-grad, >= 98% of the
+ *                 U-Net's conv FLOPs); every other conv shape keeps the SCD_MATH_X3 kernels.  Activations and
+ *                 BatchNorm stay fp32.
+ * Default: SCD_MATH_X3, or the SCD_CONV_MATH=f32|x3|bf16 environment variable at first use.  Returns the
  * previous mode; SCD_MATH_QUERY only queries.  Process-wide (not per stream).
  * ------------------------------------------------------------------------------------------- */
-enum scd_conv_math { SCD_MATH_QUERY = -1, SCD_MATH_F32 = 0, SCD_MATH_X3 = 1 };
+enum scd_conv_math { SCD_MATH_QUERY = -1, SCD_MATH_F32 = 0, SCD_MATH_X3 = 1, SCD_MATH_BF16 = 2 };
 int scd_set_conv_math(int32_t mode);
+/* The arithmetic scd_conv_igemm / scd_conv_wgrad would use for this descriptor under the current mode:
+ * SCD_MATH_F32, SCD_MATH_X3 or SCD_MATH_BF16; negative = invalid descriptor.  (Declared with the descriptors
+ * below.) */
 /* Tile selection of the 16x16x32-MFMA halo conv kernel (SCD_MATH_X3, 3x3 / stride 1, C % 32 == 0):
  * 0 = off (32x32x16 halo kernel), 1 = automatic, 2 + id = force tile id (0: 128 px x 128 ch, 1: 128 x 64,
  * 2: 64 x 128).  Returns the previous mode; -1 only queries.  Process-wide; results are identical up to
@@ -164,6 +173,7 @@ typedef struct scd_igemm {
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);
+int scd_igemm_arith(const scd_igemm_t *d); /* see scd_set_conv_math */
 /* Tiles (and *tile_pixels) of the fused BatchNorm-backward partial sums for `d`, 0 if not available. */
 int scd_igemm_bn_bwd_tiles(const scd_igemm_t *d, int32_t *tile_pixels);
 /* 1 if the kernel scd_conv_igemm would run for `d` applies the in_scale/in_shift input transform, else 0. */
@@ -197,6 +207,7 @@ typedef struct scd_wgrad {
 
 /* Number of K-splits the library will use and the slab bytes it needs. */
 int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes);
+int scd_wgrad_arith(const scd_wgrad_t *d); /* see scd_set_conv_math */
 int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream);
 /* 1 if the weight-grad kernel scd_conv_wgrad would run for `d` applies the src_scale/src_shift transform. */
 int scd_wgrad_src_bn_supported(const scd_wgrad_t *d);

@@ -13,6 +13,8 @@
 // MFMA operand trick (fp32, 32x32x2): instruction s of an 8-deep K chunk takes k = 4h + s from lane
 // half h = lane>>5, so every lane reads its 4 k-values for a row with ONE ds_read_b128 from a
 // [row][k] LDS image (row stride BK+4 floats: conflict-free b128 reads).
+#include <algorithm>
+
 #include "conv_common.h"
 
 namespace scd {
@@ -467,13 +469,15 @@ static int check_taps(int ntaps, const int8_t *dy, const int8_t *dx) {
 
 static int g_conv_math = -1;
 
-int conv_math_x3() {
+static int conv_math_mode() {
     if (g_conv_math < 0) {
         const char *e = getenv("SCD_CONV_MATH");
-        g_conv_math = (e && e[0] == 'f') ? SCD_MATH_F32 : SCD_MATH_X3;
+        g_conv_math = (e && e[0] == 'f') ? SCD_MATH_F32 : (e && e[0] == 'b') ? SCD_MATH_BF16 : SCD_MATH_X3;
     }
-    return g_conv_math == SCD_MATH_X3;
+    return g_conv_math;
 }
+int conv_math_x3() { return conv_math_mode() != SCD_MATH_F32; }
+int conv_math_planes() { return conv_math_mode() == SCD_MATH_BF16 ? 1 : 3; }
 
 }  // namespace scd
 
@@ -481,8 +485,8 @@ using namespace scd;
 
 extern "C" int scd_set_conv_math(int32_t mode) {
     clear_error();
-    const int prev = conv_math_x3() ? SCD_MATH_X3 : SCD_MATH_F32;
-    if (mode == SCD_MATH_F32 || mode == SCD_MATH_X3) {
+    const int prev = conv_math_mode();
+    if (mode == SCD_MATH_F32 || mode == SCD_MATH_X3 || mode == SCD_MATH_BF16) {
         g_conv_math = mode;
     } else if (mode != SCD_MATH_QUERY) {
         set_error("scd_set_conv_math: mode %d", mode);
@@ -605,10 +609,90 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
 }
 }  // namespace scd
 
+namespace scd {
+// Image chunking.  The buffer-load kernels address operands with 32-bit byte offsets, so a conv whose
+// operands span 2 GiB or more (e.g. the Siamese level-0 maps at bs=64: 128 x 256^2 x 64 fp32) runs as several
+// launches over image ranges.  A chunk keeps whole BatchNorm coefficient segments or divides one, so the
+// per-segment coefficient pointers are offset instead of the kernels learning an image base; fused
+// statistics / BN-backward records are per image tile, so their pointers advance by whole images.
+static int64_t img_bytes(const scd_nhwc_t &v) { return int64_t(v.h) * v.w * v.ldc * 4; }
+static int image_chunk(int64_t bytes_per_img, int n, int seg) {
+    const int64_t lim = ((int64_t(1) << 31) - 1) / std::max<int64_t>(bytes_per_img, 1);
+    if (lim >= n) return n;
+    if (lim < 1) return 0;
+    if (lim >= seg) return int(lim / seg) * seg;
+    for (int c = int(lim); c >= 1; --c)
+        if (seg % c == 0) return c;
+    return 1;
+}
+static scd_nhwc_t img_slice(scd_nhwc_t v, int img0, int cnt) {
+    v.data = static_cast<char *>(v.data) + img0 * img_bytes(v);
+    v.n = cnt;
+    return v;
+}
+
+// Images per launch for `d` (d->src.n = one launch; 0 = cannot chunk, one launch on 64-bit-offset kernels).
+static int igemm_chunk(const scd_igemm_t *d) {
+    if (d->store_mode != 0 || d->src.n != d->dst.n || d->src.n < 2) return d->src.n;
+    const int64_t per = std::max(img_bytes(d->src), std::max(img_bytes(d->dst), d->bn_bwd ? img_bytes(d->bn_bwd->y)
+                                                                                          : int64_t(0)));
+    if (int64_t(d->src.n) * per < (int64_t(1) << 31)) return d->src.n;
+    int seg = 1;  // segment size of the coefficient arrays the launch reads (1 = none)
+    if (d->in_scale && d->in_nseg > 0) seg = d->src.n / d->in_nseg;
+    if (d->bn_bwd && d->bn_bwd->nseg > 0) {
+        const int sb = d->src.n / d->bn_bwd->nseg;
+        seg = seg == 1 ? sb : (sb == seg ? seg : 0);
+    }
+    return seg > 0 ? image_chunk(per, d->src.n, seg) : 0;
+}
+
+// Descriptor of images [img0, img0 + cnt) (tiles_per_img: fused-record tiles per image).
+static scd_igemm_t igemm_slice(const scd_igemm_t *d, int img0, int cnt, int tiles_per_img, scd_bn_bwd_tiles_t &b) {
+    scd_igemm_t c = *d;
+    c.src = img_slice(d->src, img0, cnt);
+    c.dst = img_slice(d->dst, img0, cnt);
+    if (d->stat_rec) c.stat_rec = d->stat_rec + size_t(img0) * tiles_per_img * d->n_out * 2;
+    if (d->in_scale && d->in_nseg > 0) {
+        const int sg = d->src.n / d->in_nseg;
+        c.in_scale = d->in_scale + size_t(img0 / sg) * d->src.c;
+        c.in_shift = d->in_shift + size_t(img0 / sg) * d->src.c;
+        c.in_nseg = std::max(1, cnt / sg);
+    }
+    if (d->bn_bwd && d->bn_bwd->nseg > 0) {
+        b = *d->bn_bwd;
+        const int sg = d->src.n / b.nseg;
+        const size_t o = size_t(img0 / sg) * d->n_out;
+        b.y = img_slice(b.y, img0, cnt);
+        b.save_mean += o;
+        b.save_invstd += o;
+        b.scale += o;
+        b.shift += o;
+        b.nseg = std::max(1, cnt / sg);
+        b.rec += size_t(img0) * tiles_per_img * 2;
+        c.bn_bwd = &b;
+    }
+    return c;
+}
+
+// Kernel arguments as the launches will see them (the first chunk's), with n_img restored to the whole batch:
+// what the eligibility and record-tile queries evaluate.
+static int igemm_query_prepare(const scd_igemm_t *d, IgemmArgs &a) {
+    const int chunk = igemm_chunk(d);
+    if (chunk <= 0 || chunk >= d->src.n) return igemm_prepare(d, a);
+    scd_bn_bwd_tiles_t b;
+    const scd_igemm_t c = igemm_slice(d, 0, chunk, 0, b);
+    SCD_TRY(igemm_prepare(&c, a));
+    a.n_img = d->src.n;
+    return SCD_OK;
+}
+
+static int conv_igemm_run(const scd_igemm_t *d, hipStream_t s, int bb_ntiles_total);
+}  // namespace scd
+
 extern "C" int scd_igemm_stat_tiles(const scd_igemm_t *d, int32_t *tile_pixels) {
     clear_error();
     IgemmArgs a;
-    if (igemm_prepare(d, a) != SCD_OK || d->store_mode != 0) return 0;
+    if (igemm_query_prepare(d, a) != SCD_OK || d->store_mode != 0) return 0;
     int tp = 0;
     const int n = halo_stat_tiles(a, &tp);
     if (tile_pixels) *tile_pixels = tp;
@@ -618,7 +702,7 @@ extern "C" int scd_igemm_stat_tiles(const scd_igemm_t *d, int32_t *tile_pixels) 
 extern "C" int scd_igemm_bn_bwd_tiles(const scd_igemm_t *d, int32_t *tile_pixels) {
     clear_error();
     IgemmArgs a;
-    if (igemm_prepare(d, a) != SCD_OK || d->store_mode != 0 || !igemm_takes_halo16(a)) return 0;
+    if (igemm_query_prepare(d, a) != SCD_OK || d->store_mode != 0 || !igemm_takes_halo16(a)) return 0;
     int tp = 0;
     const int n = halo_stat_tiles(a, &tp);
     if (tile_pixels) *tile_pixels = tp;
@@ -628,12 +712,46 @@ extern "C" int scd_igemm_bn_bwd_tiles(const scd_igemm_t *d, int32_t *tile_pixels
 extern "C" int scd_igemm_input_bn_supported(const scd_igemm_t *d) {
     clear_error();
     IgemmArgs a;
-    if (igemm_prepare(d, a) != SCD_OK) return 0;
+    if (igemm_query_prepare(d, a) != SCD_OK) return 0;
     return igemm_takes_halo16(a) ? 1 : 0;
 }
 
+extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
+    clear_error();
+    IgemmArgs a;
+    SCD_TRY(igemm_query_prepare(d, a));
+    if (!conv_math_x3()) return SCD_MATH_F32;
+    if (igemm_takes_halo16(a)) return conv_math_planes() == 1 ? SCD_MATH_BF16 : SCD_MATH_X3;
+    return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
+}
+
+
 extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
     clear_error();
+    if (!d) {
+        set_error("igemm: null descriptor");
+        return SCD_ERR_ARG;
+    }
+    hipStream_t s = as_stream(stream);
+    const int chunk = igemm_chunk(d);
+    if (chunk <= 0 || chunk >= d->src.n) return conv_igemm_run(d, s, 0);
+    int tiles = 0, tile_pixels = 0;
+    if (d->stat_rec || d->bn_bwd) {
+        IgemmArgs a;
+        SCD_TRY(igemm_query_prepare(d, a));
+        tiles = halo_stat_tiles(a, &tile_pixels);
+    }
+    const int tiles_per_img = tiles / d->src.n;
+    for (int img0 = 0; img0 < d->src.n; img0 += chunk) {
+        scd_bn_bwd_tiles_t b;
+        const scd_igemm_t c = igemm_slice(d, img0, std::min(chunk, d->src.n - img0), tiles_per_img, b);
+        SCD_TRY(conv_igemm_run(&c, s, d->bn_bwd ? tiles : 0));
+    }
+    return SCD_OK;
+}
+
+namespace scd {
+static int conv_igemm_run(const scd_igemm_t *d, hipStream_t s, int bb_ntiles_total) {
     IgemmArgs a;
     SCD_TRY(igemm_prepare(d, a));
     if (d->stat_rec) {
@@ -643,7 +761,6 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
             return SCD_ERR_ARG;
         }
     }
-    hipStream_t s = as_stream(stream);
     if (a.bb_rec) {
         int tp = 0;
         if (!igemm_takes_halo16(a) || d->stat_rec || (a.bb_ntiles = halo_stat_tiles(a, &tp)) == 0) {
@@ -651,6 +768,7 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
                       "(check scd_igemm_bn_bwd_tiles)");
             return SCD_ERR_ARG;
         }
+        if (bb_ntiles_total) a.bb_ntiles = bb_ntiles_total;  // record row stride of the whole batch (chunks)
     }
     if (a.in_scale && !igemm_takes_halo16(a)) {
         set_error("igemm: the fused input transform is not supported for this shape/arithmetic "
@@ -666,6 +784,7 @@ extern "C" int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream) {
         launch_igemm_bk<4, 1, 2, 1>(a, s);  // 256 x 32
     return launch_status("scd_conv_igemm");
 }
+}  // namespace scd
 
 namespace scd {
 struct WgradTile {
@@ -780,8 +899,8 @@ static bool wgrad_halo_ok(const scd_wgrad_t *d) {
 }
 
 static int wgrad_halo_resident() {
-    static int caches[2] = {0, 0};  // per halo weight-grad kernel (scd_set_wgrad16)
-    int &cache = caches[wgrad16_mode() ? 1 : 0];
+    static int caches[3] = {0, 0, 0};  // per halo weight-grad kernel (scd_set_wgrad16; halo16 x3 / bf16)
+    int &cache = caches[wgrad16_mode() ? (conv_math_planes() == 1 ? 2 : 1) : 0];
     if (cache > 0) return cache;
     int per_cu = 0, cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -819,11 +938,56 @@ extern "C" int scd_wgrad_src_bn_supported(const scd_wgrad_t *d) {
     return wgrad_src_bn_ok(d) ? 1 : 0;
 }
 
+extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
+    clear_error();
+    SCD_TRY(wgrad_validate(d));
+    if (!conv_math_x3()) return SCD_MATH_F32;
+    return (wgrad_halo_ok(d) && wgrad16_mode() && conv_math_planes() == 1) ? SCD_MATH_BF16 : SCD_MATH_X3;
+}
+
+namespace scd {
+// Images per weight-grad launch (rows.n = one launch; 0 = one image alone exceeds 2 GiB), see image_chunk.
+static int wgrad_chunk(const scd_wgrad_t *d) {
+    const int64_t per = std::max(img_bytes(d->rows), img_bytes(d->src));
+    if (int64_t(d->rows.n) * per < (int64_t(1) << 31)) return d->rows.n;
+    const int seg = (d->src_scale && d->src_nseg > 0) ? d->src.n / d->src_nseg : 1;
+    return image_chunk(per, d->rows.n, seg);
+}
+static scd_wgrad_t wgrad_slice(const scd_wgrad_t *d, int img0, int cnt) {
+    scd_wgrad_t c = *d;
+    c.rows = img_slice(d->rows, img0, cnt);
+    c.src = img_slice(d->src, img0, cnt);
+    if (d->src_scale && d->src_nseg > 0) {
+        const int sg = d->src.n / d->src_nseg;
+        c.src_scale = d->src_scale + size_t(img0 / sg) * d->src.c;
+        c.src_shift = d->src_shift + size_t(img0 / sg) * d->src.c;
+        c.src_nseg = std::max(1, cnt / sg);
+    }
+    return c;
+}
+// Total K-splits over the image chunks (each chunk writes its own slab range; the finalize sums them all).
+static int wgrad_total_splits(const scd_wgrad_t *d) {
+    const int chunk = wgrad_chunk(d);
+    int total = 0;
+    for (int img0 = 0; img0 < d->rows.n; img0 += std::max(chunk, 1)) {
+        const scd_wgrad_t c = wgrad_slice(d, img0, std::min(std::max(chunk, 1), d->rows.n - img0));
+        int ns, kc;
+        wgrad_split(&c, &ns, &kc);
+        total += ns;
+    }
+    return total;
+}
+static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, hipStream_t s);
+}  // namespace scd
+
 extern "C" int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
-    int ns, kc;
-    wgrad_split(d, &ns, &kc);
+    if (wgrad_chunk(d) < 1) {
+        set_error("wgrad: one image of the operands spans 2 GiB or more (32-bit buffer offsets)");
+        return SCD_ERR_ARG;
+    }
+    const int ns = wgrad_total_splits(d);
     if (nsplit) *nsplit = ns;
     if (slab_bytes) *slab_bytes = size_t(ns) * d->rows.c * d->ntaps * d->src.c * sizeof(float);
     return SCD_OK;
@@ -832,6 +996,31 @@ extern "C" int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *sla
 extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
+    const int chunk = wgrad_chunk(d);
+    if (chunk < 1) {
+        set_error("wgrad: one image of the operands spans 2 GiB or more (32-bit buffer offsets)");
+        return SCD_ERR_ARG;
+    }
+    if (chunk >= d->rows.n) return conv_wgrad_run(d, slabs, slab_bytes, as_stream(stream));
+    const size_t slab = size_t(d->rows.c) * d->ntaps * d->src.c;
+    const size_t need = size_t(wgrad_total_splits(d)) * slab * sizeof(float);
+    if (!slabs || slab_bytes < need) {
+        set_error("wgrad: slab workspace %zu < %zu bytes", slab_bytes, need);
+        return SCD_ERR_WORKSPACE;
+    }
+    size_t used = 0;  // slabs written by the previous chunks
+    for (int img0 = 0; img0 < d->rows.n; img0 += chunk) {
+        const scd_wgrad_t c = wgrad_slice(d, img0, std::min(chunk, d->rows.n - img0));
+        int ns, kc;
+        wgrad_split(&c, &ns, &kc);
+        SCD_TRY(conv_wgrad_run(&c, slabs + used * slab, (size_t(ns)) * slab * sizeof(float), as_stream(stream)));
+        used += size_t(ns);
+    }
+    return SCD_OK;
+}
+
+namespace scd {
+static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, hipStream_t s) {
     int ns, kc;
     wgrad_split(d, &ns, &kc);
     const int Ng = d->ntaps * d->src.c;
@@ -883,7 +1072,6 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
         }
         a.src_seg_imgs = d->src.n / d->src_nseg;
     }
-    hipStream_t s = as_stream(stream);
     if (wgrad_halo_ok(d)) {
         a.n_img_w = d->rows.n;
         a.grid_r = a.R / 64;
@@ -911,6 +1099,7 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
     }
     return launch_status("scd_conv_wgrad");
 }
+}  // namespace scd
 
 extern "C" int scd_wgrad_finalize(float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C,
                                   int32_t mode, int32_t c_valid, float *out, scd_stream_t stream) {

@@ -44,7 +44,9 @@ __device__ __forceinline__ void gstore4(float *p, f32x4 v) { *(__attribute__((ad
 // DB: double-buffered halo.  The next chunk's halo is written into the other buffer in the middle of the
 // current chunk (its loads were issued at the chunk's first tap), so a chunk end costs one barrier and the
 // split/store work overlaps the MFMAs instead of stalling between two barriers.
-template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB>
+// NP: bf16 planes per operand: 3 = the exact x3 split (six products per step), 1 = bf16 operands
+// (SCD_MATH_BF16: the h term only, one product per step).
+template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int WPX = TM * 16, WCH = TN * 16;
@@ -57,7 +59,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     constexpr int PA = HR * 64;
     constexpr int RED = 2 * WAVES_M * BN * 4;
     constexpr int NBUF = DB ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * 3 * PA > RED ? NBUF * 3 * PA : RED];
+    static_assert(NP == 1 || NP == 3, "x3 or bf16 planes");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * NP * PA > RED ? NBUF * NP * PA : RED];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         }
     };
     auto store_A = [&](int buf) {
-        unsigned char *const sb = smem + buf * (3 * PA);
+        unsigned char *const sb = smem + buf * (NP * PA);
 #pragma unroll
         for (int i = 0; i < A_PER; ++i)
             if ((A_CH % NT == 0) || a_off[i] >= 0) {
@@ -139,17 +142,23 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                         v[q] = a_boff[i] == kOOB ? 0.f : fmaxf(fmaf(ra[i][q], in_sc[q], in_sh[q]), 0.f);
                     ra[i] = v;
                 }
-                split3(ra[i], h, m, l);
-                *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
-                *reinterpret_cast<u32x2 *>(sb + PA + a_off[i]) = m;
-                *reinterpret_cast<u32x2 *>(sb + 2 * PA + a_off[i]) = l;
+                if constexpr (NP == 3) {
+                    split3(ra[i], h, m, l);
+                    *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
+                    *reinterpret_cast<u32x2 *>(sb + PA + a_off[i]) = m;
+                    *reinterpret_cast<u32x2 *>(sb + 2 * PA + a_off[i]) = l;
+                } else {
+                    h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
+                    h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
+                    *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
+                }
             }
     };
     const int cpk = a.c / 32;
-    auto load_W = [&](int cc, int t, u32x4 (&wq)[3][TN]) {
+    auto load_W = [&](int cc, int t, u32x4 (&wq)[NP][TN]) {
         const uint32_t ko = uint32_t(t * cpk + cc) * 2048u;  // 32-deep step = two 16-deep fragments
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
                 wq[p][j] = bload4u(rs_w, w_base[j] == kOOB ? kOOB : w_base[j] + ko + uint32_t(p) * wplane_b);
@@ -170,7 +179,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 
     const int nsteps = cpk * a.ntaps;
     constexpr int T_STORE = 4;  // DB: tap at which the prefetched halo is written to the other buffer
-    u32x4 wq[3][TN];
+    u32x4 wq[NP][TN];
     load_A(0);
     load_W(0, 0, wq);
     store_A(0);
@@ -188,25 +197,26 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         } else {
             if (more && t1 == 0) load_A(cc1);
         }
-        const unsigned char *const sbuf = smem + (DB ? (cc & 1) * (3 * PA) : 0);
+        const unsigned char *const sbuf = smem + (DB ? (cc & 1) * (NP * PA) : 0);
         const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
-        bf16x8 xv[3][TM], wv[3][TN];
+        bf16x8 xv[NP][TM], wv[NP][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int hr = a_hr[i] + toff;
             const int ad = hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
+            for (int p = 0; p < NP; ++p)
                 xv[p][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(sbuf + p * PA + ad));
         }
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
 #pragma unroll
             for (int j = 0; j < TN; ++j) wv[p][j] = __builtin_bit_cast(bf16x8, wq[p][j]);
+        // (w, x) term pairs smallest first: mm, hl, lh, hm, mh, hh; bf16 (NP == 1) runs hh only
         constexpr int QW[6] = {1, 0, 2, 0, 1, 0};
         constexpr int QX[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
-        for (int q = 0; q < 6; ++q)
+        for (int q = NP == 3 ? 0 : 5; q < 6; ++q)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -366,7 +376,7 @@ int halo16_mode() {
     return g_halo16;
 }
 
-template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN, bool DB>
+template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN, bool DB, int NP>
 void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     IgemmArgs b = a;
@@ -379,11 +389,11 @@ void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     }
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
     if (tw == 64)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN, DB>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN, DB, NP>), grid, block, 0, s, b);
     else if (tw == 32)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN, DB>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN, DB, NP>), grid, block, 0, s, b);
     else
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN, DB>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN, DB, NP>), grid, block, 0, s, b);
 }
 
 // Double buffering where two halo buffers of every resident block still fit the CU's 160 KB of LDS.
@@ -392,22 +402,28 @@ int halo16_db() {
     return e ? atoi(e) : 1;
 }
 
-template <int WM, int WN, int TM, int TN, int OCC, bool DB>
+template <int WM, int WN, int TM, int TN, int OCC, bool DB, int NP>
 void launch16c(const IgemmArgs &a, int tw, hipStream_t s) {
     if (a.in_scale)
-        launch16b<WM, WN, TM, TN, OCC, true, DB>(a, tw, s);
+        launch16b<WM, WN, TM, TN, OCC, true, DB, NP>(a, tw, s);
     else
-        launch16b<WM, WN, TM, TN, OCC, false, DB>(a, tw, s);
+        launch16b<WM, WN, TM, TN, OCC, false, DB, NP>(a, tw, s);
 }
 
 template <int WM, int WN, int TM, int TN, int OCC>
 void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
-    if (tw != 64 && halo16_db() && OCC * 2 * 3 * hr * 64 <= 160 * 1024)
-        launch16c<WM, WN, TM, TN, OCC, true>(a, tw, s);
-    else
-        launch16c<WM, WN, TM, TN, OCC, false>(a, tw, s);
+    if (conv_math_planes() == 1) {  // one plane: double buffering always fits
+        if (halo16_db())
+            launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
+        else
+            launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
+    } else if (tw != 64 && halo16_db() && OCC * 2 * 3 * hr * 64 <= 160 * 1024) {
+        launch16c<WM, WN, TM, TN, OCC, true, 3>(a, tw, s);
+    } else {
+        launch16c<WM, WN, TM, TN, OCC, false, 3>(a, tw, s);
+    }
 }
 
 // Tile configurations: id -> (pixels, channels) per block.
@@ -470,50 +486,62 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
 namespace {
 constexpr int kW16RS = 160;
 
-template <int T, int CB, int PB, int HW_>
+// X fragments of half tap (T, CB): two transposed reads per plane (NP planes).
+template <int T, int CB, int PB, int HW_, int NP>
 __device__ __forceinline__ void w16_read_x(s16x4 (&f)[6], uint32_t xbase) {
     constexpr int toff = (T / 3) * HW_ + (T % 3);  // (1 + dy) * HW_ + (1 + dx)
     tr_read<0 * PB + toff * kW16RS + CB * 32>(f[0], xbase);
     tr_read<0 * PB + (toff + 8) * kW16RS + CB * 32>(f[1], xbase);
-    tr_read<1 * PB + toff * kW16RS + CB * 32>(f[2], xbase);
-    tr_read<1 * PB + (toff + 8) * kW16RS + CB * 32>(f[3], xbase);
-    tr_read<2 * PB + toff * kW16RS + CB * 32>(f[4], xbase);
-    tr_read<2 * PB + (toff + 8) * kW16RS + CB * 32>(f[5], xbase);
+    if constexpr (NP == 3) {
+        tr_read<1 * PB + toff * kW16RS + CB * 32>(f[2], xbase);
+        tr_read<1 * PB + (toff + 8) * kW16RS + CB * 32>(f[3], xbase);
+        tr_read<2 * PB + toff * kW16RS + CB * 32>(f[4], xbase);
+        tr_read<2 * PB + (toff + 8) * kW16RS + CB * 32>(f[5], xbase);
+    }
 }
 
-// One half tap (tap T, channel block CB): wait for its X fragments, then six split products x 2 r-blocks.
-template <int T, int CB, int WAIT>
+// One half tap (tap T, channel block CB): wait for its X fragments, then the split products (six for x3, hh
+// for bf16) x 2 r-blocks.
+template <int T, int CB, int WAIT, int NP>
 __device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f)[6]) {
     bf16x8 x0 = cat8(f[0], f[1]), x1 = cat8(f[2], f[3]), x2 = cat8(f[4], f[5]);
-    lds_wait<WAIT>(x0, x1, x2);
-    if (T == 0 && CB == 0) {
-        lds_wait<WAIT>(dv[0][0], dv[1][0], dv[2][0]);
-        lds_wait<WAIT>(dv[0][1], dv[1][1], dv[2][1]);
+    if constexpr (NP == 3) {
+        lds_wait<WAIT>(x0, x1, x2);
+        if (T == 0 && CB == 0) {
+            lds_wait<WAIT>(dv[0][0], dv[1][0], dv[2][0]);
+            lds_wait<WAIT>(dv[0][1], dv[1][1], dv[2][1]);
+        }
+    } else {
+        lds_wait<WAIT>(x0, dv[0][0], dv[0][1]);
     }
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
-        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
-        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[2][rb], acc[T][CB][rb], 0, 0, 0);
-        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
-        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
-        acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
+        if constexpr (NP == 3) {
+            acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
+            acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[2][rb], acc[T][CB][rb], 0, 0, 0);
+            acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
+            acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
+            acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
+        }
         acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
     }
 }
 
-// Half taps H = 2T + CB, one ahead: compute H from buffer H & 1, then refill that buffer with H + 2.
-template <int H, int PB, int HW_>
+// Half taps H = 2T + CB, one ahead: compute H from buffer H & 1, then refill that buffer with H + 2.  The
+// counted wait leaves the 2*NP reads of the other buffer (issued one half tap earlier) in flight.
+template <int H, int PB, int HW_, int NP>
 __device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f0)[6], s16x4 (&f1)[6],
                                           uint32_t xbase) {
     if constexpr (H < 18) {
         s16x4 (&f)[6] = (H & 1) ? f1 : f0;
-        w16_half<H / 2, H % 2, (H == 17 ? 0 : 6)>(acc, dv, f);
-        if constexpr (H + 2 < 18) w16_read_x<(H + 2) / 2, (H + 2) % 2, PB, HW_>(f, xbase);
-        w16_chain<H + 1, PB, HW_>(acc, dv, f0, f1, xbase);
+        w16_half<H / 2, H % 2, (H == 17 ? 0 : 2 * NP), NP>(acc, dv, f);
+        if constexpr (H + 2 < 18) w16_read_x<(H + 2) / 2, (H + 2) % 2, PB, HW_, NP>(f, xbase);
+        w16_chain<H + 1, PB, HW_, NP>(acc, dv, f0, f1, xbase);
     }
 }
 }  // namespace
 
+template <int NP>
 __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     constexpr int PH = 2, PW = 16, P = PH * PW;
     constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
@@ -521,7 +549,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     constexpr int PA = P * RS, PB = HP * RS;            // plane bytes
     constexpr int A_CH = P * 16, B_CH = HP * 16;        // 4-channel pieces
     constexpr int A_PER = A_CH / 256, B_PER = (B_CH + 255) / 256;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[3 * PA + 3 * PB];
+    static_assert(NP == 1 || NP == 3, "x3 or bf16 planes");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NP * PA + NP * PB];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wi = wid >> 1, wj = wid & 1;
@@ -570,13 +599,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     auto store_patch = [&]() {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
-            u32x2 h, m, l;
-            split3(ra[i], h, m, l);
             const int e = tid + i * 256;
             const int o = (e >> 4) * RS + (e & 15) * 8;
+            u32x2 h, m, l;
+            if constexpr (NP == 3) {
+                split3(ra[i], h, m, l);
+                *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
+                *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
+            } else {
+                h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
+                h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
+            }
             *reinterpret_cast<u32x2 *>(smem + o) = h;
-            *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
-            *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
@@ -587,12 +621,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], x_sc[q], x_sh[q]), 0.f) : 0.f;
                 }
-                split3(rb[i], h, m, l);
                 const int e = tid + i * 256;
-                const int o = 3 * PA + (e >> 4) * RS + (e & 15) * 8;
+                const int o = NP * PA + (e >> 4) * RS + (e & 15) * 8;
+                if constexpr (NP == 3) {
+                    split3(rb[i], h, m, l);
+                    *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
+                    *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
+                } else {
+                    h[0] = cvt_pk_bf16(rb[i][0], rb[i][1]);
+                    h[1] = cvt_pk_bf16(rb[i][2], rb[i][3]);
+                }
                 *reinterpret_cast<u32x2 *>(smem + o) = h;
-                *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
-                *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
             }
     };
 
@@ -609,7 +648,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     const int g = lane >> 4, w16 = lane & 15;
     const int py = g >> 1, pxq = 4 * (g & 1) + (w16 >> 2);
     const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RS + (32 * wi + 4 * (w16 & 3)) * 2;
-    const uint32_t xbase = lds_addr(smem) + 3 * PA + (py * HW_ + pxq) * RS + (32 * wj + 4 * (w16 & 3)) * 2;
+    const uint32_t xbase = lds_addr(smem) + NP * PA + (py * HW_ + pxq) * RS + (32 * wj + 4 * (w16 & 3)) * 2;
 
     if (pbeg < pend) {
         load_patch(pbeg);
@@ -623,23 +662,25 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             tr_read<0 * PA + 8 * RS>(fa[1], dbase);
             tr_read<0 * PA + 32>(fa[2], dbase);
             tr_read<0 * PA + 8 * RS + 32>(fa[3], dbase);
-            tr_read<1 * PA + 0>(fa[4], dbase);
-            tr_read<1 * PA + 8 * RS>(fa[5], dbase);
-            tr_read<1 * PA + 32>(fa[6], dbase);
-            tr_read<1 * PA + 8 * RS + 32>(fa[7], dbase);
-            tr_read<2 * PA + 0>(fa[8], dbase);
-            tr_read<2 * PA + 8 * RS>(fa[9], dbase);
-            tr_read<2 * PA + 32>(fa[10], dbase);
-            tr_read<2 * PA + 8 * RS + 32>(fa[11], dbase);
+            if constexpr (NP == 3) {
+                tr_read<1 * PA + 0>(fa[4], dbase);
+                tr_read<1 * PA + 8 * RS>(fa[5], dbase);
+                tr_read<1 * PA + 32>(fa[6], dbase);
+                tr_read<1 * PA + 8 * RS + 32>(fa[7], dbase);
+                tr_read<2 * PA + 0>(fa[8], dbase);
+                tr_read<2 * PA + 8 * RS>(fa[9], dbase);
+                tr_read<2 * PA + 32>(fa[10], dbase);
+                tr_read<2 * PA + 8 * RS + 32>(fa[11], dbase);
+            }
             bf16x8 dv[3][2];
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
+            for (int p = 0; p < NP; ++p)
 #pragma unroll
                 for (int r = 0; r < 2; ++r) dv[p][r] = cat8(fa[4 * p + 2 * r], fa[4 * p + 2 * r + 1]);
             s16x4 f0[6], f1[6];
-            w16_read_x<0, 0, PB, HW_>(f0, xbase);
-            w16_read_x<0, 1, PB, HW_>(f1, xbase);
-            w16_chain<0, PB, HW_>(acc, dv, f0, f1, xbase);
+            w16_read_x<0, 0, PB, HW_, NP>(f0, xbase);
+            w16_read_x<0, 1, PB, HW_, NP>(f1, xbase);
+            w16_chain<0, PB, HW_, NP>(acc, dv, f0, f1, xbase);
             if (more) {
                 __syncthreads();  // every wave is done with this patch
                 store_patch();
@@ -671,9 +712,15 @@ int wgrad16_mode() {
     }
     return g_wgrad16;
 }
-const void *wgrad_halo16_fn() { return reinterpret_cast<const void *>(&wgrad_halo16_x3); }
+const void *wgrad_halo16_fn() {
+    return conv_math_planes() == 1 ? reinterpret_cast<const void *>(&wgrad_halo16_x3<1>)
+                                   : reinterpret_cast<const void *>(&wgrad_halo16_x3<3>);
+}
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL(wgrad_halo16_x3, grid, dim3(256), 0, s, a);
+    if (conv_math_planes() == 1)
+        hipLaunchKernelGGL(wgrad_halo16_x3<1>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(wgrad_halo16_x3<3>, grid, dim3(256), 0, s, a);
 }
 
 }  // namespace scd

@@ -30,6 +30,20 @@ _F32 = torch.float32
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True}
 
 
+def conv_math_for(cfg) -> str:
+    """The conv arithmetic a config asks for: MODEL.CONV_MATH if set, else MODEL.PRECISION ('fp32' -> the
+    fp32-accurate split-bf16 'x3', 'bf16' -> 'bf16')."""
+    m = cfg.MODEL.get('CONV_MATH', None)
+    if m:
+        return str(m)
+    prec = str(cfg.MODEL.get('PRECISION', 'fp32')).lower()
+    if prec in ('bf16', 'bfloat16'):
+        return 'bf16'
+    if prec in ('fp32', 'f32', 'float32'):
+        return 'x3'
+    raise ValueError(f"MODEL.PRECISION {prec!r}: expected 'fp32' or 'bf16'")
+
+
 def option(name: str):
     return _OPTS[name]
 
@@ -64,7 +78,7 @@ def pad8(c: int) -> int:
 def pad_in(c: int) -> int:
     """Input channel padding: the MFMA K granule -- 16 under the split-bf16 arithmetic (so the input layer
     takes the halo x3 path with fused BatchNorm statistics), 8 under fp32 MFMA."""
-    g = 16 if hip.conv_math() == 'x3' else 8
+    g = 16 if hip.conv_math() != 'f32' else 8
     return (c + g - 1) // g * g
 
 

@@ -89,12 +89,14 @@ _SIGS = {
     "scd_split_frag_bytes": ([c_int32, c_int32], c_size_t),
     "scd_split_bf16x3_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
+    "scd_igemm_arith": ([POINTER(IGEMM)], c_int),
     "scd_igemm_input_bn_supported": ([POINTER(IGEMM)], c_int),
     "scd_igemm_bn_bwd_tiles": ([POINTER(IGEMM), POINTER(c_int32)], c_int),
     "scd_wgrad_src_bn_supported": ([POINTER(WGRAD)], c_int),
     "scd_igemm_stat_tiles": ([POINTER(IGEMM), POINTER(c_int32)], c_int),
     "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
     "scd_conv_wgrad": ([POINTER(WGRAD), c_void_p, c_size_t, c_void_p], c_int),
+    "scd_wgrad_arith": ([POINTER(WGRAD)], c_int),
     "scd_wgrad_finalize": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_bn_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32], c_size_t),
     "scd_bn_train_stats": (
@@ -268,17 +270,18 @@ def split_bf16x3_frag(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
 
 def _attach_split(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
     """Under the x3 conv math, pre-split packed weights once so every workgroup stages them by copy."""
-    if K % 16 == 0 and conv_math() == 'x3':
+    if K % 16 == 0 and conv_math() != 'f32':  # x3 and bf16 both read the split planes
         wpk._x3 = split_bf16x3_frag(wpk, n_out, K)
     return wpk
 
 
-MATH_F32, MATH_X3 = 0, 1
-_MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3}
+MATH_F32, MATH_X3, MATH_BF16 = 0, 1, 2
+_MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3, 'bf16': MATH_BF16}
 
 
 def set_conv_math(mode) -> str:
-    """Select the conv arithmetic ('f32' = fp32 MFMA, 'x3' = exact 3-way split-bf16 MFMA); returns the previous."""
+    """Select the conv arithmetic ('f32' = fp32 MFMA, 'x3' = exact 3-way split-bf16 MFMA, 'bf16' = bf16 operands
+    with fp32 accumulation in the halo kernels); returns the previous."""
     m = _MATH_NAMES[mode] if isinstance(mode, str) else int(mode)
     rc = lib().scd_set_conv_math(m)
     if rc < 0:
@@ -340,6 +343,22 @@ def igemm_bn_bwd_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk
     tp = c_int32(0)
     n = lib().scd_igemm_bn_bwd_tiles(ctypes.byref(d), ctypes.byref(tp))
     return (n, tp.value) if n > 0 else (0, 0)
+
+
+def igemm_arith(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
+                dst: NHWC, store_mode: int = 0) -> str:
+    """The arithmetic ('f32', 'x3', 'bf16') scd_conv_igemm would use for this conv under the current mode."""
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, store_mode)
+    rc = lib().scd_igemm_arith(ctypes.byref(d))
+    _check(min(rc, 0), "scd_igemm_arith")
+    return {v: k for k, v in _MATH_NAMES.items()}[rc]
+
+
+def wgrad_arith(d: 'WGRAD') -> str:
+    """The arithmetic scd_conv_wgrad would use for this descriptor under the current mode."""
+    rc = lib().scd_wgrad_arith(ctypes.byref(d))
+    _check(min(rc, 0), "scd_wgrad_arith")
+    return {v: k for k, v in _MATH_NAMES.items()}[rc]
 
 
 def igemm_input_bn_supported(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,

@@ -17,7 +17,7 @@ import timeit
 import numpy as np
 import torch
 
-from . import hip, parallel, trainers
+from . import engine, hip, parallel, trainers
 from .utils import datasets, evaluation, experiment_manager, networks, parsers
 
 
@@ -92,6 +92,7 @@ def main(argv=None):
     device = torch.device('cuda', local_rank)
     torch.cuda.set_device(device)
     hip.load_library()
+    hip.set_conv_math(engine.conv_math_for(cfg))
     try:
         run_training(cfg, device)
     except KeyboardInterrupt:

@@ -7,6 +7,7 @@ A variant is a comma list of knob=value with knobs:
   fuse  engine BN-apply fusion into the consuming conv (engine.set_options(fuse_input_bn=...))
   fuse_bb  BN-backward partial sums in the data-grad epilogue (engine.set_options(fuse_bn_bwd=...))
   fuse_enc  fused Siamese encoder (engine.set_options(fuse_siamese_encoder=...))
+  math  conv arithmetic (hip.set_conv_math: f32 | x3 | bf16)
   SCD_* library environment switches read at launch (e.g. SCD_HALO16_TW=64)
 Prints per-variant median / min ms per step over the rounds.
 """
@@ -27,6 +28,7 @@ from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_f
 def apply(variant: str):
     for k in [k for k in os.environ if k.startswith('SCD_')]:
         del os.environ[k]
+    hip.set_conv_math('x3')
     for kv in filter(None, variant.split(',')):
         k, v = kv.split('=')
         if k == 'h16':
@@ -37,6 +39,8 @@ def apply(variant: str):
             engine.set_options(fuse_input_bn=bool(int(v)))
         elif k == 'fuse_bb':
             engine.set_options(fuse_bn_bwd=bool(int(v)))
+        elif k == 'math':
+            hip.set_conv_math(v)
         elif k == 'fuse_enc':
             engine.set_options(fuse_siamese_encoder=bool(int(v)))
         elif k.startswith('SCD_'):  # library environment switch (read at launch)
