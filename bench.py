@@ -32,8 +32,8 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from multimodal_siamese_cd_amd import engine, hip, parallel  # noqa: E402
-from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_functions, networks  # noqa: E402
+from multimodal_siamese_cd_amd import engine, hip, parallel, trainers  # noqa: E402
+from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, networks  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # dense, MI355X_MICROARCH.md (1/16 ratio)
@@ -193,15 +193,13 @@ def main():
         opt = torch.optim.AdamW(net.parameters(), lr=float(cfg.TRAINER.LR), weight_decay=0.01, fused=True)
     except (RuntimeError, TypeError):
         opt = torch.optim.AdamW(net.parameters(), lr=float(cfg.TRAINER.LR), weight_decay=0.01)
-    crit = loss_functions.get_criterion(cfg.MODEL.LOSS_TYPE)
     gen = torch.Generator(device=dev).manual_seed(parallel.rank_seed(cfg.SEED, rank))
     b = datasets.synthetic_batch(cfg, batch, dev, gen, size)
     hip.ensure_device(b['x_t1'])
 
     def step():
         opt.zero_grad(set_to_none=True)
-        logits = net(b['x_t1'], b['x_t2'])
-        loss = crit(logits, b['y_change'])
+        loss = trainers.step_loss(cfg, net(b['x_t1'], b['x_t2']), b)  # the config's trainer recipe
         loss.backward()
         opt.step()
         return loss
