@@ -142,6 +142,8 @@ def main():
             opt.step()
             losses.append(loss.item())
         rec['losses'] = np.array(losses, dtype=np.float32)
+        if name == 'siamese_t8-16':
+            save_reference_checkpoint(networks, net, opt, ns_cfg(cfgd), name)
         for k, p in module.named_parameters():
             rec['p3/' + k] = p.detach().numpy().copy()
         for k, v in module.state_dict().items():
@@ -195,6 +197,23 @@ def make_metrics_fixture():
     path = os.path.join(HERE, 'metrics_mt.npz')
     np.savez_compressed(path, **rec)
     print(f'metrics: f1={rec["f1"]} -> {os.path.getsize(path) / 1024:.0f} KiB')
+
+
+def save_reference_checkpoint(networks, net, opt, cfg, name):
+    """The reference's own save_checkpoint (utils/networks.py:30-38) after the 3-step trajectory: a checkpoint
+    file in the reference's format ({'step', 'network' (module.-prefixed), 'optimizer' (AdamW state)})."""
+    import shutil
+    import tempfile
+    from types import SimpleNamespace as NS
+    tmp = tempfile.mkdtemp()
+    cfg.PATHS = NS(OUTPUT=tmp)
+    cfg.NAME = name
+    os.makedirs(os.path.join(tmp, 'networks'), exist_ok=True)
+    networks.save_checkpoint(net, opt, 3, 3, cfg)
+    dst = os.path.join(HERE, f'{name}_checkpoint3.pt')
+    shutil.copy(os.path.join(tmp, 'networks', f'{name}_checkpoint3.pt'), dst)
+    shutil.rmtree(tmp)
+    print(f'{name}: reference checkpoint -> {os.path.getsize(dst) / 1024:.0f} KiB')
 
 
 def _ref_step_loss(mtype, out, batch, pj):
