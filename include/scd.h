@@ -66,6 +66,17 @@ int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, int32_t w, 
  *   mode 0 (forward):   [co][9][ci_pad]           (zero for ci >= ci)
  *   mode 1 (data grad): [ci][9][co], taps flipped (W[co][ci][2-ky][2-kx])
  * replaces: nn.Conv2d(in,out,3,padding=1) parameter layout (networks.py:392,395). */
+/* Batched form for one training step's weights: per job the packed layout above into `out` and, when
+ * `split` != NULL, its fragment-major bf16x3 split (the scd_split_bf16x3_frag layout of `out`; its K, 9*ci_pad or
+ * 9*co, a multiple of 16).
+ * Any number of jobs; one launch per 48. */
+typedef struct scd_pack_job {
+    const float *w;
+    float *out;
+    uint16_t *split;
+    int32_t co, ci, ci_pad, mode;
+} scd_pack_job_t;
+int scd_pack_conv3x3_multi(const scd_pack_job_t *jobs, int32_t n, scd_stream_t stream);
 int scd_pack_conv3x3(const float *w, int32_t co, int32_t ci, int32_t ci_pad, int32_t mode, float *out,
                      scd_stream_t stream);
 

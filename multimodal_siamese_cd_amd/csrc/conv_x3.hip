@@ -20,6 +20,8 @@
 // LDS image: per stage and per operand, three planes (h, m, l) of [row][16 bf16] with 32-byte rows.  The
 // 16-byte half of a row is XOR-swizzled with row bit 3, which makes the ds_read_b128 operand reads
 // conflict-free; see the bank analysis in DESIGN.md.
+#include <algorithm>
+
 #include "x3_common.h"
 
 namespace scd {
@@ -1085,9 +1087,102 @@ __global__ void split_bf16x3_kernel(const float *__restrict__ src, int64_t n4, u
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Batched weight preparation: for up to kPackJobs conv3x3 weights per launch, the packed fp32 layout of
+// scd_pack_conv3x3 and (optionally) its fragment-major bf16x3 split of scd_split_bf16x3_frag, both read straight
+// from the OIHW parameter (one launch per training step instead of two per conv).
+// ------------------------------------------------------------------------------------------------
+constexpr int kPackJobs = 48;
+struct PackJobs {
+    scd_pack_job_t j[kPackJobs];
+    int first_block[kPackJobs + 1];
+    int n;
+};
+
+// Element (row r, column k) of the packed layout of job J.
+__device__ __forceinline__ float packed_at(const scd_pack_job_t &J, int r, int k) {
+    if (J.mode == 0) {  // [co][9][ci_pad]
+        const int t = k / J.ci_pad, c = k - t * J.ci_pad;
+        return c < J.ci ? J.w[(size_t(r) * J.ci + c) * 9 + t] : 0.f;
+    }
+    const int t = k / J.co, o = k - t * J.co;  // [ci][9][co], taps flipped
+    return J.w[(size_t(o) * J.ci + r) * 9 + (8 - t)];
+}
+
+__global__ __launch_bounds__(256) void pack_multi_kernel(PackJobs jobs) {
+    int q = 0;
+    while (q + 1 < jobs.n && int(blockIdx.x) >= jobs.first_block[q + 1]) ++q;
+    const scd_pack_job_t J = jobs.j[q];
+    const int rows = J.mode == 0 ? J.co : J.ci;
+    const int K = 9 * (J.mode == 0 ? J.ci_pad : J.co);
+    const int64_t P = int64_t(rows) * K;
+    const int KS = K / 16, NB = (rows + 31) / 32;
+    const int64_t S = J.split ? int64_t(NB) * KS * 64 : 0;
+    const int64_t plane = S * 8;
+    const int64_t stride = int64_t(jobs.first_block[q + 1] - jobs.first_block[q]) * blockDim.x;
+    for (int64_t e = int64_t(blockIdx.x - jobs.first_block[q]) * blockDim.x + threadIdx.x; e < P + S; e += stride) {
+        if (e < P) {
+            const int r = int(e / K);
+            J.out[e] = packed_at(J, r, int(e - int64_t(r) * K));
+            continue;
+        }
+        const int64_t f = e - P;  // split slot: 8 consecutive k of one row, fragment order
+        const int lane = int(f & 63);
+        const int64_t fk = f >> 6;
+        const int nb = int(fk / KS), ks = int(fk - int64_t(nb) * KS);
+        const int r = nb * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
+        f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+        if (r < rows) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v0[i] = packed_at(J, r, k0 + i);
+                v1[i] = packed_at(J, r, k0 + 4 + i);
+            }
+        }
+        u32x2 h0, m0, l0, h1, m1, l1;
+        split3(v0, h0, m0, l0);
+        split3(v1, h1, m1, l1);
+        uint16_t *o = J.split + f * 8;
+        *reinterpret_cast<u32x4 *>(o) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+        *reinterpret_cast<u32x4 *>(o + plane) = u32x4{m0[0], m0[1], m1[0], m1[1]};
+        *reinterpret_cast<u32x4 *>(o + 2 * plane) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+    }
+}
+
 }  // namespace scd
 
 using namespace scd;
+
+extern "C" int scd_pack_conv3x3_multi(const scd_pack_job_t *jobs, int32_t n, scd_stream_t stream) {
+    clear_error();
+    if (!jobs || n < 0) {
+        set_error("pack_conv3x3_multi: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    for (int base = 0; base < n; base += kPackJobs) {
+        PackJobs pj;
+        pj.n = std::min(kPackJobs, n - base);
+        pj.first_block[0] = 0;
+        for (int i = 0; i < pj.n; ++i) {
+            const scd_pack_job_t &J = jobs[base + i];
+            const int rows = J.mode == 0 ? J.co : J.ci, K = 9 * (J.mode == 0 ? J.ci_pad : J.co);
+            if (!J.w || !J.out || J.co < 1 || J.ci < 1 || J.ci_pad < J.ci || (J.mode != 0 && J.mode != 1) ||
+                (J.split && (K % 16 || !aligned16(J.split)))) {
+                set_error("pack_conv3x3_multi: job %d: bad arguments (split needs K %% 16 == 0, 16-byte alignment)",
+                          base + i);
+                return SCD_ERR_ARG;
+            }
+            const int64_t work = int64_t(rows) * K + (J.split ? int64_t((rows + 31) / 32) * (K / 16) * 64 * 8 : 0);
+            const int blocks = int(std::min<int64_t>(std::max<int64_t>((work + 2047) / 2048, 1), 1024));
+            pj.j[i] = J;
+            pj.first_block[i + 1] = pj.first_block[i] + blocks;
+        }
+        if (pj.n == 0) break;
+        hipLaunchKernelGGL(pack_multi_kernel, dim3(pj.first_block[pj.n]), dim3(256), 0, as_stream(stream), pj);
+        SCD_TRY(launch_status("scd_pack_conv3x3_multi"));
+    }
+    return SCD_OK;
+}
 
 extern "C" size_t scd_split_frag_bytes(int32_t n_out, int32_t K) {
     if (n_out < 1 || K < 16 || K % 16) return 0;

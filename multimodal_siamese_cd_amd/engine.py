@@ -17,6 +17,7 @@ exactly: per-branch batch statistics, two running-stat updates (t1 first), summe
 """
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -27,7 +28,8 @@ from .hip import TAPS_1, TAPS_2X2, TAPS_3X3, nhwc
 _F32 = torch.float32
 
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
-_OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True}
+_OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
+         'pack_cache': True}
 
 
 def conv_math_for(cfg) -> str:
@@ -61,6 +63,90 @@ def set_options(**kw) -> dict:
             raise KeyError(k)
         _OPTS[k] = v
     return prev
+
+
+# ------------------------------------------------------------------------------------------------
+# Conv weight preparation, batched per step.  Every 3x3 conv weight of a model is registered with its model's
+# group (register_weight_group, called by create_network).  The first packed-layout request after the
+# weights changed packs (and bf16x3-splits) the whole group in ONE scd_pack_conv3x3_multi launch; later
+# requests of that step hit the cache.  A cache entry is valid while the Parameter's version counter and storage
+# are unchanged (in-place optimizer updates, load_state_dict and .to() all invalidate it; a mutation through
+# `.data` does not: call invalidate_weight_cache() after one).
+# ------------------------------------------------------------------------------------------------
+class _IdentityMap:
+    """Tensor-keyed map by object identity (tensor == is elementwise), dropping entries when the key dies."""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, t):
+        ent = self._d.get(id(t))
+        return ent[1] if ent is not None and ent[0]() is t else None
+
+    def setdefault(self, t, value):
+        v = self.get(t)
+        if v is None:
+            k = id(t)
+            self._d[k] = (weakref.ref(t, lambda _r, k=k, d=self._d: d.pop(k, None)), value)
+            v = value
+        return v
+
+    def clear(self):
+        self._d.clear()
+
+
+_GROUPS = _IdentityMap()  # weight Parameter -> list of weakrefs to the group's weights
+_PACKED = _IdentityMap()  # weight Parameter -> {key: (version, data_ptr, packed tensor)}
+
+
+def register_weight_group(model: torch.nn.Module):
+    convs = [m for m in model.modules() if isinstance(m, torch.nn.Conv2d) and m.kernel_size == (3, 3)]
+    group = [weakref.ref(c.weight) for c in convs]
+    for c in convs:
+        _GROUPS.setdefault(c.weight, group)
+
+
+def invalidate_weight_cache():
+    _PACKED.clear()
+
+
+def _pack_key(mode: int, ci_pad: int):
+    return (mode, ci_pad if mode == 0 else 0, hip.conv_math() != 'f32')
+
+
+def _cached(w, key):
+    ent = (_PACKED.get(w) or {}).get(key)
+    if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
+        return ent[2]
+    return None
+
+
+def packed_conv3x3(weight: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch.Tensor:
+    """hip.pack_conv3x3(weight, mode, ci_pad) through the per-step group cache."""
+    ci_pad = weight.shape[1] if ci_pad is None else ci_pad
+    if not _OPTS['pack_cache']:
+        return hip.pack_conv3x3(weight.detach(), mode, ci_pad=ci_pad if mode == 0 else None)
+    key = _pack_key(mode, ci_pad)
+    hit = _cached(weight, key)
+    if hit is not None:
+        return hit
+    group = _GROUPS.get(weight)
+    todo = [(weight, ci_pad)]
+    if group is not None and _OPTS['batch_pack']:
+        for r in group:
+            w = r()
+            if w is None or w is weight or w.device != weight.device:
+                continue
+            cp = pad_in(w.shape[1]) if mode == 0 else w.shape[1]
+            if mode == 1 and w.shape[1] % 8:  # input-layer convs: no data grad is ever taken
+                continue
+            if _cached(w, _pack_key(mode, cp)) is None:
+                todo.append((w, cp))
+    with torch.no_grad():
+        packs = hip.pack_conv3x3_multi([(w.detach(), mode, cp) for w, cp in todo])
+    for (w, cp), pk in zip(todo, packs):
+        _PACKED.setdefault(w, {})[_pack_key(mode, cp)] = (w._version, w.data_ptr(), pk)
+    return packs[0]
 
 
 def _empty(shape, like: torch.Tensor, dtype=_F32):
@@ -178,10 +264,10 @@ def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool, mate
     cin = x.shape[3]
     if conv0.in_channels > cin:
         raise ValueError(f"DoubleConv expects {conv0.in_channels} input channels, got {cin}")
-    y0, t0 = _conv3x3_stats(x, hip.pack_conv3x3(conv0.weight.detach(), 0, ci_pad=cin), conv0.bias,
+    y0, t0 = _conv3x3_stats(x, packed_conv3x3(conv0.weight, 0, ci_pad=cin), conv0.bias,
                             conv0.out_channels, _bn_uses_batch_stats(bn0, training))
     st0 = _bn_forward(y0, bn0, nseg, training, t0)
-    wpk1 = hip.pack_conv3x3(conv1.weight.detach(), 0)
+    wpk1 = packed_conv3x3(conv1.weight, 0)
     n, h, w, _ = y0.shape
     y1 = _empty((n, h, w, conv1.out_channels), y0)
     if _can_fuse_input_bn(y0, wpk1, y1, st0, save):
@@ -256,14 +342,14 @@ def _dc_backward(g_out: torch.Tensor, saved, dc, need_dx: bool):
         gw1 = _wgrad3x3(dy1, y0, conv1.weight, (st0.scale, st0.shift, st0.nseg))
     else:
         gw1 = _wgrad3x3(dy1, a0, conv1.weight)
-    ga0, tiles0 = _dgrad_bn_bwd(dy1, hip.pack_conv3x3(conv1.weight.detach(), 1), conv1.in_channels, y0, st0)
+    ga0, tiles0 = _dgrad_bn_bwd(dy1, packed_conv3x3(conv1.weight, 1), conv1.in_channels, y0, st0)
     dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0)
     gw0 = _wgrad3x3(dy0, x, conv0.weight)
     gx = None
     if need_dx:
         if x.shape[3] != conv0.in_channels:
             raise RuntimeError("input-gradient through a channel-padded first layer is not supported")
-        gx = _conv3x3(dy0, hip.pack_conv3x3(conv0.weight.detach(), 1), None, conv0.in_channels)
+        gx = _conv3x3(dy0, packed_conv3x3(conv0.weight, 1), None, conv0.in_channels)
     return gx, [gw0, dbias0, dg0, db0, gw1, dbias1, dg1, db1]
 
 

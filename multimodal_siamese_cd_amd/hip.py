@@ -81,6 +81,7 @@ _SIGS = {
     "scd_device_check": ([c_int], c_int),
     "scd_pack_nchw": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, NHWC, c_void_p], c_int),
     "scd_pack_conv3x3": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_pack_conv3x3_multi": ([c_void_p, c_int32, c_void_p], c_int),
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_set_conv_math": ([c_int32], c_int),
     "scd_set_halo16": ([c_int32], c_int),
@@ -242,6 +243,34 @@ def pack_conv3x3(w: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch
     _check(lib().scd_pack_conv3x3(w.contiguous().data_ptr(), co, ci, ci_pad, mode, out.data_ptr(), _stream()),
            "scd_pack_conv3x3")
     return _attach_split(out, co, 9 * ci_pad) if mode == 0 else _attach_split(out, ci, 9 * co)
+
+
+class PACKJOB(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("out", c_void_p), ("split", c_void_p), ("co", c_int32), ("ci", c_int32),
+                ("ci_pad", c_int32), ("mode", c_int32)]
+
+
+def pack_conv3x3_multi(jobs) -> list:
+    """jobs: [(weight OIHW, mode, ci_pad)] -> packed tensors as pack_conv3x3 returns them (split planes
+    attached under the split conv arithmetics), all prepared in one launch per 48 weights."""
+    if not jobs:
+        return []
+    split = conv_math() != 'f32'
+    outs, keep, arr = [], [], (PACKJOB * len(jobs))()
+    for i, (w, mode, ci_pad) in enumerate(jobs):
+        co, ci = w.shape[0], w.shape[1]
+        w = w.contiguous()
+        rows, K = (co, 9 * ci_pad) if mode == 0 else (ci, 9 * co)
+        out = torch.empty(rows * K, device=w.device, dtype=torch.float32)
+        sp = None
+        if split and K % 16 == 0:
+            sp = torch.empty(lib().scd_split_frag_bytes(rows, K) // 2, dtype=torch.int16, device=w.device)
+            out._x3 = sp
+        keep.append(w)
+        arr[i] = PACKJOB(w.data_ptr(), out.data_ptr(), _ptr(sp), co, ci, ci_pad, mode)
+        outs.append(out)
+    _check(lib().scd_pack_conv3x3_multi(ctypes.cast(arr, c_void_p), len(jobs), _stream()), "scd_pack_conv3x3_multi")
+    return outs
 
 
 def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:

@@ -65,6 +65,7 @@ def create_network(cfg):
         model = WhateverNet2(cfg)
     else:
         raise Exception(f'Unknown network ({t}).')
+    engine.register_weight_group(model)  # per-step batched weight packing (engine.packed_conv3x3)
     return ModelWrapper(model)
 
 

@@ -599,3 +599,47 @@ def test_errors_are_reported(dev):
     y = torch.zeros(1, 4, 4, 8, device=dev)
     with pytest.raises(RuntimeError, match='multiples of 4'):
         hip.conv_igemm(hip.nhwc(x), 4, 4, 1, hip.TAPS_3X3, torch.zeros(8 * 9 * 6, device=dev), 8, None, hip.nhwc(y))
+
+
+def test_pack_conv3x3_multi_matches_single_packs(dev):
+    """One batched launch == scd_pack_conv3x3 + scd_split_bf16x3_frag per weight, bit for bit (both modes,
+    a channel-padded input layer, more jobs than one launch holds)."""
+    from multimodal_siamese_cd_amd import hip
+    prev = hip.set_conv_math('x3')
+    try:
+        g = torch.Generator().manual_seed(4)
+        shapes = [(64, 10, 16), (64, 64, 64), (128, 64, 64), (24, 200, 200), (512, 512, 512)] * 11
+        jobs = []
+        for i, (co, ci, cp) in enumerate(shapes):
+            w = torch.randn(co, ci, 3, 3, generator=g).to(dev)
+            jobs.append((w, i % 2 if ci % 8 == 0 else 0, cp))
+        outs = hip.pack_conv3x3_multi(jobs)
+        for (w, mode, cp), o in zip(jobs, outs):
+            ref = hip.pack_conv3x3(w, mode, ci_pad=cp if mode == 0 else None)
+            assert torch.equal(o, ref)
+            assert hasattr(o, '_x3') == hasattr(ref, '_x3')
+            if hasattr(ref, '_x3'):
+                assert torch.equal(o._x3, ref._x3)
+    finally:
+        hip.set_conv_math(prev)
+
+
+def test_weight_pack_cache_follows_parameter_updates(dev):
+    """engine.packed_conv3x3 packs a model's whole weight group once per weight version and repacks after an
+    optimizer step changes the weights."""
+    from multimodal_siamese_cd_amd import engine, hip
+    from multimodal_siamese_cd_amd.utils import experiment_manager as em, networks
+    cfg = em.load_cfg('debug')
+    net = networks.create_network(cfg).to(dev)
+    convs = [m for m in net.modules() if isinstance(m, torch.nn.Conv2d) and m.kernel_size == (3, 3)]
+    w = convs[3].weight
+    a = engine.packed_conv3x3(w, 0)
+    assert engine.packed_conv3x3(w, 0) is a  # cached
+    assert engine._cached(convs[5].weight, engine._pack_key(0, convs[5].in_channels)) is not None  # group packed
+    assert torch.equal(a, hip.pack_conv3x3(w.detach(), 0))
+    opt = torch.optim.AdamW(net.parameters(), lr=1e-2)
+    for p in net.parameters():
+        p.grad = torch.ones_like(p)
+    opt.step()
+    b = engine.packed_conv3x3(w, 0)
+    assert b is not a and torch.equal(b, hip.pack_conv3x3(w.detach(), 0))

@@ -8,6 +8,7 @@ A variant is a comma list of knob=value with knobs:
   fuse_bb  BN-backward partial sums in the data-grad epilogue (engine.set_options(fuse_bn_bwd=...))
   fuse_enc  fused Siamese encoder (engine.set_options(fuse_siamese_encoder=...))
   math  conv arithmetic (hip.set_conv_math: f32 | x3 | bf16)
+  pack  weight packing: 0 per call, 1 cached per weight, 2 batched per model (engine.packed_conv3x3)
   SCD_* library environment switches read at launch (e.g. SCD_HALO16_TW=64)
 Prints per-variant median / min ms per step over the rounds.
 """
@@ -39,6 +40,8 @@ def apply(variant: str):
             engine.set_options(fuse_input_bn=bool(int(v)))
         elif k == 'fuse_bb':
             engine.set_options(fuse_bn_bwd=bool(int(v)))
+        elif k == 'pack':  # 0 = per-call packing (no cache), 1 = per-weight cache, 2 = batched group cache
+            engine.set_options(pack_cache=int(v) > 0, batch_pack=int(v) > 1)
         elif k == 'math':
             hip.set_conv_math(v)
         elif k == 'fuse_enc':
