@@ -323,6 +323,30 @@ int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, int32_t n_o
  * D = sum(p^2 + t^2) - I + 1e-6; loss = 1 - I/D, reduced over the whole batch.
  * sums_out = {I, sum(p^2+t^2), D} (device, float[3]); loss_out device float[1].
  * ------------------------------------------------------------------------------------------- */
+/* Fused multi-term form (dual-task and MMCR trainers: train_supervised_dualtask.py:73-85,
+ * train_semisupervised.py:78-113).  Tensors are [n_samples][pixels] (B,1,H,W).  Term t is
+ * power_jaccard_loss(logits[sel], target[sel]) over the samples sel selects; a term selecting no sample is left
+ * out (the reference's `if is_labeled.any()` branches, decided on the device: no host sync, no gathers).
+ *   loss = sum_t coef_t * [|sel_t| > 0] * (1 - I_t / D_t)
+ * sums (device float[n_terms][4]) = {I, sum(p^2 + t^2), D, |sel|}.  Backward writes dL/dlogits into glogits and,
+ * for a soft target (target = sigmoid(target logits), not detached: train_semisupervised.py:107), dL/d(target
+ * logits) into gtarget, for the selected samples; zero_unselected bit 0 / bit 1 also writes 0 into glogits /
+ * gtarget for the other samples (set it where no other term covers them). */
+typedef struct scd_jaccard_term {
+    const float *logits;
+    const float *target;
+    float *glogits;
+    float *gtarget;
+    float coef;
+    int32_t select;          /* 0: all samples, 1: labeled[s] != 0, 2: labeled[s] == 0 */
+    int32_t soft_target;
+    int32_t zero_unselected; /* bit 0: glogits, bit 1: gtarget */
+} scd_jaccard_term_t;
+size_t scd_jaccard_multi_workspace_bytes(int32_t n_terms);
+int scd_jaccard_multi_fwd(const scd_jaccard_term_t *terms, int32_t n_terms, const uint8_t *labeled, int32_t n_samples,
+                          int64_t pixels, float *sums, float *loss, void *ws, size_t ws_bytes, scd_stream_t stream);
+int scd_jaccard_multi_bwd(const scd_jaccard_term_t *terms, int32_t n_terms, const uint8_t *labeled, int32_t n_samples,
+                          int64_t pixels, const float *sums, const float *gloss, scd_stream_t stream);
 size_t scd_pjaccard_workspace_bytes(int64_t n);
 int scd_pjaccard_fwd(const float *logits, const float *target, int64_t n, float *sums_out, float *loss_out,
                      void *ws, size_t ws_bytes, scd_stream_t stream);

@@ -757,3 +757,61 @@ class PJaccardFn(torch.autograd.Function):
 def power_jaccard(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     hip.ensure_device(logits)
     return PJaccardFn.apply(logits, target)
+
+
+# ------------------------------------------------------------------------------------------------
+# Fused multi-term power-Jaccard (dual-task and MMCR trainers)
+# ------------------------------------------------------------------------------------------------
+class MultiJaccardFn(torch.autograd.Function):
+    """sum_t coef_t * [|sel_t| > 0] * power_jaccard_loss(logits_t[sel_t], target_t[sel_t]) in one fused pass
+    (scd_jaccard_multi_fwd/bwd).  spec: per term (logits index, target index, coef, select, soft) into `tensors`;
+    select 0 = all samples, 1 = labelled, 2 = unlabelled; a soft target is the logits of sigmoid targets and gets a
+    gradient.  No host sync: empty subsets are dropped on the device."""
+
+    @staticmethod
+    def forward(ctx, spec, labeled, *tensors):
+        ts = [t.contiguous().float() for t in tensors]
+        n_samples = ts[0].shape[0]
+        pixels = ts[0].numel() // n_samples
+        for t in ts:
+            if t.numel() != n_samples * pixels:
+                raise ValueError(f"multi-term Jaccard: tensor of {t.numel()} elements, expected {n_samples * pixels}")
+        lab = labeled.to(device=ts[0].device, dtype=torch.uint8).contiguous()
+        terms = [dict(logits=ts[li], target=ts[ti], coef=c, select=sel, soft=soft) for li, ti, c, sel, soft in spec]
+        sums = _empty((len(spec), 4), ts[0])
+        loss = _empty((), ts[0])
+        hip.jaccard_multi_fwd(terms, lab, n_samples, pixels, sums, loss)
+        ctx.spec, ctx.dims = spec, (n_samples, pixels)
+        ctx.save_for_backward(lab, sums, *ts)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        lab, sums, *ts = ctx.saved_tensors
+        n_samples, pixels = ctx.dims
+        need = ctx.needs_input_grad[2:]
+        grads = [torch.empty_like(t) if need[i] else None for i, t in enumerate(ts)]
+        # the sample sets each gradient is written on; they must not overlap (a tensor in two terms over the same
+        # samples would need its gradients summed), and a single partial writer zero-fills the rest
+        writers = [[] for _ in ts]
+        for k, (li, ti, _, sel, soft) in enumerate(ctx.spec):
+            writers[li].append((k, 1, sel))
+            if soft:
+                writers[ti].append((k, 2, sel))
+        zero = [0] * len(ctx.spec)
+        for i, w in enumerate(writers):
+            sels = [sel for _, _, sel in w]
+            if len(sels) > 1 and (0 in sels or len(set(sels)) != len(sels)):
+                raise NotImplementedError("multi-term Jaccard: a tensor in two terms over overlapping samples")
+            if grads[i] is not None and len(w) == 1 and sels[0] != 0:
+                zero[w[0][0]] |= w[0][1]
+        terms = [dict(logits=ts[li], target=ts[ti], coef=c, select=sel, soft=soft, glogits=grads[li],
+                      gtarget=grads[ti] if soft else None, zero=zero[k])
+                 for k, (li, ti, c, sel, soft) in enumerate(ctx.spec)]
+        hip.jaccard_multi_bwd(terms, lab, n_samples, pixels, sums, g.contiguous())
+        return (None, None, *grads)
+
+
+def multi_jaccard(spec, labeled: torch.Tensor, *tensors) -> torch.Tensor:
+    hip.ensure_device(tensors[0])
+    return MultiJaccardFn.apply(spec, labeled, *tensors)

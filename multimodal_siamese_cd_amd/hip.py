@@ -139,6 +139,10 @@ _SIGS = {
     "scd_pjaccard_fwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
     "scd_pjaccard_bwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "scd_window_copy": ([NHWC, NHWC, c_int32, c_int32, c_void_p], c_int),
+    "scd_jaccard_multi_workspace_bytes": ([c_int32], c_size_t),
+    "scd_jaccard_multi_fwd": ([c_void_p, c_int32, c_void_p, c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_size_t,
+                               c_void_p], c_int),
+    "scd_jaccard_multi_bwd": ([c_void_p, c_int32, c_void_p, c_int32, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "scd_threshold_counts_workspace_bytes": ([c_int64, c_int32], c_size_t),
     "scd_threshold_counts": (
         [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
@@ -562,3 +566,32 @@ def threshold_counts(pred: torch.Tensor, truth: torch.Tensor, thresholds: torch.
     _check(lib().scd_threshold_counts(pred.data_ptr(), truth.data_ptr(), n, thresholds.data_ptr(), thresholds.numel(),
                                       int(from_logits), counts.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
            "scd_threshold_counts")
+
+
+class JTERM(ctypes.Structure):
+    _fields_ = [("logits", c_void_p), ("target", c_void_p), ("glogits", c_void_p), ("gtarget", c_void_p),
+                ("coef", c_float), ("select", c_int32), ("soft_target", c_int32), ("zero_unselected", c_int32)]
+
+
+def _jterms(terms):
+    arr = (JTERM * len(terms))()
+    for i, t in enumerate(terms):
+        arr[i] = JTERM(_ptr(t['logits']), _ptr(t['target']), _ptr(t.get('glogits')), _ptr(t.get('gtarget')),
+                       float(t['coef']), int(t['select']), int(t.get('soft', 0)), int(t.get('zero', 0)))
+    return arr
+
+
+def jaccard_multi_fwd(terms, labeled: torch.Tensor, n_samples: int, pixels: int, sums, loss):
+    """terms: dicts {logits, target, coef, select, soft}; labeled: device uint8 [n_samples]."""
+    ws = torch.empty(lib().scd_jaccard_multi_workspace_bytes(len(terms)), dtype=torch.uint8, device=labeled.device)
+    arr = _jterms(terms)
+    _check(lib().scd_jaccard_multi_fwd(ctypes.cast(arr, c_void_p), len(terms), labeled.data_ptr(), n_samples, pixels,
+                                       sums.data_ptr(), loss.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
+           "scd_jaccard_multi_fwd")
+
+
+def jaccard_multi_bwd(terms, labeled: torch.Tensor, n_samples: int, pixels: int, sums, gloss):
+    """terms as jaccard_multi_fwd plus {glogits, gtarget, zero}."""
+    arr = _jterms(terms)
+    _check(lib().scd_jaccard_multi_bwd(ctypes.cast(arr, c_void_p), len(terms), labeled.data_ptr(), n_samples, pixels,
+                                       sums.data_ptr(), _ptr(gloss), _stream()), "scd_jaccard_multi_bwd")

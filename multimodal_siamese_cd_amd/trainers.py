@@ -10,7 +10,12 @@ from __future__ import annotations
 
 import torch
 
+from . import engine
 from .utils import loss_functions
+
+
+def _fusable(*criteria) -> bool:
+    return all(c is loss_functions.power_jaccard_loss for c in criteria)
 
 
 def supervised_loss(criterion, logits, batch):
@@ -19,6 +24,11 @@ def supervised_loss(criterion, logits, batch):
 
 def dualtask_loss(change_criterion, sem_criterion, outputs, batch):
     logits_change, logits_sem_t1, logits_sem_t2 = outputs
+    if _fusable(change_criterion, sem_criterion):  # one fused pass: 0.5 L_change + 0.25 L_sem_t1 + 0.25 L_sem_t2
+        lab = torch.ones(logits_change.shape[0], dtype=torch.uint8, device=logits_change.device)
+        spec = [(0, 1, 0.5, 0, 0), (2, 3, 0.25, 0, 0), (4, 5, 0.25, 0, 0)]
+        return engine.multi_jaccard(spec, lab, logits_change, batch['y_change'], logits_sem_t1, batch['y_sem_t1'],
+                                    logits_sem_t2, batch['y_sem_t2'])
     change_loss = change_criterion(logits_change, batch['y_change'])
     sem_loss = (sem_criterion(logits_sem_t1, batch['y_sem_t1']) + sem_criterion(logits_sem_t2, batch['y_sem_t2'])) / 2
     return (change_loss + sem_loss) / 2
@@ -28,6 +38,12 @@ def mmcr_loss(sup_criterion, cons_criterion, outputs, batch, alpha: float, cons_
     logits_fusion, logits_s1, logits_s2 = outputs
     is_labeled = batch['is_labeled'].to(logits_fusion.device)
     y = batch['y_change']
+    if cons_loss_type != 'L2' and _fusable(sup_criterion, cons_criterion):
+        # one fused pass, subsets selected on the device: alpha/3 * (L_f + L_s1 + L_s2)[labelled]
+        # + (1 - alpha) * PJ(logits_s1, sigmoid(logits_s2))[unlabelled]
+        a = float(alpha)
+        spec = [(0, 3, a / 3, 1, 0), (1, 3, a / 3, 1, 0), (2, 3, a / 3, 1, 0), (1, 2, 1 - a, 2, 1)]
+        return engine.multi_jaccard(spec, is_labeled, logits_fusion, logits_s1, logits_s2, y)
     loss = None
     if bool(is_labeled.any()):
         sup = (sup_criterion(logits_fusion[is_labeled], y[is_labeled])

@@ -643,3 +643,35 @@ def test_weight_pack_cache_follows_parameter_updates(dev):
     opt.step()
     b = engine.packed_conv3x3(w, 0)
     assert b is not a and torch.equal(b, hip.pack_conv3x3(w.detach(), 0))
+
+
+@pytest.mark.parametrize('labeled', [[1, 0, 1, 0], [1, 1, 1, 1], [0, 0, 0, 0], [0, 1, 0, 0]])
+@pytest.mark.parametrize('kind', ['mmcr', 'dualtask'])
+def test_fused_multi_jaccard_matches_oracle(dev, labeled, kind):
+    """The fused multi-term Jaccard of the MMCR / dual-task trainers == the oracle's per-term recipe with boolean
+    subsets (train_semisupervised.py:78-113, train_supervised_dualtask.py:73-85), incl. all / no labelled samples:
+    loss 1e-6 absolute, every gradient 1e-5 relative (the soft target's included)."""
+    from multimodal_siamese_cd_amd import trainers
+    from multimodal_siamese_cd_amd.utils import experiment_manager as em
+    from oracle import siamese_oracle as O
+    g = torch.Generator().manual_seed(sum(labeled) + len(kind))
+    B, H, W = 4, 24, 20
+    outs = [torch.randn(B, 1, H, W, generator=g) * 2 for _ in range(3)]
+    batch = {'y_change': (torch.rand(B, 1, H, W, generator=g) > 0.7).float(),
+             'y_sem_t1': (torch.rand(B, 1, H, W, generator=g) > 0.5).float(),
+             'y_sem_t2': (torch.rand(B, 1, H, W, generator=g) > 0.5).float(),
+             'is_labeled': torch.tensor(labeled, dtype=torch.bool)}
+    mtype = 'whatevernet' if kind == 'mmcr' else 'dtsiameseunet'
+    ref_in = [o.clone().requires_grad_(True) for o in outs]
+    ref = O.step_loss(mtype, tuple(ref_in), batch, 0.5)
+    ref.backward()
+    cfg = em.load_cfg('siamese_mmcr_alpha0500' if kind == 'mmcr' else 'dtsiamese')
+    cfg.CONSISTENCY_TRAINER.LOSS_FACTOR = 0.5
+    hip_in = [o.to(dev).requires_grad_(True) for o in outs]
+    bd = {k: v.to(dev) for k, v in batch.items()}
+    loss = trainers.step_loss(cfg, tuple(hip_in), bd)
+    loss.backward()
+    assert abs(loss.item() - ref.item()) < 1e-6
+    for a, b in zip(hip_in, ref_in):
+        assert rel(a.grad, b.grad if b.grad is not None else torch.zeros_like(b)) < 1e-5 or (
+            b.grad is None and a.grad.abs().max().item() == 0)
