@@ -375,6 +375,22 @@ size_t scd_threshold_counts_workspace_bytes(int64_t n, int32_t n_thr);
 int scd_threshold_counts(const float *pred, const float *truth, int64_t n, const float *thresholds, int32_t n_thr,
                          int32_t from_logits, int64_t *counts, void *ws, size_t ws_bytes, scd_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Data pipeline: batched on-device augmentations (utils/augmentations.py:6-142).  Tiles are HWC fp32, one per
+ * sample and of any size (hw = int32[batch][2] = {H, W}); pointer tables and parameters live on the device.
+ * ------------------------------------------------------------------------------------------- */
+/* sums[b][k] = sum of labels[b][y : y + crop, x : x + crop] (one-channel HW tiles), yx = int32[batch][ncand][2]:
+ * the candidate weights of ImportanceRandomCrop (augmentations.py:129-142). */
+int scd_window_label_sums(const float *const *labels, const int32_t *hw, const int32_t *yx, int32_t batch,
+                          int32_t ncand, int32_t crop, float *sums, scd_stream_t stream);
+/* out[b][c][i][j] (NCHW, crop x crop) = the reference chain on tile src[b] (HWC, `channels` channels):
+ * UniformCrop at params[b] = {y0, x0, flip_h, flip_v, rot_k} -> RandomFlip (axis 1, then axis 0) -> RandomRotate
+ * (np.rot90 k times, axes (0, 1)) -> ColorShift (clip(x * scale[b][c], 0, 1), in double; scale NULL = off) ->
+ * GammaCorrection (clip(x ** gamma[b][c], 0, 1), in double; gamma NULL = off) -> Numpy2Torch (CHW). */
+int scd_augment_apply(const float *const *src, const int32_t *hw, int32_t batch, int32_t channels, int32_t crop,
+                      const int32_t *params, const double *scale, const double *gamma, float *out,
+                      scd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -139,6 +139,9 @@ _SIGS = {
     "scd_pjaccard_fwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
     "scd_pjaccard_bwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "scd_window_copy": ([NHWC, NHWC, c_int32, c_int32, c_void_p], c_int),
+    "scd_window_label_sums": ([c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_augment_apply": ([c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_void_p], c_int),
     "scd_jaccard_multi_workspace_bytes": ([c_int32], c_size_t),
     "scd_jaccard_multi_fwd": ([c_void_p, c_int32, c_void_p, c_int32, c_int64, c_void_p, c_void_p, c_void_p, c_size_t,
                                c_void_p], c_int),
@@ -595,3 +598,38 @@ def jaccard_multi_bwd(terms, labeled: torch.Tensor, n_samples: int, pixels: int,
     arr = _jterms(terms)
     _check(lib().scd_jaccard_multi_bwd(ctypes.cast(arr, c_void_p), len(terms), labeled.data_ptr(), n_samples, pixels,
                                        sums.data_ptr(), _ptr(gloss), _stream()), "scd_jaccard_multi_bwd")
+
+
+def _ptr_table(tensors, device):
+    return torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64).to(device)
+
+
+def window_label_sums(labels: list, yx: torch.Tensor, crop: int) -> torch.Tensor:
+    """labels: per-sample device HW(1) fp32 tiles; yx: int32 [B][ncand][2] -> sums float [B][ncand]."""
+    dev = labels[0].device
+    B, ncand = yx.shape[0], yx.shape[1]
+    hw = torch.tensor([[t.shape[0], t.shape[1]] for t in labels], dtype=torch.int32).to(dev)
+    ptrs = _ptr_table(labels, dev)
+    yx = yx.to(device=dev, dtype=torch.int32).contiguous()
+    out = torch.empty((B, ncand), dtype=torch.float32, device=dev)
+    _check(lib().scd_window_label_sums(ptrs.data_ptr(), hw.data_ptr(), yx.data_ptr(), B, ncand, crop, out.data_ptr(),
+                                       _stream()), "scd_window_label_sums")
+    return out
+
+
+def augment_apply(tiles: list, crop: int, params: torch.Tensor, scale=None, gamma=None) -> torch.Tensor:
+    """tiles: per-sample device HWC fp32 (same C); params int32 [B][5]; scale/gamma float64 [B][C] or None."""
+    dev = tiles[0].device
+    B, C = len(tiles), tiles[0].shape[2]
+    for t in tiles:
+        if t.dim() != 3 or t.shape[2] != C or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("augment_apply: tiles must be contiguous HWC fp32 with the same channel count")
+    hw = torch.tensor([[t.shape[0], t.shape[1]] for t in tiles], dtype=torch.int32).to(dev)
+    ptrs = _ptr_table(tiles, dev)
+    params = params.to(device=dev, dtype=torch.int32).contiguous()
+    sc = None if scale is None else scale.to(device=dev, dtype=torch.float64).contiguous()
+    gm = None if gamma is None else gamma.to(device=dev, dtype=torch.float64).contiguous()
+    out = torch.empty((B, C, crop, crop), dtype=torch.float32, device=dev)
+    _check(lib().scd_augment_apply(ptrs.data_ptr(), hw.data_ptr(), B, C, crop, params.data_ptr(), _ptr(sc), _ptr(gm),
+                                   out.data_ptr(), _stream()), "scd_augment_apply")
+    return out

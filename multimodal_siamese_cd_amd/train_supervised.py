@@ -45,11 +45,21 @@ def run_training(cfg, device, max_steps: int | None = None):
     if rank == 0:
         print(f"run config {cfg.NAME}: model {cfg.MODEL.TYPE} topology {list(cfg.MODEL.TOPOLOGY)} "
               f"bs {cfg.TRAINER.BATCH_SIZE}/GPU x {world} GPU, lr {cfg.TRAINER.LR}, epochs {epochs}", flush=True)
+    loader = None
+    if not cfg.DATALOADER.get('SYNTHETIC', True):  # SpaceNet7 tile cache, augmented on the device
+        ds = datasets.MultimodalCDDataset(cfg, 'training')
+        loader = datasets.DeviceDataLoader(ds, int(cfg.TRAINER.BATCH_SIZE), device, shuffle=bool(cfg.DATALOADER.SHUFFLE),
+                                           num_workers=int(cfg.DATALOADER.get('NUM_WORKER', 0)))
+        steps_per_epoch = len(loader)
     for epoch in range(1, epochs + 1):
         start = timeit.default_timer()
         losses = []
+        if loader is not None:
+            loader.set_epoch(epoch)
+        batches = iter(loader) if loader is not None else None
         for _ in range(steps_per_epoch):
-            batch = datasets.synthetic_batch(cfg, int(cfg.TRAINER.BATCH_SIZE), device, gen)
+            batch = next(batches) if batches is not None else datasets.synthetic_batch(
+                cfg, int(cfg.TRAINER.BATCH_SIZE), device, gen)
             net.train()
             optimizer.zero_grad(set_to_none=True)
             out = net(batch['x_t1'], batch['x_t2'])
