@@ -38,7 +38,8 @@ from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, networ
 FP32_MFMA_PEAK_TFLOPS = 157.3
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # dense, MI355X_MICROARCH.md (1/16 ratio)
 X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6           # six bf16 products per fp32 multiply-add
-PEAKS = {'f32': FP32_MFMA_PEAK_TFLOPS, 'x3': X3_PEAK_TFLOPS, 'bf16': BF16_MFMA_PEAK_TFLOPS}
+PEAKS = {'f32': FP32_MFMA_PEAK_TFLOPS, 'x3': X3_PEAK_TFLOPS, 'x5': BF16_MFMA_PEAK_TFLOPS / 5,
+         'bf16': BF16_MFMA_PEAK_TFLOPS}
 METRIC = "image-pairs/sec training step, 256×256 SAR+optical Siamese U-Net, 1/2/4/8 MI355X"
 
 
@@ -170,7 +171,7 @@ def main():
     ap.add_argument('--size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
-    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'bf16'],
+    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16'],
                     help='conv arithmetic (default: from the config, engine.conv_math_for: MODEL.PRECISION fp32 -> x3)')
     args = ap.parse_args()
 

@@ -100,10 +100,13 @@ int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, floa
  *                 the 16x16x32 halo kernels (3x3 stride-1 fwd / data-grad / weight-grad, >= 98% of the
  *                 U-Net's conv FLOPs); every other conv shape keeps the SCD_MATH_X3 kernels.  Activations and
  *                 BatchNorm stay fp32.
- * Default: SCD_MATH_X3, or the SCD_CONV_MATH=f32|x3|bf16 environment variable at first use.  Returns the
+ *   SCD_MATH_X5   SCD_MATH_X3 less one of its three second-order products (w_l*x_h in the fwd/data-grad halo
+ *                 kernel, x_l*dy_h in the halo weight grad; each <= 2^-18 relative, below fp32 accumulation noise
+ *                 over the contraction lengths here): five products, two weight / X planes.  Halo kernels only.
+ * Default: SCD_MATH_X3, or the SCD_CONV_MATH=f32|x3|x5|bf16 environment variable at first use.  Returns the
  * previous mode; SCD_MATH_QUERY only queries.  Process-wide (not per stream).
  * ------------------------------------------------------------------------------------------- */
-enum scd_conv_math { SCD_MATH_QUERY = -1, SCD_MATH_F32 = 0, SCD_MATH_X3 = 1, SCD_MATH_BF16 = 2 };
+enum scd_conv_math { SCD_MATH_QUERY = -1, SCD_MATH_F32 = 0, SCD_MATH_X3 = 1, SCD_MATH_BF16 = 2, SCD_MATH_X5 = 3 };
 int scd_set_conv_math(int32_t mode);
 /* The arithmetic scd_conv_igemm / scd_conv_wgrad would use for this descriptor under the current mode:
  * SCD_MATH_F32, SCD_MATH_X3 or SCD_MATH_BF16; negative = invalid descriptor.  (Declared with the descriptors

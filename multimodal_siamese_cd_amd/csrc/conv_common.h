@@ -128,6 +128,6 @@ void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
 // SCD_MATH_F32 = fp32 MFMA everywhere, SCD_MATH_BF16 = the x3 pipeline with one bf16 term per operand in the
 // 16x16x32 halo kernels.  Initial value from SCD_CONV_MATH=f32|x3|bf16 (default x3).
 int conv_math_x3();      // split-weight (x3 or bf16) pipeline
-int conv_math_planes();  // bf16 planes per operand in the halo16 kernels: 3 (x3) or 1 (bf16)
+int conv_math_planes();  // halo16 kernel arithmetic: 3 (x3), 5 (x5: x3 less one product), 1 (bf16)
 
 }  // namespace scd

@@ -472,12 +472,18 @@ static int g_conv_math = -1;
 static int conv_math_mode() {
     if (g_conv_math < 0) {
         const char *e = getenv("SCD_CONV_MATH");
-        g_conv_math = (e && e[0] == 'f') ? SCD_MATH_F32 : (e && e[0] == 'b') ? SCD_MATH_BF16 : SCD_MATH_X3;
+        g_conv_math = (e && e[0] == 'f')                   ? SCD_MATH_F32
+                      : (e && e[0] == 'b')                 ? SCD_MATH_BF16
+                      : (e && e[0] == 'x' && e[1] == '5') ? SCD_MATH_X5
+                                                           : SCD_MATH_X3;
     }
     return g_conv_math;
 }
 int conv_math_x3() { return conv_math_mode() != SCD_MATH_F32; }
-int conv_math_planes() { return conv_math_mode() == SCD_MATH_BF16 ? 1 : 3; }
+int conv_math_planes() {
+    const int m = conv_math_mode();
+    return m == SCD_MATH_BF16 ? 1 : m == SCD_MATH_X5 ? 5 : 3;
+}
 
 }  // namespace scd
 
@@ -486,7 +492,7 @@ using namespace scd;
 extern "C" int scd_set_conv_math(int32_t mode) {
     clear_error();
     const int prev = conv_math_mode();
-    if (mode == SCD_MATH_F32 || mode == SCD_MATH_X3 || mode == SCD_MATH_BF16) {
+    if (mode == SCD_MATH_F32 || mode == SCD_MATH_X3 || mode == SCD_MATH_BF16 || mode == SCD_MATH_X5) {
         g_conv_math = mode;
     } else if (mode != SCD_MATH_QUERY) {
         set_error("scd_set_conv_math: mode %d", mode);
@@ -721,7 +727,7 @@ extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
     IgemmArgs a;
     SCD_TRY(igemm_query_prepare(d, a));
     if (!conv_math_x3()) return SCD_MATH_F32;
-    if (igemm_takes_halo16(a)) return conv_math_planes() == 1 ? SCD_MATH_BF16 : SCD_MATH_X3;
+    if (igemm_takes_halo16(a)) return conv_math_mode();
     return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
 }
 
@@ -942,7 +948,7 @@ extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
     if (!conv_math_x3()) return SCD_MATH_F32;
-    return (wgrad_halo_ok(d) && wgrad16_mode() && conv_math_planes() == 1) ? SCD_MATH_BF16 : SCD_MATH_X3;
+    return (wgrad_halo_ok(d) && wgrad16_mode()) ? conv_math_mode() : SCD_MATH_X3;
 }
 
 namespace scd {

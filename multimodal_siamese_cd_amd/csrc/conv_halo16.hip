@@ -44,8 +44,8 @@ __device__ __forceinline__ void gstore4(float *p, f32x4 v) { *(__attribute__((ad
 // DB: double-buffered halo.  The next chunk's halo is written into the other buffer in the middle of the
 // current chunk (its loads were issued at the chunk's first tap), so a chunk end costs one barrier and the
 // split/store work overlaps the MFMAs instead of stalling between two barriers.
-// NP: bf16 planes per operand: 3 = the exact x3 split (six products per step), 1 = bf16 operands
-// (SCD_MATH_BF16: the h term only, one product per step).
+// NP selects the arithmetic: 3 = the exact x3 split (six products per step), 5 = x3 without the w_l * x_h product
+// (SCD_MATH_X5: weights in two planes, five products), 1 = bf16 operands (SCD_MATH_BF16: the h terms, one product).
 template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
@@ -59,8 +59,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     constexpr int PA = HR * 64;
     constexpr int RED = 2 * WAVES_M * BN * 4;
     constexpr int NBUF = DB ? 2 : 1;
-    static_assert(NP == 1 || NP == 3, "x3 or bf16 planes");
-    __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * NP * PA > RED ? NBUF * NP * PA : RED];
+    static_assert(NP == 1 || NP == 3 || NP == 5, "x3, x5 or bf16");
+    constexpr int XP = NP == 1 ? 1 : 3;               // activation planes (LDS)
+    constexpr int WP = NP == 1 ? 1 : NP == 5 ? 2 : 3;  // weight planes (registers)
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * XP * PA > RED ? NBUF * XP * PA : RED];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         }
     };
     auto store_A = [&](int buf) {
-        unsigned char *const sb = smem + buf * (NP * PA);
+        unsigned char *const sb = smem + buf * (XP * PA);
 #pragma unroll
         for (int i = 0; i < A_PER; ++i)
             if ((A_CH % NT == 0) || a_off[i] >= 0) {
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                         v[q] = a_boff[i] == kOOB ? 0.f : fmaxf(fmaf(ra[i][q], in_sc[q], in_sh[q]), 0.f);
                     ra[i] = v;
                 }
-                if constexpr (NP == 3) {
+                if constexpr (XP == 3) {
                     split3(ra[i], h, m, l);
                     *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
                     *reinterpret_cast<u32x2 *>(sb + PA + a_off[i]) = m;
@@ -155,10 +157,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             }
     };
     const int cpk = a.c / 32;
-    auto load_W = [&](int cc, int t, u32x4 (&wq)[NP][TN]) {
+    auto load_W = [&](int cc, int t, u32x4 (&wq)[WP][TN]) {
         const uint32_t ko = uint32_t(t * cpk + cc) * 2048u;  // 32-deep step = two 16-deep fragments
 #pragma unroll
-        for (int p = 0; p < NP; ++p)
+        for (int p = 0; p < WP; ++p)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
                 wq[p][j] = bload4u(rs_w, w_base[j] == kOOB ? kOOB : w_base[j] + ko + uint32_t(p) * wplane_b);
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 
     const int nsteps = cpk * a.ntaps;
     constexpr int T_STORE = 4;  // DB: tap at which the prefetched halo is written to the other buffer
-    u32x4 wq[NP][TN];
+    u32x4 wq[WP][TN];
     load_A(0);
     load_W(0, 0, wq);
     store_A(0);
@@ -197,26 +199,27 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         } else {
             if (more && t1 == 0) load_A(cc1);
         }
-        const unsigned char *const sbuf = smem + (DB ? (cc & 1) * (NP * PA) : 0);
+        const unsigned char *const sbuf = smem + (DB ? (cc & 1) * (XP * PA) : 0);
         const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
-        bf16x8 xv[NP][TM], wv[NP][TN];
+        bf16x8 xv[XP][TM], wv[WP][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int hr = a_hr[i] + toff;
             const int ad = hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
 #pragma unroll
-            for (int p = 0; p < NP; ++p)
+            for (int p = 0; p < XP; ++p)
                 xv[p][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(sbuf + p * PA + ad));
         }
 #pragma unroll
-        for (int p = 0; p < NP; ++p)
+        for (int p = 0; p < WP; ++p)
 #pragma unroll
             for (int j = 0; j < TN; ++j) wv[p][j] = __builtin_bit_cast(bf16x8, wq[p][j]);
-        // (w, x) term pairs smallest first: mm, hl, lh, hm, mh, hh; bf16 (NP == 1) runs hh only
+        // (w, x) term pairs smallest first: mm, hl, lh, hm, mh, hh; x5 drops lh (w_l * x_h), bf16 runs hh only
         constexpr int QW[6] = {1, 0, 2, 0, 1, 0};
         constexpr int QX[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
-        for (int q = NP == 3 ? 0 : 5; q < 6; ++q)
+        for (int q = NP == 1 ? 5 : 0; q < 6; ++q)
+            if (NP != 5 || QW[q] != 2)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -414,15 +417,25 @@ template <int WM, int WN, int TM, int TN, int OCC>
 void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
-    if (conv_math_planes() == 1) {  // one plane: double buffering always fits
-        if (halo16_db())
-            launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
-        else
-            launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
-    } else if (tw != 64 && halo16_db() && OCC * 2 * 3 * hr * 64 <= 160 * 1024) {
-        launch16c<WM, WN, TM, TN, OCC, true, 3>(a, tw, s);
-    } else {
-        launch16c<WM, WN, TM, TN, OCC, false, 3>(a, tw, s);
+    const bool db3 = tw != 64 && halo16_db() && OCC * 2 * 3 * hr * 64 <= 160 * 1024;
+    switch (conv_math_planes()) {
+        case 1:  // one plane: double buffering always fits
+            if (halo16_db())
+                launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
+            else
+                launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
+            break;
+        case 5:
+            if (db3)
+                launch16c<WM, WN, TM, TN, OCC, true, 5>(a, tw, s);
+            else
+                launch16c<WM, WN, TM, TN, OCC, false, 5>(a, tw, s);
+            break;
+        default:
+            if (db3)
+                launch16c<WM, WN, TM, TN, OCC, true, 3>(a, tw, s);
+            else
+                launch16c<WM, WN, TM, TN, OCC, false, 3>(a, tw, s);
     }
 }
 
@@ -486,15 +499,21 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
 namespace {
 constexpr int kW16RS = 160;
 
-// X fragments of half tap (T, CB): two transposed reads per plane (NP planes).
+// X planes of the weight-grad kernel per arithmetic: x3 3, x5 2 (its l term is the dropped product's), bf16 1.
+template <int NP>
+constexpr int w16_xp() { return NP == 1 ? 1 : NP == 5 ? 2 : 3; }
+
+// X fragments of half tap (T, CB): two transposed reads per X plane.
 template <int T, int CB, int PB, int HW_, int NP>
 __device__ __forceinline__ void w16_read_x(s16x4 (&f)[6], uint32_t xbase) {
     constexpr int toff = (T / 3) * HW_ + (T % 3);  // (1 + dy) * HW_ + (1 + dx)
     tr_read<0 * PB + toff * kW16RS + CB * 32>(f[0], xbase);
     tr_read<0 * PB + (toff + 8) * kW16RS + CB * 32>(f[1], xbase);
-    if constexpr (NP == 3) {
+    if constexpr (w16_xp<NP>() >= 2) {
         tr_read<1 * PB + toff * kW16RS + CB * 32>(f[2], xbase);
         tr_read<1 * PB + (toff + 8) * kW16RS + CB * 32>(f[3], xbase);
+    }
+    if constexpr (w16_xp<NP>() == 3) {
         tr_read<2 * PB + toff * kW16RS + CB * 32>(f[4], xbase);
         tr_read<2 * PB + (toff + 8) * kW16RS + CB * 32>(f[5], xbase);
     }
@@ -505,8 +524,11 @@ __device__ __forceinline__ void w16_read_x(s16x4 (&f)[6], uint32_t xbase) {
 template <int T, int CB, int WAIT, int NP>
 __device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f)[6]) {
     bf16x8 x0 = cat8(f[0], f[1]), x1 = cat8(f[2], f[3]), x2 = cat8(f[4], f[5]);
-    if constexpr (NP == 3) {
-        lds_wait<WAIT>(x0, x1, x2);
+    if constexpr (NP != 1) {
+        if constexpr (NP == 3)
+            lds_wait<WAIT>(x0, x1, x2);
+        else
+            lds_wait<WAIT>(x0, x1);
         if (T == 0 && CB == 0) {
             lds_wait<WAIT>(dv[0][0], dv[1][0], dv[2][0]);
             lds_wait<WAIT>(dv[0][1], dv[1][1], dv[2][1]);
@@ -516,10 +538,11 @@ __device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][
     }
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
-        if constexpr (NP == 3) {
+        if constexpr (NP != 1) {
             acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
             acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[2][rb], acc[T][CB][rb], 0, 0, 0);
-            acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
+            if constexpr (NP == 3)  // x5 drops x_l * dy_h
+                acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
             acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
             acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[0][rb], acc[T][CB][rb], 0, 0, 0);
         }
@@ -528,13 +551,13 @@ __device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][
 }
 
 // Half taps H = 2T + CB, one ahead: compute H from buffer H & 1, then refill that buffer with H + 2.  The
-// counted wait leaves the 2*NP reads of the other buffer (issued one half tap earlier) in flight.
+// counted wait leaves the reads of the other buffer (2 per X plane, issued one half tap earlier) in flight.
 template <int H, int PB, int HW_, int NP>
 __device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f0)[6], s16x4 (&f1)[6],
                                           uint32_t xbase) {
     if constexpr (H < 18) {
         s16x4 (&f)[6] = (H & 1) ? f1 : f0;
-        w16_half<H / 2, H % 2, (H == 17 ? 0 : 2 * NP), NP>(acc, dv, f);
+        w16_half<H / 2, H % 2, (H == 17 ? 0 : 2 * w16_xp<NP>()), NP>(acc, dv, f);
         if constexpr (H + 2 < 18) w16_read_x<(H + 2) / 2, (H + 2) % 2, PB, HW_, NP>(f, xbase);
         w16_chain<H + 1, PB, HW_, NP>(acc, dv, f0, f1, xbase);
     }
@@ -549,8 +572,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     constexpr int PA = P * RS, PB = HP * RS;            // plane bytes
     constexpr int A_CH = P * 16, B_CH = HP * 16;        // 4-channel pieces
     constexpr int A_PER = A_CH / 256, B_PER = (B_CH + 255) / 256;
-    static_assert(NP == 1 || NP == 3, "x3 or bf16 planes");
-    __shared__ __attribute__((aligned(16))) unsigned char smem[NP * PA + NP * PB];
+    static_assert(NP == 1 || NP == 3 || NP == 5, "x3, x5 or bf16");
+    constexpr int DP = NP == 1 ? 1 : 3;  // dY planes
+    constexpr int XP = w16_xp<NP>();      // X planes
+    __shared__ __attribute__((aligned(16))) unsigned char smem[DP * PA + XP * PB];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wi = wid >> 1, wj = wid & 1;
@@ -602,7 +627,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             const int e = tid + i * 256;
             const int o = (e >> 4) * RS + (e & 15) * 8;
             u32x2 h, m, l;
-            if constexpr (NP == 3) {
+            if constexpr (DP == 3) {
                 split3(ra[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
                 *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
@@ -622,11 +647,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
                     for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], x_sc[q], x_sh[q]), 0.f) : 0.f;
                 }
                 const int e = tid + i * 256;
-                const int o = NP * PA + (e >> 4) * RS + (e & 15) * 8;
-                if constexpr (NP == 3) {
-                    split3(rb[i], h, m, l);
+                const int o = DP * PA + (e >> 4) * RS + (e & 15) * 8;
+                if constexpr (XP >= 2) {
+                    split3(rb[i], h, m, l);  // x5: the l term is not needed (dead code)
                     *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
-                    *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
+                    if constexpr (XP == 3) *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
                 } else {
                     h[0] = cvt_pk_bf16(rb[i][0], rb[i][1]);
                     h[1] = cvt_pk_bf16(rb[i][2], rb[i][3]);
@@ -648,7 +673,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     const int g = lane >> 4, w16 = lane & 15;
     const int py = g >> 1, pxq = 4 * (g & 1) + (w16 >> 2);
     const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RS + (32 * wi + 4 * (w16 & 3)) * 2;
-    const uint32_t xbase = lds_addr(smem) + NP * PA + (py * HW_ + pxq) * RS + (32 * wj + 4 * (w16 & 3)) * 2;
+    const uint32_t xbase = lds_addr(smem) + DP * PA + (py * HW_ + pxq) * RS + (32 * wj + 4 * (w16 & 3)) * 2;
 
     if (pbeg < pend) {
         load_patch(pbeg);
@@ -662,7 +687,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             tr_read<0 * PA + 8 * RS>(fa[1], dbase);
             tr_read<0 * PA + 32>(fa[2], dbase);
             tr_read<0 * PA + 8 * RS + 32>(fa[3], dbase);
-            if constexpr (NP == 3) {
+            if constexpr (DP == 3) {
                 tr_read<1 * PA + 0>(fa[4], dbase);
                 tr_read<1 * PA + 8 * RS>(fa[5], dbase);
                 tr_read<1 * PA + 32>(fa[6], dbase);
@@ -674,7 +699,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             }
             bf16x8 dv[3][2];
 #pragma unroll
-            for (int p = 0; p < NP; ++p)
+            for (int p = 0; p < DP; ++p)
 #pragma unroll
                 for (int r = 0; r < 2; ++r) dv[p][r] = cat8(fa[4 * p + 2 * r], fa[4 * p + 2 * r + 1]);
             s16x4 f0[6], f1[6];
@@ -713,14 +738,18 @@ int wgrad16_mode() {
     return g_wgrad16;
 }
 const void *wgrad_halo16_fn() {
-    return conv_math_planes() == 1 ? reinterpret_cast<const void *>(&wgrad_halo16_x3<1>)
-                                   : reinterpret_cast<const void *>(&wgrad_halo16_x3<3>);
+    switch (conv_math_planes()) {
+        case 1: return reinterpret_cast<const void *>(&wgrad_halo16_x3<1>);
+        case 5: return reinterpret_cast<const void *>(&wgrad_halo16_x3<5>);
+        default: return reinterpret_cast<const void *>(&wgrad_halo16_x3<3>);
+    }
 }
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    if (conv_math_planes() == 1)
-        hipLaunchKernelGGL(wgrad_halo16_x3<1>, grid, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(wgrad_halo16_x3<3>, grid, dim3(256), 0, s, a);
+    switch (conv_math_planes()) {
+        case 1: hipLaunchKernelGGL(wgrad_halo16_x3<1>, grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL(wgrad_halo16_x3<5>, grid, dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL(wgrad_halo16_x3<3>, grid, dim3(256), 0, s, a);
+    }
 }
 
 }  // namespace scd

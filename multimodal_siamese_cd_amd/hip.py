@@ -311,8 +311,8 @@ def _attach_split(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
     return wpk
 
 
-MATH_F32, MATH_X3, MATH_BF16 = 0, 1, 2
-_MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3, 'bf16': MATH_BF16}
+MATH_F32, MATH_X3, MATH_BF16, MATH_X5 = 0, 1, 2, 3
+_MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3, 'bf16': MATH_BF16, 'x5': MATH_X5}
 
 
 def set_conv_math(mode) -> str:

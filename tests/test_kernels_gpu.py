@@ -675,3 +675,48 @@ def test_fused_multi_jaccard_matches_oracle(dev, labeled, kind):
     for a, b in zip(hip_in, ref_in):
         assert rel(a.grad, b.grad if b.grad is not None else torch.zeros_like(b)) < 1e-5 or (
             b.grad is None and a.grad.abs().max().item() == 0)
+
+
+@pytest.mark.parametrize('ci,co', [(64, 128), (256, 256), (128, 64), (512, 512)])
+def test_halo_math_accuracy_vs_fp64(dev, ci, co):
+    """The halo kernels (forward, data grad, weight grad) under f32 / x3 / x5 against fp64 on wide-dynamic-range
+    data.  x3 drops products of <= 2^-24 relative size and stays within 2x of the fp32-MFMA error (measured: at
+    or below it).  x5 also drops one <= 2^-18 product: measured 2.5e-6..3.9e-6 relative, 1.2-9x the fp32-MFMA
+    error (the weight grad's split-K fp32 sums are the most accurate, so its ratio is the largest)."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(ci + co)
+    n, h, w = 2, 32, 32
+    spread = lambda *s: (torch.randn(*s, generator=g, dtype=torch.float64)
+                         * 10 ** (4 * torch.rand(*s, generator=g, dtype=torch.float64) - 2)).float()
+    x, dy = spread(n, h, w, ci), spread(n, h, w, co)
+    wt = (torch.randn(co, ci, 3, 3, generator=g, dtype=torch.float64) / (3 * ci ** 0.5)).float()
+    ref_y = nhwc_t(F.conv2d(nchw(x).double(), wt.double(), None, padding=1))
+    ref_dx = nhwc_t(torch.nn.grad.conv2d_input((n, ci, h, w), wt.double(), nchw(dy).double(), padding=1))
+    ref_dw = torch.nn.grad.conv2d_weight(nchw(x).double(), (co, ci, 3, 3), nchw(dy).double(), padding=1)
+    errs = {}
+    for m in ('f32', 'x3', 'x5'):
+        prev = hip.set_conv_math(m)
+        try:
+            xd, dyd, wd = x.to(dev), dy.to(dev), wt.to(dev)
+            y = torch.empty(n, h, w, co, device=dev)
+            src = hip.nhwc(xd)
+            wpk = hip.pack_conv3x3(wd, 0)
+            if m != 'f32':
+                assert hip.igemm_arith(src, h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y)) == m
+            hip.conv_igemm(src, h, w, 1, hip.TAPS_3X3, wpk, co, None, hip.nhwc(y))
+            dx = torch.empty(n, h, w, ci, device=dev)
+            hip.conv_igemm(hip.nhwc(dyd), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wd, 1), ci, None, hip.nhwc(dx))
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dyd), hip.nhwc(xd), 1, hip.TAPS_3X3)
+            if m != 'f32':
+                assert hip.wgrad_arith(d) == m
+            slabs = torch.empty(nbytes // 4, device=dev)
+            hip.conv_wgrad(d, slabs)
+            dw = torch.empty(co, ci, 3, 3, device=dev)
+            hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
+        finally:
+            hip.set_conv_math(prev)
+        errs[m] = (rel(y, ref_y), rel(dx, ref_dx), rel(dw, ref_dw))
+    print(errs)
+    for k in range(3):  # x3: at most the fp32-MFMA error; x5: below 1e-5 (measured 2.5e-6..3.9e-6)
+        assert errs['x3'][k] <= 2 * errs['f32'][k] + 1e-7, ('x3', k, errs)
+        assert errs['x5'][k] < 1e-5, ('x5', k, errs)

@@ -54,7 +54,7 @@ def main():
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--only', default=None)
     ap.add_argument('--layer', default=None, help='run only this layer name (e.g. enc1b)')
-    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'bf16'], help='conv arithmetic (default: library default)')
+    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16'], help='conv arithmetic (default: library default)')
     ap.add_argument('--variants', default=None,
                     help='comma-separated variants, interleaved per layer; a variant is "+"-joined settings '
                          'h16=<scd_set_halo16 mode>, w16=<scd_set_wgrad16 mode> or ENVVAR=value (read by the '
