@@ -67,11 +67,11 @@ def set_options(**kw) -> dict:
 
 # ------------------------------------------------------------------------------------------------
 # Conv weight preparation, batched per step.  Every 3x3 conv weight of a model is registered with its model's
-# group (register_weight_group, called by create_network).  The first packed-layout request after the
-# weights changed packs (and bf16x3-splits) the whole group in ONE scd_pack_conv3x3_multi launch; later
-# requests of that step hit the cache.  A cache entry is valid while the Parameter's version counter and storage
-# are unchanged (in-place optimizer updates, load_state_dict and .to() all invalidate it; a mutation through
-# `.data` does not: call invalidate_weight_cache() after one).
+# group (register_weight_group, called by create_network).  The first packed-layout request of a forward pass
+# packs (and bf16x3-splits) the whole group in ONE scd_pack_conv3x3_multi launch; later requests of that
+# forward and its backward hit the cache.  A forward pre-hook on the model starts a new generation, so weights
+# are repacked once per forward pass whatever changed them (optimizers do not reliably bump parameter version
+# counters: torch's fused AdamW does not).  Weights outside a registered model are packed on every call.
 # ------------------------------------------------------------------------------------------------
 class _IdentityMap:
     """Tensor-keyed map by object identity (tensor == is elementwise), dropping entries when the key dies."""
@@ -95,15 +95,26 @@ class _IdentityMap:
         self._d.clear()
 
 
-_GROUPS = _IdentityMap()  # weight Parameter -> list of weakrefs to the group's weights
-_PACKED = _IdentityMap()  # weight Parameter -> {key: (version, data_ptr, packed tensor)}
+class _WeightGroup:
+    def __init__(self, weights):
+        self.refs = [weakref.ref(w) for w in weights]
+        self.gen = 0
+
+
+_GROUPS = _IdentityMap()  # weight Parameter -> its model's _WeightGroup
+_PACKED = _IdentityMap()  # weight Parameter -> {key: (generation, data_ptr, packed tensor)}
 
 
 def register_weight_group(model: torch.nn.Module):
     convs = [m for m in model.modules() if isinstance(m, torch.nn.Conv2d) and m.kernel_size == (3, 3)]
-    group = [weakref.ref(c.weight) for c in convs]
+    group = _WeightGroup([c.weight for c in convs])
     for c in convs:
         _GROUPS.setdefault(c.weight, group)
+
+    def new_generation(_module, _args):
+        group.gen += 1
+
+    model.register_forward_pre_hook(new_generation)
 
 
 def invalidate_weight_cache():
@@ -114,38 +125,38 @@ def _pack_key(mode: int, ci_pad: int):
     return (mode, ci_pad if mode == 0 else 0, hip.conv_math() != 'f32')
 
 
-def _cached(w, key):
+def _cached(w, key, group):
     ent = (_PACKED.get(w) or {}).get(key)
-    if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
+    if ent is not None and ent[0] == group.gen and ent[1] == w.data_ptr():
         return ent[2]
     return None
 
 
 def packed_conv3x3(weight: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch.Tensor:
-    """hip.pack_conv3x3(weight, mode, ci_pad) through the per-step group cache."""
+    """hip.pack_conv3x3(weight, mode, ci_pad) through the per-forward group cache."""
     ci_pad = weight.shape[1] if ci_pad is None else ci_pad
-    if not _OPTS['pack_cache']:
+    group = _GROUPS.get(weight)
+    if not _OPTS['pack_cache'] or group is None:
         return hip.pack_conv3x3(weight.detach(), mode, ci_pad=ci_pad if mode == 0 else None)
     key = _pack_key(mode, ci_pad)
-    hit = _cached(weight, key)
+    hit = _cached(weight, key, group)
     if hit is not None:
         return hit
-    group = _GROUPS.get(weight)
     todo = [(weight, ci_pad)]
-    if group is not None and _OPTS['batch_pack']:
-        for r in group:
+    if _OPTS['batch_pack']:
+        for r in group.refs:
             w = r()
             if w is None or w is weight or w.device != weight.device:
                 continue
             cp = pad_in(w.shape[1]) if mode == 0 else w.shape[1]
             if mode == 1 and w.shape[1] % 8:  # input-layer convs: no data grad is ever taken
                 continue
-            if _cached(w, _pack_key(mode, cp)) is None:
+            if _cached(w, _pack_key(mode, cp), group) is None:
                 todo.append((w, cp))
     with torch.no_grad():
         packs = hip.pack_conv3x3_multi([(w.detach(), mode, cp) for w, cp in todo])
     for (w, cp), pk in zip(todo, packs):
-        _PACKED.setdefault(w, {})[_pack_key(mode, cp)] = (w._version, w.data_ptr(), pk)
+        _PACKED.setdefault(w, {})[_pack_key(mode, cp)] = (group.gen, w.data_ptr(), pk)
     return packs[0]
 
 

@@ -625,24 +625,32 @@ def test_pack_conv3x3_multi_matches_single_packs(dev):
 
 
 def test_weight_pack_cache_follows_parameter_updates(dev):
-    """engine.packed_conv3x3 packs a model's whole weight group once per weight version and repacks after an
-    optimizer step changes the weights."""
+    """engine.packed_conv3x3 packs a model's whole weight group once per forward pass, and repacks after an
+    optimizer step, including torch's fused AdamW, which does not bump parameter version counters."""
     from multimodal_siamese_cd_amd import engine, hip
     from multimodal_siamese_cd_amd.utils import experiment_manager as em, networks
     cfg = em.load_cfg('debug')
     net = networks.create_network(cfg).to(dev)
     convs = [m for m in net.modules() if isinstance(m, torch.nn.Conv2d) and m.kernel_size == (3, 3)]
     w = convs[3].weight
+    x = torch.rand(1, 5, 64, 64, device=dev)
+    with torch.no_grad():
+        net(x, x)
     a = engine.packed_conv3x3(w, 0)
-    assert engine.packed_conv3x3(w, 0) is a  # cached
-    assert engine._cached(convs[5].weight, engine._pack_key(0, convs[5].in_channels)) is not None  # group packed
+    assert engine.packed_conv3x3(w, 0) is a  # cached within the pass
+    grp = engine._GROUPS.get(w)
+    assert engine._cached(convs[5].weight, engine._pack_key(0, convs[5].in_channels), grp) is not None  # group
     assert torch.equal(a, hip.pack_conv3x3(w.detach(), 0))
-    opt = torch.optim.AdamW(net.parameters(), lr=1e-2)
-    for p in net.parameters():
-        p.grad = torch.ones_like(p)
-    opt.step()
-    b = engine.packed_conv3x3(w, 0)
-    assert b is not a and torch.equal(b, hip.pack_conv3x3(w.detach(), 0))
+    for fused in (False, True):
+        opt = torch.optim.AdamW(net.parameters(), lr=1e-2, fused=fused)
+        for p in net.parameters():
+            p.grad = torch.ones_like(p)
+        opt.step()
+        with torch.no_grad():
+            net(x, x)  # the next forward pass starts a new generation
+        b = engine.packed_conv3x3(w, 0)
+        assert b is not a and torch.equal(b, hip.pack_conv3x3(w.detach(), 0)), fused
+        a = b
 
 
 @pytest.mark.parametrize('labeled', [[1, 0, 1, 0], [1, 1, 1, 1], [0, 0, 0, 0], [0, 1, 0, 0]])
