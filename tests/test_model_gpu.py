@@ -131,12 +131,15 @@ def test_eval_forward_matches_reference(dev, name):
         check_logits(o, ref)
 
 
+@pytest.mark.parametrize('fused', [False, True])
 @pytest.mark.parametrize('name', ['siamese_t8-16', 'siamese_t8-16-32', 'whatevernet_t8-16'])
-def test_adamw_trajectory_matches_reference(dev, name):
+def test_adamw_trajectory_matches_reference(dev, name, fused):
+    """3 AdamW steps; fused=True is the bench's optimizer (it does not bump parameter versions, so any cache of
+    derived weights must not key on them)."""
     from multimodal_siamese_cd_amd import trainers
     fx = Fixture(name)
     cfg, net = _build(fx, dev)
-    opt = torch.optim.AdamW(net.parameters(), lr=fx.meta['lr'], weight_decay=fx.meta['wd'])
+    opt = torch.optim.AdamW(net.parameters(), lr=fx.meta['lr'], weight_decay=fx.meta['wd'], fused=fused)
     batch = {k: v.to(dev) for k, v in fx.batch().items()}
     losses = []
     for _ in range(3):
