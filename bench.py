@@ -176,8 +176,8 @@ def main():
     args = ap.parse_args()
 
     rank, local_rank, world = parallel.init_distributed()
-    torch.cuda.set_device(local_rank)
-    dev = torch.device('cuda', local_rank)
+    dev = torch.device('cuda', parallel.device_index(local_rank))
+    torch.cuda.set_device(dev)
     hip.load_library()
 
     cfg = experiment_manager.load_cfg(args.config)

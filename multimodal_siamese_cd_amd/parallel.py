@@ -19,16 +19,24 @@ def env_rank():
     return int(os.environ.get('RANK', 0)), int(os.environ.get('LOCAL_RANK', 0)), int(os.environ.get('WORLD_SIZE', 1))
 
 
+def device_index(local_rank: int) -> int:
+    """The GPU of a rank: its local rank (one process per GPU).  SCD_RANKS_SHARE_GPU=1 folds ranks onto the
+    visible devices (a rehearsal of the multi-rank path on a one-GPU machine, with SCD_DIST_BACKEND=gloo)."""
+    if os.environ.get('SCD_RANKS_SHARE_GPU') == '1':
+        return local_rank % max(torch.cuda.device_count(), 1)
+    return local_rank
+
+
 def init_distributed(backend: str | None = None):
     """Initialise the process group from torchrun's env; returns (rank, local_rank, world_size)."""
     rank, local_rank, world = env_rank()
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+            backend = os.environ.get('SCD_DIST_BACKEND') or ('nccl' if torch.cuda.is_available() else 'gloo')
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         if backend == 'nccl':
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group(backend, device_id=torch.device('cuda', local_rank))
+            torch.cuda.set_device(device_index(local_rank))
+            dist.init_process_group(backend, device_id=torch.device('cuda', device_index(local_rank)))
         else:
             dist.init_process_group(backend)
     return rank, local_rank, world
@@ -59,14 +67,15 @@ def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 64):
 def allreduce_max(value: float, device) -> float:
     if not is_distributed():
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    on_dev = device is not None and dist.get_backend() == 'nccl'
+    t = torch.tensor([value], dtype=torch.float64, device=device if on_dev else 'cpu')
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def barrier(device=None):
     if is_distributed():
-        if device is not None and device.type == 'cuda':
+        if device is not None and device.type == 'cuda' and dist.get_backend() == 'nccl':
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()

@@ -99,7 +99,7 @@ def main(argv=None):
     rank, local_rank, world = parallel.init_distributed()
     if not torch.cuda.is_available():
         raise SystemExit('train_supervised: needs an MI355X (gfx950) GPU; the HIP path has no CPU fallback')
-    device = torch.device('cuda', local_rank)
+    device = torch.device('cuda', parallel.device_index(local_rank))
     torch.cuda.set_device(device)
     hip.load_library()
     hip.set_conv_math(engine.conv_math_for(cfg))
