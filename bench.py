@@ -251,13 +251,18 @@ def main():
             "gflop_per_pair_3x3": round(f3 / batch / 1e9, 2),
             "frac": round(f3 / batch * (value / world) / (dpeak * 1e12), 4)}
 
-    if rank == 0 and not args.no_kernel_timing:
-        timer = KernelTimer()
-        timer.install()
+    if not args.no_kernel_timing:
+        # every rank runs the instrumented steps (DDP's collectives must match); rank 0 records the HIP events
         reps = 2
-        timer.active = True
+        timer = KernelTimer() if rank == 0 else None
+        if timer is not None:
+            timer.install()
+            timer.active = True
         for _ in range(reps):
             step()
+        torch.cuda.synchronize()
+        parallel.barrier(dev)
+    if rank == 0 and not args.no_kernel_timing:
         timer.active = False
         summ = timer.summary()
         t_ms = sum(t for _, t in summ.values()) / reps
