@@ -239,19 +239,30 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
             const int di = ij >> 1, dj = ij & 1;
             const float bias = a.bias ? a.bias[oc] : 0.f;
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i) {
+                // (img, oy, ox) of the tile's first row once; the 16 rows of a lane are at offsets < 32, walked
+                // by carrying ox into oy (and oy into img) instead of two divisions per element
+                const int mb = m0 + wm * TM * 32 + i * 32 + 4 * (lane >> 5);
+                const uint32_t ib = fdiv(uint32_t(mb), a.div_hw);
+                const uint32_t rb = uint32_t(mb) - ib * uint32_t(a.ho * a.wo);
+                const uint32_t yb = fdiv(rb, a.div_w);
+                const int img0 = int(ib), oy0 = int(yb), ox0 = int(rb - yb * uint32_t(a.wo));
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                    if (m < a.M) {
-                        const uint32_t img = fdiv(uint32_t(m), a.div_hw);
-                        const uint32_t rr = uint32_t(m) - img * uint32_t(a.ho * a.wo);
-                        const uint32_t oy = fdiv(rr, a.div_w);
-                        const uint32_t ox = rr - oy * uint32_t(a.wo);
-                        const size_t pix = size_t(int(img) * a.dst_h + 2 * int(oy) + di) * a.dst_w + 2 * int(ox) + dj;
-                        gstore1(a.dst + pix * a.ldc_d + oc, acc[i][j][r] + bias);
+                    const int d = (r & 3) + 8 * (r >> 2);
+                    if (mb + d >= a.M) continue;
+                    int ox = ox0 + d, oy = oy0, img = img0;
+                    while (ox >= a.wo) {
+                        ox -= a.wo;
+                        if (++oy == a.ho) {
+                            oy = 0;
+                            ++img;
+                        }
                     }
+                    const size_t pix = size_t(img * a.dst_h + 2 * oy + di) * a.dst_w + 2 * ox + dj;
+                    gstore1(a.dst + pix * a.ldc_d + oc, acc[i][j][r] + bias);
                 }
+            }
         }
     }
 }
