@@ -310,6 +310,11 @@ int scd_siamese_diff(scd_nhwc_t a, scd_nhwc_t d, scd_stream_t stream);
  * them.  d may be a channel slice of the decoder's concat buffer (networks.py:449). */
 int scd_bn_relu_siamese_diff(scd_nhwc_t a, const float *scale, const float *shift, scd_nhwc_t d,
                              scd_stream_t stream);
+/* One level's two consumers of relu(BN1(a)) in one pass (even h, w): d as scd_bn_relu_siamese_diff and
+ * y, idx = MaxPool2d(2) of both branches as scd_bn_relu_maxpool2_fwd with nseg 2 (networks.py:147-150, 420).
+ * Bit-identical to the two calls. */
+int scd_bn_relu_pool_diff(scd_nhwc_t a, const float *scale, const float *shift, scd_nhwc_t d, scd_nhwc_t y,
+                          uint8_t *idx, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * OutConv 1x1 head (networks.py:454-461): out NCHW [n][n_out][h][w] = b + x . w   (n_out <= 4)

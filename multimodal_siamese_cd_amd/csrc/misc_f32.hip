@@ -220,6 +220,63 @@ __global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float 
     }
 }
 
+// One encoder level's two consumers of relu(BN1(y1)) in one read of y1 (even h, w): the feature difference
+// d[b] = a_t2 - a_t1 at full resolution and MaxPool2d(2) of both branches for the next level.  Same per-element
+// expressions as siamese_diff_kernel<true> and maxpool2_fwd_kernel<true>, so results are bit-identical to the
+// two-kernel path.  One thread = one pooled pixel quad of pair b, both branches; rows = pairs * hy.
+__global__ void bn_relu_pool_diff_kernel(const float *__restrict__ x, int hx, int wx, int ldx, float *__restrict__ y,
+                                         int hy, int wy, int ldy, uint8_t *__restrict__ idx, float *__restrict__ d,
+                                         int ldd, int C, int pairs, int rows, FastDiv div_cq,
+                                         const float *__restrict__ bsc, const float *__restrict__ bsh) {
+    const int cq = C / 4;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= wy * cq) return;
+    const int ox = int(fdiv(uint32_t(e), div_cq));
+    const int c = (e - ox * cq) * 4;
+    const float4 sc1 = *reinterpret_cast<const float4 *>(bsc + c), sh1 = *reinterpret_cast<const float4 *>(bsh + c);
+    const float4 sc2 = *reinterpret_cast<const float4 *>(bsc + C + c);
+    const float4 sh2 = *reinterpret_cast<const float4 *>(bsh + C + c);
+    const int64_t half = int64_t(pairs) * hx * wx;  // pixels of one branch
+    for (int row = blockIdx.y; row < rows; row += gridDim.y) {
+        const int b = row / hy, oy = row - b * hy;
+        const int64_t q[4] = {(int64_t(b) * hx + 2 * oy) * wx + 2 * ox, (int64_t(b) * hx + 2 * oy) * wx + 2 * ox + 1,
+                              (int64_t(b) * hx + 2 * oy + 1) * wx + 2 * ox,
+                              (int64_t(b) * hx + 2 * oy + 1) * wx + 2 * ox + 1};
+        float4 v1[4], v2[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v1[k] = bn_relu_f4(*reinterpret_cast<const float4 *>(x + q[k] * ldx + c), sc1, sh1);
+            v2[k] = bn_relu_f4(*reinterpret_cast<const float4 *>(x + (q[k] + half) * ldx + c), sc2, sh2);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            *reinterpret_cast<float4 *>(d + q[k] * ldd + c) =
+                make_float4(v2[k].x - v1[k].x, v2[k].y - v1[k].y, v2[k].z - v1[k].z, v2[k].w - v1[k].w);
+#pragma unroll
+        for (int br = 0; br < 2; ++br) {
+            const float4 *v = br ? v2 : v1;
+            const float a0[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, a1[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
+            const float a2[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, a3[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
+            float o[4];
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float mx = -INFINITY;
+                int id = 0;
+                pool_pick(a0[k], 0, mx, id);
+                pool_pick(a1[k], 1, mx, id);
+                pool_pick(a2[k], 2, mx, id);
+                pool_pick(a3[k], 3, mx, id);
+                o[k] = mx;
+                packed |= uint32_t(id) << (8 * k);
+            }
+            const int64_t p = (int64_t(b + br * pairs) * hy + oy) * wy + ox;
+            *reinterpret_cast<float4 *>(y + p * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<uint32_t *>(idx + p * C + c) = packed;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Wave-cooperative 1x1 conv: G = pow2 >= C/4 lanes share a pixel (each a channel quad, coalesced 16-byte
 // loads), partial dots are combined with a fixed xor-shuffle tree.  grid-stride over pixel groups.
@@ -645,4 +702,25 @@ extern "C" int scd_pjaccard_bwd(const float *logits, const float *target, int64_
     hipLaunchKernelGGL(pjaccard_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), logits, target, n, sums,
                        gloss, glogits, gtarget);
     return launch_status("scd_pjaccard_bwd");
+}
+
+extern "C" int scd_bn_relu_pool_diff(scd_nhwc_t a, const float *scale, const float *shift, scd_nhwc_t d,
+                                     scd_nhwc_t y, uint8_t *idx, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(a, "pool_diff.a"));
+    SCD_TRY(check_view(d, "pool_diff.d"));
+    SCD_TRY(check_view(y, "pool_diff.y"));
+    if (a.n != 2 * d.n || a.h != d.h || a.w != d.w || a.c != d.c || (a.h & 1) || (a.w & 1) || a.h < 2 || a.w < 2 ||
+        y.n != a.n || y.c != a.c || y.h != a.h / 2 || y.w != a.w / 2 || !idx || (reinterpret_cast<uintptr_t>(idx) & 3) ||
+        !scale || !shift || !aligned16(scale) || !aligned16(shift)) {
+        set_error("bn_relu_pool_diff: a (2n, h, w, c) with even h, w; d (n, h, w, c); y (2n, h/2, w/2, c) with idx; "
+                  "aligned coefficients [2][c]");
+        return SCD_ERR_ARG;
+    }
+    const int64_t rows = int64_t(d.n) * y.h;
+    hipLaunchKernelGGL(bn_relu_pool_diff_kernel, row_grid(y.w * (y.c / 4), rows), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(a.data), a.h, a.w, a.ldc, static_cast<float *>(y.data), y.h, y.w,
+                       y.ldc, idx, static_cast<float *>(d.data), d.ldc, d.c, d.n, int(rows),
+                       make_fastdiv(uint32_t(y.c / 4)), scale, shift);
+    return launch_status("scd_bn_relu_pool_diff");
 }

@@ -29,7 +29,7 @@ _F32 = torch.float32
 
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
-         'pack_cache': True}
+         'pack_cache': True, 'pool_diff': True}
 
 
 def conv_math_for(cfg) -> str:
@@ -488,9 +488,12 @@ class SiameseEncoderFn(torch.autograd.Function):
         diffs, saved, bufs = [], [], []
         cur = x
         prev = None  # (y1, st1) of the previous level
+        pooled = None  # (pooled input, idx) of this level when the previous level's fused pass produced them
         for level, dc in enumerate(blocks):
             idx = None
-            if level > 0:
+            if pooled is not None:
+                cur, idx = pooled
+            elif level > 0:
                 y1p, st1p = prev
                 n, h, w, c = y1p.shape
                 cur = _empty((n, h // 2, w // 2, c), y1p)
@@ -502,7 +505,15 @@ class SiameseEncoderFn(torch.autograd.Function):
             buf = _empty((n2 // 2, h, w, c + extra), y1)
             d = buf[..., :c] if extra else buf
             sc, sh = _two_seg(st1)
-            hip.bn_relu_siamese_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c))
+            pooled = None
+            if level + 1 < len(blocks) and h % 2 == 0 and w % 2 == 0 and _OPTS['pool_diff']:
+                # the difference and the next level's pooling in one read of y1
+                nxt = _empty((n2, h // 2, w // 2, c), y1)
+                nidx = _empty((n2, h // 2, w // 2, c), y1, dtype=torch.uint8)
+                hip.bn_relu_pool_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c), nhwc(nxt), nidx)
+                pooled = (nxt, nidx)
+            else:
+                hip.bn_relu_siamese_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c))
             diffs.append(d)
             bufs.append(buf if extra else None)
             saved.append((idx, sv))

@@ -127,6 +127,7 @@ _SIGS = {
     "scd_maxpool2_fwd": ([NHWC, NHWC, c_void_p, c_void_p], c_int),
     "scd_bn_relu_maxpool2_fwd": ([NHWC, c_int32, c_void_p, c_void_p, NHWC, c_void_p, c_void_p], c_int),
     "scd_bn_relu_siamese_diff": ([NHWC, c_void_p, c_void_p, NHWC, c_void_p], c_int),
+    "scd_bn_relu_pool_diff": ([NHWC, c_void_p, c_void_p, NHWC, NHWC, c_void_p, c_void_p], c_int),
     "scd_feature_grad": ([NHWC, c_void_p, NHWC, c_int32, NHWC, c_int32, c_void_p], c_int),
     "scd_siamese_diff": ([NHWC, NHWC, c_void_p], c_int),
     "scd_conv1x1_fwd": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p], c_int),
@@ -511,6 +512,12 @@ def bn_relu_siamese_diff(a: NHWC, scale, shift, d: NHWC):
     """d = relu(bn_t2(a[n:])) - relu(bn_t1(a[:n])) with per-branch coefficients [2][C]."""
     _check(lib().scd_bn_relu_siamese_diff(a, scale.data_ptr(), shift.data_ptr(), d, _stream()),
            "scd_bn_relu_siamese_diff")
+
+
+def bn_relu_pool_diff(a: NHWC, scale, shift, d: NHWC, y: NHWC, idx: torch.Tensor):
+    """bn_relu_siamese_diff(a, ..., d) and bn_relu_maxpool2_fwd(a, 2, ..., y, idx) in one read of a (even h, w)."""
+    _check(lib().scd_bn_relu_pool_diff(a, scale.data_ptr(), shift.data_ptr(), d, y, idx.data_ptr(), _stream()),
+           "scd_bn_relu_pool_diff")
 
 
 def feature_grad(gy: NHWC, idx, gskip: NHWC, skip_mode: int, gx: NHWC, accumulate: bool = False):

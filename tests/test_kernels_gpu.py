@@ -537,6 +537,13 @@ def test_bn_relu_fused_pool_and_diff(dev, n, h, w, c, nseg):
     buf = torch.full((n // 2, h, w, c + 8), 7.0, device=dev)  # write into a concat slice; the rest untouched
     hip.bn_relu_siamese_diff(hip.nhwc(y), sc2, sh2, hip.nhwc(buf, 0, c))
     assert torch.equal(buf[..., :c], d_ref) and bool((buf[..., c:] == 7.0).all())
+    if h % 2 == 0 and w % 2 == 0:  # the one-pass difference + pooling of both branches
+        p_ref2, i_ref2 = torch.empty_like(p), torch.empty_like(i)
+        hip.bn_relu_maxpool2_fwd(hip.nhwc(y), 2, sc2, sh2, hip.nhwc(p_ref2), i_ref2)
+        p2, i2 = torch.full_like(p, 3.0), torch.zeros_like(i)
+        buf2 = torch.full((n // 2, h, w, c + 8), 7.0, device=dev)
+        hip.bn_relu_pool_diff(hip.nhwc(y), sc2, sh2, hip.nhwc(buf2, 0, c), hip.nhwc(p2), i2)
+        assert torch.equal(buf2, buf) and torch.equal(p2, p_ref2) and torch.equal(i2, i_ref2)
 
 
 def test_siamese_diff(dev):

@@ -9,6 +9,7 @@ A variant is a comma list of knob=value with knobs:
   fuse_enc  fused Siamese encoder (engine.set_options(fuse_siamese_encoder=...))
   math  conv arithmetic (hip.set_conv_math: f32 | x3 | bf16)
   pack  weight packing: 0 per call, 1 cached per weight, 2 batched per model (engine.packed_conv3x3)
+  pool_diff  encoder difference + next-level pooling in one pass (engine.set_options(pool_diff=...))
   SCD_* library environment switches read at launch (e.g. SCD_HALO16_TW=64)
 Prints per-variant median / min ms per step over the rounds.
 """
@@ -26,10 +27,15 @@ from multimodal_siamese_cd_amd import engine, hip  # noqa: E402
 from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_functions, networks  # noqa: E402
 
 
+_DEFAULT_OPTS = dict(engine._OPTS)
+
+
 def apply(variant: str):
+    """Every variant starts from the defaults: library switches, engine options and x3 math."""
     for k in [k for k in os.environ if k.startswith('SCD_')]:
         del os.environ[k]
     hip.set_conv_math('x3')
+    engine.set_options(**_DEFAULT_OPTS)
     for kv in filter(None, variant.split(',')):
         k, v = kv.split('=')
         if k == 'h16':
@@ -44,6 +50,8 @@ def apply(variant: str):
             engine.set_options(pack_cache=int(v) > 0, batch_pack=int(v) > 1)
         elif k == 'math':
             hip.set_conv_math(v)
+        elif k == 'pool_diff':
+            engine.set_options(pool_diff=bool(int(v)))
         elif k == 'fuse_enc':
             engine.set_options(fuse_siamese_encoder=bool(int(v)))
         elif k.startswith('SCD_'):  # library environment switch (read at launch)
