@@ -117,6 +117,9 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
 int wgrad16_mode();
 const void *wgrad_halo16_fn();
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
+// 16-channel-source variant (the input layer), same eligibility otherwise (conv_halo16.hip).
+const void *wgrad_halo16_c16_fn();
+void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s);
 // x3 weight-grad instantiations, indexed like kWgradTiles (conv_f32.hip).
 const void *wgrad_x3_fn(int tile_id);
 void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);

@@ -896,22 +896,33 @@ static void split_units(int64_t M, int64_t tiles, int64_t cap, int64_t min_units
 
 // Halo weight grad eligibility: x3 math, 3x3 taps in standard order, stride 1, same-size maps,
 // R and C multiples of 64, maps tiled by 2x16 patches.
-static bool wgrad_halo_ok(const scd_wgrad_t *d) {
+static bool wgrad_halo_shape(const scd_wgrad_t *d) {
     if (!conv_math_x3() || d->stride != 1 || d->ntaps != 9) return false;
     for (int t = 0; t < 9; ++t)
         if (d->dy[t] != t / 3 - 1 || d->dx[t] != t % 3 - 1) return false;
-    return d->rows.h == d->src.h && d->rows.w == d->src.w && d->rows.c % 64 == 0 && d->src.c % 64 == 0 &&
-           d->rows.h % 2 == 0 && d->rows.w % 16 == 0 && halo_enabled();
+    return d->rows.h == d->src.h && d->rows.w == d->src.w && d->rows.c % 64 == 0 && d->rows.h % 2 == 0 &&
+           d->rows.w % 16 == 0 && halo_enabled();
+}
+static bool wgrad_halo_ok(const scd_wgrad_t *d) { return wgrad_halo_shape(d) && d->src.c % 64 == 0; }
+// The 16-channel-source halo kernel (the padded input layer): 16x16x32 MFMA only (scd_set_wgrad16 on).
+// SCD_WGRAD_C16=0 sends it back to the generic x3 weight grad (A/B switch, read at launch).
+static bool wgrad_c16_ok(const scd_wgrad_t *d) {
+    const char *e = getenv("SCD_WGRAD_C16");
+    return wgrad_halo_shape(d) && d->src.c == 16 && wgrad16_mode() && !(e && e[0] == '0');
 }
 
-static int wgrad_halo_resident() {
-    static int caches[3] = {0, 0, 0};  // per halo weight-grad kernel (scd_set_wgrad16; halo16 x3 / bf16)
-    int &cache = caches[wgrad16_mode() ? (conv_math_planes() == 1 ? 2 : 1) : 0];
+static int wgrad_halo_resident(bool c16 = false) {
+    // per halo weight-grad kernel: 32x32x16; 16x16x32 x3 / x5 / bf16; 16-channel x3 / x5 / bf16
+    static int caches[7] = {0, 0, 0, 0, 0, 0, 0};
+    const int planes = conv_math_planes() == 1 ? 0 : conv_math_planes() == 5 ? 1 : 2;
+    int &cache = caches[c16 ? 4 + planes : wgrad16_mode() ? 1 + planes : 0];
     if (cache > 0) return cache;
     int per_cu = 0, cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_halo_fn(), 256, 0) != hipSuccess || per_cu < 1 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c16 ? wgrad_halo16_c16_fn() : wgrad_halo_fn(), 256, 0) !=
+            hipSuccess ||
+        per_cu < 1 ||
         cus < 1) {
         (void)hipGetLastError();
         return 2 * 256;
@@ -921,10 +932,11 @@ static int wgrad_halo_resident() {
 }
 
 static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
-    if (wgrad_halo_ok(d)) {
+    if (wgrad_halo_ok(d) || wgrad_c16_ok(d)) {
+        const bool c16 = !wgrad_halo_ok(d);
         const int64_t patches = pixels(d->rows) / 32;
-        const int64_t tiles = int64_t(d->rows.c / 64) * (d->src.c / 64);
-        split_units(patches, tiles, wgrad_halo_resident(), 8, 1, nsplit, kchunk);
+        const int64_t tiles = int64_t(d->rows.c / 64) * (c16 ? 1 : d->src.c / 64);
+        split_units(patches, tiles, wgrad_halo_resident(c16), 8, 1, nsplit, kchunk);
         return;
     }
     const int Ng = d->ntaps * d->src.c;
@@ -935,7 +947,7 @@ static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
 }  // namespace scd
 
 namespace scd {
-static bool wgrad_src_bn_ok(const scd_wgrad_t *d) { return wgrad_halo_ok(d) && wgrad16_mode(); }
+static bool wgrad_src_bn_ok(const scd_wgrad_t *d) { return (wgrad_halo_ok(d) && wgrad16_mode()) || wgrad_c16_ok(d); }
 }  // namespace scd
 
 extern "C" int scd_wgrad_src_bn_supported(const scd_wgrad_t *d) {
@@ -948,7 +960,7 @@ extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
     if (!conv_math_x3()) return SCD_MATH_F32;
-    return (wgrad_halo_ok(d) && wgrad16_mode()) ? conv_math_mode() : SCD_MATH_X3;
+    return ((wgrad_halo_ok(d) && wgrad16_mode()) || wgrad_c16_ok(d)) ? conv_math_mode() : SCD_MATH_X3;
 }
 
 namespace scd {
@@ -1084,6 +1096,14 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
         a.grid_j = a.C / 64;
         a.remap = xcd_remap_enabled();
         launch_wgrad_halo_x3(a, dim3(a.grid_r * a.grid_j * ns), s);
+        return launch_status("scd_conv_wgrad");
+    }
+    if (wgrad_c16_ok(d)) {
+        a.n_img_w = d->rows.n;
+        a.grid_r = a.R / 64;
+        a.grid_j = 1;
+        a.remap = xcd_remap_enabled();
+        launch_wgrad_halo16_c16(a, dim3(a.grid_r * ns), s);
         return launch_status("scd_conv_wgrad");
     }
     const WgradTile t = wgrad_tile(a.R, Ng);

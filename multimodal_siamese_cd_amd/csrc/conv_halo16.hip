@@ -728,6 +728,223 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Halo weight gradient of a 16-channel source (the input layer: 5 bands padded to the bf16 K granule of 16).
+// Same patch walk, tap shifts and transposed-read lane roles as wgrad_halo16_x3, with the channel block cut to
+// the 16 channels that exist: a block owns 64 rows r x 16 c x 9 taps and each wave 16 r, so a patch costs
+// 9 taps x (6 | 4 | 1) MFMAs per wave and the X halo staged per patch is a quarter of the 64-channel kernel's.
+// The X plane rows are 32 bytes (16 channels, unpadded): a 32-lane half of a transposed read then covers 256
+// contiguous bytes, conflict-free.
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int kC16RS = 32;
+
+template <int T, int PB, int HW_, int NP>
+__device__ __forceinline__ void c16_read_x(s16x4 (&f)[6], uint32_t xbase) {
+    constexpr int toff = (T / 3) * HW_ + (T % 3);
+    tr_read<0 * PB + toff * kC16RS>(f[0], xbase);
+    tr_read<0 * PB + (toff + 8) * kC16RS>(f[1], xbase);
+    if constexpr (w16_xp<NP>() >= 2) {
+        tr_read<1 * PB + toff * kC16RS>(f[2], xbase);
+        tr_read<1 * PB + (toff + 8) * kC16RS>(f[3], xbase);
+    }
+    if constexpr (w16_xp<NP>() == 3) {
+        tr_read<2 * PB + toff * kC16RS>(f[4], xbase);
+        tr_read<2 * PB + (toff + 8) * kC16RS>(f[5], xbase);
+    }
+}
+
+template <int T, int WAIT, int NP>
+__device__ __forceinline__ void c16_tap(f32x4 (&acc)[9], bf16x8 (&dv)[3], s16x4 (&f)[6]) {
+    bf16x8 x0 = cat8(f[0], f[1]), x1 = cat8(f[2], f[3]), x2 = cat8(f[4], f[5]);
+    if constexpr (NP != 1) {
+        if constexpr (NP == 3)
+            lds_wait<WAIT>(x0, x1, x2);
+        else
+            lds_wait<WAIT>(x0, x1);
+        if (T == 0) lds_wait<WAIT>(dv[0], dv[1], dv[2]);
+    } else {
+        lds_wait<WAIT>(x0, dv[0]);
+    }
+    if constexpr (NP != 1) {
+        acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[1], acc[T], 0, 0, 0);
+        acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[2], acc[T], 0, 0, 0);
+        if constexpr (NP == 3) acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, dv[0], acc[T], 0, 0, 0);
+        acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[1], acc[T], 0, 0, 0);
+        acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[0], acc[T], 0, 0, 0);
+    }
+    acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[0], acc[T], 0, 0, 0);
+}
+
+// taps T = 0..8, one ahead: compute T from buffer T & 1, then refill it with tap T + 2
+template <int T, int PB, int HW_, int NP>
+__device__ __forceinline__ void c16_chain(f32x4 (&acc)[9], bf16x8 (&dv)[3], s16x4 (&f0)[6], s16x4 (&f1)[6],
+                                          uint32_t xbase) {
+    if constexpr (T < 9) {
+        s16x4 (&f)[6] = (T & 1) ? f1 : f0;
+        c16_tap<T, (T == 8 ? 0 : 2 * w16_xp<NP>()), NP>(acc, dv, f);
+        if constexpr (T + 2 < 9) c16_read_x<T + 2, PB, HW_, NP>(f, xbase);
+        c16_chain<T + 1, PB, HW_, NP>(acc, dv, f0, f1, xbase);
+    }
+}
+}  // namespace
+
+template <int NP>
+__global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
+    constexpr int PH = 2, PW = 16, P = PH * PW;
+    constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
+    constexpr int RS = kW16RS, RSX = kC16RS;
+    constexpr int PA = P * RS, PB = HP * RSX;           // plane bytes
+    constexpr int A_CH = P * 16, B_CH = HP * 4;         // 4-channel pieces: dY 32 px x 64 r, X 72 px x 16 c
+    constexpr int A_PER = A_CH / 256, B_PER = (B_CH + 255) / 256;
+    static_assert(NP == 1 || NP == 3 || NP == 5, "x3, x5 or bf16");
+    constexpr int DP = NP == 1 ? 1 : 3;
+    constexpr int XP = w16_xp<NP>();
+    __shared__ __attribute__((aligned(16))) unsigned char smem[DP * PA + XP * PB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int split = int(L / uint32_t(a.grid_r));
+    const int r0 = int(L - uint32_t(split) * uint32_t(a.grid_r)) * 64;
+    const int pw_n = a.wo / PW, ph_n = a.ho / PH, pimg = pw_n * ph_n;
+    const int npatch = a.n_img_w * pimg;
+    const int pbeg = split * a.kchunk, pend = min(npatch, pbeg + a.kchunk);
+
+    const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
+    const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
+
+    f32x4 ra[A_PER], rb[B_PER];
+    f32x4 x_sc, x_sh;      // src transform coefficients of this thread's 4 channels (cq = tid & 3)
+    uint32_t x_valid = 0;  // bit i: halo piece i is inside the image (the padding stays zero)
+    auto load_patch = [&](int pi) {
+        const int img = pi / pimg, pr = pi - img * pimg;
+        if (a.src_scale) {
+            const int ch = (img / a.src_seg_imgs) * a.C + (tid & 3) * 4;
+            x_sc = gload4(a.src_scale + ch);
+            x_sh = gload4(a.src_shift + ch);
+        }
+        x_valid = 0;
+        const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            const int e = tid + i * 256, q = e >> 4, cq = e & 15;
+            const int py = q >> 4, px = q & 15;
+            const uint32_t off = uint32_t(((img * a.ho + y0 + py) * a.wo + x0 + px) * a.ldc_r + r0 + cq * 4) * 4u;
+            ra[i] = bload4(rs_rows, off);
+        }
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i) {
+            const int e = tid + i * 256, hp = e >> 2, cq = e & 3;
+            const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
+            const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
+            const bool v = e < B_CH && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+            x_valid |= uint32_t(v) << i;
+            rb[i] = bload4(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + cq * 4) * 4u : kOOB);
+        }
+    };
+    auto store_patch = [&]() {
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            const int e = tid + i * 256;
+            const int o = (e >> 4) * RS + (e & 15) * 8;
+            u32x2 h, m, l;
+            if constexpr (DP == 3) {
+                split3(ra[i], h, m, l);
+                *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
+                *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
+            } else {
+                h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
+                h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
+            }
+            *reinterpret_cast<u32x2 *>(smem + o) = h;
+        }
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i)
+            if (tid + i * 256 < B_CH) {
+                u32x2 h, m, l;
+                if (a.src_scale) {
+                    const bool v = (x_valid >> i) & 1u;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                }
+                const int e = tid + i * 256;
+                const int o = DP * PA + (e >> 2) * RSX + (e & 3) * 8;
+                if constexpr (XP >= 2) {
+                    split3(rb[i], h, m, l);
+                    *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
+                    if constexpr (XP == 3) *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
+                } else {
+                    h[0] = cvt_pk_bf16(rb[i][0], rb[i][1]);
+                    h[1] = cvt_pk_bf16(rb[i][2], rb[i][3]);
+                }
+                *reinterpret_cast<u32x2 *>(smem + o) = h;
+            }
+    };
+
+    f32x4 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // lane roles as wgrad_halo16_x3: group g supplies patch pixels (g >> 1, 4(g & 1) + (w16 >> 2)) (+8 for the
+    // second read of a fragment) and columns 4(w16 & 3)..+3 of the wave's 16 r / the 16 channels
+    const int g = lane >> 4, w16 = lane & 15;
+    const int py = g >> 1, pxq = 4 * (g & 1) + (w16 >> 2);
+    const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RS + (16 * wid + 4 * (w16 & 3)) * 2;
+    const uint32_t xbase = lds_addr(smem) + DP * PA + (py * HW_ + pxq) * RSX + (4 * (w16 & 3)) * 2;
+
+    if (pbeg < pend) {
+        load_patch(pbeg);
+        store_patch();
+        __syncthreads();
+        for (int pi = pbeg; pi < pend; ++pi) {
+            const bool more = pi + 1 < pend;
+            if (more) load_patch(pi + 1);
+            s16x4 fa[6];
+            tr_read<0 * PA + 0>(fa[0], dbase);
+            tr_read<0 * PA + 8 * RS>(fa[1], dbase);
+            if constexpr (DP == 3) {
+                tr_read<1 * PA + 0>(fa[2], dbase);
+                tr_read<1 * PA + 8 * RS>(fa[3], dbase);
+                tr_read<2 * PA + 0>(fa[4], dbase);
+                tr_read<2 * PA + 8 * RS>(fa[5], dbase);
+            }
+            bf16x8 dv[3];
+#pragma unroll
+            for (int p = 0; p < DP; ++p) dv[p] = cat8(fa[2 * p], fa[2 * p + 1]);
+            s16x4 f0[6], f1[6];
+            c16_read_x<0, PB, HW_, NP>(f0, xbase);
+            c16_read_x<1, PB, HW_, NP>(f1, xbase);
+            c16_chain<0, PB, HW_, NP>(acc, dv, f0, f1, xbase);
+            if (more) {
+                __syncthreads();  // every wave is done with this patch
+                store_patch();
+                __syncthreads();
+            }
+        }
+    }
+
+    // acc[t][q]: r = r0 + 16 wid + (lane & 15), c = 4g + q
+    float *slab = a.slabs + size_t(split) * a.R * a.Ng;
+    const int row = r0 + 16 * wid + w16;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) gstore4(slab + size_t(row) * a.Ng + t * 16 + 4 * g, acc[t]);
+}
+
+const void *wgrad_halo16_c16_fn() {
+    switch (conv_math_planes()) {
+        case 1: return reinterpret_cast<const void *>(&wgrad_halo16_c16<1>);
+        case 5: return reinterpret_cast<const void *>(&wgrad_halo16_c16<5>);
+        default: return reinterpret_cast<const void *>(&wgrad_halo16_c16<3>);
+    }
+}
+void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
+    switch (conv_math_planes()) {
+        case 1: hipLaunchKernelGGL(wgrad_halo16_c16<1>, grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL(wgrad_halo16_c16<5>, grid, dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL(wgrad_halo16_c16<3>, grid, dim3(256), 0, s, a);
+    }
+}
+
 // 0 = the 32x32x16 halo weight-grad kernel, 1 = this one (scd_set_wgrad16; initial value from SCD_WGRAD16).
 int g_wgrad16 = -1;
 int wgrad16_mode() {

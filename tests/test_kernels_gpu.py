@@ -426,6 +426,52 @@ def test_wgrad_halo_variants(dev, variant, n, h, w, ci, co):
         hip.set_conv_math(prev_m)
 
 
+@pytest.mark.parametrize('n,h,w,co', [(2, 4, 32, 64), (3, 32, 48, 128), (1, 2, 16, 64)])
+def test_wgrad_16_channel_source(dev, n, h, w, co):
+    """The input layer's weight grad (5 bands padded to 16 channels) on its own halo kernel: against fp64 under
+    x3 / x5 / bf16 (the arithmetic query names the kernel's planes), and reading the source through BN-apply +
+    ReLU bit-identical to the materialised activation."""
+    from multimodal_siamese_cd_amd import hip
+    ci = 16
+    g = torch.Generator().manual_seed(n * h + co)
+    spread = lambda *s: (torch.randn(*s, generator=g, dtype=torch.float64)
+                         * 10 ** (4 * torch.rand(*s, generator=g, dtype=torch.float64) - 2)).float()
+    x, dy = spread(n, h, w, ci), spread(n, h, w, co)
+    ref = torch.nn.grad.conv2d_weight(nchw(x).double(), (co, ci, 3, 3), nchw(dy).double(), padding=1)
+
+    def wgrad(src, dyd, sbn=None):
+        d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dyd), hip.nhwc(src), 1, hip.TAPS_3X3, sbn)
+        slabs = torch.empty(nbytes // 4, device=dev)
+        hip.conv_wgrad(d, slabs)
+        dw = torch.empty(co, ci, 3, 3, device=dev)
+        hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
+        return d, dw
+
+    errs = {}
+    for m in ('f32', 'x3', 'x5', 'bf16'):
+        prev = hip.set_conv_math(m)
+        try:
+            d, dw = wgrad(x.to(dev), dy.to(dev))
+            if m != 'f32':
+                assert hip.wgrad_arith(d) == m
+        finally:
+            hip.set_conv_math(prev)
+        errs[m] = rel(dw, ref)
+    assert errs['x3'] <= 2 * errs['f32'] + 1e-7 and errs['x5'] < 1e-5 and errs['bf16'] < 2e-2, errs
+    prev = hip.set_conv_math('x3')
+    try:
+        y = torch.randn(2 * n, h, w, ci, generator=g).to(dev)
+        dy2 = torch.randn(2 * n, h, w, co, generator=g).to(dev)
+        sc = (torch.rand(2 * ci, generator=g) * 2 - 0.5).to(dev)
+        sh = torch.randn(2 * ci, generator=g).to(dev)
+        a = torch.empty_like(y)
+        hip.bn_relu_apply(hip.nhwc(y), 2, sc, sh, hip.nhwc(a))
+        assert hip.wgrad_src_bn_supported(hip.nhwc(dy2), hip.nhwc(y), 1, hip.TAPS_3X3, (sc, sh, 2))
+        assert torch.equal(wgrad(a, dy2)[1], wgrad(y, dy2, (sc, sh, 2))[1])
+    finally:
+        hip.set_conv_math(prev)
+
+
 @pytest.mark.parametrize('n,h,w,c,nseg', [(4, 16, 16, 8, 2), (2, 33, 17, 64, 2), (2, 64, 64, 16, 1), (6, 8, 8, 512, 2)])
 def test_batchnorm_relu_train_forward_backward(dev, n, h, w, c, nseg):
     from multimodal_siamese_cd_amd import hip

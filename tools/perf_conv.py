@@ -54,6 +54,8 @@ def main():
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--only', default=None)
     ap.add_argument('--layer', default=None, help='run only this layer name (e.g. enc1b)')
+    ap.add_argument('--cin', type=int, default=None,
+                    help='input-layer channels as stored (default: the model\'s padding of 5 bands, engine.pad_in)')
     ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16'], help='conv arithmetic (default: library default)')
     ap.add_argument('--variants', default=None,
                     help='comma-separated variants, interleaved per layer; a variant is "+"-joined settings '
@@ -70,7 +72,9 @@ def main():
     tots = {m: {'fwd': [0.0, 0.0], 'dgrad': [0.0, 0.0], 'wgrad': [0.0, 0.0]} for m in modes}
     print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"cin":>5s} {"cout":>5s} | '
           f'{"fwd ms":>8s} {"TF/s":>6s} | {"dgrad ms":>8s} {"TF/s":>6s} | {"wgrad ms":>8s} {"TF/s":>6s}')
-    for name, n, s, ci, co in layers(args.batch):
+    from multimodal_siamese_cd_amd import engine
+    cin = args.cin or engine.pad_in(5)
+    for name, n, s, ci, co in layers(args.batch, cin=cin):
         if args.layer and name != args.layer:
             continue
         x = torch.randn(n, s, s, ci, device=dev)
