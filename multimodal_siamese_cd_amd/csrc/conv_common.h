@@ -110,8 +110,12 @@ bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s);
 int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels);
 // 16x16x32-MFMA halo igemm (conv_halo16.hip): 0 when `a` does not take it, else its config; launcher.
 int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw);
+// 16-channel-source forward (the input layer), conv_halo16.hip.
+int halo16_c16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw);
+void launch_halo16_c16(const IgemmArgs &a, int tw, hipStream_t s);
 // Whether launch_igemm_x3 would run the halo16 kernel for `a` (the only one with the input transform).
 bool igemm_takes_halo16(const IgemmArgs &a);
+bool igemm_takes_c16(const IgemmArgs &a);  // igemm_halo16_c16 (16-channel source)
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
 // 16x16x32-MFMA halo weight grad (conv_halo16.hip), selected by wgrad16_mode() (scd_set_wgrad16).
 int wgrad16_mode();

@@ -727,7 +727,7 @@ extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
     IgemmArgs a;
     SCD_TRY(igemm_query_prepare(d, a));
     if (!conv_math_x3()) return SCD_MATH_F32;
-    if (igemm_takes_halo16(a)) return conv_math_mode();
+    if (igemm_takes_halo16(a) || igemm_takes_c16(a)) return conv_math_mode();
     return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
 }
 

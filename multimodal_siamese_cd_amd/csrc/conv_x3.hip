@@ -576,10 +576,17 @@ bool igemm_takes_halo16(const IgemmArgs &a) {
     return conv_math_x3() && a.c % 16 == 0 && halo16_pick(a, halo_eligible(a), &bm, &tw) != 0;
 }
 
+bool igemm_takes_c16(const IgemmArgs &a) {
+    int bm = 0, tw = 0;
+    return conv_math_x3() && halo16_c16_pick(a, halo_eligible(a), &bm, &tw) != 0;
+}
+
 int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels) {
     int bm = 0, tw = 0;
     if (!conv_math_x3()) return 0;
-    if (!halo16_pick(a, halo_eligible(a), &bm, &tw) && !halo_pick(a, &bm, &tw)) return 0;
+    if (!halo16_pick(a, halo_eligible(a), &bm, &tw) && !halo16_c16_pick(a, halo_eligible(a), &bm, &tw) &&
+        !halo_pick(a, &bm, &tw))
+        return 0;
     *tile_pixels = bm;
     return a.n_img * (a.ho * a.wo / bm);
 }
@@ -589,6 +596,10 @@ bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
     int bm = 0, tw = 0;
     if (const int c16 = halo16_pick(a, halo_eligible(a), &bm, &tw)) {
         launch_halo16(a, c16, tw, s);
+        return true;
+    }
+    if (halo16_c16_pick(a, halo_eligible(a), &bm, &tw)) {
+        launch_halo16_c16(a, tw, s);
         return true;
     }
     switch (halo_pick(a, &bm, &tw)) {

@@ -426,6 +426,47 @@ def test_wgrad_halo_variants(dev, variant, n, h, w, ci, co):
         hip.set_conv_math(prev_m)
 
 
+@pytest.mark.parametrize('n,h,w,co', [(2, 8, 64, 64), (1, 4, 64, 128), (3, 2, 64, 72), (2, 24, 48, 64)])
+def test_conv_16_channel_source_forward(dev, n, h, w, co):
+    """The input layer's forward conv (16-channel source, two taps per 32-deep MFMA step) against fp64 under
+    x3 / x5 / bf16, with bias and fused BatchNorm tile statistics (against the host on the kernel's output)."""
+    from multimodal_siamese_cd_amd import hip
+    ci = 16
+    g = torch.Generator().manual_seed(n * w + co)
+    spread = lambda *s: (torch.randn(*s, generator=g, dtype=torch.float64)
+                         * 10 ** (4 * torch.rand(*s, generator=g, dtype=torch.float64) - 2)).float()
+    x = spread(n, h, w, ci)
+    wt = (torch.randn(co, ci, 3, 3, generator=g, dtype=torch.float64) / (3 * ci ** 0.5)).float()
+    b = torch.randn(co, generator=g)
+    ref = nhwc_t(F.conv2d(nchw(x).double(), wt.double(), b.double(), padding=1))
+    errs = {}
+    for m in ('f32', 'x3', 'x5', 'bf16'):
+        prev = hip.set_conv_math(m)
+        try:
+            xd, wd, bd = x.to(dev), wt.to(dev), b.to(dev)
+            wpk = hip.pack_conv3x3(wd, 0)
+            y = torch.empty(n, h, w, co, device=dev)
+            if m == 'f32':
+                hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, bd, hip.nhwc(y))
+            else:
+                assert hip.igemm_arith(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y)) == m
+                ntiles, tpx = hip.igemm_stat_tiles(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y))
+                assert tpx == 128 and ntiles * tpx == n * h * w
+                rec = torch.empty(ntiles * co * 2, device=dev)
+                hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, bd, hip.nhwc(y), stat_rec=rec)
+                tw = next(c for c in (16, 32, 64) if w % c == 0 and h % (128 // c) == 0)
+                tr = 128 // tw
+                yy = y.double().cpu().reshape(n, h // tr, tr, w // tw, tw, co).permute(0, 1, 3, 2, 4, 5)
+                yy = yy.reshape(-1, 128, co)
+                r = rec.double().cpu().reshape(ntiles, co, 2)
+                assert rel(r[..., 0], yy.mean(1)) < 2e-6
+                assert rel(r[..., 1], ((yy - yy.mean(1, keepdim=True)) ** 2).sum(1)) < 2e-5
+        finally:
+            hip.set_conv_math(prev)
+        errs[m] = rel(y, ref)
+    assert errs['x3'] <= 2 * errs['f32'] + 1e-7 and errs['x5'] < 1e-5 and errs['bf16'] < 2e-2, errs
+
+
 @pytest.mark.parametrize('n,h,w,co', [(2, 4, 32, 64), (3, 32, 48, 128), (1, 2, 16, 64)])
 def test_wgrad_16_channel_source(dev, n, h, w, co):
     """The input layer's weight grad (5 bands padded to 16 channels) on its own halo kernel: against fp64 under
