@@ -271,6 +271,17 @@ int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float 
                          float *dgamma, float *dbeta, float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes,
                          scd_stream_t stream);
 
+/* scd_bn_relu_backward with the incoming gradient formed on the fly instead of read from a tensor:
+ *   da[img] = maxpool_bwd(gy, idx)[img] (if gy.data)  -/+ gskip[img % gskip.n] (skip_mode 1: t1 images
+ *   subtract; 0: add) (if gskip.data)
+ * -- the operand scd_feature_grad would materialise (same expressions, bit-identical results).  Used by the
+ * Siamese encoder's backward (networks.py:147-150, 420): one read of the pooled and difference gradients per
+ * pass instead of writing and twice re-reading the level's full-resolution gradient. */
+int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip,
+                                int32_t skip_mode, int32_t nseg, const float *save_mean, const float *save_invstd,
+                                const float *gamma, const float *scale, const float *shift, float *dgamma,
+                                float *dbeta, float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes,
+                                scd_stream_t stream);
 /* scd_bn_relu_backward with the partial sums taken from conv-epilogue tile records (scd_bn_bwd_tiles_t.rec,
  * ntiles tiles, image-major, split evenly into nseg segments) instead of a pass over (y, da). */
 int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,

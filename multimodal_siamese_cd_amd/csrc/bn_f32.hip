@@ -292,9 +292,57 @@ __device__ __forceinline__ f4 relu_mask(f4 y, f4 sc, f4 sf, f4 g) {
               fmaf(y.z, sc.z, sf.z) > 0.f ? g.z : 0.f, fmaf(y.w, sc.w, sf.w) > 0.f ? g.w : 0.f};
 }
 
+// Incoming gradient dL/da of the BatchNorm + ReLU backward, read at (pixel p, channel quad c).
+struct DaPlain {  // a materialised tensor
+    const float *da;
+    int ldda;
+    __device__ __forceinline__ f4 operator()(int64_t p, int c) const { return ld4(da + p * ldda + c); }
+};
+// The encoder level's gradient, formed on the fly with the expressions of feature_grad_kernel (misc_f32.hip):
+// MaxPool2d backward of the next level's input gradient gy through the argmax bytes, plus -/+ the gradient of
+// the Siamese feature difference (skip_mode 1: t1 images subtract) or a plain skip gradient (skip_mode 0).
+struct DaPooled {
+    const float *gy;  // (n, h/2, w/2, C) or null
+    const uint8_t *idx;
+    int hy, wy, ldgy;
+    const float *gs;  // (gsn, h, w, C) or null
+    int gsn, ldgs, skip_mode;
+    int hx, wx, C;
+    FastDiv div_hw, div_w;
+    __device__ __forceinline__ f4 operator()(int64_t p, int c) const {
+        const uint32_t img = fdiv(uint32_t(p), div_hw);
+        const uint32_t rr = uint32_t(p) - img * uint32_t(hx * wx);
+        const int yy = int(fdiv(rr, div_w)), x = int(rr) - yy * wx;
+        f4 r = {0.f, 0.f, 0.f, 0.f};
+        if (gy) {
+            const int oy = yy >> 1, ox = x >> 1;
+            if (oy < hy && ox < wy) {
+                const int64_t q = (int64_t(img) * hy + oy) * wy + ox;
+                const uint32_t pk = *reinterpret_cast<const uint32_t *>(idx + q * C + c);
+                const f4 g = ld4(gy + q * ldgy + c);
+                const uint32_t want = uint32_t((yy & 1) * 2 + (x & 1));
+                r.x = ((pk >> 0) & 0xff) == want ? g.x : 0.f;
+                r.y = ((pk >> 8) & 0xff) == want ? g.y : 0.f;
+                r.z = ((pk >> 16) & 0xff) == want ? g.z : 0.f;
+                r.w = ((pk >> 24) & 0xff) == want ? g.w : 0.f;
+            }
+        }
+        if (gs) {
+            const int simg = int(img) % gsn;
+            const float sg = (skip_mode == 1 && int(img) < gsn) ? -1.f : 1.f;
+            const f4 sv = ld4(gs + ((int64_t(simg) * hx + yy) * wx + x) * ldgs + c);
+            r.x += sg * sv.x;
+            r.y += sg * sv.y;
+            r.z += sg * sv.z;
+            r.w += sg * sv.w;
+        }
+        return r;
+    }
+};
+
 // per (chunk) record {sum dz, sum dz*xhat}, rec[c][chunk][2]
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__restrict__ y, int ldy,
-                                                             const float *__restrict__ da, int ldda, int C,
+template <class DA>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__restrict__ y, int ldy, DA da, int C,
                                                              int64_t pseg, int ncps, int chunk, int nrec, int qpb,
                                                              const float *smean, const float *sinv, const float *scale,
                                                              const float *shift, float *__restrict__ rec) {
@@ -311,8 +359,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__rest
         for (; p + 3 * npl < ch.end; p += 4 * npl) {
             f4 y0 = ld4(y + p * ldy + c), y1 = ld4(y + (p + npl) * ldy + c);
             f4 y2 = ld4(y + (p + 2 * npl) * ldy + c), y3 = ld4(y + (p + 3 * npl) * ldy + c);
-            f4 g0 = ld4(da + p * ldda + c), g1 = ld4(da + (p + npl) * ldda + c);
-            f4 g2 = ld4(da + (p + 2 * npl) * ldda + c), g3 = ld4(da + (p + 3 * npl) * ldda + c);
+            f4 g0 = da(p, c), g1 = da(p + npl, c);
+            f4 g2 = da(p + 2 * npl, c), g3 = da(p + 3 * npl, c);
             PIN4(y0, y1, y2, y3);
             PIN4(g0, g1, g2, g3);
             const f4 z0 = relu_mask(y0, sc, sf, g0), z1 = relu_mask(y1, sc, sf, g1);
@@ -322,7 +370,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__rest
         }
         for (; p < ch.end; p += npl) {
             const f4 y0 = ld4(y + p * ldy + c);
-            const f4 z0 = relu_mask(y0, sc, sf, ld4(da + p * ldda + c));
+            const f4 z0 = relu_mask(y0, sc, sf, da(p, c));
             s1 += z0;
             s2 += z0 * ((y0 - mu) * iv);
         }
@@ -389,8 +437,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__res
 }
 
 // dy = gamma*invstd*(dz - k1 - xhat*k2); optional per-chunk sums of dy (conv bias grad), brec[c][chunk]
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restrict__ y, int ldy,
-                                                           const float *__restrict__ da, int ldda,
+template <class DA>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restrict__ y, int ldy, DA da,
                                                            float *__restrict__ dy, int lddy, int C, int64_t pseg,
                                                            int ncps, int chunk, int nrec, int qpb, const float *smean,
                                                            const float *sinv, const float *gamma, const float *scale,
@@ -414,8 +462,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
         for (; p + 3 * npl < ch.end; p += 4 * npl) {
             f4 y0 = ld4(y + p * ldy + c), y1 = ld4(y + (p + npl) * ldy + c);
             f4 y2 = ld4(y + (p + 2 * npl) * ldy + c), y3 = ld4(y + (p + 3 * npl) * ldy + c);
-            f4 g0 = ld4(da + p * ldda + c), g1 = ld4(da + (p + npl) * ldda + c);
-            f4 g2 = ld4(da + (p + 2 * npl) * ldda + c), g3 = ld4(da + (p + 3 * npl) * ldda + c);
+            f4 g0 = da(p, c), g1 = da(p + npl, c);
+            f4 g2 = da(p + 2 * npl, c), g3 = da(p + 3 * npl, c);
             PIN4(y0, y1, y2, y3);
             PIN4(g0, g1, g2, g3);
             const f4 o0 = mul * (relu_mask(y0, sc, sf, g0) - k1 - ((y0 - mu) * iv) * k2);
@@ -430,7 +478,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
         }
         for (; p < ch.end; p += npl) {
             const f4 y0 = ld4(y + p * ldy + c);
-            const f4 o0 = mul * (relu_mask(y0, sc, sf, ld4(da + p * ldda + c)) - k1 - ((y0 - mu) * iv) * k2);
+            const f4 o0 = mul * (relu_mask(y0, sc, sf, da(p, c)) - k1 - ((y0 - mu) * iv) * k2);
             st4(dy + p * lddy + c, o0);
             acc += o0;
         }
@@ -656,6 +704,29 @@ extern "C" int scd_bn_relu_apply(scd_nhwc_t y, int32_t nseg, const float *scale,
     return launch_status("scd_bn_relu_apply");
 }
 
+namespace scd {
+// partial -> finalize -> apply (+ conv-bias sums) over a gradient source DA
+template <class DA>
+static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *save_mean, const float *save_invstd,
+                            const float *gamma, const float *scale, const float *shift, float *dgamma, float *dbeta,
+                            float *dbias_prev, const scd_nhwc_t &dy, void *ws, hipStream_t s) {
+    const BnGeom g = bn_geom(y, nseg);
+    float *rec = static_cast<float *>(ws);
+    float *brec = rec + size_t(g.nrec) * y.c * 2;
+    float *coef = brec + size_t(g.nrec) * y.c;
+    hipLaunchKernelGGL(bn_bwd_partial<DA>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       static_cast<const float *>(y.data), y.ldc, da, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb,
+                       save_mean, save_invstd, scale, shift, rec);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
+                       coef, dgamma, dbeta);
+    hipLaunchKernelGGL(bn_bwd_apply<DA>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       static_cast<const float *>(y.data), y.ldc, da, static_cast<float *>(dy.data), dy.ldc, y.c,
+                       g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
+                       dbias_prev ? brec : nullptr);
+    if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
+}
+}  // namespace scd
+
 extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
                                     const float *save_invstd, const float *gamma, const float *scale,
                                     const float *shift, float *dgamma, float *dbeta, float *dbias_prev,
@@ -673,22 +744,58 @@ extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, c
         set_error("bn_relu_backward: workspace too small");
         return SCD_ERR_WORKSPACE;
     }
-    const BnGeom g = bn_geom(y, nseg);
-    float *rec = static_cast<float *>(ws);
-    float *brec = rec + size_t(g.nrec) * y.c * 2;
-    float *coef = brec + size_t(g.nrec) * y.c;
-    hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(bn_bwd_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, static_cast<const float *>(da.data), da.ldc, y.c,
-                       g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean, save_invstd, scale, shift, rec);
-    hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
-                       coef, dgamma, dbeta);
-    hipLaunchKernelGGL(bn_bwd_apply, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, static_cast<const float *>(da.data), da.ldc,
-                       static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean,
-                       save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr);
-    if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
+    bn_backward_run(y, DaPlain{static_cast<const float *>(da.data), da.ldc}, nseg, save_mean, save_invstd, gamma, scale,
+                    shift, dgamma, dbeta, dbias_prev, dy, ws, as_stream(stream));
     return launch_status("scd_bn_relu_backward");
+}
+
+extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip,
+                                           int32_t skip_mode, int32_t nseg, const float *save_mean,
+                                           const float *save_invstd, const float *gamma, const float *scale,
+                                           const float *shift, float *dgamma, float *dbeta, float *dbias_prev,
+                                           scd_nhwc_t dy, void *ws, size_t ws_bytes, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(bn_check(y, nseg));
+    SCD_TRY(check_view(gy, "bn_bwd_pooled.gy", true));
+    SCD_TRY(check_view(gskip, "bn_bwd_pooled.gskip", true));
+    SCD_TRY(check_view(dy, "bn_bwd_pooled.dy"));
+    if (dy.n != y.n || dy.h != y.h || dy.w != y.w || dy.c != y.c || !save_mean || !save_invstd || !scale || !shift ||
+        (!gy.data && !gskip.data) || pixels(y) >= (int64_t(1) << 32)) {
+        set_error("bn_relu_backward_pooled: shape mismatch / null");
+        return SCD_ERR_ARG;
+    }
+    if (gy.data && (!idx || gy.n != y.n || gy.c != y.c || gy.h != y.h / 2 || gy.w != y.w / 2 ||
+                    (reinterpret_cast<uintptr_t>(idx) & 3))) {
+        set_error("bn_relu_backward_pooled: gy must be (n, h/2, w/2, c) with 4-byte aligned idx");
+        return SCD_ERR_ARG;
+    }
+    if (gskip.data && (gskip.c != y.c || gskip.h != y.h || gskip.w != y.w || y.n % gskip.n ||
+                       (skip_mode == 1 && y.n != 2 * gskip.n) || (skip_mode != 0 && skip_mode != 1))) {
+        set_error("bn_relu_backward_pooled: gskip shape/mode mismatch");
+        return SCD_ERR_ARG;
+    }
+    if (!ws || ws_bytes < scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg)) {
+        set_error("bn_relu_backward_pooled: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    DaPooled da;
+    da.gy = static_cast<const float *>(gy.data);
+    da.idx = idx;
+    da.hy = gy.h;
+    da.wy = gy.w;
+    da.ldgy = gy.ldc;
+    da.gs = static_cast<const float *>(gskip.data);
+    da.gsn = gskip.n > 0 ? gskip.n : 1;
+    da.ldgs = gskip.ldc;
+    da.skip_mode = skip_mode;
+    da.hx = y.h;
+    da.wx = y.w;
+    da.C = y.c;
+    da.div_hw = make_fastdiv(uint32_t(y.h * y.w));
+    da.div_w = make_fastdiv(uint32_t(y.w));
+    bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy, ws,
+                    as_stream(stream));
+    return launch_status("scd_bn_relu_backward_pooled");
 }
 
 extern "C" int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
@@ -717,8 +824,8 @@ extern "C" int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t n
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, tile_rec, y.c, nseg, ntiles / nseg, ntiles,
                        g.pseg, coef, dgamma, dbeta);
-    hipLaunchKernelGGL(bn_bwd_apply, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, static_cast<const float *>(da.data), da.ldc,
+    hipLaunchKernelGGL(bn_bwd_apply<DaPlain>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       static_cast<const float *>(y.data), y.ldc, DaPlain{static_cast<const float *>(da.data), da.ldc},
                        static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean,
                        save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);

@@ -29,7 +29,7 @@ _F32 = torch.float32
 
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
-         'pack_cache': True, 'pool_diff': True}
+         'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True}
 
 
 def conv_math_for(cfg) -> str:
@@ -307,8 +307,19 @@ def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, src_bn=No
     return gw
 
 
+@dataclass
+class _PooledGrad:
+    """An encoder level's incoming gradient, maxpool_bwd(gy, idx) -/+ gskip, left unmaterialised: the BatchNorm
+    backward forms it on the fly (scd_bn_relu_backward_pooled)."""
+    gy: torch.Tensor | None
+    idx: torch.Tensor | None
+    gskip: torch.Tensor | None
+    skip_mode: int
+
+
 def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None):
-    """`tiles` = (records, ntiles) of the partial sums from the conv epilogue that produced g."""
+    """`tiles` = (records, ntiles) of the partial sums from the conv epilogue that produced g; g may be a
+    _PooledGrad."""
     c = y.shape[3]
     dy = torch.empty_like(y)
     dgamma = _empty((c,), y)
@@ -316,7 +327,12 @@ def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None):
     dbias = _empty((c,), y) if conv_bias_grad else None
     n, h, w, _ = y.shape
     ws = _ws(hip.bn_workspace_bytes(n, h, w, c, st.nseg), y)
-    if tiles is not None:
+    if isinstance(g, _PooledGrad):
+        hip.bn_relu_backward_pooled(nhwc(y), nhwc(g.gy) if g.gy is not None else hip._NULL, g.idx,
+                                    nhwc(g.gskip) if g.gskip is not None else hip._NULL, g.skip_mode, st.nseg,
+                                    st.smean, st.sinv, bn.weight, st.scale, st.shift, dgamma, dbeta, dbias, nhwc(dy),
+                                    ws)
+    elif tiles is not None:
         hip.bn_relu_backward_tiles(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift,
                                    tiles[0], tiles[1], dgamma, dbeta, dbias, nhwc(dy), ws)
     else:
@@ -341,8 +357,9 @@ def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Te
     return ga0, None
 
 
-def _dc_backward(g_out: torch.Tensor, saved, dc, need_dx: bool):
-    """Returns (grad wrt DoubleConv input or None, [8 param grads in dc_params order])."""
+def _dc_backward(g_out, saved, dc, need_dx: bool):
+    """g_out: gradient of the block output (a tensor, or a _PooledGrad formed inside the BatchNorm backward).
+    Returns (grad wrt DoubleConv input or None, [8 param grads in dc_params order])."""
     x, y0, a0, st0, y1, st1 = saved
     s = dc.conv
     conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
@@ -443,11 +460,15 @@ class EncoderFn(torch.autograd.Function):
         dev_like = saved[0][1][1]
         for level in range(L, -1, -1):
             shape = ctx.feat_shapes[level]
-            ga = _empty(tuple(shape), dev_like)
             idx_next = saved[level + 1][0] if level < L else None
             gf = g_feats[level]
-            hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL, idx_next if g_pool is not None else None,
-                             nhwc(gf) if gf is not None else hip._NULL, 0, nhwc(ga))
+            if _OPTS['pooled_bn_bwd'] and (g_pool is not None or gf is not None):
+                ga = _PooledGrad(g_pool, idx_next if g_pool is not None else None, gf, 0)
+            else:
+                ga = _empty(tuple(shape), dev_like)
+                hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL,
+                                 idx_next if g_pool is not None else None, nhwc(gf) if gf is not None else hip._NULL,
+                                 0, nhwc(ga))
             gx, pg = _dc_backward(ga, saved[level][1], blocks[level], need_dx=level > 0)
             grads[8 * level:8 * level + 8] = pg
             g_pool = gx
@@ -535,10 +556,14 @@ class SiameseEncoderFn(torch.autograd.Function):
             idx_next = saved[level + 1][0] if level < L else None
             sv = saved[level][1]
             y1 = sv[4]
-            ga = torch.empty_like(y1)
             gd = g_diffs[level]
-            hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL, idx_next if g_pool is not None else None,
-                             nhwc(gd) if gd is not None else hip._NULL, 1, nhwc(ga))
+            if _OPTS['pooled_bn_bwd'] and (g_pool is not None or gd is not None):
+                ga = _PooledGrad(g_pool, idx_next if g_pool is not None else None, gd, 1)
+            else:
+                ga = torch.empty_like(y1)
+                hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL,
+                                 idx_next if g_pool is not None else None, nhwc(gd) if gd is not None else hip._NULL,
+                                 1, nhwc(ga))
             gx, pg = _dc_backward(ga, sv, blocks[level], need_dx=level > 0)
             grads[8 * level:8 * level + 8] = pg
             g_pool = gx

@@ -118,6 +118,9 @@ _SIGS = {
          c_void_p, c_size_t, c_void_p],
         c_int,
     ),
+    "scd_bn_relu_backward_pooled": ([NHWC, NHWC, c_void_p, NHWC, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_size_t,
+                                     c_void_p], c_int),
     "scd_bn_relu_backward_tiles": (
         [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
          c_void_p, c_void_p, NHWC, c_void_p, c_size_t, c_void_p],
@@ -482,6 +485,16 @@ def bn_relu_backward(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, 
                                    shift.data_ptr(), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), dy, ws.data_ptr(),
                                    ws.numel(), _stream()),
         "scd_bn_relu_backward")
+
+
+def bn_relu_backward_pooled(y: NHWC, gy: NHWC, idx, gskip: NHWC, skip_mode: int, nseg, smean, sinv, gamma, scale,
+                            shift, dgamma, dbeta, dbias, dy: NHWC, ws):
+    """bn_relu_backward of da = maxpool_bwd(gy, idx) -/+ gskip (feature_grad's operand, never materialised)."""
+    _check(
+        lib().scd_bn_relu_backward_pooled(y, gy, _ptr(idx), gskip, skip_mode, nseg, smean.data_ptr(), sinv.data_ptr(),
+                                          _ptr(gamma), scale.data_ptr(), shift.data_ptr(), _ptr(dgamma), _ptr(dbeta),
+                                          _ptr(dbias), dy, ws.data_ptr(), ws.numel(), _stream()),
+        "scd_bn_relu_backward_pooled")
 
 
 def bn_relu_backward_tiles(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, tile_rec, ntiles, dgamma, dbeta,

@@ -633,6 +633,47 @@ def test_bn_relu_fused_pool_and_diff(dev, n, h, w, c, nseg):
         assert torch.equal(buf2, buf) and torch.equal(p2, p_ref2) and torch.equal(i2, i_ref2)
 
 
+@pytest.mark.parametrize('n,h,w,c,mode,parts', [(4, 16, 16, 64, 1, 'both'), (4, 9, 7, 32, 1, 'both'),
+                                                 (2, 8, 8, 128, 1, 'skip'), (4, 10, 12, 64, 0, 'both'),
+                                                 (2, 16, 8, 64, 0, 'pool')])
+def test_bn_relu_backward_pooled(dev, n, h, w, c, mode, parts):
+    """The BatchNorm + ReLU backward forming its incoming gradient on the fly (maxpool_bwd -/+ skip) is
+    bit-identical to feature_grad followed by bn_relu_backward (dy, dgamma, dbeta, conv-bias grad)."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * h * w + c + mode)
+    nseg = 2
+    y = (torch.randn(n, h, w, c, generator=g) * 2 + 0.3).to(dev)
+    gamma = (torch.rand(c, generator=g) + 0.5).to(dev)
+    beta = torch.randn(c, generator=g).to(dev)
+    smean, sinv, scale, shift = (torch.empty(nseg * c, device=dev) for _ in range(4))
+    ws = torch.empty(hip.bn_workspace_bytes(n, h, w, c, nseg), dtype=torch.uint8, device=dev)
+    hip.bn_train_stats(hip.nhwc(y), nseg, gamma, beta, 1e-5, 0.1, False, None, None, smean, sinv, scale, shift, ws)
+    gy = idx = gs = None
+    if parts in ('both', 'pool'):
+        x = torch.randn(n, h, w, c, generator=g).to(dev)
+        gy = torch.randn(n, h // 2, w // 2, c, generator=g).to(dev)
+        idx = torch.empty(n, h // 2, w // 2, c, dtype=torch.uint8, device=dev)
+        hip.maxpool2_fwd(hip.nhwc(x), hip.nhwc(torch.empty_like(gy)), idx)
+    if parts in ('both', 'skip'):
+        gs = torch.randn(n // 2 if mode == 1 else n, h, w, c + 8, generator=g).to(dev)[..., 4:4 + c]  # strided view
+    nh = lambda t: hip.nhwc(t) if t is not None else hip._NULL
+    ga = torch.empty_like(y)
+    hip.feature_grad(nh(gy), idx, nh(gs), mode, hip.nhwc(ga))
+    outs = []
+    for pooled in (False, True):
+        dy = torch.empty_like(y)
+        dg, db, dbias = (torch.empty(c, device=dev) for _ in range(3))
+        if pooled:
+            hip.bn_relu_backward_pooled(hip.nhwc(y), nh(gy), idx, nh(gs), mode, nseg, smean, sinv, gamma, scale,
+                                        shift, dg, db, dbias, hip.nhwc(dy), ws)
+        else:
+            hip.bn_relu_backward(hip.nhwc(y), hip.nhwc(ga), nseg, smean, sinv, gamma, scale, shift, dg, db, dbias,
+                                 hip.nhwc(dy), ws)
+        outs.append((dy, dg, db, dbias))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_siamese_diff(dev):
     from multimodal_siamese_cd_amd import hip
     a = torch.randn(6, 5, 7, 16)
