@@ -308,7 +308,7 @@ struct DaPooled {
     const float *gs;  // (gsn, h, w, C) or null
     int gsn, ldgs, skip_mode;
     int hx, wx, C;
-    FastDiv div_hw, div_w;
+    FastDiv div_hw, div_w, div_gsn;
     __device__ __forceinline__ f4 operator()(int64_t p, int c) const {
         const uint32_t img = fdiv(uint32_t(p), div_hw);
         const uint32_t rr = uint32_t(p) - img * uint32_t(hx * wx);
@@ -328,7 +328,7 @@ struct DaPooled {
             }
         }
         if (gs) {
-            const int simg = int(img) % gsn;
+            const int simg = int(img - fdiv(img, div_gsn) * uint32_t(gsn));
             const float sg = (skip_mode == 1 && int(img) < gsn) ? -1.f : 1.f;
             const f4 sv = ld4(gs + ((int64_t(simg) * hx + yy) * wx + x) * ldgs + c);
             r.x += sg * sv.x;
@@ -760,7 +760,7 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
     SCD_TRY(check_view(gskip, "bn_bwd_pooled.gskip", true));
     SCD_TRY(check_view(dy, "bn_bwd_pooled.dy"));
     if (dy.n != y.n || dy.h != y.h || dy.w != y.w || dy.c != y.c || !save_mean || !save_invstd || !scale || !shift ||
-        (!gy.data && !gskip.data) || pixels(y) >= (int64_t(1) << 32)) {
+        (!gy.data && !gskip.data) || pixels(y) >= (int64_t(1) << 31)) {
         set_error("bn_relu_backward_pooled: shape mismatch / null");
         return SCD_ERR_ARG;
     }
@@ -793,6 +793,7 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
     da.C = y.c;
     da.div_hw = make_fastdiv(uint32_t(y.h * y.w));
     da.div_w = make_fastdiv(uint32_t(y.w));
+    da.div_gsn = make_fastdiv(uint32_t(da.gsn));
     bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy, ws,
                     as_stream(stream));
     return launch_status("scd_bn_relu_backward_pooled");
