@@ -13,4 +13,4 @@ run --config baseline_siamese --math bf16
 run --config baseline_siamese --math bf16 --batch 64
 run --config baseline_dualstream
 run --config dtsiamese
-run --config siamese_mmcr_alpha0500
+run --config siamese_mmcr_alpha0500 --batch 16
