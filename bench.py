@@ -128,8 +128,9 @@ class KernelTimer:
         return sum(ev[3] for ev in self.events) / reps
 
 
-def cpu_baseline(cfg, steps: int = 2, batch: int = 2, size: int = 256):
-    """The CPU oracle (torch fp32 on host cores) running the same training step on a bounded sample."""
+def cpu_baseline(cfg, min_seconds: float = 10.0, max_steps: int = 64, batch: int = 2, size: int = 256):
+    """The CPU oracle (torch fp32 on host cores) running the same training step on a bounded sample:
+    whole steps until `min_seconds` of CPU work have been timed (at least 2, at most `max_steps`)."""
     from oracle import siamese_oracle as O
 
     threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(os.cpu_count() or 1, 16)
@@ -152,8 +153,10 @@ def cpu_baseline(cfg, steps: int = 2, batch: int = 2, size: int = 256):
 
     step()  # warm-up
     t0 = time.perf_counter()
-    for _ in range(steps):
+    steps = 0
+    while steps < 2 or (time.perf_counter() - t0 < min_seconds and steps < max_steps):
         step()
+        steps += 1
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 4), "unit": "image-pairs/s", "cores": threads, "kind": "port",
             "sample": f"{steps} timed training steps (after 1 warm-up) of the CPU oracle ({mtype}), bs={batch}, "

@@ -191,6 +191,22 @@ class _BNSaved:
     nseg: int
 
 
+# BatchNorm `num_batches_tracked` increments of one stage, applied in one foreach launch when the stage ends
+# (flush_bn_counters) instead of one int64 add per layer.
+_NBT_PENDING: list = []
+
+
+def flush_bn_counters() -> None:
+    if not _NBT_PENDING:
+        return
+    by_inc: dict = {}
+    for t, inc in _NBT_PENDING:
+        by_inc.setdefault(inc, []).append(t)
+    _NBT_PENDING.clear()
+    for inc, ts in by_inc.items():
+        torch._foreach_add_(ts, inc)
+
+
 def _bn_uses_batch_stats(bn: torch.nn.BatchNorm2d, training: bool) -> bool:
     return training or not bn.track_running_stats or bn.running_mean is None
 
@@ -218,7 +234,7 @@ def _bn_forward(y: torch.Tensor, bn: torch.nn.BatchNorm2d, nseg: int, training: 
             hip.bn_train_stats(nhwc(y), nseg, bn.weight, bn.bias, bn.eps, mom, update, bn.running_mean,
                                bn.running_var, smean, sinv, scale, shift, ws)
         if update:
-            bn.num_batches_tracked.add_(nseg)
+            _NBT_PENDING.append((bn.num_batches_tracked, nseg))
         return _BNSaved(smean, sinv, scale, shift, nseg)
     scale, shift = _empty((c,), y), _empty((c,), y)
     hip.bn_eval_coeffs(c, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, scale, shift)
@@ -481,7 +497,10 @@ def run_encoder(inc, encoder, x: torch.Tensor, nseg: int, training: bool) -> lis
     params = [p for dc in blocks for p in dc_params(dc)]
     save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
     meta = _Meta(blocks=blocks, nseg=nseg, training=training, save=save)
-    return list(EncoderFn.apply(x, meta, *params))
+    try:
+        return list(EncoderFn.apply(x, meta, *params))
+    finally:
+        flush_bn_counters()
 
 
 # ------------------------------------------------------------------------------------------------
@@ -577,7 +596,10 @@ def run_siamese_encoder(inc, encoder, x: torch.Tensor, training: bool, extra: di
     params = [p for dc in blocks for p in dc_params(dc)]
     save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
     meta = _Meta(blocks=blocks, nseg=2, training=training, save=save, extra=extra or {})
-    diffs = list(SiameseEncoderFn.apply(x, meta, *params))
+    try:
+        diffs = list(SiameseEncoderFn.apply(x, meta, *params))
+    finally:
+        flush_bn_counters()
     return diffs, meta.cat_buffers
 
 
@@ -710,7 +732,10 @@ def run_decoder(decoder, features: list, training: bool, cat_buffers: list | Non
     params = [p for up in ups for p in up_params(up)]
     save = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or any(f.requires_grad for f in features))
     meta = _Meta(ups=ups, training=training, save=save, cat_buffers=cat_buffers)
-    return DecoderFn.apply(meta, features[0], *features[1:1 + len(ups)], *params)
+    try:
+        return DecoderFn.apply(meta, features[0], *features[1:1 + len(ups)], *params)
+    finally:
+        flush_bn_counters()
 
 
 # ------------------------------------------------------------------------------------------------
