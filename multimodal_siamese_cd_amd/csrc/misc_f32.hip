@@ -3,6 +3,8 @@
 // Reference call sites: input hand-off (train_supervised.py:68-69), nn.MaxPool2d(2) (networks.py:420),
 // torch.sub(f_t2, f_t1) (networks.py:149), OutConv 1x1 (networks.py:454-461), power_jaccard_loss
 // (utils/loss_functions.py:141-150), the parameter layouts of Conv2d / ConvTranspose2d.
+#include <algorithm>
+#include <cstdint>
 #include <cstring>
 #include <string>
 
@@ -40,15 +42,31 @@ static int grid_for(int64_t total, int cap = 4096) {
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ void pack_nchw_kernel(const float *__restrict__ src, int n, int c, int hw, int c_begin, int c_count,
+// One image per blockIdx.y, 32-bit index math only.  VEC (dc, ldc multiples of 4, 16-byte aligned destination):
+// one thread per float4 of the destination, so a wave's stores cover consecutive 16-byte groups of whole pixels;
+// the source planes are read 16 pixels x 4 channels per load.  Otherwise one thread per pixel with scalar stores,
+// so any channel offset works (the early-fusion t2 bands).
+template <bool VEC>
+__global__ void pack_nchw_kernel(const float *__restrict__ src, int c, int hw, int c_begin, int c_count,
                                  float *__restrict__ dst, int dc, int ldc) {
-    // one thread per (pixel, dst channel); scalar stores so any channel offset works (5-band inputs)
-    const int64_t total = int64_t(n) * hw * dc;
-    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
-        const int cc = int(e % dc);
-        const int64_t p = e / dc;
-        const int64_t img = p / hw, pix = p % hw;
-        dst[p * ldc + cc] = cc < c_count ? src[(img * c + c_begin + cc) * hw + pix] : 0.f;
+    const int img = blockIdx.y;
+    const float *s = src + (size_t(img) * c + c_begin) * hw;
+    float *d = dst + size_t(img) * hw * ldc;
+    if (VEC) {
+        const int q4 = dc >> 2;  // float4 groups per pixel
+        const int total = hw * q4;
+        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+            const int pix = e / q4, c0 = (e - pix * q4) * 4;
+            float4 v;
+            v.x = c0 + 0 < c_count ? s[size_t(c0 + 0) * hw + pix] : 0.f;
+            v.y = c0 + 1 < c_count ? s[size_t(c0 + 1) * hw + pix] : 0.f;
+            v.z = c0 + 2 < c_count ? s[size_t(c0 + 2) * hw + pix] : 0.f;
+            v.w = c0 + 3 < c_count ? s[size_t(c0 + 3) * hw + pix] : 0.f;
+            *reinterpret_cast<float4 *>(d + size_t(pix) * ldc + c0) = v;
+        }
+    } else {
+        for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < hw; pix += gridDim.x * blockDim.x)
+            for (int cc = 0; cc < dc; ++cc) d[size_t(pix) * ldc + cc] = cc < c_count ? s[size_t(cc) * hw + pix] : 0.f;
     }
 }
 
@@ -279,7 +297,9 @@ __global__ void bn_relu_pool_diff_kernel(const float *__restrict__ x, int hx, in
 
 // ------------------------------------------------------------------------------------------------
 // Wave-cooperative 1x1 conv: G = pow2 >= C/4 lanes share a pixel (each a channel quad, coalesced 16-byte
-// loads), partial dots are combined with a fixed xor-shuffle tree.  grid-stride over pixel groups.
+// loads), partial dots are combined with a fixed xor-shuffle tree.  grid-stride over groups of U pixel sets per
+// wave, whose loads are all issued before the arithmetic (U x the bytes in flight of one set per iteration).
+template <int U>
 __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restrict__ x, int ldx, int C, int hw,
                                                           int64_t npix, const float *__restrict__ w,
                                                           const float *__restrict__ b, int n_out, int G,
@@ -289,26 +309,46 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restric
     const int cq = C / 4;
     const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-    for (int64_t p0 = wave * ppw; p0 < npix; p0 += nwaves * ppw) {
-        const int64_t p = p0 + pp;
-        const bool ok = p < npix;
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t p0 = wave * ppw * U; p0 < npix; p0 += nwaves * ppw * U) {
+        float s[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int o = 0; o < 4; ++o) s[u][o] = 0.f;
         for (int qq = q; qq < cq; qq += G) {
-            const float4 v = ok ? *reinterpret_cast<const float4 *>(x + p * ldx + 4 * qq) : make_float4(0, 0, 0, 0);
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t p = p0 + u * ppw + pp;
+                v[u] = p < npix ? *reinterpret_cast<const float4 *>(x + p * ldx + 4 * qq) : make_float4(0, 0, 0, 0);
+            }
 #pragma unroll
             for (int o = 0; o < 4; ++o) {
                 if (o < n_out) {
                     const float4 wv = *reinterpret_cast<const float4 *>(w + int64_t(o) * C + 4 * qq);
-                    s[o] = fmaf(v.x, wv.x, fmaf(v.y, wv.y, fmaf(v.z, wv.z, fmaf(v.w, wv.w, s[o]))));
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        s[u][o] = fmaf(v[u].x, wv.x, fmaf(v[u].y, wv.y, fmaf(v[u].z, wv.z, fmaf(v[u].w, wv.w, s[u][o]))));
                 }
             }
         }
 #pragma unroll
         for (int o = 0; o < 4; ++o)
-            for (int off = G / 2; off > 0; off >>= 1) s[o] += __shfl_xor(s[o], off, 64);
-        if (ok && q == 0) {
-            const int64_t img = p / hw, pix = p - img * hw;
-            for (int o = 0; o < n_out; ++o) out[(img * n_out + o) * hw + pix] = s[o] + (b ? b[o] : 0.f);
+            if (o < n_out)
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    for (int off = G / 2; off > 0; off >>= 1) s[u][o] += __shfl_xor(s[u][o], off, 64);
+        if (q == 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t p = p0 + u * ppw + pp;
+                if (p < npix) {
+                    const int64_t img = p / hw, pix = p - img * hw;
+#pragma unroll
+                    for (int o = 0; o < 4; ++o)
+                        if (o < n_out) out[(img * n_out + o) * hw + pix] = s[u][o] + (b ? b[o] : 0.f);
+                }
+            }
         }
     }
 }
@@ -481,9 +521,26 @@ extern "C" int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, 
         set_error("pack_nchw: bad arguments");
         return SCD_ERR_ARG;
     }
-    const int64_t total = int64_t(n) * h * w * dst.c;
-    hipLaunchKernelGGL(pack_nchw_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), src, n, c, h * w,
-                       c_begin, c_count, static_cast<float *>(dst.data), dst.c, dst.ldc);
+    const int hw = h * w;
+    if (n > 65535 || int64_t(h) * w > (int64_t(1) << 30)) {
+        set_error("pack_nchw: n must be <= 65535 and h*w <= 2^30");
+        return SCD_ERR_ARG;
+    }
+    if (n == 0 || hw == 0) return SCD_OK;
+    float *d = static_cast<float *>(dst.data);
+    const bool vec = dst.c % 4 == 0 && dst.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(d) & 15) == 0;
+    const int64_t per_img = vec ? int64_t(hw) * (dst.c / 4) : hw;
+    if (per_img >= (int64_t(1) << 31)) {
+        set_error("pack_nchw: image too large");
+        return SCD_ERR_ARG;
+    }
+    const dim3 grid(unsigned(std::min<int64_t>((per_img + 255) / 256, 4096)), unsigned(n));
+    if (vec)
+        hipLaunchKernelGGL(pack_nchw_kernel<true>, grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
+                           c_count, d, dst.c, dst.ldc);
+    else
+        hipLaunchKernelGGL(pack_nchw_kernel<false>, grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
+                           c_count, d, dst.c, dst.ldc);
     return launch_status("scd_pack_nchw");
 }
 
@@ -615,10 +672,11 @@ extern "C" int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int
     const int64_t npix = pixels(x);
     int G = 1;
     while (G < x.c / 4 && G < 64) G *= 2;
-    const int64_t waves = (npix + (64 / G) - 1) / (64 / G);
+    constexpr int U = 4;
+    const int64_t waves = (npix + (64 / G) * U - 1) / ((64 / G) * U);
     int blocks = int((waves + 3) / 4);
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(conv1x1_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(conv1x1_fwd_kernel<U>, dim3(blocks), dim3(256), 0, as_stream(stream),
                        static_cast<const float *>(x.data), x.ldc, x.c, x.h * x.w, npix, w, b, n_out, G, out);
     return launch_status("scd_conv1x1_fwd");
 }

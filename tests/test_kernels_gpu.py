@@ -682,11 +682,12 @@ def test_siamese_diff(dev):
     assert torch.equal(d.cpu(), a[3:] - a[:3])
 
 
-@pytest.mark.parametrize('c,n_out', [(64, 1), (8, 1), (128, 1), (16, 3)])
-def test_head_conv1x1(dev, c, n_out):
+@pytest.mark.parametrize('c,n_out,h,w', [(64, 1, 16, 24), (8, 1, 16, 24), (128, 1, 16, 24), (16, 3, 16, 24),
+                                         (64, 1, 7, 9), (32, 4, 5, 13)])  # odd sizes: ragged last pixel group
+def test_head_conv1x1(dev, c, n_out, h, w):
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(c + n_out)
-    n, h, w = 2, 16, 24
+    n = 2
     x = torch.randn(n, c, h, w, generator=g, requires_grad=True)
     wt = torch.randn(n_out, c, 1, 1, generator=g, requires_grad=True)
     b = torch.randn(n_out, generator=g, requires_grad=True)
@@ -863,3 +864,25 @@ def test_halo_math_accuracy_vs_fp64(dev, ci, co):
     for k in range(3):  # x3: at most the fp32-MFMA error; x5: below 1e-5 (measured 2.5e-6..3.9e-6)
         assert errs['x3'][k] <= 2 * errs['f32'][k] + 1e-7, ('x3', k, errs)
         assert errs['x5'][k] < 1e-5, ('x5', k, errs)
+
+
+@pytest.mark.parametrize('n,c,h,w,c_begin,c_count,dst_c,off,ldc', [
+    (2, 5, 12, 20, 0, 5, 16, 0, 16),     # Siamese input: 5 bands zero-padded to 16 (float4 path)
+    (3, 5, 7, 9, 0, 5, 8, 0, 8),         # fp32-MFMA padding to 8
+    (2, 13, 16, 16, 2, 4, 16, 0, 16),    # band subset (dual-stream)
+    (2, 5, 11, 13, 0, 5, 5, 5, 16),      # early fusion t2 half: channel offset 5 (scalar path)
+    (1, 4, 5, 6, 0, 4, 4, 4, 12),        # aligned channel slice of a wider buffer (float4 path, ldc 12)
+    (2, 3, 300, 301, 1, 2, 3, 1, 6),     # more pixels than one grid stride, odd sizes
+])
+def test_pack_nchw(dev, n, c, h, w, c_begin, c_count, dst_c, off, ldc):
+    """scd_pack_nchw vs torch: NCHW band slice -> NHWC channel slice, zero-filled above c_count, and the
+    channels outside the slice untouched."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(n, c, h, w, generator=g)
+    buf = torch.full((n, h, w, ldc), -7.0, device=dev)
+    hip.pack_nchw(x.to(dev), c_begin, c_count, buf, off, dst_c)
+    exp = torch.full((n, h, w, ldc), -7.0)
+    exp[..., off:off + dst_c] = 0.0
+    exp[..., off:off + c_count] = x[:, c_begin:c_begin + c_count].permute(0, 2, 3, 1)
+    assert torch.equal(buf.cpu(), exp)
