@@ -608,10 +608,21 @@ bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
         case 3: launch_halo<4, 1, 2, 1>(a, tw, s); return true;
         default: break;
     }
+    // SCD_X3_TILE (tile study, tools/perf_convT.py): 1 128x128, 2 256x64, 3 256x32, 4 128x64, 5 256x128
+    if (const char *t = getenv("SCD_X3_TILE")) {
+        switch (t[0]) {
+            case '1': launch_x3<2, 2, 2, 2>(a, s); return true;
+            case '2': launch_x3<4, 1, 2, 2>(a, s); return true;
+            case '3': launch_x3<4, 1, 2, 1>(a, s); return true;
+            case '4': launch_x3<2, 2, 2, 1>(a, s); return true;
+            case '5': launch_x3<4, 2, 2, 2>(a, s); return true;
+            default: break;
+        }
+    }
     if (a.n_out >= 128)
         launch_x3<2, 2, 2, 2>(a, s);  // 128 x 128
     else if (a.n_out >= 64)
-        launch_x3<4, 1, 2, 2>(a, s);  // 256 x 64
+        launch_x3<2, 2, 2, 1>(a, s);  // 128 x 64 (tools/perf_convT.py: up1 ConvT data grad 177 -> 155 us vs 256 x 64)
     else
         launch_x3<4, 1, 2, 1>(a, s);  // 256 x 32
     return true;

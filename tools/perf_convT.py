@@ -1,0 +1,73 @@
+"""Per-level timing of the decoder's ConvTranspose2d(2, s2) GEMMs (forward: 1 tap into the pixel-shuffled concat
+slice; data grad: 4 taps, stride 2) on the per-tap x3 kernel, under tile variants (SCD_X3_TILE).
+
+    python tools/perf_convT.py [--batch 32] [--reps 10] [--tiles 0,1,2,4,5]
+
+Tile 0 is the library's own choice.  HIP events, interleaved per level.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from multimodal_siamese_cd_amd import hip  # noqa: E402
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--tiles', default='0,1,2,4,5')
+    args = ap.parse_args()
+    hip.load_library()
+    hip.set_conv_math('x3')
+    dev = torch.device('cuda:0')
+    tiles = args.tiles.split(',')
+    # (level, input size, ConvT channels (in == out, networks.py Up), skip channels) of SiameseUNet [64,128,256,512]
+    # at 256^2
+    levels = [('up4', 16, 512, 512, 512), ('up3', 32, 256, 256, 256), ('up2', 64, 128, 128, 128),
+              ('up1', 128, 64, 64, 64)]
+    tot = {t: [0.0, 0.0] for t in tiles}
+    for name, hc, ci, co, cs in levels:
+        b = args.batch
+        x = torch.randn(b, hc, hc, ci, device=dev)
+        wt = torch.randn(ci, co, 2, 2, device=dev) * 0.05
+        bias = torch.randn(co, device=dev)
+        cat = torch.empty(b, 2 * hc, 2 * hc, cs + co, device=dev)
+        gx = torch.empty(b, hc, hc, ci, device=dev)
+        wf, wb = hip.pack_convT2x2(wt, 0), hip.pack_convT2x2(wt, 1)
+        gup = hip.nhwc(cat, cs, co)
+        for t in tiles:
+            if t == '0':
+                os.environ.pop('SCD_X3_TILE', None)
+            else:
+                os.environ['SCD_X3_TILE'] = t
+            f = timeit(lambda: hip.conv_igemm(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, bias, gup,
+                                              store_mode=1), args.reps)
+            d = timeit(lambda: hip.conv_igemm(gup, hc, hc, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx)), args.reps)
+            tot[t][0] += f
+            tot[t][1] += d
+            print(f'{name} hc={hc:4d} ci={ci:4d} co={co:4d} tile {t}: fwd {f * 1e3:7.1f} us  dgrad {d * 1e3:7.1f} us',
+                  flush=True)
+    os.environ.pop('SCD_X3_TILE', None)
+    for t, (f, d) in tot.items():
+        print(f'tile {t}: fwd {f * 1e3:7.1f} us  dgrad {d * 1e3:7.1f} us  sum {(f + d) * 1e3:7.1f} us')
+
+
+if __name__ == '__main__':
+    main()
