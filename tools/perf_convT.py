@@ -33,6 +33,7 @@ def main():
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--tiles', default='0,1,2,4,5')
+    ap.add_argument('--plain', action='store_true', help='also time the forward GEMM with plain stores')
     args = ap.parse_args()
     hip.load_library()
     hip.set_conv_math('x3')
@@ -60,6 +61,11 @@ def main():
             f = timeit(lambda: hip.conv_igemm(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, bias, gup,
                                               store_mode=1), args.reps)
             d = timeit(lambda: hip.conv_igemm(gup, hc, hc, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx)), args.reps)
+            if args.plain:  # same GEMM, plain row-major stores (no pixel shuffle): isolates the epilogue
+                flat = torch.empty(b, hc, hc, 4 * co, device=dev)
+                fp = timeit(lambda: hip.conv_igemm(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, bias,
+                                                   hip.nhwc(flat)), args.reps)
+                print(f'{name} tile {t}: fwd plain-store {fp * 1e3:7.1f} us', flush=True)
             tot[t][0] += f
             tot[t][1] += d
             print(f'{name} hc={hc:4d} ci={ci:4d} co={co:4d} tile {t}: fwd {f * 1e3:7.1f} us  dgrad {d * 1e3:7.1f} us',
