@@ -400,9 +400,20 @@ def _dc_backward(g_out, saved, dc, need_dx: bool):
 # ------------------------------------------------------------------------------------------------
 # Input packing
 # ------------------------------------------------------------------------------------------------
+def _check_input_pair(x_t1: torch.Tensor, x_t2: torch.Tensor) -> None:
+    """Both inputs must be GPU tensors of one shape on one device: their data pointers go straight to a kernel."""
+    hip.ensure_device(x_t1)
+    hip.ensure_device(x_t2)
+    if x_t1.dim() != 4 or x_t1.shape != x_t2.shape:
+        raise ValueError(f"x_t1 and x_t2 must be (B, C, H, W) of one shape, got {tuple(x_t1.shape)} and "
+                         f"{tuple(x_t2.shape)}")
+    if x_t1.device != x_t2.device:
+        raise ValueError(f"x_t1 is on {x_t1.device} but x_t2 is on {x_t2.device}")
+
+
 def pack_pair(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:
     """Siamese input: [2B, H, W, pad_in(C)] NHWC with t1 images first (one shared-encoder batch)."""
-    hip.ensure_device(x_t1)
+    _check_input_pair(x_t1, x_t2)
     if x_t1.requires_grad or x_t2.requires_grad:
         raise NotImplementedError("input gradients are not computed by the HIP path")
     b, c, h, w = x_t1.shape
@@ -415,7 +426,7 @@ def pack_pair(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count:
 
 def pack_stream(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:
     """Early-fusion input cat((t1[bands], t2[bands]), dim=1) as [B, H, W, pad_in(2*nb)] NHWC."""
-    hip.ensure_device(x_t1)
+    _check_input_pair(x_t1, x_t2)
     if x_t1.requires_grad or x_t2.requires_grad:
         raise NotImplementedError("input gradients are not computed by the HIP path")
     b, c, h, w = x_t1.shape

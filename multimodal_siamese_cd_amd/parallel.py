@@ -51,17 +51,32 @@ def rank_seed(seed: int, rank: int) -> int:
     return int(seed) * 1_000_003 + 7919 * int(rank)
 
 
-def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 64):
+def params_outside_forward(module) -> tuple:
+    """Names of submodules whose parameters a model holds but never uses in forward.
+
+    The reference keeps such modules for state_dict compatibility, e.g. DualTaskSiameseUNet.outc_sem_change
+    (utils/networks.py:174): it never receives a gradient.  Models declare them in `PARAMS_OUTSIDE_FORWARD`.
+    """
+    return tuple(getattr(module, 'PARAMS_OUTSIDE_FORWARD', ()))
+
+
+def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 64, find_unused_parameters: bool | None = None):
     """Replace the DataParallel-style wrapper's pass-through by DDP when running under torchrun.
 
     Keeps the `.module` attribute and `module.` state_dict prefix of the reference's wrapper.
+    `find_unused_parameters=None` turns DDP's unused-parameter search on only for a model that declares
+    parameters outside its forward graph (`params_outside_forward`).  Without it, the bucket holding such a
+    parameter is never reduced, the replicas drift apart and the next step raises.
     """
     if not is_distributed():
         return wrapper
     module = wrapper.module if hasattr(wrapper, 'module') else wrapper
+    if find_unused_parameters is None:
+        find_unused_parameters = bool(params_outside_forward(module))
     ids = [device.index] if (device is not None and device.type == 'cuda') else None
     return torch.nn.parallel.DistributedDataParallel(module, device_ids=ids, broadcast_buffers=True,
-                                                     bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+                                                     bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
+                                                     find_unused_parameters=find_unused_parameters)
 
 
 def allreduce_max(value: float, device) -> float:

@@ -46,7 +46,7 @@ def run_training(cfg, device, max_steps: int | None = None):
         print(f"run config {cfg.NAME}: model {cfg.MODEL.TYPE} topology {list(cfg.MODEL.TOPOLOGY)} "
               f"bs {cfg.TRAINER.BATCH_SIZE}/GPU x {world} GPU, lr {cfg.TRAINER.LR}, epochs {epochs}", flush=True)
     loader = None
-    if not cfg.DATALOADER.get('SYNTHETIC', True):  # SpaceNet7 tile cache, augmented on the device
+    if not datasets.uses_synthetic_data(cfg):  # SpaceNet7 tile cache, augmented on the device
         ds = datasets.MultimodalCDDataset(cfg, 'training')
         loader = datasets.DeviceDataLoader(ds, int(cfg.TRAINER.BATCH_SIZE), device, shuffle=bool(cfg.DATALOADER.SHUFFLE),
                                            num_workers=int(cfg.DATALOADER.get('NUM_WORKER', 0)))

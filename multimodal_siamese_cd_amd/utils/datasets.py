@@ -23,6 +23,24 @@ def _channels(cfg) -> int:
     return n1 + n2
 
 
+def uses_synthetic_data(cfg) -> bool:
+    """Whether a run trains/evaluates on synthetic pairs rather than the tile cache.
+
+    DATALOADER.SYNTHETIC unset (None, the shipped default) means: synthetic exactly when the config names no
+    training AOIs, so a reference config that carries its DATASET.*_IDS split reads real tiles.  An explicit
+    True next to a non-empty split is honoured, with a loud warning.
+    """
+    flag = cfg.DATALOADER.get('SYNTHETIC', None)
+    ids = list(cfg.get('DATASET', {}).get('TRAINING_IDS', []) or [])
+    if flag is None:
+        return not ids
+    if flag and ids:
+        import warnings
+        warnings.warn(f'DATALOADER.SYNTHETIC is True although DATASET.TRAINING_IDS names {len(ids)} AOIs: '
+                      'training on synthetic noise, not on the tile cache', stacklevel=2)
+    return bool(flag)
+
+
 def synthetic_batch(cfg, batch_size: int, device, generator: torch.Generator, size=None,
                     change_rate: float = 0.05, sem_rate: float = 0.2):
     """One batch of item dicts stacked along dim 0, generated on `device`.  `size`: int or (H, W); default
@@ -229,12 +247,14 @@ class DeviceDataLoader:
     """DataLoader over MultimodalCDDataset whose workers only read tiles; batches are augmented on the device."""
 
     def __init__(self, dataset: MultimodalCDDataset, batch_size: int, device, shuffle: bool = True,
-                 drop_last: bool = True, num_workers: int = 0):
+                 drop_last: bool = True, num_workers: int = 0, distributed: bool = True):
+        """`distributed=False` never shards: the evaluation path scores the whole split on one rank."""
         import torch.distributed as dist
         from torch.utils.data import DataLoader, DistributedSampler
         self.dataset, self.device = dataset, device
         sampler = None
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:  # one shard per rank
+        if distributed and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            # one shard per rank (training)
             sampler = DistributedSampler(dataset, shuffle=shuffle, drop_last=drop_last)
             shuffle = False
         self.sampler = sampler

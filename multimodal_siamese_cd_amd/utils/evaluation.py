@@ -6,7 +6,7 @@ F1 / precision / recall at the best threshold.  Differences, by design:
   - the sigmoid and the thresholded confusion counts run as one fused HIP pass (MultiThresholdMetric.add_logits,
     `scd_threshold_counts`) instead of sigmoid + 4 boolean reductions;
   - wandb is not installed: the numbers go to `log` (default print) and are returned as a dict;
-  - with DATALOADER.SYNTHETIC: False the run's AOIs come from the tile cache (datasets.MultimodalCDDataset, as
+  - with real data (datasets.uses_synthetic_data False) the run's AOIs come from the tile cache (datasets.MultimodalCDDataset, as
     evaluation.py:15-17 builds it); otherwise `dataset` defaults to the synthetic item-dict dataset.
   - a model returning a tuple (DualTaskSiameseUNet) is scored on its change output (index 0); the reference
     would fail on it.
@@ -25,13 +25,14 @@ def model_evaluation(net, cfg, device, run_type: str, epoch: float, step: int, d
     net.eval()
     thr = torch.linspace(0.5, 1, 1) if thresholds is None else torch.as_tensor(thresholds, dtype=torch.float32)
     measurer = metrics.MultiThresholdMetric(thr)
-    if dataset is None and not cfg.DATALOADER.get('SYNTHETIC', True):  # evaluation.py:15-17
+    if dataset is None and not datasets.uses_synthetic_data(cfg):  # evaluation.py:15-17
         dataset = datasets.MultimodalCDDataset(cfg, run_type, no_augmentations=True, dataset_mode='first_last',
                                                disable_multiplier=True, disable_unlabeled=True)
     ds = dataset if dataset is not None else datasets.SyntheticCDDataset(
         cfg, run_type, length=int(cfg.get('EVAL_SAMPLES', 4)), seed=int(cfg.SEED) + 1000)
     if isinstance(ds, datasets.MultimodalCDDataset):  # full tiles, transforms (to-tensor only) on the device
-        dataloader = datasets.DeviceDataLoader(ds, 1, device, shuffle=False, drop_last=False)
+        # distributed=False: evaluation runs on rank 0 only and must see every AOI of the split, unpadded
+        dataloader = datasets.DeviceDataLoader(ds, 1, device, shuffle=False, drop_last=False, distributed=False)
     else:
         dataloader = torch_data.DataLoader(ds, batch_size=1, num_workers=0, shuffle=False, drop_last=False)
     with torch.no_grad():

@@ -82,7 +82,12 @@ class MultiThresholdMetric(object):
         self._accumulate(self._counts(y_true, y_pred, False), y_pred.numel())
 
     def add_logits(self, y_true: torch.Tensor, logits: torch.Tensor):
-        """add_sample(y_true, sigmoid(logits)) with the sigmoid fused into the counting pass (evaluation.py:25)."""
+        """add_sample(y_true, sigmoid(logits)) with the sigmoid fused into the counting pass (evaluation.py:25).
+
+        Bit-exact against the reference except for a pixel whose probability lies within 2 fp32 ulp of a
+        threshold: there the device's 1/(1+expf(-x)) and the CPU torch.sigmoid can round to neighbouring floats
+        and flip that pixel's decision (tests/test_eval_path.py::test_threshold_counts_from_logits bounds the
+        count difference by that band).  `add_sample` on probabilities is bit-exact everywhere."""
         self._accumulate(self._counts(y_true, logits, True), logits.numel())
 
     @property

@@ -166,6 +166,10 @@ class SiameseUNet(nn.Module):
 
 
 class DualTaskSiameseUNet(nn.Module):
+    # outc_sem_change is built (state_dict keys) but never called (reference networks.py:174, 176-197);
+    # parallel.wrap_ddp turns DDP's unused-parameter search on for it
+    PARAMS_OUTSIDE_FORWARD = ('outc_sem_change',)
+
     def __init__(self, cfg):
         super().__init__()
         _check_topology(cfg)

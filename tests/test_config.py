@@ -90,3 +90,22 @@ def test_criterion_registry():
         loss_functions.get_criterion('SoftDiceLoss')
     with pytest.raises(Exception, match='unknown loss'):
         loss_functions.get_criterion('Nope')
+
+
+def test_synthetic_mode_follows_the_split():
+    """SYNTHETIC unset: synthetic pairs only when no training AOIs are named (a reference config
+    carrying its split must not silently train on noise); an explicit True beside a split warns."""
+    import warnings
+    from multimodal_siamese_cd_amd.utils import datasets
+    cfg = em.load_cfg('baseline_siamese')
+    assert cfg.DATALOADER.SYNTHETIC is None and datasets.uses_synthetic_data(cfg)
+    cfg.DATASET.TRAINING_IDS = ['L15-0331E-1257N_1327_3160_13']
+    assert not datasets.uses_synthetic_data(cfg)
+    cfg.DATALOADER.SYNTHETIC = True
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        assert datasets.uses_synthetic_data(cfg)
+    assert any('synthetic noise' in str(x.message) for x in w)
+    cfg.DATALOADER.SYNTHETIC = False
+    cfg.DATASET.TRAINING_IDS = []
+    assert not datasets.uses_synthetic_data(cfg)

@@ -123,3 +123,116 @@ def test_ddp_gradient_average_world2():
     # every rank holds the identical averaged gradient
     for n in ref:
         assert torch.equal(res[0]['grads'][n], res[1]['grads'][n])
+
+
+# ---- DDP with a parameter outside the forward graph (DualTaskSiameseUNet.outc_sem_change) -------------------
+class OracleReplicaSpare(OracleReplica):
+    """As OracleReplica, plus a parameter forward never touches (the reference's outc_sem_change,
+    utils/networks.py:174); declared the way networks.DualTaskSiameseUNet declares it."""
+    PARAMS_OUTSIDE_FORWARD = ('spare',)
+
+    def __init__(self, P, B):
+        super().__init__(P, B)
+        self.spare = torch.nn.Linear(2, 1)
+
+
+def _worker_spare(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    parallel.init_distributed('gloo')
+    shapes = orc.param_shapes('siameseunet', CFG)
+    torch.manual_seed(0)
+    model = OracleReplicaSpare(orc.deterministic_params(shapes, 5), orc.fresh_buffers(shapes))
+    net = parallel.wrap_ddp(model, device=None)
+    assert net.find_unused_parameters
+    opt = torch.optim.AdamW(net.parameters(), lr=1e-3, weight_decay=0.01)
+    for step in range(2):  # the second step is where an unreduced bucket raises
+        b = orc.synthetic_batch(CFG, PER_RANK, HW, parallel.rank_seed(11 + step, rank))
+        opt.zero_grad()
+        orc.power_jaccard_loss(net(b['x_t1'], b['x_t2']), b['y_change']).backward()
+        opt.step()
+    assert model.spare.weight.grad is None
+    torch.save({n: p.detach().clone() for n, p in model.named_parameters()}, os.path.join(out_dir, f'rank{rank}.pt'))
+    torch.distributed.destroy_process_group()
+
+
+def test_wrap_ddp_unused_parameter_flag():
+    from multimodal_siamese_cd_amd.utils import networks
+    assert parallel.params_outside_forward(networks.DualTaskSiameseUNet) == ('outc_sem_change',)
+    assert parallel.params_outside_forward(networks.SiameseUNet) == ()
+
+
+@pytest.mark.timeout(300)
+def test_ddp_two_steps_with_unused_parameter_world2():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_spare, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+    for n in res[0]:  # replicas stay identical after two reduced steps
+        assert torch.equal(res[0][n], res[1][n]), n
+
+
+# ---- the evaluation path never shards (utils/evaluation.py runs on rank 0 over the whole split) -------------
+def _worker_eval_loader(rank, world, port, out_dir, root, aois):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    parallel.init_distributed('gloo')
+    from multimodal_siamese_cd_amd.utils import datasets, evaluation
+    ds = _eval_dataset(root, aois)
+    train_dl = datasets.DeviceDataLoader(ds, 1, torch.device('cpu'), shuffle=False, drop_last=False)
+    eval_dl = datasets.DeviceDataLoader(ds, 1, torch.device('cpu'), shuffle=False, drop_last=False,
+                                        distributed=False)
+    seen = {'train': [it[0]['aoi_id'] for it in train_dl.loader], 'eval': [it[0]['aoi_id'] for it in eval_dl.loader]}
+
+    captured = {}
+
+    class Stop(Exception):
+        pass
+
+    class Recorder(datasets.DeviceDataLoader):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            captured['n'] = len(self.loader)
+            raise Stop
+
+    orig = datasets.DeviceDataLoader
+    datasets.DeviceDataLoader = Recorder
+    try:
+        evaluation.model_evaluation(torch.nn.Identity(), ds.cfg, torch.device('cpu'), 'validation', 0, 0, dataset=ds)
+    except Stop:
+        pass
+    finally:
+        datasets.DeviceDataLoader = orig
+    seen['model_evaluation'] = captured['n']
+    torch.save(seen, os.path.join(out_dir, f'rank{rank}.pt'))
+    torch.distributed.destroy_process_group()
+
+
+def _eval_dataset(root, aois):
+    from multimodal_siamese_cd_amd.utils import datasets
+    from multimodal_siamese_cd_amd.utils import experiment_manager as em
+    cfg = em.load_cfg('baseline_siamese')
+    cfg.PATHS.DATASET = str(root)
+    cfg.DATASET.VALIDATION_IDS = list(aois)
+    cfg.DATALOADER.S2_BANDS = [2, 1, 0]
+    return datasets.MultimodalCDDataset(cfg, 'validation', no_augmentations=True, dataset_mode='first_last',
+                                        disable_multiplier=True, disable_unlabeled=True)
+
+
+@pytest.mark.timeout(300)
+def test_eval_loader_sees_whole_split_under_ddp(tmp_path):
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tools'))
+    import make_tile_cache
+    aois = make_tile_cache.make(str(tmp_path), aois=3, size=(40, 36), months=2)
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_eval_loader, args=(world, _free_port(), d, str(tmp_path), aois), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+    for r in range(world):
+        assert res[r]['eval'] == list(aois)          # every AOI, once, in order
+        assert res[r]['model_evaluation'] == len(aois)
+        assert len(res[r]['train']) == 2             # the training loader shards (3 AOIs padded to 2 per rank)
+    assert set(res[0]['train']) | set(res[1]['train']) == set(aois)

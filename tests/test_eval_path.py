@@ -120,13 +120,24 @@ def test_threshold_counts_bit_exact(dev, n, n_thr):
 @pytest.mark.gpu
 def test_threshold_counts_from_logits(dev):
     """Fused sigmoid: equal to counting sigmoid(logit) except where the probability sits within 2 ulp of a
-    threshold (the device expf and the CPU sigmoid may round differently there)."""
+    threshold (the device expf and the CPU sigmoid may round differently there).  The input includes 129 logits
+    straddling each threshold, so that band is populated and the bound is exercised, not vacuous."""
     from multimodal_siamese_cd_amd import hip
     rng = np.random.default_rng(5)
     n = 1 << 20
-    x = (rng.standard_normal(n) * 4).astype(np.float32)
-    y = (rng.random(n) > 0.8).astype(np.float32)
     thr = np.float32([0.5, 0.25, 0.75, 0.9])
+    # logits placed on the thresholds: logit(t) and its 64 fp32 neighbours either side (ADVICE r01)
+    edge = []
+    for t in thr.astype(np.float64):
+        x0 = np.float32(np.log(t / (1 - t)))
+        up, dn = [x0], [x0]
+        for _ in range(64):
+            up.append(np.nextafter(up[-1], np.float32(np.inf)))
+            dn.append(np.nextafter(dn[-1], np.float32(-np.inf)))
+        edge += up + dn[1:]
+    edge = np.array(edge, dtype=np.float32)
+    x = np.concatenate([(rng.standard_normal(n - edge.size) * 4).astype(np.float32), edge])
+    y = (rng.random(n) > 0.8).astype(np.float32)
     p = torch.sigmoid(torch.from_numpy(x)).numpy()
     counts = torch.empty(1 + 2 * thr.size, dtype=torch.int64, device=dev)
     ws = torch.empty(hip.threshold_counts_workspace_bytes(n, thr.size), dtype=torch.uint8, device=dev)
