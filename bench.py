@@ -38,8 +38,9 @@ from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, networ
 FP32_MFMA_PEAK_TFLOPS = 157.3
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # dense, MI355X_MICROARCH.md (1/16 ratio)
 X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6           # six bf16 products per fp32 multiply-add
+H2_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3           # three fp16 products (fp16 dense = bf16 dense)
 PEAKS = {'f32': FP32_MFMA_PEAK_TFLOPS, 'x3': X3_PEAK_TFLOPS, 'x5': BF16_MFMA_PEAK_TFLOPS / 5,
-         'bf16': BF16_MFMA_PEAK_TFLOPS}
+         'bf16': BF16_MFMA_PEAK_TFLOPS, 'h2': H2_PEAK_TFLOPS}
 METRIC = "image-pairs/sec training step, 256×256 SAR+optical Siamese U-Net, 1/2/4/8 MI355X"
 
 
@@ -85,7 +86,7 @@ class KernelTimer:
             if not timer.active:
                 return timer._igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k)
             arith = hip.igemm_arith(src, out_h, out_w, stride, taps, wpk, n_out, a[1] if len(a) > 1 else k['dst'],
-                                    a[2] if len(a) > 2 else k.get('store_mode', 0))
+                                    a[2] if len(a) > 2 else k.get('store_mode', 0), src_bound=k.get('src_bound'))
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             r = timer._igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k)
@@ -174,8 +175,8 @@ def main():
     ap.add_argument('--size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
-    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16'],
-                    help='conv arithmetic (default: from the config, engine.conv_math_for: MODEL.PRECISION fp32 -> x3)')
+    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16', 'h2'],
+                    help='conv arithmetic (default: from the config, engine.conv_math_for: MODEL.PRECISION fp32 -> h2)')
     args = ap.parse_args()
 
     rank, local_rank, world = parallel.init_distributed()
@@ -273,22 +274,26 @@ def main():
         flop_step = f3 + fT if cfg.MODEL.TYPE == 'siameseunet' else timer.launched_flops(reps)
         achieved = flop_step / (t_ms * 1e-3) / 1e12
         traffic = None
-        pmc = sorted(f for f in os.listdir(os.path.join(ROOT, 'profiles')) if f.endswith('_pmc_traffic.json'))
-        if pmc and args.config == 'baseline_siamese' and batch == 32 and size == 256 and math == 'x3':
-            with open(os.path.join(ROOT, 'profiles', pmc[-1])) as f:
+        pmc = []  # the latest round's PMC traffic of this workload and arithmetic (profiles/rNN_pmc_traffic.json)
+        for fn in sorted(f for f in os.listdir(os.path.join(ROOT, 'profiles')) if f.endswith('_pmc_traffic.json')):
+            with open(os.path.join(ROOT, 'profiles', fn)) as f:
                 tr = json.load(f)
+            if tr.get('math', 'x3') == math:
+                pmc.append((fn, tr))
+        if pmc and args.config == 'baseline_siamese' and batch == 32 and size == 256:
+            fn, tr = pmc[-1]
             traffic = {"bytes_per_step": round(tr['per_step_bytes']['total']),
                        "by_family": {k: round(v) for k, v in tr['per_step_bytes'].items() if k != 'total'},
-                       "source": f"profiles/{pmc[-1]}: {tr['source']}; L2-miss fabric bytes (Infinity-Cache "
+                       "source": f"profiles/{fn}: {tr['source']}; L2-miss fabric bytes (Infinity-Cache "
                                  "hits included, MI355X_MICROARCH.md HBM)"}
         peak, shares = timer.peak()
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "peak_basis": f"conv math {math}: share of executed conv FLOPs per arithmetic {shares} (peaks: x3 "
-                          f"{X3_PEAK_TFLOPS:.1f} = bf16 dense {BF16_MFMA_PEAK_TFLOPS:.1f} / 6 products, bf16 "
-                          f"{BF16_MFMA_PEAK_TFLOPS:.1f}, fp32 MFMA {FP32_MFMA_PEAK_TFLOPS}); combined flop-weighted "
-                          "harmonically",
+                          f"{X3_PEAK_TFLOPS:.1f} = bf16 dense {BF16_MFMA_PEAK_TFLOPS:.1f} / 6 products, h2 "
+                          f"{H2_PEAK_TFLOPS:.1f} = fp16 dense / 3 products, bf16 {BF16_MFMA_PEAK_TFLOPS:.1f}, fp32 MFMA "
+                          f"{FP32_MFMA_PEAK_TFLOPS}); combined flop-weighted harmonically",
             "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
             "kernel": "igemm + wgrad (all conv launches of one training step: 3x3 fwd/dgrad/wgrad, "
                       "ConvT fwd/dgrad/wgrad)",

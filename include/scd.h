@@ -106,7 +106,14 @@ int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, floa
  * Default: SCD_MATH_X3, or the SCD_CONV_MATH=f32|x3|x5|bf16 environment variable at first use.  Returns the
  * previous mode; SCD_MATH_QUERY only queries.  Process-wide (not per stream).
  * ------------------------------------------------------------------------------------------- */
-enum scd_conv_math { SCD_MATH_QUERY = -1, SCD_MATH_F32 = 0, SCD_MATH_X3 = 1, SCD_MATH_BF16 = 2, SCD_MATH_X5 = 3 };
+enum scd_conv_math {
+    SCD_MATH_QUERY = -1,
+    SCD_MATH_F32 = 0,
+    SCD_MATH_X3 = 1,
+    SCD_MATH_BF16 = 2,
+    SCD_MATH_X5 = 3,
+    SCD_MATH_H2 = 4
+};
 int scd_set_conv_math(int32_t mode);
 /* The arithmetic scd_conv_igemm / scd_conv_wgrad would use for this descriptor under the current mode:
  * SCD_MATH_F32, SCD_MATH_X3 or SCD_MATH_BF16; negative = invalid descriptor.  (Declared with the descriptors
@@ -127,6 +134,12 @@ int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t st
  * k = 16ks + 8(lane >> 5) + j (zero for n >= n_out), so one wave's B fragment is one 1 KB load. */
 size_t scd_split_frag_bytes(int32_t n_out, int32_t K);
 int scd_split_bf16x3_frag(const float *w, int32_t n_out, int32_t K, uint16_t *dst, scd_stream_t stream);
+/* SCD_MATH_H2 weight split of a packed [n_out][K] matrix into a buffer of scd_split_frag_bytes(n_out, K): per
+ * row r the power-of-two scale s_r that brings max_k |w[r][k]| below 2^15, the fp16 h and m planes of w * s_r in
+ * the fragment order above (planes 0 and 1), then float inv[NB * 32] = 1 / s_r after the planes (1 for padding
+ * rows).  scd_pack_conv3x3_multi writes this format instead of the bf16x3 split for 3x3 jobs whose K / 9 is a
+ * multiple of 32 while the mode is SCD_MATH_H2 (including the per-row scales of the data-grad layout). */
+int scd_split_h2_frag(const float *w, int32_t n_out, int32_t K, uint16_t *dst, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Implicit-GEMM convolution on MFMA (arithmetic: scd_set_conv_math).
@@ -184,6 +197,13 @@ typedef struct scd_igemm {
     /* Optional fused BatchNorm backward partial sums of the stored output (see scd_bn_bwd_tiles_t); only
      * where scd_igemm_bn_bwd_tiles() reports > 0 tiles.  NULL = off. */
     const scd_bn_bwd_tiles_t *bn_bwd;
+    /* SCD_MATH_H2 only: device float holding an upper bound U >= |every src element as read| (after the input
+     * transform).  A 3x3 conv with src.c % 32 == 0 then runs the two-term fp16 split: src scaled by the power of
+     * two that brings U below 2^15, weights from the h2 split of wsplit (scd_pack_conv3x3_multi /
+     * scd_split_h2_frag), both scales undone exactly in the epilogue.  A bound below the true maximum overflows
+     * fp16 (inf / NaN outputs); a loose one only lowers the absolute floor (2^-39 U).  NULL = the x3 kernels
+     * (per-tap, fp32 weights split on the fly). */
+    const float *src_bound;
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);
@@ -217,6 +237,10 @@ typedef struct scd_wgrad {
     const float *src_scale;
     const float *src_shift;
     int32_t src_nseg;
+    /* SCD_MATH_H2 only: device floats bounding |rows| and |src| (as read, after the src transform), as
+     * scd_igemm_t.src_bound.  With both set the 16x16x32 halo weight grad runs the fp16 two-term split; else x3. */
+    const float *rows_bound;
+    const float *src_bound;
 } scd_wgrad_t;
 
 /* Number of K-splits the library will use and the slab bytes it needs. */
@@ -244,9 +268,13 @@ size_t scd_bn_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t c, int32_
 /* Batch statistics of y per segment -> save_mean/save_invstd [nseg][C], scale/shift [nseg][C]
  * (scale = gamma*invstd, shift = beta - mean*scale).  If update_running != 0 the running buffers are
  * updated once per segment in segment order: r = (1-momentum)*r + momentum*stat (unbiased var). */
+/* act_bound (optional, device float, caller-zeroed or holding an earlier bound): raised to an upper bound of
+ * |relu(y * scale + shift)| over every segment -- |gamma| sqrt(n - 1) + |beta| per channel and segment of n values
+ * (a value lies within sqrt(n - 1) standard deviations of its mean), plus rounding slack.  No pass over y.
+ * The operand bound of the SCD_MATH_H2 convs reading this activation (scd_igemm_t.src_bound). */
 int scd_bn_train_stats(scd_nhwc_t y, int32_t nseg, const float *gamma, const float *beta, float eps,
                        float momentum, int32_t update_running, float *running_mean, float *running_var,
-                       float *save_mean, float *save_invstd, float *scale, float *shift, void *ws,
+                       float *save_mean, float *save_invstd, float *scale, float *shift, float *act_bound, void *ws,
                        size_t ws_bytes, scd_stream_t stream);
 /* Same outputs as scd_bn_train_stats, from the conv-fused tile records of scd_conv_igemm (stat_rec):
  * ntiles tiles of tile_pixels pixels each, image-major, split evenly into nseg segments. */
@@ -254,10 +282,16 @@ size_t scd_bn_tile_stats_workspace_bytes(int32_t ntiles, int32_t c, int32_t nseg
 int scd_bn_stats_from_tiles(const float *tile_rec, int32_t ntiles, int32_t tile_pixels, int32_t c, int32_t nseg,
                             const float *gamma, const float *beta, float eps, float momentum, int32_t update_running,
                             float *running_mean, float *running_var, float *save_mean, float *save_invstd,
-                            float *scale, float *shift, void *ws, size_t ws_bytes, scd_stream_t stream);
+                            float *scale, float *shift, float *act_bound, void *ws, size_t ws_bytes,
+                            scd_stream_t stream);
 /* Eval: scale/shift [C] from running statistics. */
 int scd_bn_eval_coeffs(int32_t c, const float *gamma, const float *beta, const float *running_mean,
                        const float *running_var, float eps, float *scale, float *shift, scd_stream_t stream);
+/* *bound = max(*bound, max |v|) over the view (atomic integer max on the float bits: order-independent), v = x, or
+ * relu(x * scale[g][c] + shift[g][c]) per segment g when scale/shift are given.  The caller zeroes *bound first.
+ * The SCD_MATH_H2 operand bound where no producer supplies one (eval-mode BatchNorm, the decoder's upsampled half). */
+int scd_absmax_bound(scd_nhwc_t x, int32_t nseg, const float *scale, const float *shift, float *bound,
+                     scd_stream_t stream);
 /* a = max(y*scale[seg] + shift[seg], 0); nseg = 1 with [C] coefficients in eval mode. */
 int scd_bn_relu_apply(scd_nhwc_t y, int32_t nseg, const float *scale, const float *shift, scd_nhwc_t a,
                       scd_stream_t stream);
@@ -268,8 +302,10 @@ int scd_bn_relu_apply(scd_nhwc_t y, int32_t nseg, const float *scale, const floa
  * replaces: native_batch_norm_backward + threshold_backward (+ the conv bias-grad reduction). */
 int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
                          const float *save_invstd, const float *gamma, const float *scale, const float *shift,
-                         float *dgamma, float *dbeta, float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes,
-                         scd_stream_t stream);
+                         float *dgamma, float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws,
+                         size_t ws_bytes, scd_stream_t stream);
+/* dy_bound (optional, all three backward forms): *dy_bound = max(*dy_bound, max |dy|) as dy is written (the
+ * SCD_MATH_H2 bound of the data-grad / weight-grad convs reading dy; caller-zeroed). */
 
 /* scd_bn_relu_backward with the incoming gradient formed on the fly instead of read from a tensor:
  *   da[img] = maxpool_bwd(gy, idx)[img] (if gy.data)  -/+ gskip[img % gskip.n] (skip_mode 1: t1 images
@@ -280,14 +316,15 @@ int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float 
 int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip,
                                 int32_t skip_mode, int32_t nseg, const float *save_mean, const float *save_invstd,
                                 const float *gamma, const float *scale, const float *shift, float *dgamma,
-                                float *dbeta, float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes,
-                                scd_stream_t stream);
+                                float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws,
+                                size_t ws_bytes, scd_stream_t stream);
 /* scd_bn_relu_backward with the partial sums taken from conv-epilogue tile records (scd_bn_bwd_tiles_t.rec,
  * ntiles tiles, image-major, split evenly into nseg segments) instead of a pass over (y, da). */
 int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
                                const float *save_invstd, const float *gamma, const float *scale, const float *shift,
                                const float *tile_rec, int32_t ntiles, float *dgamma, float *dbeta,
-                               float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes, scd_stream_t stream);
+                               float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws, size_t ws_bytes,
+                               scd_stream_t stream);
 
 /* out[c] = sum over all pixels of x[., c] (ConvTranspose2d bias grad, networks.py:433); workspace as
  * scd_bn_workspace_bytes(n, h, w, c, 1).  replaces: the bias-grad reduction of convolution_backward. */

@@ -28,15 +28,29 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in deps())
 
 
-def build_lib(force: bool = False, verbose: bool = True) -> str:
+def build_lib(force: bool = False, verbose: bool = True, jobs: int | None = None) -> str:
+    """One object per translation unit, compiled in parallel (the units share no device code), then linked."""
     if not force and up_to_date():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    objdir = os.path.join(os.path.dirname(OUT), 'obj')
+    os.makedirs(objdir, exist_ok=True)
+    cflags = [f for f in FLAGS if f != '-shared']
+    procs, objs = [], []
+    jobs = jobs or min(8, os.cpu_count() or 1)
+    for src in sources():
+        obj = os.path.join(objdir, os.path.basename(src) + '.o')
+        objs.append(obj)
+        cmd = [HIPCC, *cflags, '-c', '-o', obj, src]
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+        while sum(p.poll() is None for p in procs) >= jobs:
+            procs[[p.poll() is None for p in procs].index(True)].wait()
+    if any(p.wait() != 0 for p in procs):
+        raise RuntimeError('hipcc failed (see the compiler output above)')
     tmp = OUT + '.tmp'
-    cmd = [HIPCC, *FLAGS, '-o', tmp, *sources()]
-    if verbose:
-        print(' '.join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    subprocess.run([HIPCC, *FLAGS, '-o', tmp, *objs], check=True)
     os.replace(tmp, OUT)
     return OUT
 

@@ -50,6 +50,10 @@ static BnGeom bn_geom(const scd_nhwc_t &y, int nseg) {
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4 ld4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
+__device__ __forceinline__ f4 fabs4(f4 v) { return f4{fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)}; }
+__device__ __forceinline__ f4 fmax4(f4 a, f4 b) {
+    return f4{fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)};
+}
 __device__ __forceinline__ void st4(float *p, f4 v) { *reinterpret_cast<f4 *>(p) = v; }
 // Keep a batch of loads in flight: an opaque use of the loaded registers right after issuing them stops
 // hipcc from sinking each load next to its consumer (which serialised the loop at vmcnt(0) per load).
@@ -180,12 +184,22 @@ __device__ __forceinline__ void dmerge(DWelford &a, const DWelford &b) {
     a.n = n;
 }
 
+// Upper bound of |relu(fma(y, scale, shift))| over the n values of one segment and channel, from the statistics
+// alone (SCD_MATH_H2 operand scaling): every value lies within sqrt(n - 1) population standard deviations of the
+// mean, and scale = gamma * invstd with invstd <= 1 / std, so |scale * (y - mean)| <= |gamma| sqrt(n - 1).  The
+// slack terms cover the rounding of the statistics and of the fma (relative 2^-20 of each addend).
+__device__ __forceinline__ float bn_act_bound(double n, double gamma, double beta, double shift) {
+    const double dev = fabs(gamma) * sqrt(n > 1 ? n - 1 : 0.0);
+    return float((dev + fabs(beta)) * (1.0 + 0x1p-10) + (fabs(shift) + fabs(beta)) * 0x1p-16);
+}
+
 // one workgroup per channel; segments in order (t1 first), running stats updated once per segment
 __global__ __launch_bounds__(BN_THREADS) void bn_stats_finalize(const float *__restrict__ rec, int C, int nseg,
                                                                 int ncps, int nrec, const float *gamma,
                                                                 const float *beta, float eps, float momentum,
                                                                 int update, float *rmean, float *rvar, float *smean,
-                                                                float *sinv, float *scale, float *shift) {
+                                                                float *sinv, float *scale, float *shift,
+                                                                float *act_bound) {
     __shared__ DWelford sh[BN_THREADS];
     const int c = blockIdx.x;
     const int t = threadIdx.x;
@@ -216,6 +230,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_finalize(const float *__r
             const float sc = float(g * inv);
             scale[s * C + c] = sc;
             shift[s * C + c] = float(b - a.mean * double(sc));
+            if (act_bound) atomic_max_bound(act_bound, bn_act_bound(a.n, g, b, double(shift[s * C + c])));
             if (update) {
                 const double uvar = a.n > 1 ? a.m2 / (a.n - 1) : var;
                 rmean[c] = float((1.0 - momentum) * rmean[c] + momentum * a.mean);
@@ -443,13 +458,14 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
                                                            int ncps, int chunk, int nrec, int qpb, const float *smean,
                                                            const float *sinv, const float *gamma, const float *scale,
                                                            const float *shift, const float *coef,
-                                                           float *__restrict__ brec) {
+                                                           float *__restrict__ brec, float *dy_bound) {
     __shared__ f4 sh[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
     const int c = (blockIdx.y * qpb + q) * 4;
     const Chunk ch = chunk_of(pseg, ncps, chunk);
     f4 acc = {0.f, 0.f, 0.f, 0.f};
+    f4 amax = acc;  // max |dy| of this thread (dy_bound)
     if (c < C) {
         const int o = ch.seg * C + c;
         const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
@@ -475,14 +491,17 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
             st4(dy + (p + 2 * npl) * lddy + c, o2);
             st4(dy + (p + 3 * npl) * lddy + c, o3);
             acc += (o0 + o1) + (o2 + o3);
+            if (dy_bound) amax = fmax4(amax, fmax4(fmax4(fabs4(o0), fabs4(o1)), fmax4(fabs4(o2), fabs4(o3))));
         }
         for (; p < ch.end; p += npl) {
             const f4 y0 = ld4(y + p * ldy + c);
             const f4 o0 = mul * (relu_mask(y0, sc, sf, da(p, c)) - k1 - ((y0 - mu) * iv) * k2);
             st4(dy + p * lddy + c, o0);
             acc += o0;
+            if (dy_bound) amax = fmax4(amax, fabs4(o0));
         }
     }
+    if (dy_bound) wave_max_bound(dy_bound, fmaxf(fmaxf(amax.x, amax.y), fmaxf(amax.z, amax.w)));
     if (!brec) return;  // uniform
     sh[tid] = acc;
     __syncthreads();
@@ -609,8 +628,8 @@ extern "C" size_t scd_bn_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_
 
 extern "C" int scd_bn_train_stats(scd_nhwc_t y, int32_t nseg, const float *gamma, const float *beta, float eps,
                                   float momentum, int32_t update_running, float *running_mean, float *running_var,
-                                  float *save_mean, float *save_invstd, float *scale, float *shift, void *ws,
-                                  size_t ws_bytes, scd_stream_t stream) {
+                                  float *save_mean, float *save_invstd, float *scale, float *shift, float *act_bound,
+                                  void *ws, size_t ws_bytes, scd_stream_t stream) {
     clear_error();
     SCD_TRY(bn_check(y, nseg));
     if (!save_mean || !save_invstd || !scale || !shift || (update_running && (!running_mean || !running_var))) {
@@ -628,7 +647,7 @@ extern "C" int scd_bn_train_stats(scd_nhwc_t y, int32_t nseg, const float *gamma
                        static_cast<const float *>(y.data), y.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, rec);
     hipLaunchKernelGGL(bn_stats_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, gamma,
                        beta, eps, momentum, update_running, running_mean, running_var, save_mean, save_invstd, scale,
-                       shift);
+                       shift, act_bound);
     return launch_status("scd_bn_train_stats");
 }
 
@@ -648,8 +667,8 @@ extern "C" size_t scd_bn_tile_stats_workspace_bytes(int32_t ntiles, int32_t c, i
 extern "C" int scd_bn_stats_from_tiles(const float *tile_rec, int32_t ntiles, int32_t tile_pixels, int32_t c,
                                        int32_t nseg, const float *gamma, const float *beta, float eps, float momentum,
                                        int32_t update_running, float *running_mean, float *running_var,
-                                       float *save_mean, float *save_invstd, float *scale, float *shift, void *ws,
-                                       size_t ws_bytes, scd_stream_t stream) {
+                                       float *save_mean, float *save_invstd, float *scale, float *shift,
+                                       float *act_bound, void *ws, size_t ws_bytes, scd_stream_t stream) {
     clear_error();
     if (!tile_rec || ntiles < 1 || tile_pixels < 1 || c < 1 || nseg < 1 || ntiles % nseg || !save_mean ||
         !save_invstd || !scale || !shift || (update_running && (!running_mean || !running_var))) {
@@ -668,7 +687,8 @@ extern "C" int scd_bn_stats_from_tiles(const float *tile_rec, int32_t ntiles, in
     hipLaunchKernelGGL(bn_tile_merge, dim3(nrec, (c + BN_THREADS - 1) / BN_THREADS), dim3(BN_THREADS), 0, s, tile_rec,
                        c, tps, group, ncps, nrec, float(tile_pixels), rec);
     hipLaunchKernelGGL(bn_stats_finalize, dim3(c), dim3(BN_THREADS), 0, s, rec, c, nseg, ncps, nrec, gamma, beta, eps,
-                       momentum, update_running, running_mean, running_var, save_mean, save_invstd, scale, shift);
+                       momentum, update_running, running_mean, running_var, save_mean, save_invstd, scale, shift,
+                       act_bound);
     return launch_status("scd_bn_stats_from_tiles");
 }
 
@@ -709,7 +729,7 @@ namespace scd {
 template <class DA>
 static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *save_mean, const float *save_invstd,
                             const float *gamma, const float *scale, const float *shift, float *dgamma, float *dbeta,
-                            float *dbias_prev, const scd_nhwc_t &dy, void *ws, hipStream_t s) {
+                            float *dbias_prev, const scd_nhwc_t &dy, float *dy_bound, void *ws, hipStream_t s) {
     const BnGeom g = bn_geom(y, nseg);
     float *rec = static_cast<float *>(ws);
     float *brec = rec + size_t(g.nrec) * y.c * 2;
@@ -722,7 +742,7 @@ static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *s
     hipLaunchKernelGGL(bn_bwd_apply<DA>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        static_cast<const float *>(y.data), y.ldc, da, static_cast<float *>(dy.data), dy.ldc, y.c,
                        g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
-                       dbias_prev ? brec : nullptr);
+                       dbias_prev ? brec : nullptr, dy_bound);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
 }
 }  // namespace scd
@@ -730,7 +750,7 @@ static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *s
 extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
                                     const float *save_invstd, const float *gamma, const float *scale,
                                     const float *shift, float *dgamma, float *dbeta, float *dbias_prev,
-                                    scd_nhwc_t dy, void *ws, size_t ws_bytes, scd_stream_t stream) {
+                                    scd_nhwc_t dy, float *dy_bound, void *ws, size_t ws_bytes, scd_stream_t stream) {
     clear_error();
     SCD_TRY(bn_check(y, nseg));
     SCD_TRY(check_view(da, "bn_bwd.da"));
@@ -745,7 +765,7 @@ extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, c
         return SCD_ERR_WORKSPACE;
     }
     bn_backward_run(y, DaPlain{static_cast<const float *>(da.data), da.ldc}, nseg, save_mean, save_invstd, gamma, scale,
-                    shift, dgamma, dbeta, dbias_prev, dy, ws, as_stream(stream));
+                    shift, dgamma, dbeta, dbias_prev, dy, dy_bound, ws, as_stream(stream));
     return launch_status("scd_bn_relu_backward");
 }
 
@@ -753,7 +773,7 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
                                            int32_t skip_mode, int32_t nseg, const float *save_mean,
                                            const float *save_invstd, const float *gamma, const float *scale,
                                            const float *shift, float *dgamma, float *dbeta, float *dbias_prev,
-                                           scd_nhwc_t dy, void *ws, size_t ws_bytes, scd_stream_t stream) {
+                                           scd_nhwc_t dy, float *dy_bound, void *ws, size_t ws_bytes, scd_stream_t stream) {
     clear_error();
     SCD_TRY(bn_check(y, nseg));
     SCD_TRY(check_view(gy, "bn_bwd_pooled.gy", true));
@@ -794,15 +814,15 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
     da.div_hw = make_fastdiv(uint32_t(y.h * y.w));
     da.div_w = make_fastdiv(uint32_t(y.w));
     da.div_gsn = make_fastdiv(uint32_t(da.gsn));
-    bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy, ws,
-                    as_stream(stream));
+    bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy, dy_bound,
+                    ws, as_stream(stream));
     return launch_status("scd_bn_relu_backward_pooled");
 }
 
 extern "C" int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
                                           const float *save_invstd, const float *gamma, const float *scale,
                                           const float *shift, const float *tile_rec, int32_t ntiles, float *dgamma,
-                                          float *dbeta, float *dbias_prev, scd_nhwc_t dy, void *ws, size_t ws_bytes,
+                                          float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws, size_t ws_bytes,
                                           scd_stream_t stream) {
     clear_error();
     SCD_TRY(bn_check(y, nseg));
@@ -828,7 +848,7 @@ extern "C" int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t n
     hipLaunchKernelGGL(bn_bwd_apply<DaPlain>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        static_cast<const float *>(y.data), y.ldc, DaPlain{static_cast<const float *>(da.data), da.ldc},
                        static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean,
-                       save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr);
+                       save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr, dy_bound);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
     return launch_status("scd_bn_relu_backward_tiles");
 }
@@ -842,4 +862,41 @@ extern "C" int scd_channel_sum(scd_nhwc_t x, float *out, void *ws, size_t ws_byt
     }
     SCD_TRY(weighted_channel_sum(x, nullptr, 1, 0, out, ws, ws_bytes, as_stream(stream)));
     return launch_status("scd_channel_sum");
+}
+
+namespace scd {
+// bound = max(bound, max |v|) over an NHWC view, v = x or relu(fma(x, scale[g][c], shift[g][c])) (g = segment).
+__global__ __launch_bounds__(256) void absmax_bound_kernel(const float *__restrict__ x, int ldx, int C, int64_t pseg,
+                                                           const float *__restrict__ scale,
+                                                           const float *__restrict__ shift, float *bound) {
+    const int seg = blockIdx.y;
+    const int cq = C / 4;
+    const int64_t total = pseg * cq;
+    f4 m = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t p = seg * pseg + e / cq;
+        const int c = int(e % cq) * 4;
+        f4 v = ld4(x + p * ldx + c);
+        if (scale) v = bn_relu4(v, ld4(scale + seg * C + c), ld4(shift + seg * C + c));
+        m = fmax4(m, fabs4(v));
+    }
+    wave_max_bound(bound, fmaxf(fmaxf(m.x, m.y), fmaxf(m.z, m.w)));
+}
+}  // namespace scd
+
+extern "C" int scd_absmax_bound(scd_nhwc_t x, int32_t nseg, const float *scale, const float *shift, float *bound,
+                                scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(bn_check(x, nseg));
+    if (!bound || (!scale) != (!shift) || (scale && (!aligned16(scale) || !aligned16(shift)))) {
+        set_error("absmax_bound: null bound or unpaired / unaligned coefficients");
+        return SCD_ERR_ARG;
+    }
+    const int64_t pseg = pixels(x) / nseg;
+    const int64_t total = pseg * (x.c / 4);
+    int blocks = int((total + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(absmax_bound_kernel, dim3(blocks, nseg), dim3(256), 0, as_stream(stream),
+                       static_cast<const float *>(x.data), x.ldc, x.c, pseg, scale, shift, bound);
+    return launch_status("scd_absmax_bound");
 }

@@ -73,6 +73,19 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
     return (__umulhi(n, f.mul) + n) >> f.shr;
 }
 
+// Magnitude bounds (SCD_MATH_H2 operand scaling): a non-negative float's bits order as unsigned integers, so an
+// integer atomic max keeps max(*bound, v) whatever the arrival order (deterministic).  NaN compares above +inf.
+__device__ __forceinline__ void atomic_max_bound(float *bound, float v) {
+    atomicMax(reinterpret_cast<unsigned int *>(bound), __float_as_uint(fabsf(v)));
+}
+// Max of v over the wave, then one atomic from lane 0.
+__device__ __forceinline__ void wave_max_bound(float *bound, float v) {
+    v = fabsf(v);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    if ((threadIdx.x & 63) == 0) atomic_max_bound(bound, v);
+}
+
 // Device-side NHWC element pointer helpers.
 struct View {
     float *p;

@@ -84,6 +84,9 @@ struct IgemmArgs {
     int bb_ldy, bb_seg_imgs, bb_ntiles;
     const float *bb_mean, *bb_inv, *bb_scale, *bb_shift;
     float *bb_rec;
+    // SCD_MATH_H2: device pointer to an upper bound of |src| as the kernel reads it (after the input transform);
+    // the weight planes in wsplit are then the fp16 two-term split with per-row inverse scales (h2_wsplit_bytes)
+    const float *src_bound;
 };
 
 struct WgradArgs {
@@ -101,6 +104,7 @@ struct WgradArgs {
     FastDiv div_hw, div_w, div_c;
     const float *src_scale, *src_shift;  // optional fused src BN-apply + ReLU (halo16 weight grad only)
     int src_seg_imgs;
+    const float *rows_bound, *src_bound;  // SCD_MATH_H2: upper bounds of |rows| and |src| (as read), both or neither
 };
 
 // Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels
@@ -119,7 +123,7 @@ bool igemm_takes_c16(const IgemmArgs &a);  // igemm_halo16_c16 (16-channel sourc
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
 // 16x16x32-MFMA halo weight grad (conv_halo16.hip), selected by wgrad16_mode() (scd_set_wgrad16).
 int wgrad16_mode();
-const void *wgrad_halo16_fn();
+const void *wgrad_halo16_fn(bool bounded);  // bounded: h2 under SCD_MATH_H2
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
 // 16-channel-source variant (the input layer), same eligibility otherwise (conv_halo16.hip).
 const void *wgrad_halo16_c16_fn();
@@ -128,13 +132,18 @@ void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s);
 const void *wgrad_x3_fn(int tile_id);
 void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
 // Halo weight grad (3x3 / stride 1 / same size, R and C multiples of 64, maps in 2x16 patches).
-const void *wgrad_halo_fn();
+const void *wgrad_halo_fn(bool bounded);
 void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
 
 // Conv math selection (scd_set_conv_math): SCD_MATH_X3 = split-bf16 MFMA where the shape allows it,
 // SCD_MATH_F32 = fp32 MFMA everywhere, SCD_MATH_BF16 = the x3 pipeline with one bf16 term per operand in the
 // 16x16x32 halo kernels.  Initial value from SCD_CONV_MATH=f32|x3|bf16 (default x3).
-int conv_math_x3();      // split-weight (x3 or bf16) pipeline
-int conv_math_planes();  // halo16 kernel arithmetic: 3 (x3), 5 (x5: x3 less one product), 1 (bf16)
+int conv_math_x3();      // split-weight (x3, x5, bf16 or h2) pipeline
+int conv_math_mode();    // the SCD_MATH_* mode
+// halo16 kernel arithmetic: 3 (x3), 5 (x5: x3 less one product), 1 (bf16), 2 (h2: two-term fp16 split)
+int conv_math_planes();
+// SCD_MATH_H2 weight splits exist for 3x3 convs whose source channels are a multiple of 32 (the halo16 kernels'
+// shapes); every other conv keeps the x3 split.  wsplit of such a conv is in the h2 format.
+inline bool h2_weight_format(int ntaps, int c) { return conv_math_mode() == SCD_MATH_H2 && ntaps == 9 && c % 32 == 0; }
 
 }  // namespace scd

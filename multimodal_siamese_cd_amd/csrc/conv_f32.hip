@@ -469,12 +469,13 @@ static int check_taps(int ntaps, const int8_t *dy, const int8_t *dx) {
 
 static int g_conv_math = -1;
 
-static int conv_math_mode() {
+int conv_math_mode() {
     if (g_conv_math < 0) {
         const char *e = getenv("SCD_CONV_MATH");
         g_conv_math = (e && e[0] == 'f')                   ? SCD_MATH_F32
                       : (e && e[0] == 'b')                 ? SCD_MATH_BF16
                       : (e && e[0] == 'x' && e[1] == '5') ? SCD_MATH_X5
+                      : (e && e[0] == 'h' && e[1] == '2') ? SCD_MATH_H2
                                                            : SCD_MATH_X3;
     }
     return g_conv_math;
@@ -482,7 +483,7 @@ static int conv_math_mode() {
 int conv_math_x3() { return conv_math_mode() != SCD_MATH_F32; }
 int conv_math_planes() {
     const int m = conv_math_mode();
-    return m == SCD_MATH_BF16 ? 1 : m == SCD_MATH_X5 ? 5 : 3;
+    return m == SCD_MATH_BF16 ? 1 : m == SCD_MATH_X5 ? 5 : m == SCD_MATH_H2 ? 2 : 3;
 }
 
 }  // namespace scd
@@ -492,7 +493,8 @@ using namespace scd;
 extern "C" int scd_set_conv_math(int32_t mode) {
     clear_error();
     const int prev = conv_math_mode();
-    if (mode == SCD_MATH_F32 || mode == SCD_MATH_X3 || mode == SCD_MATH_BF16 || mode == SCD_MATH_X5) {
+    if (mode == SCD_MATH_F32 || mode == SCD_MATH_X3 || mode == SCD_MATH_BF16 || mode == SCD_MATH_X5 ||
+        mode == SCD_MATH_H2) {
         g_conv_math = mode;
     } else if (mode != SCD_MATH_QUERY) {
         set_error("scd_set_conv_math: mode %d", mode);
@@ -607,6 +609,7 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
         const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * 4 + int64_t(d->src.c) * 4;
         a.src_bytes = sb < (int64_t(1) << 31) ? uint32_t(sb) : 0u;
     }
+    a.src_bound = d->src_bound;
     if (d->wsplit && !aligned16(d->wsplit)) {
         set_error("igemm: wsplit must be 16-byte aligned");
         return SCD_ERR_ALIGN;
@@ -727,7 +730,8 @@ extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
     IgemmArgs a;
     SCD_TRY(igemm_query_prepare(d, a));
     if (!conv_math_x3()) return SCD_MATH_F32;
-    if (igemm_takes_halo16(a) || igemm_takes_c16(a)) return conv_math_mode();
+    if (igemm_takes_halo16(a)) return conv_math_mode();  // under SCD_MATH_H2 only bounded h2-split convs take it
+    if (igemm_takes_c16(a)) return conv_math_mode() == SCD_MATH_H2 ? SCD_MATH_X3 : conv_math_mode();
     return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
 }
 
@@ -858,7 +862,10 @@ static int wgrad_resident_blocks(const WgradTile &t) {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, t.threads, 0) != hipSuccess || per_cu < 1 ||
         cus < 1) {
         (void)hipGetLastError();
-        return 2 * 256;  // MI355X: 256 CUs, >= 2 resident 256-thread blocks
+        // MI355X: 256 CUs, >= 2 resident 256-thread blocks; cached like a successful query so the split plan
+        // (scd_wgrad_plan) and the launch never disagree
+        cache[x3][t.id] = 2 * 256;
+        return cache[x3][t.id];
     }
     cache[x3][t.id] = per_cu * cus;
     return cache[x3][t.id];
@@ -911,21 +918,27 @@ static bool wgrad_c16_ok(const scd_wgrad_t *d) {
     return wgrad_halo_shape(d) && d->src.c == 16 && wgrad16_mode() && !(e && e[0] == '0');
 }
 
-static int wgrad_halo_resident(bool c16 = false) {
-    // per halo weight-grad kernel: 32x32x16; 16x16x32 x3 / x5 / bf16; 16-channel x3 / x5 / bf16
-    static int caches[7] = {0, 0, 0, 0, 0, 0, 0};
-    const int planes = conv_math_planes() == 1 ? 0 : conv_math_planes() == 5 ? 1 : 2;
-    int &cache = caches[c16 ? 4 + planes : wgrad16_mode() ? 1 + planes : 0];
+// Both operands bounded: the h2 weight grad under SCD_MATH_H2 (x3 otherwise).
+static bool wgrad_bounded(const scd_wgrad_t *d) { return d->rows_bound && d->src_bound; }
+
+static int wgrad_halo_resident(bool c16, bool bounded) {
+    // per halo weight-grad kernel: 32x32x16; 16x16x32 x3 / x5 / bf16 / h2; 16-channel x3 / x5 / bf16
+    static int caches[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const int m = conv_math_planes();
+    const int planes = m == 1 ? 0 : m == 5 ? 1 : (m == 2 && bounded && !c16) ? 3 : 2;
+    int &cache = caches[c16 ? 5 + planes : wgrad16_mode() ? 1 + planes : 0];
     if (cache > 0) return cache;
     int per_cu = 0, cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c16 ? wgrad_halo16_c16_fn() : wgrad_halo_fn(), 256, 0) !=
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c16 ? wgrad_halo16_c16_fn() : wgrad_halo_fn(bounded),
+                                                     256, 0) !=
             hipSuccess ||
         per_cu < 1 ||
         cus < 1) {
         (void)hipGetLastError();
-        return 2 * 256;
+        cache = 2 * 256;  // cached: plan and launch must see the same capacity
+        return cache;
     }
     cache = per_cu * cus;
     return cache;
@@ -936,7 +949,7 @@ static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
         const bool c16 = !wgrad_halo_ok(d);
         const int64_t patches = pixels(d->rows) / 32;
         const int64_t tiles = int64_t(d->rows.c / 64) * (c16 ? 1 : d->src.c / 64);
-        split_units(patches, tiles, wgrad_halo_resident(c16), 8, 1, nsplit, kchunk);
+        split_units(patches, tiles, wgrad_halo_resident(c16, wgrad_bounded(d)), 8, 1, nsplit, kchunk);
         return;
     }
     const int Ng = d->ntaps * d->src.c;
@@ -960,7 +973,10 @@ extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
     if (!conv_math_x3()) return SCD_MATH_F32;
-    return ((wgrad_halo_ok(d) && wgrad16_mode()) || wgrad_c16_ok(d)) ? conv_math_mode() : SCD_MATH_X3;
+    if (wgrad_halo_ok(d) && wgrad16_mode())
+        return conv_math_mode() == SCD_MATH_H2 && !wgrad_bounded(d) ? SCD_MATH_X3 : conv_math_mode();
+    if (wgrad_c16_ok(d)) return conv_math_mode() == SCD_MATH_H2 ? SCD_MATH_X3 : conv_math_mode();
+    return SCD_MATH_X3;
 }
 
 namespace scd {
@@ -1081,6 +1097,8 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     a.src_scale = d->src_scale;
     a.src_shift = d->src_shift;
     a.src_seg_imgs = d->src.n;
+    a.rows_bound = d->rows_bound;
+    a.src_bound = d->src_bound;
     if (d->src_scale || d->src_shift) {
         if (!d->src_scale || !d->src_shift || d->src_nseg < 1 || d->src.n % d->src_nseg ||
             !aligned16(d->src_scale) || !aligned16(d->src_shift) || !wgrad_src_bn_ok(d)) {

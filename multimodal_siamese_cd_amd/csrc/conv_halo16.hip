@@ -45,7 +45,10 @@ __device__ __forceinline__ void gstore4(float *p, f32x4 v) { *(__attribute__((ad
 // current chunk (its loads were issued at the chunk's first tap), so a chunk end costs one barrier and the
 // split/store work overlaps the MFMAs instead of stalling between two barriers.
 // NP selects the arithmetic: 3 = the exact x3 split (six products per step), 5 = x3 without the w_l * x_h product
-// (SCD_MATH_X5: weights in two planes, five products), 1 = bf16 operands (SCD_MATH_BF16: the h terms, one product).
+// (SCD_MATH_X5: weights in two planes, five products), 1 = bf16 operands (SCD_MATH_BF16: the h terms, one product),
+// 2 = the two-term fp16 split (SCD_MATH_H2, x3_common.h: three v_mfma_f32_16x16x32_f16 products; the halo is
+// scaled by the power of two of *src_bound while staged, the weights come pre-scaled per output channel, and the
+// epilogue multiplies both inverse scales back out -- exact, powers of two).
 template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
     constexpr int NT = 64 * WAVES_M * WAVES_N;
@@ -59,10 +62,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     constexpr int PA = HR * 64;
     constexpr int RED = 2 * WAVES_M * BN * 4;
     constexpr int NBUF = DB ? 2 : 1;
-    static_assert(NP == 1 || NP == 3 || NP == 5, "x3, x5 or bf16");
-    constexpr int XP = NP == 1 ? 1 : 3;               // activation planes (LDS)
-    constexpr int WP = NP == 1 ? 1 : NP == 5 ? 2 : 3;  // weight planes (registers)
+    static_assert(NP == 1 || NP == 2 || NP == 3 || NP == 4 || NP == 5, "x3, x5, bf16 or h2");
+    constexpr bool H2 = NP == 2 || NP == 4;  // 4: h2 with the activations' low term pre-scaled (x3_common.h)
+    constexpr int XP = NP == 1 ? 1 : H2 ? 2 : 3;               // activation planes (LDS)
+    constexpr int WP = NP == 1 ? 1 : (NP == 5 || H2) ? 2 : 3;  // weight planes (registers)
     __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * XP * PA > RED ? NBUF * XP * PA : RED];
+    float xs = 1.f, xs_inv = 1.f;  // h2: power-of-two scale of the staged activations and its inverse
+    if constexpr (H2) h2_scale(*a.src_bound, xs, xs_inv);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     f32x4 ra[A_PER];
     f32x4 in_sc, in_sh;  // IN_BN coefficients of this thread's 4 channels (col = tid & 7 for every piece)
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
-    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, 3u * wplane_b);
+    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, uint32_t(WP) * wplane_b);
     auto load_A = [&](int cc) {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) ra[i] = bload4(rs_src, a_boff[i] == kOOB ? kOOB : a_boff[i] + cc * 128u);
@@ -129,6 +135,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             const int ch = (img / a.in_seg_imgs) * a.c + cc * 32 + (tid & 7) * 4;
             in_sc = gload4(a.in_scale + ch);
             in_sh = gload4(a.in_shift + ch);
+            if constexpr (H2) {  // fma(y, sc * s, sh * s) == s * fma(y, sc, sh) exactly (s a power of two)
+                in_sc *= xs;
+                in_sh *= xs;
+            }
         }
     };
     auto store_A = [&](int buf) {
@@ -144,7 +154,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                         v[q] = a_boff[i] == kOOB ? 0.f : fmaxf(fmaf(ra[i][q], in_sc[q], in_sh[q]), 0.f);
                     ra[i] = v;
                 }
-                if constexpr (XP == 3) {
+                if constexpr (H2) {
+                    if constexpr (!IN_BN) ra[i] *= xs;
+                    if constexpr (NP == 4)
+                        split2h_pre(ra[i], h, m);
+                    else
+                        split2h(ra[i], h, m);
+                    *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
+                    *reinterpret_cast<u32x2 *>(sb + PA + a_off[i]) = m;
+                } else if constexpr (XP == 3) {
                     split3(ra[i], h, m, l);
                     *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
                     *reinterpret_cast<u32x2 *>(sb + PA + a_off[i]) = m;
@@ -214,17 +232,34 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         for (int p = 0; p < WP; ++p)
 #pragma unroll
             for (int j = 0; j < TN; ++j) wv[p][j] = __builtin_bit_cast(bf16x8, wq[p][j]);
-        // (w, x) term pairs smallest first: mm, hl, lh, hm, mh, hh; x5 drops lh (w_l * x_h), bf16 runs hh only
-        constexpr int QW[6] = {1, 0, 2, 0, 1, 0};
-        constexpr int QX[6] = {1, 2, 0, 1, 0, 0};
+        if constexpr (H2) {
+            // h2: w_h x_m (NP 4: (w_h 2^-11) x_m', x_m' pre-scaled by 2^11), w_m x_h, w_h x_h on the fp16 planes
 #pragma unroll
-        for (int q = NP == 1 ? 5 : 0; q < 6; ++q)
-            if (NP != 5 || QW[q] != 2)
+            for (int j = 0; j < TN; ++j) {
+                const u32x4 wh = __builtin_bit_cast(u32x4, wv[0][j]), wm = __builtin_bit_cast(u32x4, wv[1][j]);
+                const u32x4 wh_lo = NP == 4 ? f16_down11(wh) : wh;
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
+                for (int i = 0; i < TM; ++i) {
+                    const u32x4 xh = __builtin_bit_cast(u32x4, xv[0][i]), xm = __builtin_bit_cast(u32x4, xv[1][i]);
+                    acc[j][i] = mfma16_f16(wh_lo, xm, acc[j][i]);
+                    acc[j][i] = mfma16_f16(wm, xh, acc[j][i]);
+                    acc[j][i] = mfma16_f16(wh, xh, acc[j][i]);
+                }
+            }
+        } else {
+            // (w, x) term pairs smallest first: mm, hl, lh, hm, mh, hh; x5 drops lh (w_l * x_h), bf16 runs hh only
+            constexpr int QW[6] = {1, 0, 2, 0, 1, 0};
+            constexpr int QX[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
-                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[QW[q]][j], xv[QX[q]][i], acc[j][i], 0, 0, 0);
+            for (int q = NP == 1 ? 5 : 0; q < 6; ++q)
+                if (NP != 5 || QW[q] != 2)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int i = 0; i < TM; ++i)
+                            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[QW[q]][j], xv[QX[q]][i], acc[j][i],
+                                                                                0, 0, 0);
+        }
         if (more) load_W(cc1, t1, wq);
         if constexpr (DB) {
             // the other buffer was last read in the previous chunk, which every wave has left (barrier below)
@@ -241,6 +276,18 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         cc = cc1;
     }
     __syncthreads();  // the epilogue reuses smem for the statistics reduction
+
+    if constexpr (H2) {  // undo the operand scales: per-channel weight inverse scales after the planes
+        const float *winv = reinterpret_cast<const float *>(reinterpret_cast<const unsigned char *>(a.wsplit) +
+                                                            2u * wplane_b);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WCH + j * 16 + 4 * g;
+            const f32x4 sc = (n < NB32 * 32 ? gload4(winv + n) : f32x4{0.f, 0.f, 0.f, 0.f}) * xs_inv;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[j][i] *= sc;
+        }
+    }
 
     // acc[j][i][r]: channel n0 + wn*WCH + 16j + 4g + r, pixel wm*WPX + 16i + l16
     f32x4 bias4[TN];
@@ -399,6 +446,13 @@ void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
         hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN, DB, NP>), grid, block, 0, s, b);
 }
 
+// h2: the activation / gradient operand's low term pre-scaled by 2^11 (x3_common.h; floor 2^-36 instead of 2^-25
+// of the scaled bound).  SCD_H2_PRESCALE=0 drops it (A/B switch, read at launch).
+int h2_prescale() {
+    const char *e = getenv("SCD_H2_PRESCALE");
+    return !(e && e[0] == '0');
+}
+
 // Double buffering where two halo buffers of every resident block still fit the CU's 160 KB of LDS.
 int halo16_db() {
     const char *e = getenv("SCD_HALO16_DB");  // experiment switch
@@ -418,12 +472,29 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
     const bool db3 = tw != 64 && halo16_db() && OCC * 2 * 3 * hr * 64 <= 160 * 1024;
-    switch (conv_math_planes()) {
+    const bool db2 = tw != 64 && halo16_db() && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
+    // h2 needs the h2 weight split and a bound (igemm_takes_halo16); otherwise x3 (h2 mode: other shapes)
+    const int planes = a.src_bound && h2_weight_format(a.ntaps, a.c) ? (h2_prescale() ? 4 : 2)
+                       : conv_math_planes() == 2                      ? 3
+                                                                      : conv_math_planes();
+    switch (planes) {
         case 1:  // one plane: double buffering always fits
             if (halo16_db())
                 launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
             else
                 launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
+            break;
+        case 2:
+            if (db2)
+                launch16c<WM, WN, TM, TN, OCC, true, 2>(a, tw, s);
+            else
+                launch16c<WM, WN, TM, TN, OCC, false, 2>(a, tw, s);
+            break;
+        case 4:
+            if (db2)
+                launch16c<WM, WN, TM, TN, OCC, true, 4>(a, tw, s);
+            else
+                launch16c<WM, WN, TM, TN, OCC, false, 4>(a, tw, s);
             break;
         case 5:
             if (db3)
@@ -731,9 +802,13 @@ int halo16_c16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     return 0;
 }
 
+// Arithmetic of the kernels that keep the split-bf16 planes under every mode (the 16-channel input layer): the
+// mode's own, except h2 (whose fp16 weight split exists only for 32-channel multiples), which runs x3 here.
+static int bf16_planes() { return conv_math_planes() == 2 ? 3 : conv_math_planes(); }
+
 template <int TW>
 static void launch_c16_tw(const IgemmArgs &b, dim3 grid, hipStream_t s) {
-    switch (conv_math_planes()) {
+    switch (bf16_planes()) {
         case 1: hipLaunchKernelGGL((igemm_halo16_c16<TW, 1>), grid, dim3(256), 0, s, b); break;
         case 5: hipLaunchKernelGGL((igemm_halo16_c16<TW, 5>), grid, dim3(256), 0, s, b); break;
         default: hipLaunchKernelGGL((igemm_halo16_c16<TW, 3>), grid, dim3(256), 0, s, b);
@@ -743,7 +818,7 @@ static void launch_c16_tw(const IgemmArgs &b, dim3 grid, hipStream_t s) {
 template <int TW>
 static int c16_resident() {
     static int cache[3] = {0, 0, 0};  // per arithmetic: bf16, x5, x3
-    const int k = conv_math_planes() == 1 ? 0 : conv_math_planes() == 5 ? 1 : 2;
+    const int k = bf16_planes() == 1 ? 0 : bf16_planes() == 5 ? 1 : 2;
     if (cache[k] > 0) return cache[k];
     const void *fn = k == 0   ? reinterpret_cast<const void *>(&igemm_halo16_c16<TW, 1>)
                      : k == 1 ? reinterpret_cast<const void *>(&igemm_halo16_c16<TW, 5>)
@@ -753,7 +828,8 @@ static int c16_resident() {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu < 1 || cus < 1) {
         (void)hipGetLastError();
-        return 2 * 256;
+        cache[k] = 2 * 256;  // cached: every launch of a shape sees the same capacity
+        return cache[k];
     }
     cache[k] = per_cu * cus;
     return cache[k];
@@ -797,9 +873,12 @@ void launch_halo16_c16(const IgemmArgs &a, int tw, hipStream_t s) {
 namespace {
 constexpr int kW16RS = 160;
 
-// X planes of the weight-grad kernel per arithmetic: x3 3, x5 2 (its l term is the dropped product's), bf16 1.
+// X planes of the weight-grad kernel per arithmetic: x3 3, x5 2 (its l term is the dropped product's), bf16 1,
+// h2 2 (fp16 h, m).  dY planes: x3 / x5 3, bf16 1, h2 2.
 template <int NP>
-constexpr int w16_xp() { return NP == 1 ? 1 : NP == 5 ? 2 : 3; }
+constexpr int w16_xp() { return NP == 1 ? 1 : (NP == 5 || NP == 2 || NP == 4) ? 2 : 3; }
+template <int NP>
+constexpr int w16_dp() { return NP == 1 ? 1 : (NP == 2 || NP == 4) ? 2 : 3; }
 
 // X fragments of half tap (T, CB): two transposed reads per X plane.
 template <int T, int CB, int PB, int HW_, int NP>
@@ -822,6 +901,24 @@ __device__ __forceinline__ void w16_read_x(s16x4 (&f)[6], uint32_t xbase) {
 template <int T, int CB, int WAIT, int NP>
 __device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f)[6]) {
     bf16x8 x0 = cat8(f[0], f[1]), x1 = cat8(f[2], f[3]), x2 = cat8(f[4], f[5]);
+    if constexpr (NP == 2 || NP == 4) {  // fp16 planes: x_m dy_h, x_h dy_m (NP 4: (x_h 2^-11) dy_m', dY's low
+                                         // term pre-scaled), x_h dy_h
+        lds_wait<WAIT>(x0, x1);
+        if (T == 0 && CB == 0) {
+            lds_wait<WAIT>(dv[0][0], dv[1][0]);
+            lds_wait<WAIT>(dv[0][1], dv[1][1]);
+        }
+        const u32x4 xh = __builtin_bit_cast(u32x4, x0), xm = __builtin_bit_cast(u32x4, x1);
+        const u32x4 xh_lo = NP == 4 ? f16_down11(xh) : xh;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const u32x4 dh = __builtin_bit_cast(u32x4, dv[0][rb]), dm = __builtin_bit_cast(u32x4, dv[1][rb]);
+            acc[T][CB][rb] = mfma16_f16(xm, dh, acc[T][CB][rb]);
+            acc[T][CB][rb] = mfma16_f16(xh_lo, dm, acc[T][CB][rb]);
+            acc[T][CB][rb] = mfma16_f16(xh, dh, acc[T][CB][rb]);
+        }
+        return;
+    }
     if constexpr (NP != 1) {
         if constexpr (NP == 3)
             lds_wait<WAIT>(x0, x1, x2);
@@ -870,10 +967,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     constexpr int PA = P * RS, PB = HP * RS;            // plane bytes
     constexpr int A_CH = P * 16, B_CH = HP * 16;        // 4-channel pieces
     constexpr int A_PER = A_CH / 256, B_PER = (B_CH + 255) / 256;
-    static_assert(NP == 1 || NP == 3 || NP == 5, "x3, x5 or bf16");
-    constexpr int DP = NP == 1 ? 1 : 3;  // dY planes
-    constexpr int XP = w16_xp<NP>();      // X planes
+    static_assert(NP == 1 || NP == 2 || NP == 3 || NP == 4 || NP == 5, "x3, x5, bf16 or h2");
+    constexpr bool H2 = NP == 2 || NP == 4;
+    constexpr int DP = w16_dp<NP>();  // dY planes
+    constexpr int XP = w16_xp<NP>();  // X planes
     __shared__ __attribute__((aligned(16))) unsigned char smem[DP * PA + XP * PB];
+    float ds = 1.f, ds_inv = 1.f, xs = 1.f, xs_inv = 1.f;  // h2: power-of-two operand scales
+    if constexpr (H2) {
+        h2_scale(*a.rows_bound, ds, ds_inv);
+        h2_scale(*a.src_bound, xs, xs_inv);
+    }
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wi = wid >> 1, wj = wid & 1;
@@ -897,8 +1000,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
         const int img = pi / pimg, pr = pi - img * pimg;
         if (a.src_scale) {
             const int ch = (img / a.src_seg_imgs) * a.C + c0 + (tid & 15) * 4;
-            x_sc = gload4(a.src_scale + ch);
-            x_sh = gload4(a.src_shift + ch);
+            x_sc = gload4(a.src_scale + ch) * xs;  // h2: the scale folds into the transform exactly
+            x_sh = gload4(a.src_shift + ch) * xs;
         }
         x_valid = 0;
         const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
@@ -925,7 +1028,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             const int e = tid + i * 256;
             const int o = (e >> 4) * RS + (e & 15) * 8;
             u32x2 h, m, l;
-            if constexpr (DP == 3) {
+            if constexpr (H2) {
+                if constexpr (NP == 4)
+                    split2h_pre(ra[i] * ds, h, m);
+                else
+                    split2h(ra[i] * ds, h, m);
+                *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
+            } else if constexpr (DP == 3) {
                 split3(ra[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
                 *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
@@ -943,10 +1052,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
                     const bool v = (x_valid >> i) & 1u;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                } else if constexpr (H2) {
+                    rb[i] *= xs;
                 }
                 const int e = tid + i * 256;
                 const int o = DP * PA + (e >> 4) * RS + (e & 15) * 8;
-                if constexpr (XP >= 2) {
+                if constexpr (H2) {
+                    split2h(rb[i], h, m);
+                    *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
+                } else if constexpr (XP >= 2) {
                     split3(rb[i], h, m, l);  // x5: the l term is not needed (dead code)
                     *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
                     if constexpr (XP == 3) *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
@@ -985,11 +1099,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             tr_read<0 * PA + 8 * RS>(fa[1], dbase);
             tr_read<0 * PA + 32>(fa[2], dbase);
             tr_read<0 * PA + 8 * RS + 32>(fa[3], dbase);
-            if constexpr (DP == 3) {
+            if constexpr (DP >= 2) {
                 tr_read<1 * PA + 0>(fa[4], dbase);
                 tr_read<1 * PA + 8 * RS>(fa[5], dbase);
                 tr_read<1 * PA + 32>(fa[6], dbase);
                 tr_read<1 * PA + 8 * RS + 32>(fa[7], dbase);
+            }
+            if constexpr (DP == 3) {
                 tr_read<2 * PA + 0>(fa[8], dbase);
                 tr_read<2 * PA + 8 * RS>(fa[9], dbase);
                 tr_read<2 * PA + 32>(fa[10], dbase);
@@ -1012,6 +1128,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
         }
     }
 
+    if constexpr (H2) {
+        const float k = ds_inv * xs_inv;  // exact: a power of two
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                for (int r = 0; r < 2; ++r) acc[t][cb][r] *= k;
+    }
     // acc[t][cb][rb][q]: r = r0 + 32wi + 16rb + (lane & 15), c = c0 + 32wj + 16cb + 4g + q
     float *slab = a.slabs + size_t(split) * a.R * a.Ng;
 #pragma unroll
@@ -1229,14 +1354,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
 }
 
 const void *wgrad_halo16_c16_fn() {
-    switch (conv_math_planes()) {
+    switch (bf16_planes()) {
         case 1: return reinterpret_cast<const void *>(&wgrad_halo16_c16<1>);
         case 5: return reinterpret_cast<const void *>(&wgrad_halo16_c16<5>);
         default: return reinterpret_cast<const void *>(&wgrad_halo16_c16<3>);
     }
 }
 void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    switch (conv_math_planes()) {
+    switch (bf16_planes()) {
         case 1: hipLaunchKernelGGL(wgrad_halo16_c16<1>, grid, dim3(256), 0, s, a); break;
         case 5: hipLaunchKernelGGL(wgrad_halo16_c16<5>, grid, dim3(256), 0, s, a); break;
         default: hipLaunchKernelGGL(wgrad_halo16_c16<3>, grid, dim3(256), 0, s, a);
@@ -1252,16 +1377,24 @@ int wgrad16_mode() {
     }
     return g_wgrad16;
 }
-const void *wgrad_halo16_fn() {
-    switch (conv_math_planes()) {
+// h2 runs where both operands are bounded, x3 otherwise.
+static int wgrad16_planes(bool bounded) {
+    return conv_math_planes() == 2 ? (bounded ? (h2_prescale() ? 4 : 2) : 3) : conv_math_planes();
+}
+const void *wgrad_halo16_fn(bool bounded) {
+    switch (wgrad16_planes(bounded)) {
         case 1: return reinterpret_cast<const void *>(&wgrad_halo16_x3<1>);
+        case 2: return reinterpret_cast<const void *>(&wgrad_halo16_x3<2>);
+        case 4: return reinterpret_cast<const void *>(&wgrad_halo16_x3<4>);
         case 5: return reinterpret_cast<const void *>(&wgrad_halo16_x3<5>);
         default: return reinterpret_cast<const void *>(&wgrad_halo16_x3<3>);
     }
 }
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    switch (conv_math_planes()) {
+    switch (wgrad16_planes(a.rows_bound && a.src_bound)) {
         case 1: hipLaunchKernelGGL(wgrad_halo16_x3<1>, grid, dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(wgrad_halo16_x3<2>, grid, dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL(wgrad_halo16_x3<4>, grid, dim3(256), 0, s, a); break;
         case 5: hipLaunchKernelGGL(wgrad_halo16_x3<5>, grid, dim3(256), 0, s, a); break;
         default: hipLaunchKernelGGL(wgrad_halo16_x3<3>, grid, dim3(256), 0, s, a);
     }

@@ -571,18 +571,32 @@ static int halo_pick(const IgemmArgs &a, int *bm, int *tw) {
     return 0;
 }
 
-bool igemm_takes_halo16(const IgemmArgs &a) {
+// SCD_MATH_H2: a 3x3 conv whose weight split is in the h2 format runs the h2 halo16 kernel when the descriptor
+// bounds its source and the kernel tiles the shape; otherwise the x3 kernels split the fp32 weights on the fly
+// (the h2 split is ignored).
+static IgemmArgs x3_view(const IgemmArgs &a) {
+    IgemmArgs b = a;
     int bm = 0, tw = 0;
+    if (h2_weight_format(a.ntaps, a.c) && (!a.src_bound || !halo16_pick(a, halo_eligible(a), &bm, &tw)))
+        b.wsplit = nullptr;
+    return b;
+}
+
+bool igemm_takes_halo16(const IgemmArgs &a0) {
+    int bm = 0, tw = 0;
+    const IgemmArgs a = x3_view(a0);
     return conv_math_x3() && a.c % 16 == 0 && halo16_pick(a, halo_eligible(a), &bm, &tw) != 0;
 }
 
-bool igemm_takes_c16(const IgemmArgs &a) {
+bool igemm_takes_c16(const IgemmArgs &a0) {
     int bm = 0, tw = 0;
+    const IgemmArgs a = x3_view(a0);
     return conv_math_x3() && halo16_c16_pick(a, halo_eligible(a), &bm, &tw) != 0;
 }
 
-int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels) {
+int halo_stat_tiles(const IgemmArgs &a0, int *tile_pixels) {
     int bm = 0, tw = 0;
+    const IgemmArgs a = x3_view(a0);
     if (!conv_math_x3()) return 0;
     if (!halo16_pick(a, halo_eligible(a), &bm, &tw) && !halo16_c16_pick(a, halo_eligible(a), &bm, &tw) &&
         !halo_pick(a, &bm, &tw))
@@ -591,8 +605,9 @@ int halo_stat_tiles(const IgemmArgs &a, int *tile_pixels) {
     return a.n_img * (a.ho * a.wo / bm);
 }
 
-bool launch_igemm_x3(const IgemmArgs &a, hipStream_t s) {
-    if (a.c % 16) return false;
+bool launch_igemm_x3(const IgemmArgs &a0, hipStream_t s) {
+    if (a0.c % 16) return false;
+    const IgemmArgs a = x3_view(a0);
     int bm = 0, tw = 0;
     if (const int c16 = halo16_pick(a, halo_eligible(a), &bm, &tw)) {
         launch_halo16(a, c16, tw, s);
@@ -1052,8 +1067,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_x3(WgradArgs a) {
         }
 }
 
-const void *wgrad_halo_fn() {
-    return wgrad16_mode() ? wgrad_halo16_fn() : reinterpret_cast<const void *>(&wgrad_halo_x3);
+const void *wgrad_halo_fn(bool bounded) {
+    return wgrad16_mode() ? wgrad_halo16_fn(bounded) : reinterpret_cast<const void *>(&wgrad_halo_x3);
 }
 
 void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
@@ -1129,8 +1144,49 @@ constexpr int kPackJobs = 48;
 struct PackJobs {
     scd_pack_job_t j[kPackJobs];
     int first_block[kPackJobs + 1];
+    int first_row[kPackJobs + 1];  // h2 jobs: padded split rows (NB * 32) of the row-scale pass, prefix sums
+    int h2[kPackJobs];             // split in the SCD_MATH_H2 format (fp16 h, m planes + per-row inverse scales)
     int n;
 };
+
+// Per-row inverse scales of an h2 split: float [NB * 32] after the two fp16 planes.
+__device__ __forceinline__ float *h2_row_inv(uint16_t *split, int64_t plane) {
+    return reinterpret_cast<float *>(split + 2 * plane);
+}
+
+// One wave per padded split row of every h2 job: the row's max |w| -> its power-of-two inverse scale (the split
+// pass below scales the row by the reciprocal).  Rows of the packed layout are output channels (mode 0) or input
+// channels (mode 1, the data-grad layout); the max is read from the OIHW parameter directly.
+__global__ __launch_bounds__(256) void pack_rowscale_kernel(PackJobs jobs) {
+    const int wave = int(blockIdx.x) * 4 + int(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (wave >= jobs.first_row[jobs.n]) return;
+    int q = 0;
+    while (q + 1 < jobs.n && wave >= jobs.first_row[q + 1]) ++q;
+    const scd_pack_job_t J = jobs.j[q];
+    const int r = wave - jobs.first_row[q];
+    const int rows = J.mode == 0 ? J.co : J.ci;
+    const int K = 9 * (J.mode == 0 ? J.ci_pad : J.co);
+    float mx = 0.f;
+    if (r < rows) {
+        if (J.mode == 0) {
+            const int n = J.ci * 9;
+            for (int e = lane; e < n; e += 64) mx = fmaxf(mx, fabsf(J.w[size_t(r) * n + e]));
+        } else {
+            const int n = J.co * 9;
+            for (int e = lane; e < n; e += 64) {
+                const int o = e / 9, t = e - o * 9;
+                mx = fmaxf(mx, fabsf(J.w[(size_t(o) * J.ci + r) * 9 + t]));
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    if (lane == 0) {
+        float sc, inv;
+        h2_scale(mx, sc, inv);
+        h2_row_inv(J.split, int64_t((rows + 31) / 32) * 32 * K)[r] = inv;
+    }
+}
 
 // Element (row r, column k) of the packed layout of job J.
 __device__ __forceinline__ float packed_at(const scd_pack_job_t &J, int r, int k) {
@@ -1172,10 +1228,18 @@ __global__ __launch_bounds__(256) void pack_multi_kernel(PackJobs jobs) {
                 v1[i] = packed_at(J, r, k0 + 4 + i);
             }
         }
+        uint16_t *o = J.split + f * 8;
         u32x2 h0, m0, l0, h1, m1, l1;
+        if (jobs.h2[q]) {
+            const float sc = 1.f / h2_row_inv(J.split, plane)[r];  // exact: a power of two
+            split2h(v0 * sc, h0, m0);
+            split2h(v1 * sc, h1, m1);
+            *reinterpret_cast<u32x4 *>(o) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+            *reinterpret_cast<u32x4 *>(o + plane) = u32x4{m0[0], m0[1], m1[0], m1[1]};
+            continue;
+        }
         split3(v0, h0, m0, l0);
         split3(v1, h1, m1, l1);
-        uint16_t *o = J.split + f * 8;
         *reinterpret_cast<u32x4 *>(o) = u32x4{h0[0], h0[1], h1[0], h1[1]};
         *reinterpret_cast<u32x4 *>(o + plane) = u32x4{m0[0], m0[1], m1[0], m1[1]};
         *reinterpret_cast<u32x4 *>(o + 2 * plane) = u32x4{l0[0], l0[1], l1[0], l1[1]};
@@ -1196,9 +1260,12 @@ extern "C" int scd_pack_conv3x3_multi(const scd_pack_job_t *jobs, int32_t n, scd
         PackJobs pj;
         pj.n = std::min(kPackJobs, n - base);
         pj.first_block[0] = 0;
+        pj.first_row[0] = 0;
         for (int i = 0; i < pj.n; ++i) {
             const scd_pack_job_t &J = jobs[base + i];
             const int rows = J.mode == 0 ? J.co : J.ci, K = 9 * (J.mode == 0 ? J.ci_pad : J.co);
+            pj.h2[i] = J.split && h2_weight_format(9, K / 9);
+            pj.first_row[i + 1] = pj.first_row[i] + (pj.h2[i] ? (rows + 31) / 32 * 32 : 0);
             if (!J.w || !J.out || J.co < 1 || J.ci < 1 || J.ci_pad < J.ci || (J.mode != 0 && J.mode != 1) ||
                 (J.split && (K % 16 || !aligned16(J.split)))) {
                 set_error("pack_conv3x3_multi: job %d: bad arguments (split needs K %% 16 == 0, 16-byte alignment)",
@@ -1211,6 +1278,9 @@ extern "C" int scd_pack_conv3x3_multi(const scd_pack_job_t *jobs, int32_t n, scd
             pj.first_block[i + 1] = pj.first_block[i] + blocks;
         }
         if (pj.n == 0) break;
+        if (pj.first_row[pj.n] > 0)
+            hipLaunchKernelGGL(pack_rowscale_kernel, dim3((pj.first_row[pj.n] + 3) / 4), dim3(256), 0,
+                               as_stream(stream), pj);
         hipLaunchKernelGGL(pack_multi_kernel, dim3(pj.first_block[pj.n]), dim3(256), 0, as_stream(stream), pj);
         SCD_TRY(launch_status("scd_pack_conv3x3_multi"));
     }
@@ -1234,6 +1304,66 @@ extern "C" int scd_split_bf16x3_frag(const float *w, int32_t n_out, int32_t K, u
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(split_frag_kernel, dim3(unsigned(blocks)), dim3(256), 0, as_stream(stream), w, n_out, K, NB, dst);
     return launch_status("scd_split_bf16x3_frag");
+}
+
+namespace scd {
+// h2 split of a packed [n_out][K] matrix in fragment order: per-row inverse scales (one wave per padded row), then
+// the two fp16 planes of the scaled rows (scd_split_h2_frag).
+__global__ __launch_bounds__(256) void h2_rowscale_kernel(const float *__restrict__ w, int n_out, int K, int NB,
+                                                          uint16_t *__restrict__ dst) {
+    const int r = int(blockIdx.x) * 4 + int(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= NB * 32) return;
+    float mx = 0.f;
+    if (r < n_out)
+        for (int k = lane; k < K; k += 64) mx = fmaxf(mx, fabsf(w[size_t(r) * K + k]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    if (lane == 0) {
+        float sc, inv;
+        h2_scale(mx, sc, inv);
+        h2_row_inv(dst, int64_t(NB) * 32 * K)[r] = inv;
+    }
+}
+__global__ void h2_split_frag_kernel(const float *__restrict__ w, int n_out, int K, int NB, uint16_t *__restrict__ dst) {
+    const int KS = K / 16;
+    const int64_t total = int64_t(NB) * KS * 64;
+    const int64_t plane = total * 8;
+    const float *inv = h2_row_inv(dst, plane);
+    for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
+        const int lane = int(e & 63);
+        const int64_t fk = e >> 6;
+        const int nb = int(fk / KS), ks = int(fk - int64_t(nb) * KS);
+        const int n = nb * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
+        f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+        if (n < n_out) {
+            const float sc = 1.f / inv[n];
+            v0 = gload4(w + size_t(n) * K + k0) * sc;
+            v1 = gload4(w + size_t(n) * K + k0 + 4) * sc;
+        }
+        u32x2 h0, m0, h1, m1;
+        split2h(v0, h0, m0);
+        split2h(v1, h1, m1);
+        uint16_t *o = dst + e * 8;
+        *reinterpret_cast<u32x4 *>(o) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+        *reinterpret_cast<u32x4 *>(o + plane) = u32x4{m0[0], m0[1], m1[0], m1[1]};
+    }
+}
+}  // namespace scd
+
+extern "C" int scd_split_h2_frag(const float *w, int32_t n_out, int32_t K, uint16_t *dst, scd_stream_t stream) {
+    clear_error();
+    if (!w || !dst || n_out < 1 || K < 16 || K % 16 || !aligned16(w) || !aligned16(dst)) {
+        set_error("split_h2_frag: need K %% 16 == 0 and 16-byte aligned w/dst (n_out=%d K=%d)", n_out, K);
+        return SCD_ERR_ARG;
+    }
+    const int NB = (n_out + 31) / 32;
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(h2_rowscale_kernel, dim3(NB * 8), dim3(256), 0, s, w, n_out, K, NB, dst);
+    const int64_t total = int64_t(NB) * (K / 16) * 64;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(h2_split_frag_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, w, n_out, K, NB, dst);
+    return launch_status("scd_split_h2_frag");
 }
 
 extern "C" int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream) {

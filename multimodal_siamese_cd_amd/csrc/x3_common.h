@@ -34,6 +34,69 @@ __device__ __forceinline__ void split3(const f32x4 v, u32x2 &h, u32x2 &m, u32x2 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Two-term fp16 split ("h2", SCD_MATH_H2).  A power-of-two scale s brings an operand's magnitude bound U
+// to U * s < 2^15 (< fp16 max 65504); x * s = h + m with h = fp16(x * s) and m = fp16(x * s - h), both rounded
+// to nearest.  The subtraction is exact, h and m carry 11 significant bits each, so h + m represents x * s to
+// 2^-22 relative while m stays in the fp16 normal range (x * s >= 2^-3), with a floor of 2^-25 absolute
+// below.  A product keeps hh + hm + mh (the dropped mm is <= 2^-24 relative): three MFMAs against x3's six.
+//
+// Activations and gradients can span far more than the 2^17 binades above that floor (a few large gradient
+// values over a bulk 2^20 below them), so their low term is kept pre-scaled: m' = fp16((x * s - h) * 2^11),
+// normal down to x * s = 2^-14, floor 2^-36 absolute.  The product against the other operand's h then takes
+// that operand's h * 2^-11 (formed in registers, exact while it is an fp16 normal): one MFMA accumulator.
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t cvt_pk_f16(float a, float b) {
+    const f32x2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));  // RNE
+}
+__device__ __forceinline__ float f16_lo(uint32_t p) { return float(__builtin_bit_cast(f16x2, p)[0]); }
+__device__ __forceinline__ float f16_hi(uint32_t p) { return float(__builtin_bit_cast(f16x2, p)[1]); }
+
+// Split four consecutive (already scaled) fp32 values into their h, m fp16 terms (4 fp16 = 8 bytes each).
+__device__ __forceinline__ void split2h(const f32x4 v, u32x2 &h, u32x2 &m) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const float x0 = v[2 * p], x1 = v[2 * p + 1];
+        const uint32_t ph = cvt_pk_f16(x0, x1);
+        h[p] = ph;
+        m[p] = cvt_pk_f16(x0 - f16_lo(ph), x1 - f16_hi(ph));
+    }
+}
+
+// The same with the low term pre-scaled by 2^11 (activation / gradient operands, see above).
+__device__ __forceinline__ void split2h_pre(const f32x4 v, u32x2 &h, u32x2 &m) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const float x0 = v[2 * p], x1 = v[2 * p + 1];
+        const uint32_t ph = cvt_pk_f16(x0, x1);
+        h[p] = ph;
+        m[p] = cvt_pk_f16((x0 - f16_lo(ph)) * 2048.f, (x1 - f16_hi(ph)) * 2048.f);
+    }
+}
+// h * 2^-11 of an fp16 fragment (v_pk_mul_f16): the partner of a pre-scaled low term.
+__device__ __forceinline__ u32x4 f16_down11(const u32x4 v) {
+    const f16x8 r = __builtin_bit_cast(f16x8, v) * (_Float16)0x1p-11f;
+    return __builtin_bit_cast(u32x4, r);
+}
+
+// Power-of-two scale for a magnitude bound ub: s = 2^k with ub * s < 2^15, k clamped to [-126, 126] so s and 1/s
+// are normal floats (0 -> 1; a non-finite bound gives a finite scale and the garbage it describes).
+__device__ __forceinline__ void h2_scale(float ub, float &s, float &inv) {
+    const uint32_t b = __builtin_bit_cast(uint32_t, ub) & 0x7fffffffu;
+    int k = b ? 14 - (int(b >> 23) - 127) : 0;
+    k = k < -126 ? -126 : (k > 126 ? 126 : k);
+    s = __builtin_bit_cast(float, uint32_t(127 + k) << 23);
+    inv = __builtin_bit_cast(float, uint32_t(127 - k) << 23);
+}
+
+__device__ __forceinline__ f32x4 mfma16_f16(const u32x4 a, const u32x4 b, const f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
 // Raw buffer loads: 32-bit byte offsets with the hardware range check, so an out-of-range offset
 // (kOOB) returns zeros with no branch, no exec-mask juggling and no zero-fill moves.
 constexpr uint32_t kOOB = 0x80000000u;

@@ -34,7 +34,8 @@ _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': Tru
 
 def conv_math_for(cfg) -> str:
     """The conv arithmetic a config asks for: MODEL.CONV_MATH if set, else MODEL.PRECISION ('fp32' -> the
-    fp32-accurate split-bf16 'x3', 'bf16' -> 'bf16')."""
+    fp32-accurate two-term fp16 split 'h2' (bounded operands; every other conv runs the split-bf16 'x3'),
+    'bf16' -> 'bf16')."""
     m = cfg.MODEL.get('CONV_MATH', None)
     if m:
         return str(m)
@@ -42,7 +43,7 @@ def conv_math_for(cfg) -> str:
     if prec in ('bf16', 'bfloat16'):
         return 'bf16'
     if prec in ('fp32', 'f32', 'float32'):
-        return 'x3'
+        return 'h2'
     raise ValueError(f"MODEL.PRECISION {prec!r}: expected 'fp32' or 'bf16'")
 
 
@@ -122,7 +123,7 @@ def invalidate_weight_cache():
 
 
 def _pack_key(mode: int, ci_pad: int):
-    return (mode, ci_pad if mode == 0 else 0, hip.conv_math() != 'f32')
+    return (mode, ci_pad if mode == 0 else 0, hip.conv_math())
 
 
 def _cached(w, key, group):
@@ -168,6 +169,56 @@ def _ws(nbytes: int, like: torch.Tensor):
     return torch.empty(int(nbytes), device=like.device, dtype=torch.uint8)
 
 
+# ------------------------------------------------------------------------------------------------
+# SCD_MATH_H2 operand bounds.  The h2 conv arithmetic scales each activation operand by the power of two of an
+# upper bound of its magnitude (scd_igemm_t.src_bound).  The bounds come from the producers at no extra pass:
+# a BatchNorm's statistics bound its ReLU output (scd_bn_*_stats act_bound), the BatchNorm backward raises a bound
+# to max |dy| as it writes dy (dy_bound); scd_absmax_bound covers the rest (eval mode, the ConvT half of a concat).
+# A bound is a one-float device tensor; bounds are only allocated under h2.
+# ------------------------------------------------------------------------------------------------
+class _Bounds:
+    """Zero-initialised device floats handed out one at a time (one fill launch per 64)."""
+
+    def __init__(self, like: torch.Tensor, chunk: int = 64):
+        self.device, self.chunk = like.device, chunk
+        self.buf, self.i = None, 0
+
+    def take(self) -> torch.Tensor:
+        if self.buf is None or self.i == self.chunk:
+            self.buf, self.i = torch.zeros(self.chunk, device=self.device, dtype=_F32), 0
+        self.i += 1
+        return self.buf[self.i - 1:self.i]
+
+
+def _bounds(like: torch.Tensor):
+    """A bound pool under the h2 arithmetic, else None (no bounds anywhere)."""
+    return _Bounds(like) if hip.conv_math() == 'h2' else None
+
+
+def _take(pool):
+    return pool.take() if pool is not None else None
+
+
+_ACT_BOUND = _IdentityMap()  # activation tensor handed between stages -> its bound
+
+
+def _set_bound(t: torch.Tensor, b):
+    if b is not None:
+        _ACT_BOUND.setdefault(t, b)
+    return t
+
+
+def _bound_of(t: torch.Tensor, pool, nseg: int = 1, scale=None, shift=None):
+    """The registered bound of t, or (under h2) a fresh one from a pass over t."""
+    if pool is None:
+        return None
+    b = _ACT_BOUND.get(t)
+    if b is None:
+        b = pool.take()
+        hip.absmax_bound(nhwc(t), b, nseg, scale, shift)
+    return b
+
+
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8
 
@@ -211,11 +262,13 @@ def _bn_uses_batch_stats(bn: torch.nn.BatchNorm2d, training: bool) -> bool:
     return training or not bn.track_running_stats or bn.running_mean is None
 
 
-def _bn_forward(y: torch.Tensor, bn: torch.nn.BatchNorm2d, nseg: int, training: bool, tiles=None) -> _BNSaved:
+def _bn_forward(y: torch.Tensor, bn: torch.nn.BatchNorm2d, nseg: int, training: bool, tiles=None,
+                bound=None) -> _BNSaved:
     """Batch statistics (train) or running statistics (eval) -> per-segment scale/shift.
 
     `tiles` = (tile records, ntiles, pixels per tile) from the conv that produced y (fused statistics);
-    without it the statistics are a separate pass over y.
+    without it the statistics are a separate pass over y.  `bound` (h2): a zeroed device float raised to a bound
+    of the activation relu(BN(y)) -- from the statistics in train mode, by a pass over y in eval mode.
     """
     n, h, w, c = y.shape
     if _bn_uses_batch_stats(bn, training):
@@ -228,16 +281,18 @@ def _bn_forward(y: torch.Tensor, bn: torch.nn.BatchNorm2d, nseg: int, training: 
             rec, ntiles, tpx = tiles
             ws = _ws(hip.bn_tile_stats_workspace_bytes(ntiles, c, nseg), y)
             hip.bn_stats_from_tiles(rec, ntiles, tpx, c, nseg, bn.weight, bn.bias, bn.eps, mom, update,
-                                    bn.running_mean, bn.running_var, smean, sinv, scale, shift, ws)
+                                    bn.running_mean, bn.running_var, smean, sinv, scale, shift, ws, act_bound=bound)
         else:
             ws = _ws(hip.bn_workspace_bytes(n, h, w, c, nseg), y)
             hip.bn_train_stats(nhwc(y), nseg, bn.weight, bn.bias, bn.eps, mom, update, bn.running_mean,
-                               bn.running_var, smean, sinv, scale, shift, ws)
+                               bn.running_var, smean, sinv, scale, shift, ws, act_bound=bound)
         if update:
             _NBT_PENDING.append((bn.num_batches_tracked, nseg))
         return _BNSaved(smean, sinv, scale, shift, nseg)
     scale, shift = _empty((c,), y), _empty((c,), y)
     hip.bn_eval_coeffs(c, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, scale, shift)
+    if bound is not None:
+        hip.absmax_bound(nhwc(y), bound, 1, scale, shift)
     return _BNSaved(None, None, scale, shift, 1)
 
 
@@ -249,73 +304,79 @@ def dc_params(dc) -> list:
     return [s[0].weight, s[0].bias, s[1].weight, s[1].bias, s[3].weight, s[3].bias, s[4].weight, s[4].bias]
 
 
-def _conv3x3(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int) -> torch.Tensor:
-    n, h, w, _ = x.shape
-    y = _empty((n, h, w, n_out), x)
-    hip.conv_igemm(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, bias, nhwc(y))
-    return y
-
-
-def _conv3x3_stats(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int, want: bool, in_bn=None, y=None):
+def _conv3x3_stats(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int, want: bool, in_bn=None, y=None,
+                   src_bound=None):
     """Conv 3x3 forward; with `want`, also the fused per-tile BatchNorm statistics when the conv provides them.
-    `in_bn` = (scale, shift, nseg): x is the previous conv's output, read through its BatchNorm + ReLU."""
+    `in_bn` = (scale, shift, nseg): x is the previous conv's output, read through its BatchNorm + ReLU.
+    `src_bound` (h2): the bound of x as read."""
     n, h, w, _ = x.shape
     y = _empty((n, h, w, n_out), x) if y is None else y
     tiles = None
     if want:
-        ntiles, tpx = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(y))
+        ntiles, tpx = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(y), src_bound=src_bound)
         if ntiles:
             rec = _empty((ntiles * n_out * 2,), x)
             tiles = (rec, ntiles, tpx)
     hip.conv_igemm(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, bias, nhwc(y),
-                   stat_rec=None if tiles is None else tiles[0], in_bn=in_bn)
+                   stat_rec=None if tiles is None else tiles[0], in_bn=in_bn, src_bound=src_bound)
     return y, tiles
 
 
-def _can_fuse_input_bn(y0: torch.Tensor, wpk1: torch.Tensor, y1: torch.Tensor, st: '_BNSaved', save: bool) -> bool:
+def _can_fuse_input_bn(y0: torch.Tensor, wpk1: torch.Tensor, y1: torch.Tensor, st: '_BNSaved', save: bool,
+                       bound=None) -> bool:
     """Whether conv1 (and, when training, its weight grad) can read y0 through BN0 + ReLU directly."""
     if not _OPTS['fuse_input_bn']:
         return False
     n, h, w, _ = y0.shape
     bn = (st.scale, st.shift, st.nseg)
-    if not hip.igemm_input_bn_supported(nhwc(y0), h, w, 1, TAPS_3X3, wpk1, y1.shape[3], nhwc(y1), bn):
+    if not hip.igemm_input_bn_supported(nhwc(y0), h, w, 1, TAPS_3X3, wpk1, y1.shape[3], nhwc(y1), bn, bound):
         return False
     return not save or hip.wgrad_src_bn_supported(nhwc(y1), nhwc(y0), 1, TAPS_3X3, bn)
 
 
-def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool, materialize: bool = True):
-    """(a1, saved, y1, st1); with materialize=False the output activation a1 = relu(BN1(y1)) is left to the
-    consumers (None is returned for it)."""
+def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool, materialize: bool = True,
+                pool=None, x_bound=None):
+    """(a1, saved, y1, st1, b1); with materialize=False the output activation a1 = relu(BN1(y1)) is left to the
+    consumers (None is returned for it).  Under h2 (`pool` given) `x_bound` bounds x and b1 bounds a1."""
     s = dc.conv
     conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
     cin = x.shape[3]
     if conv0.in_channels > cin:
         raise ValueError(f"DoubleConv expects {conv0.in_channels} input channels, got {cin}")
+    if pool is not None and x_bound is None and cin % 32 == 0:
+        x_bound = _bound_of(x, pool)
     y0, t0 = _conv3x3_stats(x, packed_conv3x3(conv0.weight, 0, ci_pad=cin), conv0.bias,
-                            conv0.out_channels, _bn_uses_batch_stats(bn0, training))
-    st0 = _bn_forward(y0, bn0, nseg, training, t0)
+                            conv0.out_channels, _bn_uses_batch_stats(bn0, training), src_bound=x_bound)
+    b0 = _take(pool)
+    st0 = _bn_forward(y0, bn0, nseg, training, t0, b0)
     wpk1 = packed_conv3x3(conv1.weight, 0)
     n, h, w, _ = y0.shape
     y1 = _empty((n, h, w, conv1.out_channels), y0)
-    if _can_fuse_input_bn(y0, wpk1, y1, st0, save):
+    if _can_fuse_input_bn(y0, wpk1, y1, st0, save, b0):
         a0 = None  # never materialised: conv1 and its weight grad apply BN0 + ReLU while staging y0
         y1, t1 = _conv3x3_stats(y0, wpk1, conv1.bias, conv1.out_channels, _bn_uses_batch_stats(bn1, training),
-                                in_bn=(st0.scale, st0.shift, st0.nseg), y=y1)
+                                in_bn=(st0.scale, st0.shift, st0.nseg), y=y1, src_bound=b0)
     else:
         a0 = torch.empty_like(y0)
         hip.bn_relu_apply(nhwc(y0), st0.nseg, st0.scale, st0.shift, nhwc(a0))
-        y1, t1 = _conv3x3_stats(a0, wpk1, conv1.bias, conv1.out_channels, _bn_uses_batch_stats(bn1, training), y=y1)
-    st1 = _bn_forward(y1, bn1, nseg, training, t1)
+        y1, t1 = _conv3x3_stats(a0, wpk1, conv1.bias, conv1.out_channels, _bn_uses_batch_stats(bn1, training), y=y1,
+                                src_bound=b0)
+    b1 = _take(pool)
+    st1 = _bn_forward(y1, bn1, nseg, training, t1, b1)
     a1 = None
     if materialize:
         a1 = torch.empty_like(y1)
         hip.bn_relu_apply(nhwc(y1), st1.nseg, st1.scale, st1.shift, nhwc(a1))
-    saved = (x, y0, a0, st0, y1, st1) if save else None
-    return a1, saved, y1, st1
+        _set_bound(a1, b1)
+    saved = (x, y0, a0, st0, y1, st1, x_bound, b0) if save else None
+    return a1, saved, y1, st1, b1
 
 
-def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, src_bn=None) -> torch.Tensor:
-    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3, src_bn)
+def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, src_bn=None, rows_bound=None,
+              src_bound=None) -> torch.Tensor:
+    if rows_bound is None or src_bound is None:
+        rows_bound = src_bound = None
+    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3, src_bn, rows_bound, src_bound)
     slabs = _empty((nbytes // 4,), dy)
     hip.conv_wgrad(d, slabs)
     gw = torch.empty_like(weight)
@@ -333,9 +394,9 @@ class _PooledGrad:
     skip_mode: int
 
 
-def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None):
+def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, dy_bound=None):
     """`tiles` = (records, ntiles) of the partial sums from the conv epilogue that produced g; g may be a
-    _PooledGrad."""
+    _PooledGrad.  `dy_bound` (h2): a zeroed device float raised to max |dy|."""
     c = y.shape[3]
     dy = torch.empty_like(y)
     dgamma = _empty((c,), y)
@@ -347,53 +408,60 @@ def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None):
         hip.bn_relu_backward_pooled(nhwc(y), nhwc(g.gy) if g.gy is not None else hip._NULL, g.idx,
                                     nhwc(g.gskip) if g.gskip is not None else hip._NULL, g.skip_mode, st.nseg,
                                     st.smean, st.sinv, bn.weight, st.scale, st.shift, dgamma, dbeta, dbias, nhwc(dy),
-                                    ws)
+                                    ws, dy_bound)
     elif tiles is not None:
         hip.bn_relu_backward_tiles(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift,
-                                   tiles[0], tiles[1], dgamma, dbeta, dbias, nhwc(dy), ws)
+                                   tiles[0], tiles[1], dgamma, dbeta, dbias, nhwc(dy), ws, dy_bound)
     else:
         hip.bn_relu_backward(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift, dgamma,
-                             dbeta, dbias, nhwc(dy), ws)
+                             dbeta, dbias, nhwc(dy), ws, dy_bound)
     return dy, dgamma, dbeta, dbias
 
 
-def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Tensor, st0: _BNSaved):
+def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Tensor, st0: _BNSaved,
+                  src_bound=None):
     """Data-grad conv producing dL/da0, with BN0's backward partial sums fused into its epilogue when the kernel
     offers them.  Returns (ga0, tiles or None)."""
     n, h, w, _ = dy1.shape
     ga0 = _empty((n, h, w, n_out), dy1)
     if _OPTS['fuse_bn_bwd'] and st0.smean is not None:
-        ntiles, _ = hip.igemm_bn_bwd_tiles(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(ga0))
+        ntiles, _ = hip.igemm_bn_bwd_tiles(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(ga0), src_bound)
         if ntiles and ntiles % st0.nseg == 0:
             rec = _empty((n_out * ntiles * 2,), dy1)
             hip.conv_igemm(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, None, nhwc(ga0),
-                           bn_bwd=(y0, st0.nseg, st0.smean, st0.sinv, st0.scale, st0.shift, rec))
+                           bn_bwd=(y0, st0.nseg, st0.smean, st0.sinv, st0.scale, st0.shift, rec), src_bound=src_bound)
             return ga0, (rec, ntiles)
-    hip.conv_igemm(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, None, nhwc(ga0))
+    hip.conv_igemm(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, None, nhwc(ga0), src_bound=src_bound)
     return ga0, None
 
 
-def _dc_backward(g_out, saved, dc, need_dx: bool):
+def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None):
     """g_out: gradient of the block output (a tensor, or a _PooledGrad formed inside the BatchNorm backward).
-    Returns (grad wrt DoubleConv input or None, [8 param grads in dc_params order])."""
-    x, y0, a0, st0, y1, st1 = saved
+    Returns (grad wrt DoubleConv input or None, [8 param grads in dc_params order]).  `pool` (h2): bounds of the
+    two BatchNorm-backward outputs, the operands of the data-grad and weight-grad convs."""
+    x, y0, a0, st0, y1, st1, x_bound, b0 = saved
     s = dc.conv
     conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
     if st1.smean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported (call net.train())")
-    dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None)
+    d1 = _take(pool)
+    dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None, dy_bound=d1)
     if a0 is None:  # fused forward: the weight grad reads y0 through BN0 + ReLU as well
-        gw1 = _wgrad3x3(dy1, y0, conv1.weight, (st0.scale, st0.shift, st0.nseg))
+        gw1 = _wgrad3x3(dy1, y0, conv1.weight, (st0.scale, st0.shift, st0.nseg), d1, b0)
     else:
-        gw1 = _wgrad3x3(dy1, a0, conv1.weight)
-    ga0, tiles0 = _dgrad_bn_bwd(dy1, packed_conv3x3(conv1.weight, 1), conv1.in_channels, y0, st0)
-    dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0)
-    gw0 = _wgrad3x3(dy0, x, conv0.weight)
+        gw1 = _wgrad3x3(dy1, a0, conv1.weight, None, d1, b0)
+    ga0, tiles0 = _dgrad_bn_bwd(dy1, packed_conv3x3(conv1.weight, 1), conv1.in_channels, y0, st0, d1)
+    d0 = _take(pool)
+    dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0, d0)
+    gw0 = _wgrad3x3(dy0, x, conv0.weight, None, d0, x_bound)
     gx = None
     if need_dx:
         if x.shape[3] != conv0.in_channels:
             raise RuntimeError("input-gradient through a channel-padded first layer is not supported")
-        gx = _conv3x3(dy0, packed_conv3x3(conv0.weight, 1), None, conv0.in_channels)
+        n, h, w, _ = dy0.shape
+        gx = _empty((n, h, w, conv0.in_channels), dy0)
+        hip.conv_igemm(nhwc(dy0), h, w, 1, TAPS_3X3, packed_conv3x3(conv0.weight, 1), conv0.in_channels, None,
+                       nhwc(gx), src_bound=d0)
     return gx, [gw0, dbias0, dg0, db0, gw1, dbias1, dg1, db1]
 
 
@@ -460,6 +528,7 @@ class EncoderFn(torch.autograd.Function):
         blocks = meta.blocks
         feats, saved = [], []
         cur = x
+        pool, bound = _bounds(x), None
         for level, dc in enumerate(blocks):
             idx = None
             if level > 0:
@@ -467,8 +536,8 @@ class EncoderFn(torch.autograd.Function):
                 n, h, w, c = prev.shape
                 cur = _empty((n, h // 2, w // 2, c), prev)
                 idx = _empty((n, h // 2, w // 2, c), prev, dtype=torch.uint8)
-                hip.maxpool2_fwd(nhwc(prev), nhwc(cur), idx)
-            a, sv, _, _ = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save)
+                hip.maxpool2_fwd(nhwc(prev), nhwc(cur), idx)  # the pooled map keeps the level's bound
+            a, sv, _, _, bound = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save, pool=pool, x_bound=bound)
             feats.append(a)
             saved.append((idx, sv))
         if meta.save:
@@ -485,6 +554,7 @@ class EncoderFn(torch.autograd.Function):
         grads = [None] * (8 * len(blocks))
         g_pool = None
         dev_like = saved[0][1][1]
+        pool = _bounds(dev_like)
         for level in range(L, -1, -1):
             shape = ctx.feat_shapes[level]
             idx_next = saved[level + 1][0] if level < L else None
@@ -496,7 +566,7 @@ class EncoderFn(torch.autograd.Function):
                 hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL,
                                  idx_next if g_pool is not None else None, nhwc(gf) if gf is not None else hip._NULL,
                                  0, nhwc(ga))
-            gx, pg = _dc_backward(ga, saved[level][1], blocks[level], need_dx=level > 0)
+            gx, pg = _dc_backward(ga, saved[level][1], blocks[level], need_dx=level > 0, pool=pool)
             grads[8 * level:8 * level + 8] = pg
             g_pool = gx
         ctx.saved = None
@@ -540,6 +610,7 @@ class SiameseEncoderFn(torch.autograd.Function):
         cur = x
         prev = None  # (y1, st1) of the previous level
         pooled = None  # (pooled input, idx) of this level when the previous level's fused pass produced them
+        pool, bound = _bounds(x), None  # h2: bound of the previous level's activation = of this level's input
         for level, dc in enumerate(blocks):
             idx = None
             if pooled is not None:
@@ -550,7 +621,8 @@ class SiameseEncoderFn(torch.autograd.Function):
                 cur = _empty((n, h // 2, w // 2, c), y1p)
                 idx = _empty((n, h // 2, w // 2, c), y1p, dtype=torch.uint8)
                 hip.bn_relu_maxpool2_fwd(nhwc(y1p), st1p.nseg, st1p.scale, st1p.shift, nhwc(cur), idx)
-            _, sv, y1, st1 = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save, materialize=False)
+            _, sv, y1, st1, bound = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save, materialize=False,
+                                                pool=pool, x_bound=bound)
             n2, h, w, c = y1.shape
             extra = meta.extra.get(level, 0)
             buf = _empty((n2 // 2, h, w, c + extra), y1)
@@ -565,7 +637,7 @@ class SiameseEncoderFn(torch.autograd.Function):
                 pooled = (nxt, nidx)
             else:
                 hip.bn_relu_siamese_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c))
-            diffs.append(d)
+            diffs.append(_set_bound(d, bound))  # |a_t2 - a_t1| <= max(a_t1, a_t2) for ReLU outputs
             bufs.append(buf if extra else None)
             saved.append((idx, sv))
             prev = (y1, st1)
@@ -582,6 +654,7 @@ class SiameseEncoderFn(torch.autograd.Function):
         L = len(blocks) - 1
         grads = [None] * (8 * len(blocks))
         g_pool = None
+        pool = _bounds(saved[0][1][1])
         for level in range(L, -1, -1):
             idx_next = saved[level + 1][0] if level < L else None
             sv = saved[level][1]
@@ -594,7 +667,7 @@ class SiameseEncoderFn(torch.autograd.Function):
                 hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL,
                                  idx_next if g_pool is not None else None, nhwc(gd) if gd is not None else hip._NULL,
                                  1, nhwc(ga))
-            gx, pg = _dc_backward(ga, sv, blocks[level], need_dx=level > 0)
+            gx, pg = _dc_backward(ga, sv, blocks[level], need_dx=level > 0, pool=pool)
             grads[8 * level:8 * level + 8] = pg
             g_pool = gx
         ctx.saved = None
@@ -652,6 +725,7 @@ class DecoderFn(torch.autograd.Function):
         skips = rest[:len(ups)]
         cur = x_deep
         saved = []
+        pool = _bounds(x_deep)
         for k, up in enumerate(ups):
             skip = skips[k]
             b, h, w, cs = skip.shape
@@ -677,7 +751,11 @@ class DecoderFn(torch.autograd.Function):
             else:
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto),
                                store_mode=1)
-            a, sv, _, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save)
+            cat_bound = None
+            if pool is not None:  # the concat's bound: the skip's (raised in place: still a bound of the skip)
+                cat_bound = _bound_of(skip, pool)
+                hip.absmax_bound(nhwc(cat, cs, cto), cat_bound)
+            a, sv, _, _, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save, pool=pool, x_bound=cat_bound)
             saved.append((cur, cat, cs, sv))
             cur = a
         if meta.save:
@@ -695,10 +773,11 @@ class DecoderFn(torch.autograd.Function):
         g = g_out
         if g is None:
             return (None, None, *g_skips, *grads)
+        pool = _bounds(g)
         for k in range(n - 1, -1, -1):
             up = ups[k]
             cur, cat, cs, sv = saved[k]
-            g_cat, pg = _dc_backward(g, sv, up.conv, need_dx=True)
+            g_cat, pg = _dc_backward(g, sv, up.conv, need_dx=True, pool=pool)
             g_skips[k] = g_cat[..., :cs]
             convT = up.up
             cto = convT.out_channels

@@ -48,6 +48,7 @@ class IGEMM(ctypes.Structure):
         ("in_shift", c_void_p),
         ("in_nseg", c_int32),
         ("bn_bwd", POINTER(BNBWD)),
+        ("src_bound", c_void_p),
     ]
 
 
@@ -62,6 +63,8 @@ class WGRAD(ctypes.Structure):
         ("src_scale", c_void_p),
         ("src_shift", c_void_p),
         ("src_nseg", c_int32),
+        ("rows_bound", c_void_p),
+        ("src_bound", c_void_p),
     ]
 
 
@@ -89,6 +92,8 @@ _SIGS = {
     "scd_split_bf16x3": ([c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "scd_split_frag_bytes": ([c_int32, c_int32], c_size_t),
     "scd_split_bf16x3_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_split_h2_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_absmax_bound": ([NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "scd_conv_igemm": ([POINTER(IGEMM), c_void_p], c_int),
     "scd_igemm_arith": ([POINTER(IGEMM)], c_int),
     "scd_igemm_input_bn_supported": ([POINTER(IGEMM)], c_int),
@@ -102,28 +107,28 @@ _SIGS = {
     "scd_bn_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32], c_size_t),
     "scd_bn_train_stats": (
         [NHWC, c_int32, c_void_p, c_void_p, c_float, c_float, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
-         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+         c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
         c_int,
     ),
     "scd_bn_tile_stats_workspace_bytes": ([c_int32, c_int32, c_int32], c_size_t),
     "scd_bn_stats_from_tiles": (
         [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_float, c_float, c_int32, c_void_p,
-         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
         c_int,
     ),
     "scd_bn_eval_coeffs": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p], c_int),
     "scd_bn_relu_apply": ([NHWC, c_int32, c_void_p, c_void_p, NHWC, c_void_p], c_int),
     "scd_bn_relu_backward": (
         [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC,
-         c_void_p, c_size_t, c_void_p],
+         c_void_p, c_void_p, c_size_t, c_void_p],
         c_int,
     ),
     "scd_bn_relu_backward_pooled": ([NHWC, NHWC, c_void_p, NHWC, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
-                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_size_t,
-                                     c_void_p], c_int),
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p,
+                                     c_size_t, c_void_p], c_int),
     "scd_bn_relu_backward_tiles": (
         [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
-         c_void_p, c_void_p, NHWC, c_void_p, c_size_t, c_void_p],
+         c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_size_t, c_void_p],
         c_int,
     ),
     "scd_channel_sum": ([NHWC, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
@@ -253,7 +258,7 @@ def pack_conv3x3(w: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch
     out = torch.empty((co * 9 * ci_pad) if mode == 0 else (ci * 9 * co), device=w.device, dtype=torch.float32)
     _check(lib().scd_pack_conv3x3(w.contiguous().data_ptr(), co, ci, ci_pad, mode, out.data_ptr(), _stream()),
            "scd_pack_conv3x3")
-    return _attach_split(out, co, 9 * ci_pad) if mode == 0 else _attach_split(out, ci, 9 * co)
+    return _attach_split(out, co, 9 * ci_pad, True) if mode == 0 else _attach_split(out, ci, 9 * co, True)
 
 
 class PACKJOB(ctypes.Structure):
@@ -300,6 +305,15 @@ def split_bf16x3(src: torch.Tensor) -> torch.Tensor:
     return dst
 
 
+def split_h2_frag(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
+    """SCD_MATH_H2 weight split of a packed [n_out][K] fp32 matrix: fp16 h, m planes of the per-row power-of-two
+    scaled rows, then the float inverse row scales (see scd.h)."""
+    nbytes = lib().scd_split_frag_bytes(n_out, K)
+    dst = torch.empty(nbytes // 2, dtype=torch.int16, device=wpk.device)
+    _check(lib().scd_split_h2_frag(wpk.data_ptr(), n_out, K, dst.data_ptr(), _stream()), "scd_split_h2_frag")
+    return dst
+
+
 def split_bf16x3_frag(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
     """Fragment-major exact 3-way bf16 split of a packed [n_out][K] fp32 weight matrix (see scd.h)."""
     nbytes = lib().scd_split_frag_bytes(n_out, K)
@@ -308,15 +322,21 @@ def split_bf16x3_frag(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
     return dst
 
 
-def _attach_split(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
-    """Under the x3 conv math, pre-split packed weights once so every workgroup stages them by copy."""
-    if K % 16 == 0 and conv_math() != 'f32':  # x3 and bf16 both read the split planes
-        wpk._x3 = split_bf16x3_frag(wpk, n_out, K)
+def h2_weight_format(K: int, conv3x3: bool) -> bool:
+    """Whether the library expects the h2 split for a conv of this contraction (mirrors h2_weight_format in
+    conv_common.h: 3x3 convs whose source channels are a multiple of 32, under SCD_MATH_H2)."""
+    return conv3x3 and K % 9 == 0 and (K // 9) % 32 == 0 and conv_math() == 'h2'
+
+
+def _attach_split(wpk: torch.Tensor, n_out: int, K: int, conv3x3: bool = False) -> torch.Tensor:
+    """Under the split conv arithmetics, pre-split packed weights once so every workgroup stages them by copy."""
+    if K % 16 == 0 and conv_math() != 'f32':  # x3, x5, bf16 and h2 all read split planes
+        wpk._x3 = split_h2_frag(wpk, n_out, K) if h2_weight_format(K, conv3x3) else split_bf16x3_frag(wpk, n_out, K)
     return wpk
 
 
-MATH_F32, MATH_X3, MATH_BF16, MATH_X5 = 0, 1, 2, 3
-_MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3, 'bf16': MATH_BF16, 'x5': MATH_X5}
+MATH_F32, MATH_X3, MATH_BF16, MATH_X5, MATH_H2 = 0, 1, 2, 3, 4
+_MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3, 'bf16': MATH_BF16, 'x5': MATH_X5, 'h2': MATH_H2}
 
 
 def set_conv_math(mode) -> str:
@@ -356,7 +376,7 @@ def conv_math() -> str:
 
 
 def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None, in_bn=None,
-                bn_bwd=None):
+                bn_bwd=None, src_bound=None):
     nt, dy, dx = _taps(taps)
     sc, sh, nseg = in_bn if in_bn is not None else (None, None, 0)
     bb = None
@@ -364,31 +384,35 @@ def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mo
         y, bseg, mu, iv, bsc, bsh, rec = bn_bwd
         bb = ctypes.pointer(BNBWD(nhwc(y), bseg, _ptr(mu), _ptr(iv), _ptr(bsc), _ptr(bsh), _ptr(rec)))
     return IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
-                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg, bb)
+                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg, bb, _ptr(src_bound))
 
 
 def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
-               bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None, in_bn=None, bn_bwd=None):
+               bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None, in_bn=None, bn_bwd=None,
+               src_bound: torch.Tensor | None = None):
     """`in_bn` = (scale, shift, nseg): read src through the producing layer's BatchNorm-apply + ReLU.
     `bn_bwd` = (y, nseg, save_mean, save_invstd, scale, shift, rec): also emit the BatchNorm-backward partial
-    sums of the stored output into rec (see scd_bn_bwd_tiles_t)."""
-    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec, in_bn, bn_bwd)
+    sums of the stored output into rec (see scd_bn_bwd_tiles_t).
+    `src_bound`: device float >= max |src as read| (SCD_MATH_H2 operand scaling; see scd_igemm_t.src_bound)."""
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec, in_bn, bn_bwd,
+                    src_bound)
     _check(lib().scd_conv_igemm(ctypes.byref(d), _stream()), "scd_conv_igemm")
 
 
 def igemm_bn_bwd_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
-                       dst: NHWC) -> tuple[int, int]:
+                       dst: NHWC, src_bound=None) -> tuple[int, int]:
     """(tiles, pixels per tile) of the fused BatchNorm-backward partial sums for this conv, (0, 0) if unavailable."""
-    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0)
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0, src_bound=src_bound)
     tp = c_int32(0)
     n = lib().scd_igemm_bn_bwd_tiles(ctypes.byref(d), ctypes.byref(tp))
     return (n, tp.value) if n > 0 else (0, 0)
 
 
 def igemm_arith(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
-                dst: NHWC, store_mode: int = 0) -> str:
-    """The arithmetic ('f32', 'x3', 'bf16') scd_conv_igemm would use for this conv under the current mode."""
-    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, store_mode)
+                dst: NHWC, store_mode: int = 0, src_bound=None) -> str:
+    """The arithmetic ('f32', 'x3', 'x5', 'bf16', 'h2') scd_conv_igemm would use for this conv under the current
+    mode."""
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, store_mode, src_bound=src_bound)
     rc = lib().scd_igemm_arith(ctypes.byref(d))
     _check(min(rc, 0), "scd_igemm_arith")
     return {v: k for k, v in _MATH_NAMES.items()}[rc]
@@ -402,25 +426,27 @@ def wgrad_arith(d: 'WGRAD') -> str:
 
 
 def igemm_input_bn_supported(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
-                             dst: NHWC, in_bn) -> bool:
-    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0, None, in_bn)
+                             dst: NHWC, in_bn, src_bound=None) -> bool:
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0, None, in_bn, src_bound=src_bound)
     return lib().scd_igemm_input_bn_supported(ctypes.byref(d)) == 1
 
 
 def igemm_stat_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
-                     dst: NHWC) -> tuple[int, int]:
+                     dst: NHWC, src_bound=None) -> tuple[int, int]:
     """(tiles, pixels per tile) of the conv-fused BatchNorm statistics for this conv, (0, 0) if unavailable."""
-    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0)
+    d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, 0, src_bound=src_bound)
     tp = c_int32(0)
     n = lib().scd_igemm_stat_tiles(ctypes.byref(d), ctypes.byref(tp))
     return (n, tp.value) if n > 0 else (0, 0)
 
 
-def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None):
-    """`src_bn` = (scale, shift, nseg): read src through its BatchNorm-apply + ReLU (see scd_wgrad_t)."""
+def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None, rows_bound=None, src_bound=None):
+    """`src_bn` = (scale, shift, nseg): read src through its BatchNorm-apply + ReLU (see scd_wgrad_t).
+    `rows_bound` / `src_bound`: device floats bounding |rows| and |src as read| (SCD_MATH_H2; both or neither)."""
     nt, dy, dx = _taps(taps)
     sc, sh, nseg = src_bn if src_bn is not None else (None, None, 0)
-    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg)
+    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg, _ptr(rows_bound), _ptr(src_bound))
+    d._keep = (rows_bound, src_bound)
     ns = c_int32(0)
     nb = c_size_t(0)
     _check(lib().scd_wgrad_plan(ctypes.byref(d), ctypes.byref(ns), ctypes.byref(nb)), "scd_wgrad_plan")
@@ -430,7 +456,7 @@ def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None):
 def wgrad_src_bn_supported(rows: NHWC, src: NHWC, stride: int, taps, src_bn) -> bool:
     nt, dy, dx = _taps(taps)
     sc, sh, nseg = src_bn
-    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg)
+    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg, None, None)
     return lib().scd_wgrad_src_bn_supported(ctypes.byref(d)) == 1
 
 
@@ -447,11 +473,13 @@ def bn_workspace_bytes(n, h, w, c, nseg) -> int:
     return lib().scd_bn_workspace_bytes(n, h, w, c, nseg)
 
 
-def bn_train_stats(y: NHWC, nseg, gamma, beta, eps, momentum, update, rmean, rvar, smean, sinv, scale, shift, ws):
+def bn_train_stats(y: NHWC, nseg, gamma, beta, eps, momentum, update, rmean, rvar, smean, sinv, scale, shift, ws,
+                   act_bound=None):
+    """`act_bound`: device float raised to a bound of |relu(BN(y))| (SCD_MATH_H2 operand scaling)."""
     _check(
         lib().scd_bn_train_stats(y, nseg, _ptr(gamma), _ptr(beta), eps, momentum, int(update), _ptr(rmean), _ptr(rvar),
-                                 smean.data_ptr(), sinv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(),
-                                 ws.numel(), _stream()),
+                                 smean.data_ptr(), sinv.data_ptr(), scale.data_ptr(), shift.data_ptr(), _ptr(act_bound),
+                                 ws.data_ptr(), ws.numel(), _stream()),
         "scd_bn_train_stats")
 
 
@@ -460,12 +488,12 @@ def bn_tile_stats_workspace_bytes(ntiles, c, nseg) -> int:
 
 
 def bn_stats_from_tiles(tile_rec, ntiles, tile_px, c, nseg, gamma, beta, eps, momentum, update, rmean, rvar, smean,
-                        sinv, scale, shift, ws):
+                        sinv, scale, shift, ws, act_bound=None):
     _check(
         lib().scd_bn_stats_from_tiles(tile_rec.data_ptr(), ntiles, tile_px, c, nseg, _ptr(gamma), _ptr(beta), eps,
                                       momentum, int(update), _ptr(rmean), _ptr(rvar), smean.data_ptr(),
-                                      sinv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(), ws.numel(),
-                                      _stream()),
+                                      sinv.data_ptr(), scale.data_ptr(), shift.data_ptr(), _ptr(act_bound),
+                                      ws.data_ptr(), ws.numel(), _stream()),
         "scd_bn_stats_from_tiles",
     )
 
@@ -475,35 +503,42 @@ def bn_eval_coeffs(c, gamma, beta, rmean, rvar, eps, scale, shift):
                                     scale.data_ptr(), shift.data_ptr(), _stream()), "scd_bn_eval_coeffs")
 
 
+def absmax_bound(x: NHWC, bound: torch.Tensor, nseg: int = 1, scale=None, shift=None):
+    """bound = max(bound, max |x|) (or of relu(x * scale + shift) per segment); bound is a device float."""
+    _check(lib().scd_absmax_bound(x, nseg, _ptr(scale), _ptr(shift), bound.data_ptr(), _stream()), "scd_absmax_bound")
+
+
 def bn_relu_apply(y: NHWC, nseg, scale, shift, a: NHWC):
     _check(lib().scd_bn_relu_apply(y, nseg, scale.data_ptr(), shift.data_ptr(), a, _stream()), "scd_bn_relu_apply")
 
 
-def bn_relu_backward(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, dgamma, dbeta, dbias, dy: NHWC, ws):
+def bn_relu_backward(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, dgamma, dbeta, dbias, dy: NHWC, ws,
+                     dy_bound=None):
+    """`dy_bound`: device float raised to max |dy| (SCD_MATH_H2 operand scaling of the convs reading dy)."""
     _check(
         lib().scd_bn_relu_backward(y, da, nseg, smean.data_ptr(), sinv.data_ptr(), _ptr(gamma), scale.data_ptr(),
-                                   shift.data_ptr(), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), dy, ws.data_ptr(),
-                                   ws.numel(), _stream()),
+                                   shift.data_ptr(), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), dy, _ptr(dy_bound),
+                                   ws.data_ptr(), ws.numel(), _stream()),
         "scd_bn_relu_backward")
 
 
 def bn_relu_backward_pooled(y: NHWC, gy: NHWC, idx, gskip: NHWC, skip_mode: int, nseg, smean, sinv, gamma, scale,
-                            shift, dgamma, dbeta, dbias, dy: NHWC, ws):
+                            shift, dgamma, dbeta, dbias, dy: NHWC, ws, dy_bound=None):
     """bn_relu_backward of da = maxpool_bwd(gy, idx) -/+ gskip (feature_grad's operand, never materialised)."""
     _check(
         lib().scd_bn_relu_backward_pooled(y, gy, _ptr(idx), gskip, skip_mode, nseg, smean.data_ptr(), sinv.data_ptr(),
                                           _ptr(gamma), scale.data_ptr(), shift.data_ptr(), _ptr(dgamma), _ptr(dbeta),
-                                          _ptr(dbias), dy, ws.data_ptr(), ws.numel(), _stream()),
+                                          _ptr(dbias), dy, _ptr(dy_bound), ws.data_ptr(), ws.numel(), _stream()),
         "scd_bn_relu_backward_pooled")
 
 
 def bn_relu_backward_tiles(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, tile_rec, ntiles, dgamma, dbeta,
-                           dbias, dy: NHWC, ws):
+                           dbias, dy: NHWC, ws, dy_bound=None):
     """bn_relu_backward with the partial sums from conv-epilogue tile records (conv_igemm(..., bn_bwd=...))."""
     _check(
         lib().scd_bn_relu_backward_tiles(y, da, nseg, smean.data_ptr(), sinv.data_ptr(), _ptr(gamma), scale.data_ptr(),
                                          shift.data_ptr(), tile_rec.data_ptr(), ntiles, _ptr(dgamma), _ptr(dbeta),
-                                         _ptr(dbias), dy, ws.data_ptr(), ws.numel(), _stream()),
+                                         _ptr(dbias), dy, _ptr(dy_bound), ws.data_ptr(), ws.numel(), _stream()),
         "scd_bn_relu_backward_tiles")
 
 

@@ -7,6 +7,7 @@ import sys
 
 import numpy as np
 import torch
+
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -61,9 +62,9 @@ def run(n, h, w, cin_real, cpad, cout, nseg, seed=0):
     xp = torch.empty(n, h, w, cpad, device=dev)
     xd = x.to(dev)
     hip.pack_nchw(xd, 0, cin_real, xp)
-    a1h, saved = engine._dc_forward(xp, dcd, nseg, True, True)
+    a1h, saved, *_ = engine._dc_forward(xp, dcd, nseg, True, True)
     gd = nhwc(g).to(dev)
-    xs, y0h, a0h, st0, y1h, st1 = saved
+    xs, y0h, a0h, st0, y1h, st1 = saved[:6]
     print(f'n={n} {h}x{w} cin={cin_real}(pad {cpad}) cout={cout} nseg={nseg}')
     print(f'  fwd  y0 {rel(y0h.cpu(), nhwc(y0)):.1e} a0 {rel(a0h.cpu(), nhwc(a0)):.1e} y1 {rel(y1h.cpu(), nhwc(y1)):.1e}'
           f' a1 {rel(a1h.cpu(), nhwc(a1)):.1e}')
@@ -71,7 +72,9 @@ def run(n, h, w, cin_real, cpad, cout, nseg, seed=0):
     dy1, dg1, db1, dbias1 = engine._bn_backward(y1h, gd, st1, bn1, True)
     print(f'  bn1  dy1 {rel(dy1.cpu(), nhwc(y1.grad)):.1e} dgamma {rel(dg1.cpu(), P["conv.4.weight"].grad):.1e}'
           f' dbeta {rel(db1.cpu(), P["conv.4.bias"].grad):.1e}')
-    ga0 = engine._conv3x3(dy1, hip.pack_conv3x3(conv1.weight.detach(), 1), None, conv1.in_channels)
+    ga0 = torch.empty(dy1.shape[:3] + (conv1.in_channels,), device=dev)
+    hip.conv_igemm(hip.nhwc(dy1), dy1.shape[1], dy1.shape[2], 1, hip.TAPS_3X3, hip.pack_conv3x3(conv1.weight.detach(), 1),
+                   conv1.in_channels, None, hip.nhwc(ga0))
     print(f'  dX1  ga0 {rel(ga0.cpu(), nhwc(a0.grad)):.1e}')
     gw1 = engine._wgrad3x3(dy1, a0h, conv1.weight)
     print(f'  dW1  {rel(gw1.cpu(), P["conv.3.weight"].grad):.1e}')
@@ -164,8 +167,8 @@ def run_fixture(name='siamese_t8-16'):
     xp = torch.empty(n, x.shape[2], x.shape[3], 8, device=dev)
     xd = x.to(dev)
     hip.pack_nchw(xd, 0, 5, xp)
-    a1h, saved = engine._dc_forward(xp, dcd, 2, True, True)
-    xs, y0h, a0h, st0, y1h, st1 = saved
+    a1h, saved, *_ = engine._dc_forward(xp, dcd, 2, True, True)
+    xs, y0h, a0h, st0, y1h, st1 = saved[:6]
     am, bm = (a0h.cpu() > 0), (nhwc(a0) > 0)
     bad = (am != bm).nonzero()
     print('  a0 mask mismatches', bad.shape[0], 'z at mismatches', nhwc(torch.cat(z0))[am != bm][:8].tolist())

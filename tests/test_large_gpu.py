@@ -30,10 +30,11 @@ def big(dev):
     return x
 
 
-@pytest.mark.parametrize('math', ['x3', 'bf16'])
+@pytest.mark.parametrize('math', ['x3', 'bf16', 'h2'])
 def test_igemm_over_2gib_matches_image_halves(dev, big, math):
     from multimodal_siamese_cd_amd import hip
     prev = hip.set_conv_math(math)
+    ub = torch.full((1,), 64.0, device=dev) if math == 'h2' else None  # h2: a (loose) bound of the BN'd input
     try:
         g = torch.Generator(device=dev).manual_seed(6)
         wt = torch.randn(CO, C, 3, 3, device=dev, generator=g) / 24
@@ -42,12 +43,14 @@ def test_igemm_over_2gib_matches_image_halves(dev, big, math):
         sh = torch.randn(2 * C, device=dev, generator=g)
         wpk = hip.pack_conv3x3(wt, 0)
         y = torch.empty(N, H, W, CO, device=dev)
-        ntiles, tpx = hip.igemm_stat_tiles(hip.nhwc(big), H, W, 1, hip.TAPS_3X3, wpk, CO, hip.nhwc(y))
+        ntiles, tpx = hip.igemm_stat_tiles(hip.nhwc(big), H, W, 1, hip.TAPS_3X3, wpk, CO, hip.nhwc(y), src_bound=ub)
         assert ntiles > 0, 'fused statistics must stay available above 2 GiB'
         bn = (sc, sh, 2)
-        assert hip.igemm_input_bn_supported(hip.nhwc(big), H, W, 1, hip.TAPS_3X3, wpk, CO, hip.nhwc(y), bn)
+        assert hip.igemm_input_bn_supported(hip.nhwc(big), H, W, 1, hip.TAPS_3X3, wpk, CO, hip.nhwc(y), bn, ub)
+        assert hip.igemm_arith(hip.nhwc(big), H, W, 1, hip.TAPS_3X3, wpk, CO, hip.nhwc(y), src_bound=ub) == math
         rec = torch.empty(ntiles * CO * 2, device=dev)
-        hip.conv_igemm(hip.nhwc(big), H, W, 1, hip.TAPS_3X3, wpk, CO, b, hip.nhwc(y), stat_rec=rec, in_bn=bn)
+        hip.conv_igemm(hip.nhwc(big), H, W, 1, hip.TAPS_3X3, wpk, CO, b, hip.nhwc(y), stat_rec=rec, in_bn=bn,
+                       src_bound=ub)
         half = N // 2  # one BatchNorm segment each
         tpi = ntiles // N
         for i in range(2):
@@ -55,23 +58,25 @@ def test_igemm_over_2gib_matches_image_halves(dev, big, math):
             ys = torch.empty(half, H, W, CO, device=dev)
             rs = torch.empty(tpi * half * CO * 2, device=dev)
             hip.conv_igemm(hip.nhwc(xs), H, W, 1, hip.TAPS_3X3, wpk, CO, b, hip.nhwc(ys), stat_rec=rs,
-                           in_bn=(sc[i * C:(i + 1) * C], sh[i * C:(i + 1) * C], 1))
+                           in_bn=(sc[i * C:(i + 1) * C], sh[i * C:(i + 1) * C], 1), src_bound=ub)
             assert torch.equal(ys, y[i * half:(i + 1) * half])
             assert torch.equal(rs, rec[i * tpi * half * CO * 2:(i + 1) * tpi * half * CO * 2])
     finally:
         hip.set_conv_math(prev)
 
 
-@pytest.mark.parametrize('math', ['x3', 'bf16'])
+@pytest.mark.parametrize('math', ['x3', 'bf16', 'h2'])
 def test_wgrad_over_2gib_matches_sum_of_halves(dev, big, math):
     from multimodal_siamese_cd_amd import hip
     prev = hip.set_conv_math(math)
+    ub = torch.full((1,), 16.0, device=dev) if math == 'h2' else None  # h2: bound of the N(0, 1) operands
     try:
         g = torch.Generator(device=dev).manual_seed(8)
         dy = torch.randn(N, H, W, CO, device=dev, generator=g)
 
         def wgrad(rows, src):
-            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(rows), hip.nhwc(src), 1, hip.TAPS_3X3)
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(rows), hip.nhwc(src), 1, hip.TAPS_3X3, None, ub, ub)
+            assert hip.wgrad_arith(d) == math
             slabs = torch.empty(nbytes // 4, device=dev)
             hip.conv_wgrad(d, slabs)
             dw = torch.empty(CO, C, 3, 3, device=dev)

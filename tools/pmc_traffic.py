@@ -55,6 +55,7 @@ def main():
     ap.add_argument('dir')
     ap.add_argument('--steps', type=int, required=True, help='training steps covered by the pass')
     ap.add_argument('--out', default=None)
+    ap.add_argument('--math', default='h2', help='conv arithmetic the profiled bench ran (bench.py matches it)')
     ap.add_argument('--summaries', default=None,
                     help='prefix for per-kernel CSVs: <prefix>_pmc_fetch_summary.csv / _pmc_write_summary.csv')
     args = ap.parse_args()
@@ -66,7 +67,7 @@ def main():
     write, nw = load(os.path.join(args.dir, 'write', 'run_counter_collection.csv'), 'WRITE_SIZE')
     res = {'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over bench.py, '
                      'FETCH_SIZE x2 (gfx950 wide-read correction), KiB x 1024',
-           'steps': args.steps, 'per_step_bytes': {}, 'launches_per_step': {}}
+           'steps': args.steps, 'math': args.math, 'per_step_bytes': {}, 'launches_per_step': {}}
     total = 0.0
     for fam in FAMILIES.values():
         b = (2.0 * fetch[fam] + write[fam]) * 1024.0 / args.steps
