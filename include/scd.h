@@ -204,6 +204,10 @@ typedef struct scd_igemm {
      * fp16 (inf / NaN outputs); a loose one only lowers the absolute floor (2^-39 U).  NULL = the x3 kernels
      * (per-tap, fp32 weights split on the fly). */
     const float *src_bound;
+    /* Optional (store_mode 1, the ConvTranspose forward): device float raised to max |stored output| as the
+     * epilogue writes it (atomic integer max; caller-zeroed or holding an earlier bound) -- the SCD_MATH_H2 bound of
+     * the concat buffer the output lands in, without a pass over it.  NULL = off. */
+    float *dst_bound;
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);

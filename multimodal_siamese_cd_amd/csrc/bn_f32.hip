@@ -355,6 +355,165 @@ struct DaPooled {
     }
 };
 
+// The DaPooled gradient over 2x2 cells: cell (img, cy, cx) covers the full-resolution pixels (2cy + i, 2cx + j) that
+// exist (ceil(h/2) x ceil(w/2) cells per image), so the pooled gradient and its argmax bytes are read and decoded once
+// per cell instead of once per pixel, with the cell's four pixels' loads in flight together.
+struct PooledCells {
+    DaPooled da;
+    int ch, cw;                 // cells per image column / row
+    FastDiv div_cimg, div_cw;   // ch * cw, cw
+};
+
+// dL/da of the four pixels of `cell` (flat cell index over images) at channel quad c; ok[k]: pixel k exists.
+__device__ __forceinline__ void cell_grads(const PooledCells &P, uint32_t cell, int c, f4 (&g)[4], int64_t (&pix)[4],
+                                           bool (&ok)[4]) {
+    const DaPooled &d = P.da;
+    const uint32_t img = fdiv(cell, P.div_cimg);
+    const uint32_t r = cell - img * uint32_t(P.ch * P.cw);
+    const int cy = int(fdiv(r, P.div_cw)), cx = int(r) - cy * P.cw;
+    f4 gp = {0.f, 0.f, 0.f, 0.f};
+    uint32_t pk = 0xffffffffu;  // no pooled gradient: no byte matches a sub-pixel
+    if (d.gy && cy < d.hy && cx < d.wy) {
+        const int64_t q = (int64_t(img) * d.hy + cy) * d.wy + cx;
+        pk = *reinterpret_cast<const uint32_t *>(d.idx + q * d.C + c);
+        gp = ld4(d.gy + q * d.ldgy + c);
+    }
+    int simg = 0;
+    float sg = 1.f;
+    if (d.gs) {
+        simg = int(img - fdiv(img, d.div_gsn) * uint32_t(d.gsn));
+        sg = (d.skip_mode == 1 && int(img) < d.gsn) ? -1.f : 1.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int yy = 2 * cy + (k >> 1), xx = 2 * cx + (k & 1);
+        ok[k] = yy < d.hx && xx < d.wx;
+        pix[k] = (int64_t(img) * d.hx + yy) * d.wx + xx;
+        const uint32_t want = uint32_t(k);
+        f4 v = {((pk >> 0) & 0xff) == want ? gp.x : 0.f, ((pk >> 8) & 0xff) == want ? gp.y : 0.f,
+                ((pk >> 16) & 0xff) == want ? gp.z : 0.f, ((pk >> 24) & 0xff) == want ? gp.w : 0.f};
+        if (d.gs && ok[k]) {
+            const f4 sv = ld4(d.gs + ((int64_t(simg) * d.hx + yy) * d.wx + xx) * d.ldgs + c);
+            v.x += sg * sv.x;
+            v.y += sg * sv.y;
+            v.z += sg * sv.z;
+            v.w += sg * sv.w;
+        }
+        g[k] = v;
+    }
+}
+
+// bn_bwd_partial over cells: rec[c][chunk][2] = {sum dz, sum dz*xhat} of the chunk's cells' pixels.
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const float *__restrict__ y, int ldy, PooledCells P,
+                                                                    int C, int64_t cseg, int ncps, int chunk, int nrec,
+                                                                    int qpb, const float *smean, const float *sinv,
+                                                                    const float *scale, const float *shift,
+                                                                    float *__restrict__ rec) {
+    __shared__ f4 sh1[BN_THREADS], sh2[BN_THREADS];
+    const int tid = threadIdx.x;
+    const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
+    const int c = (blockIdx.y * qpb + q) * 4;
+    const Chunk ch = chunk_of(cseg, ncps, chunk);
+    f4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
+    if (c < C) {
+        const int o = ch.seg * C + c;
+        const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
+        for (int64_t cell = ch.beg + pl; cell < ch.end; cell += npl) {
+            f4 g[4];
+            int64_t pix[4];
+            bool ok[4];
+            cell_grads(P, uint32_t(cell), c, g, pix, ok);
+            f4 yv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) yv[k] = ok[k] ? ld4(y + pix[k] * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) {
+                    const f4 z = relu_mask(yv[k], sc, sf, g[k]);
+                    s1 += z;
+                    s2 += z * ((yv[k] - mu) * iv);
+                }
+        }
+    }
+    sh1[tid] = s1;
+    sh2[tid] = s2;
+    __syncthreads();
+    for (int off = npl / 2; off > 0; off >>= 1) {
+        if (pl < off) {
+            sh1[tid] += sh1[tid + off * qpb];
+            sh2[tid] += sh2[tid + off * qpb];
+        }
+        __syncthreads();
+    }
+    if (pl == 0 && c < C) {
+        const f4 a = sh1[tid], b = sh2[tid];
+        const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float *r = rec + (size_t(c + k) * nrec + blockIdx.x) * 2;
+            r[0] = av[k];
+            r[1] = bv[k];
+        }
+    }
+}
+
+// bn_bwd_apply over cells (see bn_bwd_pooled_partial); brec[c][chunk] (conv bias grad) and dy_bound optional.
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const float *__restrict__ y, int ldy, PooledCells P,
+                                                                  float *__restrict__ dy, int lddy, int C, int64_t cseg,
+                                                                  int ncps, int chunk, int nrec, int qpb,
+                                                                  const float *smean, const float *sinv,
+                                                                  const float *gamma, const float *scale,
+                                                                  const float *shift, const float *coef,
+                                                                  float *__restrict__ brec, float *dy_bound) {
+    __shared__ f4 sh[BN_THREADS];
+    const int tid = threadIdx.x;
+    const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
+    const int c = (blockIdx.y * qpb + q) * 4;
+    const Chunk ch = chunk_of(cseg, ncps, chunk);
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    f4 amax = acc;
+    if (c < C) {
+        const int o = ch.seg * C + c;
+        const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
+        const float *cf = coef + size_t(o) * 2;
+        const f4 k1 = {cf[0], cf[2], cf[4], cf[6]};
+        const f4 k2 = {cf[1], cf[3], cf[5], cf[7]};
+        const f4 gm = gamma ? ld4(gamma + c) : f4{1.f, 1.f, 1.f, 1.f};
+        const f4 mul = gm * iv;
+        for (int64_t cell = ch.beg + pl; cell < ch.end; cell += npl) {
+            f4 g[4];
+            int64_t pix[4];
+            bool ok[4];
+            cell_grads(P, uint32_t(cell), c, g, pix, ok);
+            f4 yv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) yv[k] = ok[k] ? ld4(y + pix[k] * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) {
+                    const f4 ov = mul * (relu_mask(yv[k], sc, sf, g[k]) - k1 - ((yv[k] - mu) * iv) * k2);
+                    st4(dy + pix[k] * lddy + c, ov);
+                    acc += ov;
+                    amax = fmax4(amax, fabs4(ov));
+                }
+        }
+    }
+    if (dy_bound) wave_max_bound(dy_bound, fmaxf(fmaxf(amax.x, amax.y), fmaxf(amax.z, amax.w)));
+    if (!brec) return;  // uniform
+    sh[tid] = acc;
+    __syncthreads();
+    for (int off = npl / 2; off > 0; off >>= 1) {
+        if (pl < off) sh[tid] += sh[tid + off * qpb];
+        __syncthreads();
+    }
+    if (pl == 0 && c < C) {
+        const f4 a = sh[tid];
+        const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) brec[size_t(c + k) * nrec + blockIdx.x] = av[k];
+    }
+}
+
 // per (chunk) record {sum dz, sum dz*xhat}, rec[c][chunk][2]
 template <class DA>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__restrict__ y, int ldy, DA da, int C,
@@ -745,6 +904,44 @@ static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *s
                        dbias_prev ? brec : nullptr, dy_bound);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
 }
+// The encoder levels' BatchNorm backward with the pooled gradient (DaPooled) over 2x2 cells.  The chunks partition
+// each segment's cells into at most bn_geom's chunk count, so the records fit the same workspace.
+// SCD_BN_POOLED_CELLS=0 runs the per-pixel kernels instead (A/B switch, read at launch).
+static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled &da, int nseg, const float *save_mean,
+                                   const float *save_invstd, const float *gamma, const float *scale, const float *shift,
+                                   float *dgamma, float *dbeta, float *dbias_prev, const scd_nhwc_t &dy,
+                                   float *dy_bound, void *ws, hipStream_t s) {
+    const char *e = getenv("SCD_BN_POOLED_CELLS");
+    if (e && e[0] == '0') {
+        bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy,
+                        dy_bound, ws, s);
+        return;
+    }
+    const BnGeom g = bn_geom(y, nseg);
+    PooledCells P;
+    P.da = da;
+    P.ch = (y.h + 1) / 2;
+    P.cw = (y.w + 1) / 2;
+    P.div_cimg = make_fastdiv(uint32_t(P.ch * P.cw));
+    P.div_cw = make_fastdiv(uint32_t(P.cw));
+    const int64_t cseg = int64_t(y.n / nseg) * P.ch * P.cw;
+    const int chunk = int((cseg + g.ncps - 1) / g.ncps);
+    const int ncps = int((cseg + chunk - 1) / chunk);
+    const int nrec = nseg * ncps;
+    float *rec = static_cast<float *>(ws);
+    float *brec = rec + size_t(g.nrec) * y.c * 2;
+    float *coef = brec + size_t(g.nrec) * y.c;
+    hipLaunchKernelGGL(bn_bwd_pooled_partial, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       static_cast<const float *>(y.data), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
+                       save_invstd, scale, shift, rec);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, ncps, nrec, g.pseg, coef,
+                       dgamma, dbeta);
+    hipLaunchKernelGGL(bn_bwd_pooled_apply, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       static_cast<const float *>(y.data), y.ldc, P, static_cast<float *>(dy.data), dy.ldc, y.c, cseg,
+                       ncps, chunk, nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
+                       dbias_prev ? brec : nullptr, dy_bound);
+    if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, nrec, dbias_prev);
+}
 }  // namespace scd
 
 extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
@@ -814,8 +1011,8 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
     da.div_hw = make_fastdiv(uint32_t(y.h * y.w));
     da.div_w = make_fastdiv(uint32_t(y.w));
     da.div_gsn = make_fastdiv(uint32_t(da.gsn));
-    bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy, dy_bound,
-                    ws, as_stream(stream));
+    bn_backward_run_pooled(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy,
+                           dy_bound, ws, as_stream(stream));
     return launch_status("scd_bn_relu_backward_pooled");
 }
 

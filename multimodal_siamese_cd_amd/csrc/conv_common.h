@@ -87,6 +87,7 @@ struct IgemmArgs {
     // SCD_MATH_H2: device pointer to an upper bound of |src| as the kernel reads it (after the input transform);
     // the weight planes in wsplit are then the fp16 two-term split with per-row inverse scales (h2_wsplit_bytes)
     const float *src_bound;
+    float *dst_bound;  // optional: raised to max |stored output| (per-tap x3 kernel only; scd_igemm_t.dst_bound)
 };
 
 struct WgradArgs {

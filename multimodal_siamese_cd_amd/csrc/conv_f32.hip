@@ -610,6 +610,11 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
         a.src_bytes = sb < (int64_t(1) << 31) ? uint32_t(sb) : 0u;
     }
     a.src_bound = d->src_bound;
+    a.dst_bound = d->dst_bound;
+    if (d->dst_bound && d->store_mode != 1) {
+        set_error("igemm: dst_bound is produced by the ConvTranspose (store_mode 1) kernels only");
+        return SCD_ERR_ARG;
+    }
     if (d->wsplit && !aligned16(d->wsplit)) {
         set_error("igemm: wsplit must be 16-byte aligned");
         return SCD_ERR_ALIGN;
@@ -786,6 +791,10 @@ static int conv_igemm_run(const scd_igemm_t *d, hipStream_t s, int bb_ntiles_tot
         return SCD_ERR_ARG;
     }
     if (conv_math_x3() && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");
+    if (a.dst_bound) {
+        set_error("igemm: dst_bound needs the split-bf16 kernels (conv math x3 / h2 and src.c %% 16 == 0)");
+        return SCD_ERR_ARG;
+    }
     if (d->n_out >= 128)
         launch_igemm_bk<2, 2, 2, 2>(a, s);  // 128 x 128
     else if (d->n_out >= 64)

@@ -453,6 +453,12 @@ int h2_prescale() {
     return !(e && e[0] == '0');
 }
 
+// h2, >= 128 output channels: the 1 x 4 wave layout of the 128 x 128 tile (SCD_H2_TILE=0: 2 x 2; read at launch).
+int h2_wide_tile() {
+    const char *e = getenv("SCD_H2_TILE");
+    return !(e && e[0] == '0');
+}
+
 // Double buffering where two halo buffers of every resident block still fit the CU's 160 KB of LDS.
 int halo16_db() {
     const char *e = getenv("SCD_HALO16_DB");  // experiment switch
@@ -514,7 +520,21 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
 //   0: 2x2 waves of 64 px x 64 ch  (128 x 128), 2 waves/SIMD
 //   1: 2x2 waves of 64 px x 32 ch  (128 x 64),  3 waves/SIMD
 //   2: 2x2 waves of 32 px x 64 ch  (64 x 128),  3 waves/SIMD
-constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}};
+//   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 only (experiment: no duplicated weight loads)
+//   4: 4x1 waves of 32 px x 128 ch (128 x 128), 2 waves/SIMD, h2 only (experiment: least LDS traffic)
+constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}, {4, 128, 128}};
+
+// The h2 arithmetics only (tile experiments that instantiate no x3 / x5 / bf16 variants).
+template <int WM, int WN, int TM, int TN, int OCC>
+void launch16_h2only(const IgemmArgs &a, int tw, hipStream_t s) {
+    constexpr int BM = WM * TM * 16;
+    const int hr = (BM / tw + 2) * (tw + 2);
+    const bool db2 = tw != 64 && halo16_db() && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
+    if (db2)
+        launch16c<WM, WN, TM, TN, OCC, true, 4>(a, tw, s);
+    else
+        launch16c<WM, WN, TM, TN, OCC, false, 4>(a, tw, s);
+}
 
 }  // namespace
 
@@ -528,12 +548,14 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     if (mode >= 2)
         id = mode - 2;
     else if (a.n_out >= 128)
-        id = 0;  // 128 x 128 at 2 waves/SIMD: +4..17% over the 32x32x16 halo kernel on the 128..512-channel layers
+        // 128 x 128 at 2 waves/SIMD: +4..17% over the 32x32x16 halo kernel on the 128..512-channel layers; under h2
+        // as 1 x 4 waves of 128 px x 32 ch (no weight fragment loaded by two waves; SCD_H2_TILE=0: 2 x 2)
+        id = (a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale() && h2_wide_tile()) ? 3 : 0;
     else if (a.n_out >= 64)
         id = 1;  // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
     else
         return 0;
-    if (id < 0 || id > 2) return 0;
+    if (id < 0 || id > 4 || (id > 2 && !(a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale()))) return 0;
     *bm = kCfg[id].bm;
     const char *twe = getenv("SCD_HALO16_TW");  // preferred tile width (hip.halo16_tile_width_pref mirrors it)
     const int pref = twe ? atoi(twe) : 16;  // 16: smallest halo per pixel (180 rows for 128 px)
@@ -549,6 +571,8 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
     switch (cfg - 1) {
         case 0: launch16<2, 2, 4, 4, 2>(a, tw, s); break;
         case 1: launch16<2, 2, 4, 2, 3>(a, tw, s); break;
+        case 3: launch16_h2only<1, 4, 8, 2, 2>(a, tw, s); break;
+        case 4: launch16_h2only<4, 1, 2, 8, 2>(a, tw, s); break;
         default: launch16<2, 2, 2, 4, 3>(a, tw, s); break;
     }
 }
@@ -1420,7 +1444,7 @@ extern "C" int scd_set_wgrad16(int32_t mode) {
 extern "C" int scd_set_halo16(int32_t mode) {
     clear_error();
     const int prev = scd::halo16_mode();
-    if (mode >= 0 && mode <= 4) {
+    if (mode >= 0 && mode <= 6) {
         scd::g_halo16 = mode;
     } else if (mode != -1) {
         set_error("scd_set_halo16: mode %d", mode);

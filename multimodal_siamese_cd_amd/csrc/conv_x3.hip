@@ -221,6 +221,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
         __syncthreads();
     }
 
+    float omax = 0.f;  // max |stored value| of this lane (dst_bound)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * TN * 32 + j * 32 + (lane & 31);
@@ -260,11 +261,14 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
                         }
                     }
                     const size_t pix = size_t(img * a.dst_h + 2 * oy + di) * a.dst_w + 2 * ox + dj;
-                    gstore1(a.dst + pix * a.ldc_d + oc, acc[i][j][r] + bias);
+                    const float v = acc[i][j][r] + bias;
+                    gstore1(a.dst + pix * a.ldc_d + oc, v);
+                    omax = fmaxf(omax, fabsf(v));
                 }
             }
         }
     }
+    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the wave takes part
 }
 
 template <int WM, int WN, int TM, int TN>

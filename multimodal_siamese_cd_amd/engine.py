@@ -743,18 +743,18 @@ class DecoderFn(torch.autograd.Function):
                 cat = _empty((b, h, w, cs + cto), skip)
                 hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
             wT = hip.pack_convT2x2(convT.weight.detach(), 0)
+            # h2: the concat's bound is the skip's, raised in place by the ConvT epilogue to max |up| (still a
+            # bound of the skip; F.pad's zero border adds nothing)
+            cat_bound = _bound_of(skip, pool) if pool is not None else None
             if pad_y or pad_x:
                 # ConvT into its own map, then F.pad's zero border and placement in one window copy
                 upm = _empty((b, 2 * hc, 2 * wc, cto), skip)
-                hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(upm), store_mode=1)
+                hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(upm), store_mode=1,
+                               dst_bound=cat_bound)
                 hip.window_copy(nhwc(upm), nhwc(cat, cs, cto), -(pad_y // 2), -(pad_x // 2))
             else:
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto),
-                               store_mode=1)
-            cat_bound = None
-            if pool is not None:  # the concat's bound: the skip's (raised in place: still a bound of the skip)
-                cat_bound = _bound_of(skip, pool)
-                hip.absmax_bound(nhwc(cat, cs, cto), cat_bound)
+                               store_mode=1, dst_bound=cat_bound)
             a, sv, _, _, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save, pool=pool, x_bound=cat_bound)
             saved.append((cur, cat, cs, sv))
             cur = a

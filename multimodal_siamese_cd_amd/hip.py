@@ -49,6 +49,7 @@ class IGEMM(ctypes.Structure):
         ("in_nseg", c_int32),
         ("bn_bwd", POINTER(BNBWD)),
         ("src_bound", c_void_p),
+        ("dst_bound", c_void_p),
     ]
 
 
@@ -376,7 +377,7 @@ def conv_math() -> str:
 
 
 def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None, in_bn=None,
-                bn_bwd=None, src_bound=None):
+                bn_bwd=None, src_bound=None, dst_bound=None):
     nt, dy, dx = _taps(taps)
     sc, sh, nseg = in_bn if in_bn is not None else (None, None, 0)
     bb = None
@@ -384,18 +385,20 @@ def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mo
         y, bseg, mu, iv, bsc, bsh, rec = bn_bwd
         bb = ctypes.pointer(BNBWD(nhwc(y), bseg, _ptr(mu), _ptr(iv), _ptr(bsc), _ptr(bsh), _ptr(rec)))
     return IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
-                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg, bb, _ptr(src_bound))
+                 _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg, bb, _ptr(src_bound),
+                 _ptr(dst_bound))
 
 
 def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
                bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None, in_bn=None, bn_bwd=None,
-               src_bound: torch.Tensor | None = None):
+               src_bound: torch.Tensor | None = None, dst_bound: torch.Tensor | None = None):
     """`in_bn` = (scale, shift, nseg): read src through the producing layer's BatchNorm-apply + ReLU.
     `bn_bwd` = (y, nseg, save_mean, save_invstd, scale, shift, rec): also emit the BatchNorm-backward partial
     sums of the stored output into rec (see scd_bn_bwd_tiles_t).
-    `src_bound`: device float >= max |src as read| (SCD_MATH_H2 operand scaling; see scd_igemm_t.src_bound)."""
+    `src_bound`: device float >= max |src as read| (SCD_MATH_H2 operand scaling; see scd_igemm_t.src_bound).
+    `dst_bound`: device float raised to max |stored output| (ConvTranspose forward, store_mode 1)."""
     d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec, in_bn, bn_bwd,
-                    src_bound)
+                    src_bound, dst_bound)
     _check(lib().scd_conv_igemm(ctypes.byref(d), _stream()), "scd_conv_igemm")
 
 

@@ -392,3 +392,26 @@ def test_h2_wide_dynamic_range(dev, h2, tiny_exp):
     errs = (far(y, ref_y), far(dx, ref_dx), rel(dw, ref_dw))
     print(f'bulk at 2^{tiny_exp}: rel err fwd {errs[0]:.2e} dgrad {errs[1]:.2e} wgrad {errs[2]:.2e}')
     assert max(errs) < 1e-5, errs
+
+
+@pytest.mark.parametrize('n,h,w,ci,co', [(2, 8, 8, 64, 64), (3, 5, 7, 128, 64)])
+def test_convT_dst_bound(dev, h2, n, h, w, ci, co):
+    """The ConvTranspose forward raises dst_bound to exactly max |output| while it stores into the concat slice (the
+    bound of the decoder's concat without a pass over it); other store modes refuse the request."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * h + w)
+    x = torch.randn(n, h, w, ci, generator=g).to(dev)
+    wt = (torch.randn(ci, co, 2, 2, generator=g) / 8).to(dev)
+    b = torch.randn(co, generator=g).to(dev)
+    cat = torch.zeros(n, 2 * h, 2 * w, co + 32, device=dev)
+    bound = torch.full((1,), 0.5, device=dev)  # an earlier (smaller) bound is raised, never lowered
+    hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_1, hip.pack_convT2x2(wt, 0), 4 * co, b, hip.nhwc(cat, 32, co),
+                   store_mode=1, dst_bound=bound)
+    up = cat[..., 32:]
+    ref = F.conv_transpose2d(nchw(x).cpu(), wt.cpu(), b.cpu(), stride=2)
+    assert rel(nchw(up), ref) < 1e-5
+    assert bound.item() == max(0.5, up.abs().max().item())
+    y = torch.empty(n, h, w, co, device=dev)
+    with pytest.raises(RuntimeError, match='dst_bound'):
+        hip.conv_igemm(hip.nhwc(y), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(torch.randn(co, co, 3, 3, device=dev), 0),
+                       co, None, hip.nhwc(torch.empty_like(y)), dst_bound=bound)

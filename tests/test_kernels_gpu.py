@@ -637,8 +637,10 @@ def test_bn_relu_fused_pool_and_diff(dev, n, h, w, c, nseg):
                                                  (2, 8, 8, 128, 1, 'skip'), (4, 10, 12, 64, 0, 'both'),
                                                  (2, 16, 8, 64, 0, 'pool')])
 def test_bn_relu_backward_pooled(dev, n, h, w, c, mode, parts):
-    """The BatchNorm + ReLU backward forming its incoming gradient on the fly (maxpool_bwd -/+ skip) is
-    bit-identical to feature_grad followed by bn_relu_backward (dy, dgamma, dbeta, conv-bias grad)."""
+    """The BatchNorm + ReLU backward forming its incoming gradient on the fly (maxpool_bwd -/+ skip): per pixel
+    (SCD_BN_POOLED_CELLS=0) bit-identical to feature_grad followed by bn_relu_backward (dy, dgamma, dbeta, conv-bias
+    grad); over 2x2 cells (default) the same up to the order of the per-chunk sums (2e-6)."""
+    import os
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(n * h * w + c + mode)
     nseg = 2
@@ -660,18 +662,26 @@ def test_bn_relu_backward_pooled(dev, n, h, w, c, mode, parts):
     ga = torch.empty_like(y)
     hip.feature_grad(nh(gy), idx, nh(gs), mode, hip.nhwc(ga))
     outs = []
-    for pooled in (False, True):
+    for pooled in (False, 'pixels', 'cells'):
         dy = torch.empty_like(y)
         dg, db, dbias = (torch.empty(c, device=dev) for _ in range(3))
         if pooled:
-            hip.bn_relu_backward_pooled(hip.nhwc(y), nh(gy), idx, nh(gs), mode, nseg, smean, sinv, gamma, scale,
-                                        shift, dg, db, dbias, hip.nhwc(dy), ws)
+            os.environ['SCD_BN_POOLED_CELLS'] = '0' if pooled == 'pixels' else '1'
+            try:
+                hip.bn_relu_backward_pooled(hip.nhwc(y), nh(gy), idx, nh(gs), mode, nseg, smean, sinv, gamma, scale,
+                                            shift, dg, db, dbias, hip.nhwc(dy), ws)
+            finally:
+                os.environ.pop('SCD_BN_POOLED_CELLS')
         else:
             hip.bn_relu_backward(hip.nhwc(y), hip.nhwc(ga), nseg, smean, sinv, gamma, scale, shift, dg, db, dbias,
                                  hip.nhwc(dy), ws)
         outs.append((dy, dg, db, dbias))
-    for a, b in zip(*outs):
+    for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+    for a, b in zip(outs[0][:3], outs[2][:3]):
+        assert rel(a, b) < 2e-6
+    # the conv-bias grad is a sum of dy that cancels to ~0 (a pre-BN bias): judged against the sum of |dy|
+    assert ((outs[0][3] - outs[2][3]).abs() <= 2e-6 * outs[0][0].abs().sum(dim=(0, 1, 2))).all()
 
 
 def test_siamese_diff(dev):

@@ -56,7 +56,8 @@ def main():
     ap.add_argument('--layer', default=None, help='run only this layer name (e.g. enc1b)')
     ap.add_argument('--cin', type=int, default=None,
                     help='input-layer channels as stored (default: the model\'s padding of 5 bands, engine.pad_in)')
-    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16'], help='conv arithmetic (default: library default)')
+    ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16', 'h2'],
+                    help='conv arithmetic (default: library default; h2 gets absmax operand bounds)')
     ap.add_argument('--variants', default=None,
                     help='comma-separated variants, interleaved per layer; a variant is "+"-joined settings '
                          'h16=<scd_set_halo16 mode>, w16=<scd_set_wgrad16 mode> or ENVVAR=value (read by the '
@@ -85,6 +86,11 @@ def main():
         wf = hip.pack_conv3x3(w, 0)
         wb = hip.pack_conv3x3(w, 1)
         flops = 2.0 * n * s * s * co * 9 * ci
+        xb = db = None
+        if hip.conv_math() == 'h2':  # the operand bounds the engine's producers would supply
+            xb, db = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+            hip.absmax_bound(hip.nhwc(x), xb)
+            hip.absmax_bound(hip.nhwc(dy), db)
         for mode in modes:
             if mode is not None:
                 for kv in mode.split('+'):
@@ -103,12 +109,12 @@ def main():
             res = {}
             if args.only in (None, 'fwd'):
                 res['fwd'] = timeit(lambda: hip.conv_igemm(hip.nhwc(x), s, s, 1, hip.TAPS_3X3, wf, co, None,
-                                                           hip.nhwc(y)), args.reps)
+                                                           hip.nhwc(y), src_bound=xb), args.reps)
             if args.only in (None, 'dgrad') and not name.startswith('enc0a'):
                 res['dgrad'] = timeit(lambda: hip.conv_igemm(hip.nhwc(dy), s, s, 1, hip.TAPS_3X3, wb, ci, None,
-                                                             hip.nhwc(dx)), args.reps)
+                                                             hip.nhwc(dx), src_bound=db), args.reps)
             if args.only in (None, 'wgrad'):
-                d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dy), hip.nhwc(x), 1, hip.TAPS_3X3)
+                d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dy), hip.nhwc(x), 1, hip.TAPS_3X3, None, db, xb)
                 slabs = torch.empty(nbytes // 4, device=dev)
                 res['wgrad'] = timeit(lambda: hip.conv_wgrad(d, slabs), args.reps)
             cells = []
