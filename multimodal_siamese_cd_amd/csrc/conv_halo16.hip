@@ -904,6 +904,17 @@ constexpr int w16_xp() { return NP == 1 ? 1 : (NP == 5 || NP == 2 || NP == 4) ? 
 template <int NP>
 constexpr int w16_dp() { return NP == 1 ? 1 : (NP == 2 || NP == 4) ? 2 : 3; }
 
+// Wave layouts of the halo weight grad's 64 r x 64 c block: LC 0 = 2 x 2 waves of 32 r x 32 c (two 16-channel X
+// blocks, two 16-row dY blocks per wave); LC 1 = 4 waves of 64 r x 16 c along c (one X block, four dY blocks per wave):
+// the X fragments, re-read for every tap, are then read by one wave instead of two (-35% LDS bytes per patch) at the
+// same accumulator count.
+template <int LC>
+struct W16L {
+    static constexpr int CB = LC ? 1 : 2;  // 16-channel X blocks per wave
+    static constexpr int RB = LC ? 4 : 2;  // 16-row dY blocks per wave
+    static constexpr int NH = 9 * CB;      // half taps (tap, channel block) per patch
+};
+
 // X fragments of half tap (T, CB): two transposed reads per X plane.
 template <int T, int CB, int PB, int HW_, int NP>
 __device__ __forceinline__ void w16_read_x(s16x4 (&f)[6], uint32_t xbase) {
@@ -920,22 +931,36 @@ __device__ __forceinline__ void w16_read_x(s16x4 (&f)[6], uint32_t xbase) {
     }
 }
 
+// dY fragments of a patch, I = plane * NRB + rb: two transposed reads of 16 rows r (32 bytes) each.
+template <int I, int PA, int NRB, int DP>
+__device__ __forceinline__ void w16_read_dy(bf16x8 (&dv)[3][NRB], uint32_t dbase) {
+    if constexpr (I < DP * NRB) {
+        constexpr int p = I / NRB, rb = I % NRB;
+        s16x4 lo, hi;
+        tr_read<p * PA + rb * 32>(lo, dbase);
+        tr_read<p * PA + 8 * kW16RS + rb * 32>(hi, dbase);
+        dv[p][rb] = cat8(lo, hi);
+        w16_read_dy<I + 1, PA, NRB, DP>(dv, dbase);
+    }
+}
+
 // One half tap (tap T, channel block CB): wait for its X fragments, then the split products (six for x3, hh
 // for bf16) x 2 r-blocks.
-template <int T, int CB, int WAIT, int NP>
-__device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f)[6]) {
+template <int T, int CB, int WAIT, int NP, int LC>
+__device__ __forceinline__ void w16_half(f32x4 (&acc)[9][W16L<LC>::CB][W16L<LC>::RB],
+                                         bf16x8 (&dv)[3][W16L<LC>::RB], s16x4 (&f)[6]) {
     bf16x8 x0 = cat8(f[0], f[1]), x1 = cat8(f[2], f[3]), x2 = cat8(f[4], f[5]);
     if constexpr (NP == 2 || NP == 4) {  // fp16 planes: x_m dy_h, x_h dy_m (NP 4: (x_h 2^-11) dy_m', dY's low
                                          // term pre-scaled), x_h dy_h
         lds_wait<WAIT>(x0, x1);
         if (T == 0 && CB == 0) {
-            lds_wait<WAIT>(dv[0][0], dv[1][0]);
-            lds_wait<WAIT>(dv[0][1], dv[1][1]);
+#pragma unroll
+            for (int rb = 0; rb < W16L<LC>::RB; ++rb) lds_wait<WAIT>(dv[0][rb], dv[1][rb]);
         }
         const u32x4 xh = __builtin_bit_cast(u32x4, x0), xm = __builtin_bit_cast(u32x4, x1);
         const u32x4 xh_lo = NP == 4 ? f16_down11(xh) : xh;
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
+        for (int rb = 0; rb < W16L<LC>::RB; ++rb) {
             const u32x4 dh = __builtin_bit_cast(u32x4, dv[0][rb]), dm = __builtin_bit_cast(u32x4, dv[1][rb]);
             acc[T][CB][rb] = mfma16_f16(xm, dh, acc[T][CB][rb]);
             acc[T][CB][rb] = mfma16_f16(xh_lo, dm, acc[T][CB][rb]);
@@ -949,14 +974,18 @@ __device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][
         else
             lds_wait<WAIT>(x0, x1);
         if (T == 0 && CB == 0) {
-            lds_wait<WAIT>(dv[0][0], dv[1][0], dv[2][0]);
-            lds_wait<WAIT>(dv[0][1], dv[1][1], dv[2][1]);
+#pragma unroll
+            for (int rb = 0; rb < W16L<LC>::RB; ++rb) lds_wait<WAIT>(dv[0][rb], dv[1][rb], dv[2][rb]);
         }
     } else {
-        lds_wait<WAIT>(x0, dv[0][0], dv[0][1]);
+        lds_wait<WAIT>(x0);
+        if (T == 0 && CB == 0) {
+#pragma unroll
+            for (int rb = 0; rb < W16L<LC>::RB; ++rb) lds_wait<WAIT>(dv[0][rb]);
+        }
     }
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
+    for (int rb = 0; rb < W16L<LC>::RB; ++rb) {
         if constexpr (NP != 1) {
             acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, dv[1][rb], acc[T][CB][rb], 0, 0, 0);
             acc[T][CB][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, dv[2][rb], acc[T][CB][rb], 0, 0, 0);
@@ -969,21 +998,22 @@ __device__ __forceinline__ void w16_half(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][
     }
 }
 
-// Half taps H = 2T + CB, one ahead: compute H from buffer H & 1, then refill that buffer with H + 2.  The
-// counted wait leaves the reads of the other buffer (2 per X plane, issued one half tap earlier) in flight.
-template <int H, int PB, int HW_, int NP>
-__device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][2][2], bf16x8 (&dv)[3][2], s16x4 (&f0)[6], s16x4 (&f1)[6],
-                                          uint32_t xbase) {
-    if constexpr (H < 18) {
+// Half taps H = CB_per_wave * T + CB, one ahead: compute H from buffer H & 1, then refill that buffer with H + 2.
+// The counted wait leaves the reads of the other buffer (2 per X plane, issued one half tap earlier) in flight.
+template <int H, int PB, int HW_, int NP, int LC>
+__device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][W16L<LC>::CB][W16L<LC>::RB], bf16x8 (&dv)[3][W16L<LC>::RB],
+                                          s16x4 (&f0)[6], s16x4 (&f1)[6], uint32_t xbase) {
+    constexpr int NCB = W16L<LC>::CB, NH = W16L<LC>::NH;
+    if constexpr (H < NH) {
         s16x4 (&f)[6] = (H & 1) ? f1 : f0;
-        w16_half<H / 2, H % 2, (H == 17 ? 0 : 2 * w16_xp<NP>()), NP>(acc, dv, f);
-        if constexpr (H + 2 < 18) w16_read_x<(H + 2) / 2, (H + 2) % 2, PB, HW_, NP>(f, xbase);
-        w16_chain<H + 1, PB, HW_, NP>(acc, dv, f0, f1, xbase);
+        w16_half<H / NCB, H % NCB, (H == NH - 1 ? 0 : 2 * w16_xp<NP>()), NP, LC>(acc, dv, f);
+        if constexpr (H + 2 < NH) w16_read_x<(H + 2) / NCB, (H + 2) % NCB, PB, HW_, NP>(f, xbase);
+        w16_chain<H + 1, PB, HW_, NP, LC>(acc, dv, f0, f1, xbase);
     }
 }
 }  // namespace
 
-template <int NP>
+template <int NP, int LC>
 __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     constexpr int PH = 2, PW = 16, P = PH * PW;
     constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
@@ -1003,7 +1033,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     }
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wi = wid >> 1, wj = wid & 1;
+    constexpr int NCB = W16L<LC>::CB, NRB = W16L<LC>::RB;
+    const int wi = LC ? 0 : wid >> 1, wj = LC ? wid : wid & 1;  // wave's dY / X block (in units of its width)
     const uint32_t per_split = uint32_t(a.grid_r * a.grid_j);
     const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
     const int split = int(L / per_split);
@@ -1096,20 +1127,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             }
     };
 
-    f32x4 acc[9][2][2];
+    f32x4 acc[9][NCB][NRB];
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < NCB; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < NRB; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // transposed-read lane roles: 16-lane group g supplies patch pixels (g >> 1, 4(g & 1) + (w16 >> 2)) (+8
     // for the second read of a fragment) and channel columns 4(w16 & 3)..+3 of a 16-channel block
     const int g = lane >> 4, w16 = lane & 15;
     const int py = g >> 1, pxq = 4 * (g & 1) + (w16 >> 2);
-    const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RS + (32 * wi + 4 * (w16 & 3)) * 2;
-    const uint32_t xbase = lds_addr(smem) + DP * PA + (py * HW_ + pxq) * RS + (32 * wj + 4 * (w16 & 3)) * 2;
+    const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RS + (16 * NRB * wi + 4 * (w16 & 3)) * 2;
+    const uint32_t xbase = lds_addr(smem) + DP * PA + (py * HW_ + pxq) * RS + (16 * NCB * wj + 4 * (w16 & 3)) * 2;
 
     if (pbeg < pend) {
         load_patch(pbeg);
@@ -1118,32 +1149,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
         for (int pi = pbeg; pi < pend; ++pi) {
             const bool more = pi + 1 < pend;
             if (more) load_patch(pi + 1);
-            s16x4 fa[12];
-            tr_read<0 * PA + 0>(fa[0], dbase);
-            tr_read<0 * PA + 8 * RS>(fa[1], dbase);
-            tr_read<0 * PA + 32>(fa[2], dbase);
-            tr_read<0 * PA + 8 * RS + 32>(fa[3], dbase);
-            if constexpr (DP >= 2) {
-                tr_read<1 * PA + 0>(fa[4], dbase);
-                tr_read<1 * PA + 8 * RS>(fa[5], dbase);
-                tr_read<1 * PA + 32>(fa[6], dbase);
-                tr_read<1 * PA + 8 * RS + 32>(fa[7], dbase);
-            }
-            if constexpr (DP == 3) {
-                tr_read<2 * PA + 0>(fa[8], dbase);
-                tr_read<2 * PA + 8 * RS>(fa[9], dbase);
-                tr_read<2 * PA + 32>(fa[10], dbase);
-                tr_read<2 * PA + 8 * RS + 32>(fa[11], dbase);
-            }
-            bf16x8 dv[3][2];
-#pragma unroll
-            for (int p = 0; p < DP; ++p)
-#pragma unroll
-                for (int r = 0; r < 2; ++r) dv[p][r] = cat8(fa[4 * p + 2 * r], fa[4 * p + 2 * r + 1]);
+            bf16x8 dv[3][NRB];
+            w16_read_dy<0, PA, NRB, DP>(dv, dbase);
             s16x4 f0[6], f1[6];
-            w16_read_x<0, 0, PB, HW_, NP>(f0, xbase);
-            w16_read_x<0, 1, PB, HW_, NP>(f1, xbase);
-            w16_chain<0, PB, HW_, NP>(acc, dv, f0, f1, xbase);
+            w16_read_x<0 / NCB, 0 % NCB, PB, HW_, NP>(f0, xbase);
+            w16_read_x<1 / NCB, 1 % NCB, PB, HW_, NP>(f1, xbase);
+            w16_chain<0, PB, HW_, NP, LC>(acc, dv, f0, f1, xbase);
             if (more) {
                 __syncthreads();  // every wave is done with this patch
                 store_patch();
@@ -1157,20 +1168,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
 #pragma unroll
         for (int t = 0; t < 9; ++t)
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb)
+            for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-                for (int r = 0; r < 2; ++r) acc[t][cb][r] *= k;
+                for (int r = 0; r < NRB; ++r) acc[t][cb][r] *= k;
     }
-    // acc[t][cb][rb][q]: r = r0 + 32wi + 16rb + (lane & 15), c = c0 + 32wj + 16cb + 4g + q
+    // acc[t][cb][rb][q]: r = r0 + 16 NRB wi + 16rb + (lane & 15), c = c0 + 16 NCB wj + 16cb + 4g + q
     float *slab = a.slabs + size_t(split) * a.R * a.Ng;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
+        for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const int row = r0 + 32 * wi + 16 * r + w16;
-                const int col = c0 + 32 * wj + 16 * cb + 4 * g;
+            for (int r = 0; r < NRB; ++r) {
+                const int row = r0 + 16 * NRB * wi + 16 * r + w16;
+                const int col = c0 + 16 * NCB * wj + 16 * cb + 4 * g;
                 gstore4(slab + size_t(row) * a.Ng + t * a.C + col, acc[t][cb][r]);
             }
 }
@@ -1405,22 +1416,41 @@ int wgrad16_mode() {
 static int wgrad16_planes(bool bounded) {
     return conv_math_planes() == 2 ? (bounded ? (h2_prescale() ? 4 : 2) : 3) : conv_math_planes();
 }
+// Wave layout of the h2 and bf16 variants (W16L): SCD_W16_LAYOUT=0 keeps the 2x2 layout, default 1 (along c).
+// x3 / x5 keep 2x2: their third dY plane does not fit four r blocks in registers.
+static int w16_layout() {  // read at launch, like the other A/B switches
+    const char *e = getenv("SCD_W16_LAYOUT");
+    return (e && e[0] == '0') ? 0 : 1;
+}
+template <int NP>
+static const void *w16_kernel(int lc) {
+    return lc ? reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 1>)
+              : reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 0>);
+}
+template <int NP>
+static void w16_launch(int lc, const WgradArgs &a, dim3 grid, hipStream_t s) {
+    if (lc)
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1>), grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 0>), grid, dim3(256), 0, s, a);
+}
 const void *wgrad_halo16_fn(bool bounded) {
     switch (wgrad16_planes(bounded)) {
-        case 1: return reinterpret_cast<const void *>(&wgrad_halo16_x3<1>);
-        case 2: return reinterpret_cast<const void *>(&wgrad_halo16_x3<2>);
-        case 4: return reinterpret_cast<const void *>(&wgrad_halo16_x3<4>);
-        case 5: return reinterpret_cast<const void *>(&wgrad_halo16_x3<5>);
-        default: return reinterpret_cast<const void *>(&wgrad_halo16_x3<3>);
+        case 1: return w16_kernel<1>(w16_layout());
+        case 2: return w16_kernel<2>(w16_layout());
+        case 4: return w16_kernel<4>(w16_layout());
+        case 5: return reinterpret_cast<const void *>(&wgrad_halo16_x3<5, 0>);
+        default: return reinterpret_cast<const void *>(&wgrad_halo16_x3<3, 0>);
     }
 }
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
+    const int lc = w16_layout();
     switch (wgrad16_planes(a.rows_bound && a.src_bound)) {
-        case 1: hipLaunchKernelGGL(wgrad_halo16_x3<1>, grid, dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL(wgrad_halo16_x3<2>, grid, dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL(wgrad_halo16_x3<4>, grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL(wgrad_halo16_x3<5>, grid, dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL(wgrad_halo16_x3<3>, grid, dim3(256), 0, s, a);
+        case 1: w16_launch<1>(lc, a, grid, s); break;
+        case 2: w16_launch<2>(lc, a, grid, s); break;
+        case 4: w16_launch<4>(lc, a, grid, s); break;
+        case 5: hipLaunchKernelGGL((wgrad_halo16_x3<5, 0>), grid, dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL((wgrad_halo16_x3<3, 0>), grid, dim3(256), 0, s, a);
     }
 }
 

@@ -142,6 +142,10 @@ template <int N>
 __device__ __forceinline__ void lds_wait(bf16x8 &a, bf16x8 &b) {
     asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
 }
+template <int N>
+__device__ __forceinline__ void lds_wait(bf16x8 &a) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N));
+}
 
 __device__ __forceinline__ bf16x8 cat8(s16x4 lo, s16x4 hi) {
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
