@@ -250,6 +250,9 @@ typedef struct scd_wgrad {
 /* Number of K-splits the library will use and the slab bytes it needs. */
 int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes);
 int scd_wgrad_arith(const scd_wgrad_t *d); /* see scd_set_conv_math */
+/* Rows of dY (output channels) per workgroup of the halo weight-grad kernel scd_conv_wgrad would run for `d`:
+ * 64 or 128 (SCD_W16_R128=0 keeps 64); 0 when `d` takes another weight-grad kernel.  Diagnostic. */
+int scd_wgrad_rows_per_block(const scd_wgrad_t *d);
 int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream);
 /* 1 if the weight-grad kernel scd_conv_wgrad would run for `d` applies the src_scale/src_shift transform. */
 int scd_wgrad_src_bn_supported(const scd_wgrad_t *d);

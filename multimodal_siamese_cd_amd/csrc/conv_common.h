@@ -124,8 +124,10 @@ bool igemm_takes_c16(const IgemmArgs &a);  // igemm_halo16_c16 (16-channel sourc
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
 // 16x16x32-MFMA halo weight grad (conv_halo16.hip), selected by wgrad16_mode() (scd_set_wgrad16).
 int wgrad16_mode();
-const void *wgrad_halo16_fn(bool bounded);  // bounded: h2 under SCD_MATH_H2
+const void *wgrad_halo16_fn(bool bounded, int rblock);  // bounded: h2 under SCD_MATH_H2
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
+// dY rows per block of the halo weight grad (64 or 128; threads = 4 * rows): plan and launch use the same value.
+int wgrad16_rblock(int R, bool bounded);
 // 16-channel-source variant (the input layer), same eligibility otherwise (conv_halo16.hip).
 const void *wgrad_halo16_c16_fn();
 void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s);
@@ -133,7 +135,8 @@ void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s);
 const void *wgrad_x3_fn(int tile_id);
 void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
 // Halo weight grad (3x3 / stride 1 / same size, R and C multiples of 64, maps in 2x16 patches).
-const void *wgrad_halo_fn(bool bounded);
+const void *wgrad_halo_fn(bool bounded, int rblock);
+int wgrad_halo_rblock(int R, bool bounded);  // 64, or wgrad16_rblock under scd_set_wgrad16
 void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
 
 // Conv math selection (scd_set_conv_math): SCD_MATH_X3 = split-bf16 MFMA where the shape allows it,

@@ -930,23 +930,26 @@ static bool wgrad_c16_ok(const scd_wgrad_t *d) {
 // Both operands bounded: the h2 weight grad under SCD_MATH_H2 (x3 otherwise).
 static bool wgrad_bounded(const scd_wgrad_t *d) { return d->rows_bound && d->src_bound; }
 
-static int wgrad_halo_resident(bool c16, bool bounded) {
-    // per halo weight-grad kernel: 32x32x16; 16x16x32 x3 / x5 / bf16 / h2; 16-channel x3 / x5 / bf16
-    static int caches[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+static int wgrad_halo_resident(bool c16, bool bounded, int rblock) {
+    // per halo weight-grad kernel: 32x32x16; 16x16x32 x3 / x5 / bf16 / h2; 16-channel x3 / x5 / bf16; the
+    // 128-row bf16 / h2 blocks
+    static int caches[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const int m = conv_math_planes();
     const int planes = m == 1 ? 0 : m == 5 ? 1 : (m == 2 && bounded && !c16) ? 3 : 2;
-    int &cache = caches[c16 ? 5 + planes : wgrad16_mode() ? 1 + planes : 0];
+    const bool r128 = !c16 && rblock == 128;
+    int &cache = caches[r128 ? 9 + (planes == 3) : c16 ? 5 + planes : wgrad16_mode() ? 1 + planes : 0];
     if (cache > 0) return cache;
     int per_cu = 0, cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c16 ? wgrad_halo16_c16_fn() : wgrad_halo_fn(bounded),
-                                                     256, 0) !=
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu,
+                                                     c16 ? wgrad_halo16_c16_fn() : wgrad_halo_fn(bounded, rblock),
+                                                     r128 ? 512 : 256, 0) !=
             hipSuccess ||
         per_cu < 1 ||
         cus < 1) {
         (void)hipGetLastError();
-        cache = 2 * 256;  // cached: plan and launch must see the same capacity
+        cache = (r128 ? 1 : 2) * 256;  // cached: plan and launch must see the same capacity
         return cache;
     }
     cache = per_cu * cus;
@@ -956,9 +959,10 @@ static int wgrad_halo_resident(bool c16, bool bounded) {
 static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
     if (wgrad_halo_ok(d) || wgrad_c16_ok(d)) {
         const bool c16 = !wgrad_halo_ok(d);
+        const int rb = c16 ? 64 : wgrad_halo_rblock(d->rows.c, wgrad_bounded(d));
         const int64_t patches = pixels(d->rows) / 32;
-        const int64_t tiles = int64_t(d->rows.c / 64) * (c16 ? 1 : d->src.c / 64);
-        split_units(patches, tiles, wgrad_halo_resident(c16, wgrad_bounded(d)), 8, 1, nsplit, kchunk);
+        const int64_t tiles = int64_t(d->rows.c / rb) * (c16 ? 1 : d->src.c / 64);
+        split_units(patches, tiles, wgrad_halo_resident(c16, wgrad_bounded(d), rb), 8, 1, nsplit, kchunk);
         return;
     }
     const int Ng = d->ntaps * d->src.c;
@@ -986,6 +990,13 @@ extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
         return conv_math_mode() == SCD_MATH_H2 && !wgrad_bounded(d) ? SCD_MATH_X3 : conv_math_mode();
     if (wgrad_c16_ok(d)) return conv_math_mode() == SCD_MATH_H2 ? SCD_MATH_X3 : conv_math_mode();
     return SCD_MATH_X3;
+}
+
+extern "C" int scd_wgrad_rows_per_block(const scd_wgrad_t *d) {
+    clear_error();
+    SCD_TRY(wgrad_validate(d));
+    if (wgrad_halo_ok(d)) return wgrad_halo_rblock(d->rows.c, wgrad_bounded(d));
+    return wgrad_c16_ok(d) ? 64 : 0;
 }
 
 namespace scd {
@@ -1119,7 +1130,7 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     }
     if (wgrad_halo_ok(d)) {
         a.n_img_w = d->rows.n;
-        a.grid_r = a.R / 64;
+        a.grid_r = a.R / wgrad_halo_rblock(a.R, wgrad_bounded(d));
         a.grid_j = a.C / 64;
         a.remap = xcd_remap_enabled();
         launch_wgrad_halo_x3(a, dim3(a.grid_r * a.grid_j * ns), s);

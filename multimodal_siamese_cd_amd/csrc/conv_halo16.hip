@@ -931,16 +931,17 @@ __device__ __forceinline__ void w16_read_x(s16x4 (&f)[6], uint32_t xbase) {
     }
 }
 
-// dY fragments of a patch, I = plane * NRB + rb: two transposed reads of 16 rows r (32 bytes) each.
-template <int I, int PA, int NRB, int DP>
+// dY fragments of a patch, I = plane * NRB + rb: two transposed reads of 16 rows r (32 bytes) each; RSD = the
+// staged dY row stride.
+template <int I, int PA, int NRB, int DP, int RSD>
 __device__ __forceinline__ void w16_read_dy(bf16x8 (&dv)[3][NRB], uint32_t dbase) {
     if constexpr (I < DP * NRB) {
         constexpr int p = I / NRB, rb = I % NRB;
         s16x4 lo, hi;
         tr_read<p * PA + rb * 32>(lo, dbase);
-        tr_read<p * PA + 8 * kW16RS + rb * 32>(hi, dbase);
+        tr_read<p * PA + 8 * RSD + rb * 32>(hi, dbase);
         dv[p][rb] = cat8(lo, hi);
-        w16_read_dy<I + 1, PA, NRB, DP>(dv, dbase);
+        w16_read_dy<I + 1, PA, NRB, DP, RSD>(dv, dbase);
     }
 }
 
@@ -1013,14 +1014,21 @@ __device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][W16L<LC>::CB][W16L<LC>
 }
 }  // namespace
 
-template <int NP, int LC>
-__global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
+// RG = 2 (LC 1 only): a block of 8 waves owns 128 rows r x 64 channels c; the two 4-wave groups share the
+// staged X halo, which is then split and stored once per 128 rows instead of per 64 (the staging per MFMA,
+// a third of the kernel's time at RG 1, drops by ~35%).
+template <int NP, int LC, int RG>
+__global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a) {
+    constexpr int NT = 256 * RG;
     constexpr int PH = 2, PW = 16, P = PH * PW;
     constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
-    constexpr int RS = kW16RS;
-    constexpr int PA = P * RS, PB = HP * RS;            // plane bytes
-    constexpr int A_CH = P * 16, B_CH = HP * 16;        // 4-channel pieces
-    constexpr int A_PER = A_CH / 256, B_PER = (B_CH + 255) / 256;
+    constexpr int RS = kW16RS;                        // X row stride (64 channels + 32 bytes)
+    constexpr int RSD = 128 * RG + 32;                // dY row stride (64 RG rows + 32 bytes: conflict-free reads)
+    constexpr int CQ = 16 * RG;                       // 4-row pieces per dY pixel
+    constexpr int PA = P * RSD, PB = HP * RS;         // plane bytes
+    constexpr int A_CH = P * CQ, B_CH = HP * 16;      // 4-channel pieces
+    constexpr int A_PER = A_CH / NT, B_PER = (B_CH + NT - 1) / NT;
+    static_assert(RG == 1 || (RG == 2 && LC == 1), "128-row blocks use the along-c wave layout");
     static_assert(NP == 1 || NP == 2 || NP == 3 || NP == 4 || NP == 5, "x3, x5, bf16 or h2");
     constexpr bool H2 = NP == 2 || NP == 4;
     constexpr int DP = w16_dp<NP>();  // dY planes
@@ -1034,13 +1042,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     constexpr int NCB = W16L<LC>::CB, NRB = W16L<LC>::RB;
-    const int wi = LC ? 0 : wid >> 1, wj = LC ? wid : wid & 1;  // wave's dY / X block (in units of its width)
+    // wave's dY / X block (in units of its width)
+    const int wi = LC ? (RG == 1 ? 0 : wid >> 2) : wid >> 1, wj = LC ? (RG == 1 ? wid : wid & 3) : wid & 1;
     const uint32_t per_split = uint32_t(a.grid_r * a.grid_j);
     const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
     const int split = int(L / per_split);
     const int rem = int(L - uint32_t(split) * per_split);
     const int ct = rem / a.grid_r;
-    const int r0 = (rem - ct * a.grid_r) * 64, c0 = ct * 64;
+    const int r0 = (rem - ct * a.grid_r) * 64 * RG, c0 = ct * 64;
     const int pw_n = a.wo / PW, ph_n = a.ho / PH, pimg = pw_n * ph_n;
     const int npatch = a.n_img_w * pimg;
     const int pbeg = split * a.kchunk, pend = min(npatch, pbeg + a.kchunk);
@@ -1062,14 +1071,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
         const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
-            const int e = tid + i * 256, q = e >> 4, cq = e & 15;
+            const int e = tid + i * NT, q = e / CQ, cq = e % CQ;
             const int py = q >> 4, px = q & 15;
             const uint32_t off = uint32_t(((img * a.ho + y0 + py) * a.wo + x0 + px) * a.ldc_r + r0 + cq * 4) * 4u;
             ra[i] = bload4(rs_rows, off);
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
-            const int e = tid + i * 256, hp = e >> 4, cq = e & 15;
+            const int e = tid + i * NT, hp = e >> 4, cq = e & 15;
             const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
             const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
             const bool v = e < B_CH && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
@@ -1080,8 +1089,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     auto store_patch = [&]() {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
-            const int e = tid + i * 256;
-            const int o = (e >> 4) * RS + (e & 15) * 8;
+            const int e = tid + i * NT;
+            const int o = (e / CQ) * RSD + (e % CQ) * 8;
             u32x2 h, m, l;
             if constexpr (H2) {
                 if constexpr (NP == 4)
@@ -1101,7 +1110,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
-            if (tid + i * 256 < B_CH) {
+            if (tid + i * NT < B_CH) {
                 u32x2 h, m, l;
                 if (a.src_scale) {
                     const bool v = (x_valid >> i) & 1u;
@@ -1110,7 +1119,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
                 } else if constexpr (H2) {
                     rb[i] *= xs;
                 }
-                const int e = tid + i * 256;
+                const int e = tid + i * NT;
                 const int o = DP * PA + (e >> 4) * RS + (e & 15) * 8;
                 if constexpr (H2) {
                     split2h(rb[i], h, m);
@@ -1139,7 +1148,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
     // for the second read of a fragment) and channel columns 4(w16 & 3)..+3 of a 16-channel block
     const int g = lane >> 4, w16 = lane & 15;
     const int py = g >> 1, pxq = 4 * (g & 1) + (w16 >> 2);
-    const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RS + (16 * NRB * wi + 4 * (w16 & 3)) * 2;
+    const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RSD + (16 * NRB * wi + 4 * (w16 & 3)) * 2;
     const uint32_t xbase = lds_addr(smem) + DP * PA + (py * HW_ + pxq) * RS + (16 * NCB * wj + 4 * (w16 & 3)) * 2;
 
     if (pbeg < pend) {
@@ -1150,7 +1159,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_x3(WgradArgs a) {
             const bool more = pi + 1 < pend;
             if (more) load_patch(pi + 1);
             bf16x8 dv[3][NRB];
-            w16_read_dy<0, PA, NRB, DP>(dv, dbase);
+            w16_read_dy<0, PA, NRB, DP, RSD>(dv, dbase);
             s16x4 f0[6], f1[6];
             w16_read_x<0 / NCB, 0 % NCB, PB, HW_, NP>(f0, xbase);
             w16_read_x<1 / NCB, 1 % NCB, PB, HW_, NP>(f1, xbase);
@@ -1422,35 +1431,48 @@ static int w16_layout() {  // read at launch, like the other A/B switches
     const char *e = getenv("SCD_W16_LAYOUT");
     return (e && e[0] == '0') ? 0 : 1;
 }
-template <int NP>
-static const void *w16_kernel(int lc) {
-    return lc ? reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 1>)
-              : reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 0>);
+// Rows of dY per block: 128 (RG 2) for the h2 / bf16 variants in the along-c layout when R % 128 == 0, else 64
+// (SCD_W16_R128=0: always 64; read at plan and launch time alike).
+int wgrad16_rblock(int R, bool bounded) {
+    const int np = wgrad16_planes(bounded);
+    if (!(np == 1 || np == 2 || np == 4) || !w16_layout() || R % 128) return 64;
+    const char *e = getenv("SCD_W16_R128");
+    return (e && e[0] == '0') ? 64 : 128;
 }
 template <int NP>
-static void w16_launch(int lc, const WgradArgs &a, dim3 grid, hipStream_t s) {
-    if (lc)
-        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1>), grid, dim3(256), 0, s, a);
+static const void *w16_kernel(int lc, int rb) {
+    return rb == 128 ? reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 1, 2>)
+           : lc      ? reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 1, 1>)
+                     : reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 0, 1>);
+}
+template <int NP>
+static void w16_launch(int lc, int rb, const WgradArgs &a, dim3 grid, hipStream_t s) {
+    if (rb == 128)
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 2>), grid, dim3(512), 0, s, a);
+    else if (lc)
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 1>), grid, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 0>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 0, 1>), grid, dim3(256), 0, s, a);
 }
-const void *wgrad_halo16_fn(bool bounded) {
+const void *wgrad_halo16_fn(bool bounded, int rblock) {
     switch (wgrad16_planes(bounded)) {
-        case 1: return w16_kernel<1>(w16_layout());
-        case 2: return w16_kernel<2>(w16_layout());
-        case 4: return w16_kernel<4>(w16_layout());
-        case 5: return reinterpret_cast<const void *>(&wgrad_halo16_x3<5, 0>);
-        default: return reinterpret_cast<const void *>(&wgrad_halo16_x3<3, 0>);
+        case 1: return w16_kernel<1>(w16_layout(), rblock);
+        case 2: return w16_kernel<2>(w16_layout(), rblock);
+        case 4: return w16_kernel<4>(w16_layout(), rblock);
+        case 5: return reinterpret_cast<const void *>(&wgrad_halo16_x3<5, 0, 1>);
+        default: return reinterpret_cast<const void *>(&wgrad_halo16_x3<3, 0, 1>);
     }
 }
+// a.grid_r = R / wgrad16_rblock(R, bounded) (the caller plans with the same choice).
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    const int lc = w16_layout();
-    switch (wgrad16_planes(a.rows_bound && a.src_bound)) {
-        case 1: w16_launch<1>(lc, a, grid, s); break;
-        case 2: w16_launch<2>(lc, a, grid, s); break;
-        case 4: w16_launch<4>(lc, a, grid, s); break;
-        case 5: hipLaunchKernelGGL((wgrad_halo16_x3<5, 0>), grid, dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL((wgrad_halo16_x3<3, 0>), grid, dim3(256), 0, s, a);
+    const bool bounded = a.rows_bound && a.src_bound;
+    const int lc = w16_layout(), rb = wgrad16_rblock(a.R, bounded);
+    switch (wgrad16_planes(bounded)) {
+        case 1: w16_launch<1>(lc, rb, a, grid, s); break;
+        case 2: w16_launch<2>(lc, rb, a, grid, s); break;
+        case 4: w16_launch<4>(lc, rb, a, grid, s); break;
+        case 5: hipLaunchKernelGGL((wgrad_halo16_x3<5, 0, 1>), grid, dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL((wgrad_halo16_x3<3, 0, 1>), grid, dim3(256), 0, s, a);
     }
 }
 

@@ -1071,9 +1071,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo_x3(WgradArgs a) {
         }
 }
 
-const void *wgrad_halo_fn(bool bounded) {
-    return wgrad16_mode() ? wgrad_halo16_fn(bounded) : reinterpret_cast<const void *>(&wgrad_halo_x3);
+const void *wgrad_halo_fn(bool bounded, int rblock) {
+    return wgrad16_mode() ? wgrad_halo16_fn(bounded, rblock) : reinterpret_cast<const void *>(&wgrad_halo_x3);
 }
+int wgrad_halo_rblock(int R, bool bounded) { return wgrad16_mode() ? wgrad16_rblock(R, bounded) : 64; }
 
 void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
     if (wgrad16_mode())

@@ -104,6 +104,7 @@ _SIGS = {
     "scd_wgrad_plan": ([POINTER(WGRAD), POINTER(c_int32), POINTER(c_size_t)], c_int),
     "scd_conv_wgrad": ([POINTER(WGRAD), c_void_p, c_size_t, c_void_p], c_int),
     "scd_wgrad_arith": ([POINTER(WGRAD)], c_int),
+    "scd_wgrad_rows_per_block": ([POINTER(WGRAD)], c_int),
     "scd_wgrad_finalize": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_bn_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32], c_size_t),
     "scd_bn_train_stats": (
@@ -426,6 +427,13 @@ def wgrad_arith(d: 'WGRAD') -> str:
     rc = lib().scd_wgrad_arith(ctypes.byref(d))
     _check(min(rc, 0), "scd_wgrad_arith")
     return {v: k for k, v in _MATH_NAMES.items()}[rc]
+
+
+def wgrad_rows_per_block(d: 'WGRAD') -> int:
+    """dY rows per workgroup of the halo weight-grad kernel for this descriptor (64 / 128; 0: another kernel)."""
+    rc = lib().scd_wgrad_rows_per_block(ctypes.byref(d))
+    _check(min(rc, 0), "scd_wgrad_rows_per_block")
+    return rc
 
 
 def igemm_input_bn_supported(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
