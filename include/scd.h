@@ -245,6 +245,16 @@ typedef struct scd_wgrad {
      * scd_igemm_t.src_bound.  With both set the 16x16x32 halo weight grad runs the fp16 two-term split; else x3. */
     const float *rows_bound;
     const float *src_bound;
+    /* Optional fused BatchNorm + ReLU backward of the rows (the input layer's: its dy is read by this weight grad
+     * only): `rows` then holds dL/da of a = relu(BN(y)) and every dY element is formed while staging exactly as
+     * scd_bn_relu_backward would write it, dy = gamma*invstd*(dz - k1 - xhat*k2), dz = da*[y*scale+shift > 0],
+     * xhat = (y-mean)*invstd, so that dy is never written.  rows_y = y (same n, h, w, c as rows); rows_nseg
+     * segments of images; save_mean / save_invstd / scale / shift [nseg][c] from the forward; gamma [c] (NULL = 1);
+     * coef [nseg][c][2] = {k1, k2} from scd_bn_relu_backward_coef.  rows_y.data NULL = off.  Only where
+     * scd_wgrad_rows_bn_supported() returns 1. */
+    scd_nhwc_t rows_y;
+    int32_t rows_nseg;
+    const float *rows_mean, *rows_invstd, *rows_gamma, *rows_scale, *rows_shift, *rows_coef;
 } scd_wgrad_t;
 
 /* Number of K-splits the library will use and the slab bytes it needs. */
@@ -256,6 +266,8 @@ int scd_wgrad_rows_per_block(const scd_wgrad_t *d);
 int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream);
 /* 1 if the weight-grad kernel scd_conv_wgrad would run for `d` applies the src_scale/src_shift transform. */
 int scd_wgrad_src_bn_supported(const scd_wgrad_t *d);
+/* 1 if it forms the rows through the fused BatchNorm backward (scd_wgrad_t.rows_y): the 16-channel-source kernel. */
+int scd_wgrad_rows_bn_supported(const scd_wgrad_t *d);
 /* Sum the slabs (deterministic fixed-order two-level reduction; the slabs are scratch and are
  * overwritten) and unpack to the parameter layout.
  * mode 0: out OIHW [R][c_valid][3][3]  (slab cols (ky*3+kx)*C + c)
@@ -332,6 +344,15 @@ int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const 
                                const float *tile_rec, int32_t ntiles, float *dgamma, float *dbeta,
                                float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws, size_t ws_bytes,
                                scd_stream_t stream);
+
+/* The statistics half of scd_bn_relu_backward(_tiles), for a consumer that forms dy itself (scd_wgrad_t.rows_y):
+ * coef[nseg][c][2] = {mean(dz), mean(dz*xhat)} per segment, dgamma, dbeta, and dbias_prev = sum(dy) formed from the
+ * sums (zero up to rounding: the BatchNorm removes the mean).  tile_rec = conv-epilogue records as in
+ * scd_bn_relu_backward_tiles (da may then be null), or NULL for a partial pass over (y, da). */
+int scd_bn_relu_backward_coef(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
+                              const float *save_invstd, const float *gamma, const float *scale, const float *shift,
+                              const float *tile_rec, int32_t ntiles, float *coef, float *dgamma, float *dbeta,
+                              float *dbias_prev, void *ws, size_t ws_bytes, scd_stream_t stream);
 
 /* out[c] = sum over all pixels of x[., c] (ConvTranspose2d bias grad, networks.py:433); workspace as
  * scd_bn_workspace_bytes(n, h, w, c, 1).  replaces: the bias-grad reduction of convolution_backward. */

@@ -302,10 +302,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(const float *__restr
 // ------------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ f4 relu_mask(f4 y, f4 sc, f4 sf, f4 g) {
-    return f4{fmaf(y.x, sc.x, sf.x) > 0.f ? g.x : 0.f, fmaf(y.y, sc.y, sf.y) > 0.f ? g.y : 0.f,
-              fmaf(y.z, sc.z, sf.z) > 0.f ? g.z : 0.f, fmaf(y.w, sc.w, sf.w) > 0.f ? g.w : 0.f};
-}
+// relu_mask / bn_bwd_dy4: common.h (shared with the weight grad's fused dY staging)
 
 // Incoming gradient dL/da of the BatchNorm + ReLU backward, read at (pixel p, channel quad c).
 struct DaPlain {  // a materialised tensor
@@ -491,7 +488,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const float *_
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (ok[k]) {
-                    const f4 ov = mul * (relu_mask(yv[k], sc, sf, g[k]) - k1 - ((yv[k] - mu) * iv) * k2);
+                    const f4 ov = bn_bwd_dy4(yv[k], g[k], mu, iv, sc, sf, k1, k2, mul);
                     st4(dy + pix[k] * lddy + c, ov);
                     acc += ov;
                     amax = fmax4(amax, fabs4(ov));
@@ -571,15 +568,18 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__rest
     }
 }
 
-// one workgroup per channel: coef[seg][C][2] = {mean(dz), mean(dz*xhat)}; dgamma/dbeta summed over segments
+// one workgroup per channel: coef[seg][C][2] = {mean(dz), mean(dz*xhat)}; dgamma/dbeta summed over segments.
+// dbias (optional; the deferred form, whose dy is formed by its consumer and never summed): sum(dy) from the sums,
+// sum_seg gamma*invstd * (S1 - pseg * k1) -- zero but for the rounding of k1, as BatchNorm removes the mean.
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__restrict__ rec, int C, int nseg,
                                                               int ncps, int nrec, int64_t pseg, float *coef,
-                                                              float *dgamma, float *dbeta) {
+                                                              float *dgamma, float *dbeta, const float *gamma = nullptr,
+                                                              const float *sinv = nullptr, float *dbias = nullptr) {
     __shared__ double a1[BN_THREADS], a2[BN_THREADS];
     const int c = blockIdx.x;
     const int t = threadIdx.x;
     const float *rc = rec + size_t(c) * nrec * 2;
-    double tg = 0, tb = 0;
+    double tg = 0, tb = 0, db = 0;
     for (int s = 0; s < nseg; ++s) {
         double s1 = 0, s2 = 0;
         for (int k = t; k < ncps; k += BN_THREADS) {
@@ -597,16 +597,22 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__res
             __syncthreads();
         }
         if (t == 0) {
-            coef[(s * C + c) * 2 + 0] = float(a1[0] / double(pseg));
+            const float k1 = float(a1[0] / double(pseg));
+            coef[(s * C + c) * 2 + 0] = k1;
             coef[(s * C + c) * 2 + 1] = float(a2[0] / double(pseg));
             tb += a1[0];
             tg += a2[0];
+            if (dbias) {
+                const float mul = (gamma ? gamma[c] : 1.f) * sinv[s * C + c];
+                db += double(mul) * (a1[0] - double(pseg) * double(k1));
+            }
         }
         __syncthreads();
     }
     if (t == 0) {
         if (dgamma) dgamma[c] = float(tg);
         if (dbeta) dbeta[c] = float(tb);
+        if (dbias) dbias[c] = float(db);
     }
 }
 
@@ -641,10 +647,10 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
             f4 g2 = da(p + 2 * npl, c), g3 = da(p + 3 * npl, c);
             PIN4(y0, y1, y2, y3);
             PIN4(g0, g1, g2, g3);
-            const f4 o0 = mul * (relu_mask(y0, sc, sf, g0) - k1 - ((y0 - mu) * iv) * k2);
-            const f4 o1 = mul * (relu_mask(y1, sc, sf, g1) - k1 - ((y1 - mu) * iv) * k2);
-            const f4 o2 = mul * (relu_mask(y2, sc, sf, g2) - k1 - ((y2 - mu) * iv) * k2);
-            const f4 o3 = mul * (relu_mask(y3, sc, sf, g3) - k1 - ((y3 - mu) * iv) * k2);
+            const f4 o0 = bn_bwd_dy4(y0, g0, mu, iv, sc, sf, k1, k2, mul);
+            const f4 o1 = bn_bwd_dy4(y1, g1, mu, iv, sc, sf, k1, k2, mul);
+            const f4 o2 = bn_bwd_dy4(y2, g2, mu, iv, sc, sf, k1, k2, mul);
+            const f4 o3 = bn_bwd_dy4(y3, g3, mu, iv, sc, sf, k1, k2, mul);
             st4(dy + p * lddy + c, o0);
             st4(dy + (p + npl) * lddy + c, o1);
             st4(dy + (p + 2 * npl) * lddy + c, o2);
@@ -654,7 +660,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
         }
         for (; p < ch.end; p += npl) {
             const f4 y0 = ld4(y + p * ldy + c);
-            const f4 o0 = mul * (relu_mask(y0, sc, sf, da(p, c)) - k1 - ((y0 - mu) * iv) * k2);
+            const f4 o0 = bn_bwd_dy4(y0, da(p, c), mu, iv, sc, sf, k1, k2, mul);
             st4(dy + p * lddy + c, o0);
             acc += o0;
             if (dy_bound) amax = fmax4(amax, fabs4(o0));
@@ -1048,6 +1054,41 @@ extern "C" int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t n
                        save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr, dy_bound);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
     return launch_status("scd_bn_relu_backward_tiles");
+}
+
+extern "C" int scd_bn_relu_backward_coef(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
+                                         const float *save_invstd, const float *gamma, const float *scale,
+                                         const float *shift, const float *tile_rec, int32_t ntiles, float *coef,
+                                         float *dgamma, float *dbeta, float *dbias_prev, void *ws, size_t ws_bytes,
+                                         scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(bn_check(y, nseg));
+    SCD_TRY(check_view(da, "bn_bwd_coef.da", tile_rec != nullptr));
+    if ((!tile_rec && (da.n != y.n || da.h != y.h || da.w != y.w || da.c != y.c)) || !save_mean || !save_invstd ||
+        !scale || !shift || !coef || (tile_rec && (ntiles < nseg || ntiles % nseg || pixels(y) % ntiles))) {
+        set_error("bn_relu_backward_coef: shape mismatch / null / %d tiles not divisible into %d segments", ntiles,
+                  nseg);
+        return SCD_ERR_ARG;
+    }
+    if (!ws || ws_bytes < scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg)) {
+        set_error("bn_relu_backward_coef: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    const BnGeom g = bn_geom(y, nseg);
+    hipStream_t s = as_stream(stream);
+    if (tile_rec) {
+        hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, tile_rec, y.c, nseg, ntiles / nseg,
+                           ntiles, g.pseg, coef, dgamma, dbeta, gamma, save_invstd, dbias_prev);
+    } else {
+        float *rec = static_cast<float *>(ws);
+        hipLaunchKernelGGL(bn_bwd_partial<DaPlain>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                           static_cast<const float *>(y.data), y.ldc,
+                           DaPlain{static_cast<const float *>(da.data), da.ldc}, y.c, g.pseg, g.ncps, g.chunk, g.nrec,
+                           g.qpb, save_mean, save_invstd, scale, shift, rec);
+        hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
+                           coef, dgamma, dbeta, gamma, save_invstd, dbias_prev);
+    }
+    return launch_status("scd_bn_relu_backward_coef");
 }
 
 extern "C" int scd_channel_sum(scd_nhwc_t x, float *out, void *ws, size_t ws_bytes, scd_stream_t stream) {

@@ -86,6 +86,20 @@ __device__ __forceinline__ void wave_max_bound(float *bound, float v) {
     if ((threadIdx.x & 63) == 0) atomic_max_bound(bound, v);
 }
 
+// BatchNorm + ReLU backward of one channel quad, shared by bn_bwd_apply and the weight grad's fused dY staging so
+// both form the same bits:  dz = g where fma(y, sc, sf) > 0 (the forward's exact ReLU test), else 0;
+//   dy = mul * (dz - k1 - ((y - mu) * iv) * k2),  mul = gamma * invstd, k1 = mean(dz), k2 = mean(dz * xhat).
+typedef float bnf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bnf4 relu_mask(bnf4 y, bnf4 sc, bnf4 sf, bnf4 g) {
+    return bnf4{fmaf(y.x, sc.x, sf.x) > 0.f ? g.x : 0.f, fmaf(y.y, sc.y, sf.y) > 0.f ? g.y : 0.f,
+                fmaf(y.z, sc.z, sf.z) > 0.f ? g.z : 0.f, fmaf(y.w, sc.w, sf.w) > 0.f ? g.w : 0.f};
+}
+__device__ __forceinline__ bnf4 bn_bwd_dy4(bnf4 y, bnf4 g, bnf4 mu, bnf4 iv, bnf4 sc, bnf4 sf, bnf4 k1, bnf4 k2,
+                                           bnf4 mul) {
+#pragma clang fp contract(off)  // no fma formation that could differ between the two call sites
+    return mul * (relu_mask(y, sc, sf, g) - k1 - ((y - mu) * iv) * k2);
+}
+
 // Device-side NHWC element pointer helpers.
 struct View {
     float *p;

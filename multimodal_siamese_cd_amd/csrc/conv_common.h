@@ -106,6 +106,13 @@ struct WgradArgs {
     const float *src_scale, *src_shift;  // optional fused src BN-apply + ReLU (halo16 weight grad only)
     int src_seg_imgs;
     const float *rows_bound, *src_bound;  // SCD_MATH_H2: upper bounds of |rows| and |src| (as read), both or neither
+    // optional fused BatchNorm + ReLU backward of the rows (16-channel-source weight grad only): rows hold dL/da,
+    // the kernel forms dy = bn_bwd_dy4(y, da, ...) while staging; coefficients per segment of rows_seg_imgs images
+    const float *rows_y;
+    int ldc_y;
+    uint32_t y_bytes;
+    const float *rbn_mean, *rbn_inv, *rbn_gamma, *rbn_scale, *rbn_shift, *rbn_coef;
+    int rows_seg_imgs;
 };
 
 // Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels

@@ -982,6 +982,12 @@ extern "C" int scd_wgrad_src_bn_supported(const scd_wgrad_t *d) {
     return wgrad_src_bn_ok(d) ? 1 : 0;
 }
 
+extern "C" int scd_wgrad_rows_bn_supported(const scd_wgrad_t *d) {
+    clear_error();
+    if (wgrad_validate(d) != SCD_OK) return 0;
+    return wgrad_c16_ok(d) ? 1 : 0;
+}
+
 extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
@@ -1002,9 +1008,11 @@ extern "C" int scd_wgrad_rows_per_block(const scd_wgrad_t *d) {
 namespace scd {
 // Images per weight-grad launch (rows.n = one launch; 0 = one image alone exceeds 2 GiB), see image_chunk.
 static int wgrad_chunk(const scd_wgrad_t *d) {
-    const int64_t per = std::max(img_bytes(d->rows), img_bytes(d->src));
+    int64_t per = std::max(img_bytes(d->rows), img_bytes(d->src));
+    if (d->rows_y.data) per = std::max(per, img_bytes(d->rows_y));
     if (int64_t(d->rows.n) * per < (int64_t(1) << 31)) return d->rows.n;
-    const int seg = (d->src_scale && d->src_nseg > 0) ? d->src.n / d->src_nseg : 1;
+    int seg = (d->src_scale && d->src_nseg > 0) ? d->src.n / d->src_nseg : 1;
+    if (d->rows_y.data && d->rows_nseg > 0) seg = std::max(seg, d->rows.n / d->rows_nseg);
     return image_chunk(per, d->rows.n, seg);
 }
 static scd_wgrad_t wgrad_slice(const scd_wgrad_t *d, int img0, int cnt) {
@@ -1016,6 +1024,17 @@ static scd_wgrad_t wgrad_slice(const scd_wgrad_t *d, int img0, int cnt) {
         c.src_scale = d->src_scale + size_t(img0 / sg) * d->src.c;
         c.src_shift = d->src_shift + size_t(img0 / sg) * d->src.c;
         c.src_nseg = std::max(1, cnt / sg);
+    }
+    if (d->rows_y.data && d->rows_nseg > 0) {
+        const int sg = d->rows.n / d->rows_nseg;
+        const size_t o = size_t(img0 / sg) * d->rows.c;
+        c.rows_y = img_slice(d->rows_y, img0, cnt);
+        c.rows_mean = d->rows_mean + o;
+        c.rows_invstd = d->rows_invstd + o;
+        c.rows_scale = d->rows_scale + o;
+        c.rows_shift = d->rows_shift + o;
+        c.rows_coef = d->rows_coef + 2 * o;
+        c.rows_nseg = std::max(1, cnt / sg);
     }
     return c;
 }
@@ -1119,6 +1138,35 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     a.src_seg_imgs = d->src.n;
     a.rows_bound = d->rows_bound;
     a.src_bound = d->src_bound;
+    a.rows_y = nullptr;
+    a.ldc_y = 0;
+    a.y_bytes = 0;
+    a.rbn_mean = a.rbn_inv = a.rbn_gamma = a.rbn_scale = a.rbn_shift = a.rbn_coef = nullptr;
+    a.rows_seg_imgs = d->rows.n;
+    if (d->rows_y.data) {
+        const scd_nhwc_t &y = d->rows_y;
+        const int64_t yb = (pixels(y) - 1) * y.ldc * 4 + int64_t(y.c) * 4;
+        if (check_view(y, "wgrad.rows_y") != SCD_OK || y.n != d->rows.n || y.h != d->rows.h || y.w != d->rows.w ||
+            y.c != d->rows.c || y.ldc % 4 || d->rows_nseg < 1 || d->rows.n % d->rows_nseg || !d->rows_mean ||
+            !d->rows_invstd || !d->rows_scale || !d->rows_shift || !d->rows_coef || !aligned16(d->rows_mean) ||
+            !aligned16(d->rows_invstd) || !aligned16(d->rows_scale) || !aligned16(d->rows_shift) ||
+            !aligned16(d->rows_coef) || (d->rows_gamma && !aligned16(d->rows_gamma)) || !wgrad_c16_ok(d) ||
+            yb >= (int64_t(1) << 31)) {
+            set_error("wgrad: the rows BatchNorm backward needs y shaped as rows, rows_nseg | rows.n, 16-byte "
+                      "aligned coefficient arrays and a supported shape (check scd_wgrad_rows_bn_supported)");
+            return SCD_ERR_ARG;
+        }
+        a.rows_y = static_cast<const float *>(y.data);
+        a.ldc_y = y.ldc;
+        a.y_bytes = uint32_t(yb);
+        a.rbn_mean = d->rows_mean;
+        a.rbn_inv = d->rows_invstd;
+        a.rbn_gamma = d->rows_gamma;
+        a.rbn_scale = d->rows_scale;
+        a.rbn_shift = d->rows_shift;
+        a.rbn_coef = d->rows_coef;
+        a.rows_seg_imgs = d->rows.n / d->rows_nseg;
+    }
     if (d->src_scale || d->src_shift) {
         if (!d->src_scale || !d->src_shift || d->src_nseg < 1 || d->src.n % d->src_nseg ||
             !aligned16(d->src_scale) || !aligned16(d->src_shift) || !wgrad_src_bn_ok(d)) {

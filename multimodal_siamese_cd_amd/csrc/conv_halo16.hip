@@ -1256,7 +1256,9 @@ __device__ __forceinline__ void c16_chain(f32x4 (&acc)[9], bf16x8 (&dv)[3], s16x
 }
 }  // namespace
 
-template <int NP>
+// RBN: the rows are dL/da of a = relu(BN(y)) and each staged dY piece is formed as the BatchNorm backward's apply
+// would write it (bn_bwd_dy4, the same bits), so that gradient is never written or re-read (the input layer's).
+template <int NP, bool RBN>
 __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
     constexpr int PH = 2, PW = 16, P = PH * PW;
     constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
@@ -1279,9 +1281,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
 
     const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
+    const __amdgpu_buffer_rsrc_t rs_y = make_rsrc(RBN ? a.rows_y : a.rows, RBN ? a.y_bytes : 0u);
 
-    f32x4 ra[A_PER], rb[B_PER];
+    f32x4 ra[A_PER], rb[B_PER], ya[RBN ? A_PER : 1];
     f32x4 x_sc, x_sh;      // src transform coefficients of this thread's 4 channels (cq = tid & 3)
+    f32x4 r_mu, r_iv, r_sc, r_sf, r_k1, r_k2, r_mul;  // RBN: this thread's 4 rows r0 + 4 (tid & 15) + 0..3
     uint32_t x_valid = 0;  // bit i: halo piece i is inside the image (the padding stays zero)
     auto load_patch = [&](int pi) {
         const int img = pi / pimg, pr = pi - img * pimg;
@@ -1290,14 +1294,26 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
             x_sc = gload4(a.src_scale + ch);
             x_sh = gload4(a.src_shift + ch);
         }
+        if constexpr (RBN) {
+            const int c = r0 + (tid & 15) * 4, o = (img / a.rows_seg_imgs) * a.R + c;
+            r_mu = gload4(a.rbn_mean + o);
+            r_iv = gload4(a.rbn_inv + o);
+            r_sc = gload4(a.rbn_scale + o);
+            r_sf = gload4(a.rbn_shift + o);
+            const f32x4 c0 = gload4(a.rbn_coef + 2 * o), c1 = gload4(a.rbn_coef + 2 * o + 4);
+            r_k1 = f32x4{c0[0], c0[2], c1[0], c1[2]};
+            r_k2 = f32x4{c0[1], c0[3], c1[1], c1[3]};
+            r_mul = (a.rbn_gamma ? gload4(a.rbn_gamma + c) : f32x4{1.f, 1.f, 1.f, 1.f}) * r_iv;
+        }
         x_valid = 0;
         const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * 256, q = e >> 4, cq = e & 15;
             const int py = q >> 4, px = q & 15;
-            const uint32_t off = uint32_t(((img * a.ho + y0 + py) * a.wo + x0 + px) * a.ldc_r + r0 + cq * 4) * 4u;
-            ra[i] = bload4(rs_rows, off);
+            const int pix = (img * a.ho + y0 + py) * a.wo + x0 + px;
+            ra[i] = bload4(rs_rows, uint32_t(pix * a.ldc_r + r0 + cq * 4) * 4u);
+            if constexpr (RBN) ya[i] = bload4(rs_y, uint32_t(pix * a.ldc_y + r0 + cq * 4) * 4u);
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
@@ -1315,6 +1331,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
             const int e = tid + i * 256;
             const int o = (e >> 4) * RS + (e & 15) * 8;
             u32x2 h, m, l;
+            if constexpr (RBN) ra[i] = bn_bwd_dy4(ya[i], ra[i], r_mu, r_iv, r_sc, r_sf, r_k1, r_k2, r_mul);
             if constexpr (DP == 3) {
                 split3(ra[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
@@ -1399,17 +1416,24 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
 
 const void *wgrad_halo16_c16_fn() {
     switch (bf16_planes()) {
-        case 1: return reinterpret_cast<const void *>(&wgrad_halo16_c16<1>);
-        case 5: return reinterpret_cast<const void *>(&wgrad_halo16_c16<5>);
-        default: return reinterpret_cast<const void *>(&wgrad_halo16_c16<3>);
+        case 1: return reinterpret_cast<const void *>(&wgrad_halo16_c16<1, false>);
+        case 5: return reinterpret_cast<const void *>(&wgrad_halo16_c16<5, false>);
+        default: return reinterpret_cast<const void *>(&wgrad_halo16_c16<3, false>);
+    }
+}
+template <bool RBN>
+static void launch_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
+    switch (bf16_planes()) {
+        case 1: hipLaunchKernelGGL((wgrad_halo16_c16<1, RBN>), grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((wgrad_halo16_c16<5, RBN>), grid, dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL((wgrad_halo16_c16<3, RBN>), grid, dim3(256), 0, s, a);
     }
 }
 void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    switch (bf16_planes()) {
-        case 1: hipLaunchKernelGGL(wgrad_halo16_c16<1>, grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL(wgrad_halo16_c16<5>, grid, dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL(wgrad_halo16_c16<3>, grid, dim3(256), 0, s, a);
-    }
+    if (a.rows_y)
+        launch_c16<true>(a, grid, s);
+    else
+        launch_c16<false>(a, grid, s);
 }
 
 // 0 = the 32x32x16 halo weight-grad kernel, 1 = this one (scd_set_wgrad16; initial value from SCD_WGRAD16).

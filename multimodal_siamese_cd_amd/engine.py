@@ -29,7 +29,7 @@ _F32 = torch.float32
 
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
-         'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True}
+         'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True, 'defer_bn_bwd': True}
 
 
 def conv_math_for(cfg) -> str:
@@ -57,7 +57,9 @@ def set_options(**kw) -> dict:
     fuse_bn_bwd: compute the first BatchNorm's backward partial sums in the epilogue of the data-grad conv that
     produces its incoming gradient, instead of a separate pass.
     fuse_siamese_encoder: Siamese streams run SiameseEncoderFn (BN1 + ReLU fused into the next MaxPool and the
-    feature difference, differences written into the decoder's concat buffers).  Returns the previous options."""
+    feature difference, differences written into the decoder's concat buffers).
+    defer_bn_bwd: the input layer's BatchNorm backward stops at its statistics and the weight grad (its only
+    reader) forms dy while staging, so that gradient is never written.  Returns the previous options."""
     prev = dict(_OPTS)
     for k, v in kw.items():
         if k not in _OPTS:
@@ -373,10 +375,11 @@ def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool, mate
 
 
 def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, src_bn=None, rows_bound=None,
-              src_bound=None) -> torch.Tensor:
+              src_bound=None, rows_bn=None) -> torch.Tensor:
+    """`rows_bn` (hip._rows_bn_fields): dy is dL/da, formed into the BatchNorm backward's dy while staging."""
     if rows_bound is None or src_bound is None:
         rows_bound = src_bound = None
-    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3, src_bn, rows_bound, src_bound)
+    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3, src_bn, rows_bound, src_bound, rows_bn)
     slabs = _empty((nbytes // 4,), dy)
     hip.conv_wgrad(d, slabs)
     gw = torch.empty_like(weight)
@@ -418,6 +421,20 @@ def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, dy_bo
     return dy, dgamma, dbeta, dbias
 
 
+def _bn_backward_coef(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None):
+    """The statistics half of _bn_backward (hip.bn_relu_backward_coef): (dgamma, dbeta, dbias, coef)."""
+    c = y.shape[3]
+    dgamma, dbeta = _empty((c,), y), _empty((c,), y)
+    dbias = _empty((c,), y) if conv_bias_grad else None
+    coef = _empty((st.nseg * c * 2,), y)
+    n, h, w, _ = y.shape
+    ws = _ws(hip.bn_workspace_bytes(n, h, w, c, st.nseg), y)
+    hip.bn_relu_backward_coef(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift,
+                              tiles[0] if tiles is not None else None, tiles[1] if tiles is not None else 0, coef,
+                              dgamma, dbeta, dbias, ws)
+    return dgamma, dbeta, dbias, coef
+
+
 def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Tensor, st0: _BNSaved,
                   src_bound=None):
     """Data-grad conv producing dL/da0, with BN0's backward partial sums fused into its epilogue when the kernel
@@ -452,6 +469,12 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None):
         gw1 = _wgrad3x3(dy1, a0, conv1.weight, None, d1, b0)
     ga0, tiles0 = _dgrad_bn_bwd(dy1, packed_conv3x3(conv1.weight, 1), conv1.in_channels, y0, st0, d1)
     d0 = _take(pool)
+    if not need_dx and _OPTS['defer_bn_bwd'] and hip.wgrad_rows_bn_supported(nhwc(ga0), nhwc(x), 1, TAPS_3X3):
+        # the input layer: dy0 has one reader, the weight grad, which forms it while staging
+        dg0, db0, dbias0, coef = _bn_backward_coef(y0, ga0, st0, bn0, conv0.bias is not None, tiles0)
+        rows_bn = (nhwc(y0), st0.nseg, st0.smean, st0.sinv, bn0.weight, st0.scale, st0.shift, coef)
+        gw0 = _wgrad3x3(ga0, x, conv0.weight, None, None, None, rows_bn)
+        return None, [gw0, dbias0, dg0, db0, gw1, dbias1, dg1, db1]
     dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0, d0)
     gw0 = _wgrad3x3(dy0, x, conv0.weight, None, d0, x_bound)
     gx = None

@@ -66,6 +66,14 @@ class WGRAD(ctypes.Structure):
         ("src_nseg", c_int32),
         ("rows_bound", c_void_p),
         ("src_bound", c_void_p),
+        ("rows_y", NHWC),
+        ("rows_nseg", c_int32),
+        ("rows_mean", c_void_p),
+        ("rows_invstd", c_void_p),
+        ("rows_gamma", c_void_p),
+        ("rows_scale", c_void_p),
+        ("rows_shift", c_void_p),
+        ("rows_coef", c_void_p),
     ]
 
 
@@ -105,6 +113,7 @@ _SIGS = {
     "scd_conv_wgrad": ([POINTER(WGRAD), c_void_p, c_size_t, c_void_p], c_int),
     "scd_wgrad_arith": ([POINTER(WGRAD)], c_int),
     "scd_wgrad_rows_per_block": ([POINTER(WGRAD)], c_int),
+    "scd_wgrad_rows_bn_supported": ([POINTER(WGRAD)], c_int),
     "scd_wgrad_finalize": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_bn_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32], c_size_t),
     "scd_bn_train_stats": (
@@ -131,6 +140,11 @@ _SIGS = {
     "scd_bn_relu_backward_tiles": (
         [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
          c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_size_t, c_void_p],
+        c_int,
+    ),
+    "scd_bn_relu_backward_coef": (
+        [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
         c_int,
     ),
     "scd_channel_sum": ([NHWC, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
@@ -451,13 +465,27 @@ def igemm_stat_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: 
     return (n, tp.value) if n > 0 else (0, 0)
 
 
-def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None, rows_bound=None, src_bound=None):
+def _rows_bn_fields(d: 'WGRAD', rows_bn):
+    """rows_bn = (y NHWC, nseg, save_mean, save_invstd, gamma or None, scale, shift, coef): the rows are dL/da and
+    the kernel forms dy through the BatchNorm backward while staging (scd_wgrad_t.rows_y)."""
+    y, nseg, mean, inv, gamma, sc, sh, coef = rows_bn
+    d.rows_y = y
+    d.rows_nseg = nseg
+    d.rows_mean, d.rows_invstd, d.rows_gamma = _ptr(mean), _ptr(inv), _ptr(gamma)
+    d.rows_scale, d.rows_shift, d.rows_coef = _ptr(sc), _ptr(sh), _ptr(coef)
+
+
+def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None, rows_bound=None, src_bound=None,
+               rows_bn=None):
     """`src_bn` = (scale, shift, nseg): read src through its BatchNorm-apply + ReLU (see scd_wgrad_t).
-    `rows_bound` / `src_bound`: device floats bounding |rows| and |src as read| (SCD_MATH_H2; both or neither)."""
+    `rows_bound` / `src_bound`: device floats bounding |rows| and |src as read| (SCD_MATH_H2; both or neither).
+    `rows_bn`: see _rows_bn_fields (only where wgrad_rows_bn_supported)."""
     nt, dy, dx = _taps(taps)
     sc, sh, nseg = src_bn if src_bn is not None else (None, None, 0)
     d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg, _ptr(rows_bound), _ptr(src_bound))
-    d._keep = (rows_bound, src_bound)
+    if rows_bn is not None:
+        _rows_bn_fields(d, rows_bn)
+    d._keep = (rows_bound, src_bound, rows_bn)
     ns = c_int32(0)
     nb = c_size_t(0)
     _check(lib().scd_wgrad_plan(ctypes.byref(d), ctypes.byref(ns), ctypes.byref(nb)), "scd_wgrad_plan")
@@ -469,6 +497,13 @@ def wgrad_src_bn_supported(rows: NHWC, src: NHWC, stride: int, taps, src_bn) -> 
     sc, sh, nseg = src_bn
     d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg, None, None)
     return lib().scd_wgrad_src_bn_supported(ctypes.byref(d)) == 1
+
+
+def wgrad_rows_bn_supported(rows: NHWC, src: NHWC, stride: int, taps) -> bool:
+    """Whether the weight grad for (rows, src) can form its rows through the fused BatchNorm backward."""
+    nt, dy, dx = _taps(taps)
+    d = WGRAD(rows, src, stride, nt, dy, dx, None, None, 0, None, None)
+    return lib().scd_wgrad_rows_bn_supported(ctypes.byref(d)) == 1
 
 
 def conv_wgrad(d: WGRAD, slabs: torch.Tensor):
@@ -551,6 +586,17 @@ def bn_relu_backward_tiles(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, s
                                          shift.data_ptr(), tile_rec.data_ptr(), ntiles, _ptr(dgamma), _ptr(dbeta),
                                          _ptr(dbias), dy, _ptr(dy_bound), ws.data_ptr(), ws.numel(), _stream()),
         "scd_bn_relu_backward_tiles")
+
+
+def bn_relu_backward_coef(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, tile_rec, ntiles, coef, dgamma,
+                          dbeta, dbias, ws):
+    """The statistics half of bn_relu_backward(_tiles): coef [nseg][C][2], dgamma, dbeta, dbias (sum dy, from the
+    sums) for a consumer that forms dy itself (wgrad_plan(..., rows_bn=...)).  tile_rec None: a pass over (y, da)."""
+    _check(
+        lib().scd_bn_relu_backward_coef(y, da, nseg, smean.data_ptr(), sinv.data_ptr(), _ptr(gamma), scale.data_ptr(),
+                                        shift.data_ptr(), _ptr(tile_rec), ntiles, coef.data_ptr(), _ptr(dgamma),
+                                        _ptr(dbeta), _ptr(dbias), ws.data_ptr(), ws.numel(), _stream()),
+        "scd_bn_relu_backward_coef")
 
 
 def channel_sum(x: NHWC, out: torch.Tensor, ws: torch.Tensor):

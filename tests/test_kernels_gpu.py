@@ -550,6 +550,70 @@ def test_batchnorm_relu_train_forward_backward(dev, n, h, w, c, nseg):
     assert (dbias.cpu() - y.grad.sum((0, 1, 2))).abs().max() < 1e-3 * y.grad.abs().max()
 
 
+@pytest.mark.parametrize('math', ['x3', 'bf16'])
+@pytest.mark.parametrize('n,h,w,co,nseg,tiles', [(4, 8, 32, 64, 2, False), (2, 4, 16, 128, 1, False),
+                                                 (4, 16, 16, 64, 2, True)])
+def test_wgrad_c16_deferred_bn_backward(dev, math, n, h, w, co, nseg, tiles):
+    """The input layer's weight grad forming dy = BN-backward(y, da) while staging (scd_wgrad_t.rows_y, coefficients
+    from scd_bn_relu_backward_coef) equals the BatchNorm backward's materialised dy fed to the same kernel, bit for
+    bit; dgamma / dbeta are the full backward's; the conv-bias grad (sum dy, 0 in exact arithmetic) stays ~0."""
+    from multimodal_siamese_cd_amd import hip
+    ci = 16
+    g = torch.Generator().manual_seed(n * co + nseg + h)
+    y = (torch.randn(n, h, w, co, generator=g) * 2 + 0.3).to(dev)
+    da = torch.randn(n, h, w, co, generator=g).to(dev)
+    x = torch.randn(n, h, w, ci, generator=g).to(dev)
+    gamma = (torch.rand(co, generator=g) + 0.5).to(dev)
+    beta = torch.randn(co, generator=g).to(dev)
+    smean, sinv, scale, shift = (torch.empty(nseg * co, device=dev) for _ in range(4))
+    ws = torch.empty(hip.bn_workspace_bytes(n, h, w, co, nseg), dtype=torch.uint8, device=dev)
+    hip.bn_train_stats(hip.nhwc(y), nseg, gamma, beta, 1e-5, 0.1, False, None, None, smean, sinv, scale, shift, ws)
+    rec, ntiles = None, 0
+    if tiles:  # partial sums as a conv epilogue would record them: one tile per 128 pixels, from the host
+        per, tp = n // nseg, 128
+        yy = y.double().cpu().reshape(-1, tp, co)
+        z = torch.where(y.double().cpu() * scale.double().cpu().reshape(nseg, 1, 1, 1, co).repeat_interleave(
+            per, 0).reshape(n, 1, 1, co) + shift.double().cpu().reshape(nseg, co).repeat_interleave(per, 0).reshape(
+            n, 1, 1, co) > 0, da.double().cpu(), torch.zeros(()).double())
+        mu = smean.double().cpu().reshape(nseg, co).repeat_interleave(per, 0).reshape(n, 1, 1, co)
+        iv = sinv.double().cpu().reshape(nseg, co).repeat_interleave(per, 0).reshape(n, 1, 1, co)
+        xh = ((y.double().cpu() - mu) * iv).reshape(-1, tp, co)
+        zz = z.reshape(-1, tp, co)
+        ntiles = zz.shape[0]
+        rec = torch.stack([zz.sum(1), (zz * xh).sum(1)], -1).permute(1, 0, 2).contiguous().float().to(dev)
+    prev = hip.set_conv_math(math)
+    try:
+        dy = torch.empty_like(y)
+        o = [torch.empty(co, device=dev) for _ in range(3)]
+        if tiles:
+            hip.bn_relu_backward_tiles(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, rec, ntiles,
+                                       *o, hip.nhwc(dy), ws)
+        else:
+            hip.bn_relu_backward(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, *o, hip.nhwc(dy), ws)
+        assert hip.wgrad_rows_bn_supported(hip.nhwc(da), hip.nhwc(x), 1, hip.TAPS_3X3)
+
+        def wgrad(rows, rows_bn=None):
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(rows), hip.nhwc(x), 1, hip.TAPS_3X3, rows_bn=rows_bn)
+            slabs = torch.empty(nbytes // 4, device=dev)
+            hip.conv_wgrad(d, slabs)
+            dw = torch.empty(co, ci, 3, 3, device=dev)
+            hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
+            return dw
+
+        ref = wgrad(dy)
+        coef = torch.empty(nseg * co * 2, device=dev)
+        q = [torch.empty(co, device=dev) for _ in range(3)]
+        hip.bn_relu_backward_coef(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, rec, ntiles, coef,
+                                  *q, ws)
+        out = wgrad(da, (hip.nhwc(y), nseg, smean, sinv, gamma, scale, shift, coef))
+    finally:
+        hip.set_conv_math(prev)
+    assert torch.equal(out, ref)
+    assert torch.equal(q[0], o[0]) and torch.equal(q[1], o[1])
+    scale_dy = dy.abs().max().item()
+    assert q[2].abs().max().item() < 1e-3 * scale_dy and o[2].abs().max().item() < 1e-3 * scale_dy
+
+
 def test_batchnorm_eval(dev):
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(5)

@@ -11,6 +11,7 @@ A variant is a comma list of knob=value with knobs:
   pack  weight packing: 0 per call, 1 cached per weight, 2 batched per model (engine.packed_conv3x3)
   pool_diff  encoder difference + next-level pooling in one pass (engine.set_options(pool_diff=...))
   pooled_bn_bwd  encoder BN backward forms maxpool_bwd -/+ diff grad on the fly (engine.set_options(...))
+  defer_bn_bwd  input layer's BN backward formed inside its weight grad (engine.set_options(defer_bn_bwd=...))
   SCD_* library environment switches read at launch (e.g. SCD_HALO16_TW=64)
 Prints per-variant median / min ms per step over the rounds.
 """
@@ -55,6 +56,8 @@ def apply(variant: str):
             engine.set_options(pool_diff=bool(int(v)))
         elif k == 'pooled_bn_bwd':
             engine.set_options(pooled_bn_bwd=bool(int(v)))
+        elif k == 'defer_bn_bwd':
+            engine.set_options(defer_bn_bwd=bool(int(v)))
         elif k == 'fuse_enc':
             engine.set_options(fuse_siamese_encoder=bool(int(v)))
         elif k.startswith('SCD_'):  # library environment switch (read at launch)
