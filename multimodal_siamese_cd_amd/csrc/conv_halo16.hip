@@ -459,10 +459,11 @@ int h2_wide_tile() {
     return !(e && e[0] == '0');
 }
 
-// Double buffering where two halo buffers of every resident block still fit the CU's 160 KB of LDS.
-int halo16_db() {
+// Double buffering where two halo buffers of every resident block still fit the CU's 160 KB of LDS: for x3 / x5 /
+// bf16; h2 runs single-buffered (same-box A/B: data grad -2.3%, step +0.5%).  SCD_HALO16_DB=0|1 forces it.
+int halo16_db(bool h2) {
     const char *e = getenv("SCD_HALO16_DB");  // experiment switch
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : (h2 ? 0 : 1);
 }
 
 template <int WM, int WN, int TM, int TN, int OCC, bool DB, int NP>
@@ -477,27 +478,27 @@ template <int WM, int WN, int TM, int TN, int OCC>
 void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
-    const bool db3 = tw != 64 && halo16_db() && OCC * 2 * 3 * hr * 64 <= 160 * 1024;
-    const bool db2 = tw != 64 && halo16_db() && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
+    const bool db3 = tw != 64 && halo16_db(false) && OCC * 2 * 3 * hr * 64 <= 160 * 1024;
+    const bool db_h2 = tw != 64 && halo16_db(true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
     // h2 needs the h2 weight split and a bound (igemm_takes_halo16); otherwise x3 (h2 mode: other shapes)
     const int planes = a.src_bound && h2_weight_format(a.ntaps, a.c) ? (h2_prescale() ? 4 : 2)
                        : conv_math_planes() == 2                      ? 3
                                                                       : conv_math_planes();
     switch (planes) {
         case 1:  // one plane: double buffering always fits
-            if (halo16_db())
+            if (halo16_db(false))
                 launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
             else
                 launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
             break;
         case 2:
-            if (db2)
+            if (db_h2)
                 launch16c<WM, WN, TM, TN, OCC, true, 2>(a, tw, s);
             else
                 launch16c<WM, WN, TM, TN, OCC, false, 2>(a, tw, s);
             break;
         case 4:
-            if (db2)
+            if (db_h2)
                 launch16c<WM, WN, TM, TN, OCC, true, 4>(a, tw, s);
             else
                 launch16c<WM, WN, TM, TN, OCC, false, 4>(a, tw, s);
@@ -529,7 +530,7 @@ template <int WM, int WN, int TM, int TN, int OCC>
 void launch16_h2only(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
-    const bool db2 = tw != 64 && halo16_db() && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
+    const bool db2 = tw != 64 && halo16_db(true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
     if (db2)
         launch16c<WM, WN, TM, TN, OCC, true, 4>(a, tw, s);
     else
