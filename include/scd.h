@@ -120,8 +120,8 @@ int scd_set_conv_math(int32_t mode);
  * below.) */
 /* Tile selection of the 16x16x32-MFMA halo conv kernel (SCD_MATH_X3, 3x3 / stride 1, C % 32 == 0):
  * 0 = off (32x32x16 halo kernel), 1 = automatic, 2 + id = force tile id (0: 128 px x 128 ch, 1: 128 x 64,
- * 2: 64 x 128).  Returns the previous mode; -1 only queries.  Process-wide; results are identical up to
- * summation order. */
+ * 2: 64 x 128, 3: 128 x 128 as 1 x 4 waves, h2 only).  Returns the previous mode; -1 only queries.
+ * Process-wide; results are identical up to summation order. */
 int scd_set_halo16(int32_t mode);
 /* Halo weight-grad kernel selection (SCD_MATH_X3, 3x3 / stride 1, R and C multiples of 64): 0 = 32x32x16
  * MFMA kernel, 1 = 16x16x32 MFMA kernel (default).  Returns the previous mode; -1 only queries. */

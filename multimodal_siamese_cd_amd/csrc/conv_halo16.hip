@@ -522,8 +522,7 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
 //   1: 2x2 waves of 64 px x 32 ch  (128 x 64),  3 waves/SIMD
 //   2: 2x2 waves of 32 px x 64 ch  (64 x 128),  3 waves/SIMD
 //   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 only (experiment: no duplicated weight loads)
-//   4: 4x1 waves of 32 px x 128 ch (128 x 128), 2 waves/SIMD, h2 only (experiment: least LDS traffic)
-constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}, {4, 128, 128}};
+constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}};
 
 // The h2 arithmetics only (tile experiments that instantiate no x3 / x5 / bf16 variants).
 template <int WM, int WN, int TM, int TN, int OCC>
@@ -556,7 +555,7 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
         id = 1;  // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
     else
         return 0;
-    if (id < 0 || id > 4 || (id > 2 && !(a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale()))) return 0;
+    if (id < 0 || id > 3 || (id > 2 && !(a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale()))) return 0;
     *bm = kCfg[id].bm;
     const char *twe = getenv("SCD_HALO16_TW");  // preferred tile width (hip.halo16_tile_width_pref mirrors it)
     const int pref = twe ? atoi(twe) : 16;  // 16: smallest halo per pixel (180 rows for 128 px)
@@ -573,7 +572,6 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
         case 0: launch16<2, 2, 4, 4, 2>(a, tw, s); break;
         case 1: launch16<2, 2, 4, 2, 3>(a, tw, s); break;
         case 3: launch16_h2only<1, 4, 8, 2, 2>(a, tw, s); break;
-        case 4: launch16_h2only<4, 1, 2, 8, 2>(a, tw, s); break;
         default: launch16<2, 2, 2, 4, 3>(a, tw, s); break;
     }
 }
@@ -1521,7 +1519,7 @@ extern "C" int scd_set_wgrad16(int32_t mode) {
 extern "C" int scd_set_halo16(int32_t mode) {
     clear_error();
     const int prev = scd::halo16_mode();
-    if (mode >= 0 && mode <= 6) {
+    if (mode >= 0 && mode <= 5) {
         scd::g_halo16 = mode;
     } else if (mode != -1) {
         set_error("scd_set_halo16: mode %d", mode);
