@@ -254,14 +254,22 @@ __global__ __launch_bounds__(BN_THREADS) void bn_tile_merge(const float *__restr
     const int t0 = seg * tiles_per_seg + k * group;
     const int t1 = min(t0 + group, (seg + 1) * tiles_per_seg);
     float n = 0.f, mean = 0.f, m2 = 0.f;
-    for (int t = t0; t < t1; ++t) {
-        const float2 r = *reinterpret_cast<const float2 *>(trec + (size_t(t) * C + c) * 2);
+    auto merge = [&](float2 r) {
         const float nn = n + tile_px;
         const float d = r.x - mean;
         mean += d * (tile_px / nn);
         m2 += r.y + d * d * (n * tile_px / nn);
         n = nn;
+    };
+    int t = t0;
+    for (; t + 8 <= t1; t += 8) {  // 8 records loaded together, merged in tile order (latency, not the merge, bound)
+        float2 r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = *reinterpret_cast<const float2 *>(trec + (size_t(t + u) * C + c) * 2);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) merge(r[u]);
     }
+    for (; t < t1; ++t) merge(*reinterpret_cast<const float2 *>(trec + (size_t(t) * C + c) * 2));
     float *o = rec + (size_t(c) * nrec + g) * 3;
     o[0] = n;
     o[1] = mean;
@@ -581,13 +589,28 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__res
     const float *rc = rec + size_t(c) * nrec * 2;
     double tg = 0, tb = 0, db = 0;
     for (int s = 0; s < nseg; ++s) {
-        double s1 = 0, s2 = 0;
-        for (int k = t; k < ncps; k += BN_THREADS) {
-            s1 += rc[size_t(s * ncps + k) * 2];
-            s2 += rc[size_t(s * ncps + k) * 2 + 1];
+        // 4 records per thread and trip, loads issued together (long tile-record lists are latency-bound otherwise);
+        // fixed order: record k goes to accumulator (k / BN_THREADS) % 4
+        double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+        const float2 *rs = reinterpret_cast<const float2 *>(rc) + size_t(s) * ncps;
+        int k = t;
+        for (; k + 3 * BN_THREADS < ncps; k += 4 * BN_THREADS) {
+            float2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = rs[k + u * BN_THREADS];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s1[u] += v[u].x;
+                s2[u] += v[u].y;
+            }
         }
-        a1[t] = s1;
-        a2[t] = s2;
+        for (int u = 0; k < ncps; k += BN_THREADS, ++u) {
+            const float2 v = rs[k];
+            s1[u] += v.x;
+            s2[u] += v.y;
+        }
+        a1[t] = (s1[0] + s1[1]) + (s1[2] + s1[3]);
+        a2[t] = (s2[0] + s2[1]) + (s2[2] + s2[3]);
         __syncthreads();
         for (int off = BN_THREADS / 2; off > 0; off >>= 1) {
             if (t < off) {

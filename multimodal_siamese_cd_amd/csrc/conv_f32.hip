@@ -411,7 +411,47 @@ __global__ void wgrad_group_sum(float *__restrict__ slabs, int nsplit, int per, 
     slabs[e + size_t(k0) * total] = (s0 + s1) + (s2 + s3);
 }
 
-// Level 2: sum the (group) slabs at stride `gstride` slabs and scatter into the parameter layout.
+// Level 2, one workgroup per (row r, block of kFinCB channels): sum the (group) slabs of the block's 9 column runs
+// [t][c0, c0 + kFinCB) into LDS (coalesced reads; the slab loads of one element issued together, summed in slab
+// order), then write the parameter-order run [c0, c0 + kFinCB)[t] (coalesced writes; LDS rows padded by one float
+// so the transposed reads do not conflict).
+constexpr int kFinCB = 64, kFinMaxTaps = 9;
+__global__ __launch_bounds__(256) void wgrad_finalize_rows(const float *__restrict__ slabs, int nsum, int gstride,
+                                                           int R, int ntaps, int C, int mode, int c_valid,
+                                                           float *__restrict__ out) {
+    __shared__ float tile[kFinMaxTaps * (kFinCB + 1)];
+    const int r = blockIdx.x, c0 = blockIdx.y * kFinCB;
+    const int cb = min(kFinCB, C - c0);
+    const int Ng = ntaps * C;
+    const size_t total = size_t(R) * Ng, kstride = size_t(gstride) * total;
+    const float *row = slabs + size_t(r) * Ng + c0;
+    for (int e = threadIdx.x; e < ntaps * cb; e += blockDim.x) {
+        const int t = e / cb, c = e - t * cb;
+        const float *p = row + t * C + c;
+        float s = 0.f;
+        int k = 0;
+        for (; k + 4 <= nsum; k += 4) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = p[size_t(k + u) * kstride];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s += v[u];
+        }
+        for (; k < nsum; ++k) s += p[size_t(k) * kstride];
+        tile[t * (kFinCB + 1) + c] = s;
+    }
+    __syncthreads();
+    // mode 0: OIHW [R][c_valid][taps]; mode 1: ConvT [R][C][taps]
+    const int cw = mode == 0 ? c_valid : C, cv = max(0, min(cb, cw - c0));
+    float *o = out + (size_t(r) * cw + c0) * ntaps;
+    for (int j = threadIdx.x; j < cv * ntaps; j += blockDim.x) {
+        const int c = j / ntaps, t = j - c * ntaps;
+        o[j] = tile[t * (kFinCB + 1) + c];
+    }
+}
+
+// Level 2 (more than kFinMaxTaps taps): sum the (group) slabs at stride `gstride` slabs and scatter into the
+// parameter layout.
 __global__ void wgrad_finalize_kernel(const float *__restrict__ slabs, int nsum, int gstride, int R, int ntaps,
                                       int C, int mode, int c_valid, float *__restrict__ out) {
     const int Ng = ntaps * C;
@@ -1235,6 +1275,11 @@ extern "C" int scd_wgrad_finalize(float *slabs, int32_t nsplit, int32_t R, int32
         hipLaunchKernelGGL(wgrad_group_sum, dim3(base_blocks, G), dim3(256), 0, s, slabs, nsplit, per, total);
         nsum = G;
         gstride = per;
+    }
+    if (ntaps <= kFinMaxTaps) {
+        hipLaunchKernelGGL(wgrad_finalize_rows, dim3(R, (C + kFinCB - 1) / kFinCB), dim3(256), 0, s, slabs, nsum,
+                           gstride, R, ntaps, C, mode, c_valid, out);
+        return launch_status("scd_wgrad_finalize");
     }
     const int blocks = base_blocks > 4096 ? 4096 : base_blocks;
     hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, slabs, nsum, gstride, R, ntaps, C, mode,
