@@ -184,6 +184,24 @@ __device__ __forceinline__ void dmerge(DWelford &a, const DWelford &b) {
     a.n = n;
 }
 
+// Block merge of per-thread Welford states in a fixed order: xor-shuffle tree within each wave, then the waves'
+// results in wave order by thread 0 (one barrier instead of a log2(BN_THREADS)-level LDS tree).  Valid in thread 0.
+__device__ __forceinline__ DWelford block_dmerge(DWelford w, DWelford *sh) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const DWelford o{__shfl_xor(w.n, off), __shfl_xor(w.mean, off), __shfl_xor(w.m2, off)};
+        dmerge(w, o);
+    }
+    const int t = threadIdx.x;
+    if ((t & 63) == 0) sh[t >> 6] = w;
+    __syncthreads();
+    DWelford a = sh[0];
+    if (t == 0)
+        for (int k = 1; k < BN_THREADS / 64; ++k) dmerge(a, sh[k]);
+    __syncthreads();  // sh is reused by the next call
+    return a;
+}
+
 // Upper bound of |relu(fma(y, scale, shift))| over the n values of one segment and channel, from the statistics
 // alone (SCD_MATH_H2 operand scaling): every value lies within sqrt(n - 1) population standard deviations of the
 // mean, and scale = gamma * invstd with invstd <= 1 / std, so |scale * (y - mean)| <= |gamma| sqrt(n - 1).  The
@@ -200,7 +218,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_finalize(const float *__r
                                                                 int update, float *rmean, float *rvar, float *smean,
                                                                 float *sinv, float *scale, float *shift,
                                                                 float *act_bound) {
-    __shared__ DWelford sh[BN_THREADS];
+    __shared__ DWelford sh[BN_THREADS / 64];
     const int c = blockIdx.x;
     const int t = threadIdx.x;
     const float *rc = rec + size_t(c) * nrec * 3;
@@ -210,18 +228,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_finalize(const float *__r
             const float *r = rc + size_t(s * ncps + k) * 3;
             dmerge(w, DWelford{r[0], r[1], r[2]});
         }
-        sh[t] = w;
-        __syncthreads();
-        for (int off = BN_THREADS / 2; off > 0; off >>= 1) {
-            if (t < off) {
-                DWelford a = sh[t];
-                dmerge(a, sh[t + off]);
-                sh[t] = a;
-            }
-            __syncthreads();
-        }
+        const DWelford a = block_dmerge(w, sh);
         if (t == 0) {
-            const DWelford a = sh[0];
             const double g = gamma ? gamma[c] : 1.0, b = beta ? beta[c] : 0.0;
             const double var = a.n > 0 ? a.m2 / a.n : 0.0;
             const double inv = 1.0 / sqrt(var + double(eps));
@@ -237,7 +245,6 @@ __global__ __launch_bounds__(BN_THREADS) void bn_stats_finalize(const float *__r
                 rvar[c] = float((1.0 - momentum) * rvar[c] + momentum * uvar);
             }
         }
-        __syncthreads();
     }
 }
 
@@ -609,17 +616,22 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__res
             s1[u] += v.x;
             s2[u] += v.y;
         }
-        a1[t] = (s1[0] + s1[1]) + (s1[2] + s1[3]);
-        a2[t] = (s2[0] + s2[1]) + (s2[2] + s2[3]);
-        __syncthreads();
-        for (int off = BN_THREADS / 2; off > 0; off >>= 1) {
-            if (t < off) {
-                a1[t] += a1[t + off];
-                a2[t] += a2[t + off];
-            }
-            __syncthreads();
+        double v1 = (s1[0] + s1[1]) + (s1[2] + s1[3]), v2 = (s2[0] + s2[1]) + (s2[2] + s2[3]);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {  // fixed-order xor tree in the wave, then the waves in order
+            v1 += __shfl_xor(v1, off);
+            v2 += __shfl_xor(v2, off);
         }
+        if ((t & 63) == 0) {
+            a1[t >> 6] = v1;
+            a2[t >> 6] = v2;
+        }
+        __syncthreads();
         if (t == 0) {
+            for (int k = 1; k < BN_THREADS / 64; ++k) {
+                a1[0] += a1[k];
+                a2[0] += a2[k];
+            }
             const float k1 = float(a1[0] / double(pseg));
             coef[(s * C + c) * 2 + 0] = k1;
             coef[(s * C + c) * 2 + 1] = float(a2[0] / double(pseg));
