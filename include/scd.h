@@ -198,15 +198,18 @@ typedef struct scd_igemm {
      * where scd_igemm_bn_bwd_tiles() reports > 0 tiles.  NULL = off. */
     const scd_bn_bwd_tiles_t *bn_bwd;
     /* SCD_MATH_H2 only: device float holding an upper bound U >= |every src element as read| (after the input
-     * transform).  A 3x3 conv with src.c % 32 == 0 then runs the two-term fp16 split: src scaled by the power of
-     * two that brings U below 2^15, weights from the h2 split of wsplit (scd_pack_conv3x3_multi /
-     * scd_split_h2_frag), both scales undone exactly in the epilogue.  A bound below the true maximum overflows
+     * transform).  A 3x3 conv with src.c % 32 == 0 (halo16 kernel), or a 1- / 4-tap conv with src.c % 32 == 0 and
+     * n_out % 64 == 0 (the ConvTranspose forward and data grad: gather16 kernel), then runs the two-term fp16 split:
+     * src scaled by the power of two that brings U below 2^15, weights from the h2 split of wsplit
+     * (scd_pack_conv3x3_multi / scd_split_h2_frag), both scales undone exactly in the epilogue.  A bound below the true maximum overflows
      * fp16 (inf / NaN outputs); a loose one only lowers the absolute floor (2^-39 U).  NULL = the x3 kernels
      * (per-tap, fp32 weights split on the fly). */
     const float *src_bound;
-    /* Optional (store_mode 1, the ConvTranspose forward): device float raised to max |stored output| as the
-     * epilogue writes it (atomic integer max; caller-zeroed or holding an earlier bound) -- the SCD_MATH_H2 bound of
-     * the concat buffer the output lands in, without a pass over it.  NULL = off. */
+    /* Optional: device float raised to max |stored output| as the epilogue writes it (atomic integer max;
+     * caller-zeroed or holding an earlier bound) -- the SCD_MATH_H2 bound of the buffer the output lands in,
+     * without a pass over it: the ConvTranspose forward (store_mode 1) on every split-bf16 kernel, store_mode 0
+     * convs where scd_igemm_arith reports the halo16 / gather16 h2 path (the decoder's concat-gradient data grad).
+     * NULL = off. */
     float *dst_bound;
 } scd_igemm_t;
 

@@ -75,8 +75,13 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv &f) {
 
 // Magnitude bounds (SCD_MATH_H2 operand scaling): a non-negative float's bits order as unsigned integers, so an
 // integer atomic max keeps max(*bound, v) whatever the arrival order (deterministic).  NaN compares above +inf.
+// A bound only grows, so the atomic is skipped when a plain read (possibly stale: then smaller) already covers v --
+// the same final value with far fewer same-address atomics, which serialise in one L2 channel (a ConvTranspose
+// forward issuing one per wave ran 2x slower).
 __device__ __forceinline__ void atomic_max_bound(float *bound, float v) {
-    atomicMax(reinterpret_cast<unsigned int *>(bound), __float_as_uint(fabsf(v)));
+    unsigned int *const p = reinterpret_cast<unsigned int *>(bound);
+    const unsigned int u = __float_as_uint(fabsf(v));
+    if (u > __atomic_load_n(p, __ATOMIC_RELAXED)) atomicMax(p, u);
 }
 // Max of v over the wave, then one atomic from lane 0.
 __device__ __forceinline__ void wave_max_bound(float *bound, float v) {

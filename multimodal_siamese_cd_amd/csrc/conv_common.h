@@ -87,7 +87,7 @@ struct IgemmArgs {
     // SCD_MATH_H2: device pointer to an upper bound of |src| as the kernel reads it (after the input transform);
     // the weight planes in wsplit are then the fp16 two-term split with per-row inverse scales (h2_wsplit_bytes)
     const float *src_bound;
-    float *dst_bound;  // optional: raised to max |stored output| (per-tap x3 kernel only; scd_igemm_t.dst_bound)
+    float *dst_bound;  // optional: raised to max |stored output| (x3 / halo16 / gather16 kernels; scd_igemm_t.dst_bound)
 };
 
 struct WgradArgs {
@@ -128,6 +128,7 @@ void launch_halo16_c16(const IgemmArgs &a, int tw, hipStream_t s);
 // Whether launch_igemm_x3 would run the halo16 kernel for `a` (the only one with the input transform).
 bool igemm_takes_halo16(const IgemmArgs &a);
 bool igemm_takes_c16(const IgemmArgs &a);  // igemm_halo16_c16 (16-channel source)
+bool igemm_takes_gather16(const IgemmArgs &a);  // igemm_gather16_h2 (ConvTranspose forward / data grad)
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
 // 16x16x32-MFMA halo weight grad (conv_halo16.hip), selected by wgrad16_mode() (scd_set_wgrad16).
 int wgrad16_mode();
@@ -153,8 +154,14 @@ int conv_math_x3();      // split-weight (x3, x5, bf16 or h2) pipeline
 int conv_math_mode();    // the SCD_MATH_* mode
 // halo16 kernel arithmetic: 3 (x3), 5 (x5: x3 less one product), 1 (bf16), 2 (h2: two-term fp16 split)
 int conv_math_planes();
-// SCD_MATH_H2 weight splits exist for 3x3 convs whose source channels are a multiple of 32 (the halo16 kernels'
-// shapes); every other conv keeps the x3 split.  wsplit of such a conv is in the h2 format.
-inline bool h2_weight_format(int ntaps, int c) { return conv_math_mode() == SCD_MATH_H2 && ntaps == 9 && c % 32 == 0; }
+// SCD_MATH_H2 weight splits exist for 3x3 convs (the halo16 kernels) and 1- / 4-tap convs (the ConvTranspose forward
+// and data grad, the gather16 kernel) whose source channels are a multiple of 32; every other conv keeps the x3
+// split.  wsplit of such a conv is in the h2 format.
+inline bool h2_weight_format(int ntaps, int c) {
+    return conv_math_mode() == SCD_MATH_H2 && (ntaps == 9 || ntaps == 1 || ntaps == 4) && c % 32 == 0;
+}
+// h2 gather igemm (conv_gather16.hip): 0 when `a` does not take it, else 1 + tile id; launcher.
+int gather16_pick(const IgemmArgs &a);
+void launch_gather16(const IgemmArgs &a, int cfg, hipStream_t s);
 
 }  // namespace scd

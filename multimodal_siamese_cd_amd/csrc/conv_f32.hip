@@ -651,10 +651,6 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     }
     a.src_bound = d->src_bound;
     a.dst_bound = d->dst_bound;
-    if (d->dst_bound && d->store_mode != 1) {
-        set_error("igemm: dst_bound is produced by the ConvTranspose (store_mode 1) kernels only");
-        return SCD_ERR_ARG;
-    }
     if (d->wsplit && !aligned16(d->wsplit)) {
         set_error("igemm: wsplit must be 16-byte aligned");
         return SCD_ERR_ALIGN;
@@ -776,6 +772,7 @@ extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
     SCD_TRY(igemm_query_prepare(d, a));
     if (!conv_math_x3()) return SCD_MATH_F32;
     if (igemm_takes_halo16(a)) return conv_math_mode();  // under SCD_MATH_H2 only bounded h2-split convs take it
+    if (igemm_takes_gather16(a)) return SCD_MATH_H2;
     if (igemm_takes_c16(a)) return conv_math_mode() == SCD_MATH_H2 ? SCD_MATH_X3 : conv_math_mode();
     return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
 }
@@ -828,6 +825,11 @@ static int conv_igemm_run(const scd_igemm_t *d, hipStream_t s, int bb_ntiles_tot
     if (a.in_scale && !igemm_takes_halo16(a)) {
         set_error("igemm: the fused input transform is not supported for this shape/arithmetic "
                   "(check scd_igemm_input_bn_supported)");
+        return SCD_ERR_ARG;
+    }
+    if (a.dst_bound && a.store_mode != 1 && !igemm_takes_halo16(a) && !igemm_takes_gather16(a)) {
+        set_error("igemm: dst_bound of a store_mode 0 conv needs the halo16 or gather16 kernel "
+                  "(ConvTranspose store_mode 1 convs take it on every split-bf16 kernel)");
         return SCD_ERR_ARG;
     }
     if (conv_math_x3() && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");

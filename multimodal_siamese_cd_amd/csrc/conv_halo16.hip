@@ -296,6 +296,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         const int n = n0 + wn * WCH + j * 16 + 4 * g;
         bias4[j] = (a.bias && n < a.n_out) ? *reinterpret_cast<const f32x4 *>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    float omax = 0.f;  // max |stored value| of this lane (dst_bound)
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int p = wm * WPX + i * 16 + l16;
@@ -303,9 +304,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int n = n0 + wn * WCH + j * 16 + 4 * g;
-            if (n < a.n_out) gstore4(a.dst + pix * a.ldc_d + n, acc[j][i] + bias4[j]);
+            if (n < a.n_out) {
+                const f32x4 v = acc[j][i] + bias4[j];
+                gstore4(a.dst + pix * a.ldc_d + n, v);
+                omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+            }
         }
     }
+    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the wave takes part
 
     // Fused BatchNorm statistics of this tile (BM pixels of one image) per channel: mean, then M2 about it.
     if (a.stat_rec) {

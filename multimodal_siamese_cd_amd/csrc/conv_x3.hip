@@ -575,16 +575,19 @@ static int halo_pick(const IgemmArgs &a, int *bm, int *tw) {
     return 0;
 }
 
-// SCD_MATH_H2: a 3x3 conv whose weight split is in the h2 format runs the h2 halo16 kernel when the descriptor
-// bounds its source and the kernel tiles the shape; otherwise the x3 kernels split the fp32 weights on the fly
-// (the h2 split is ignored).
+// SCD_MATH_H2: a conv whose weight split is in the h2 format runs the h2 halo16 kernel (3x3) or the h2 gather16
+// kernel (ConvTranspose forward / data grad) when the descriptor bounds its source and the kernel takes the shape;
+// otherwise the x3 kernels split the fp32 weights on the fly (the h2 split is ignored).
 static IgemmArgs x3_view(const IgemmArgs &a) {
     IgemmArgs b = a;
     int bm = 0, tw = 0;
-    if (h2_weight_format(a.ntaps, a.c) && (!a.src_bound || !halo16_pick(a, halo_eligible(a), &bm, &tw)))
+    if (h2_weight_format(a.ntaps, a.c) &&
+        (!a.src_bound || (a.ntaps == 9 ? !halo16_pick(a, halo_eligible(a), &bm, &tw) : !gather16_pick(a))))
         b.wsplit = nullptr;
     return b;
 }
+
+bool igemm_takes_gather16(const IgemmArgs &a) { return conv_math_x3() && a.c % 16 == 0 && gather16_pick(a) != 0; }
 
 bool igemm_takes_halo16(const IgemmArgs &a0) {
     int bm = 0, tw = 0;
@@ -615,6 +618,10 @@ bool launch_igemm_x3(const IgemmArgs &a0, hipStream_t s) {
     int bm = 0, tw = 0;
     if (const int c16 = halo16_pick(a, halo_eligible(a), &bm, &tw)) {
         launch_halo16(a, c16, tw, s);
+        return true;
+    }
+    if (const int g16 = gather16_pick(a)) {
+        launch_gather16(a, g16, s);
         return true;
     }
     if (halo16_c16_pick(a, halo_eligible(a), &bm, &tw)) {

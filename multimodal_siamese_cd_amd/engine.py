@@ -483,8 +483,15 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None):
             raise RuntimeError("input-gradient through a channel-padded first layer is not supported")
         n, h, w, _ = dy0.shape
         gx = _empty((n, h, w, conv0.in_channels), dy0)
-        hip.conv_igemm(nhwc(dy0), h, w, 1, TAPS_3X3, packed_conv3x3(conv0.weight, 1), conv0.in_channels, None,
-                       nhwc(gx), src_bound=d0)
+        wd = packed_conv3x3(conv0.weight, 1)
+        # h2: the kernel raises gx's bound as it stores (the decoder's ConvT data grad reads gx through it)
+        gxb = None
+        if pool is not None and hip.igemm_arith(nhwc(dy0), h, w, 1, TAPS_3X3, wd, conv0.in_channels, nhwc(gx),
+                                                src_bound=d0) == 'h2':
+            gxb = pool.take()
+        hip.conv_igemm(nhwc(dy0), h, w, 1, TAPS_3X3, wd, conv0.in_channels, None, nhwc(gx), src_bound=d0,
+                       dst_bound=gxb)
+        _set_bound(gx, gxb)
     return gx, [gw0, dbias0, dg0, db0, gw1, dbias1, dg1, db1]
 
 
@@ -767,17 +774,18 @@ class DecoderFn(torch.autograd.Function):
                 hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
             wT = hip.pack_convT2x2(convT.weight.detach(), 0)
             # h2: the concat's bound is the skip's, raised in place by the ConvT epilogue to max |up| (still a
-            # bound of the skip; F.pad's zero border adds nothing)
+            # bound of the skip; F.pad's zero border adds nothing); the ConvT reads cur through cur's bound
+            cur_bound = _bound_of(cur, pool)
             cat_bound = _bound_of(skip, pool) if pool is not None else None
             if pad_y or pad_x:
                 # ConvT into its own map, then F.pad's zero border and placement in one window copy
                 upm = _empty((b, 2 * hc, 2 * wc, cto), skip)
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(upm), store_mode=1,
-                               dst_bound=cat_bound)
+                               src_bound=cur_bound, dst_bound=cat_bound)
                 hip.window_copy(nhwc(upm), nhwc(cat, cs, cto), -(pad_y // 2), -(pad_x // 2))
             else:
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto),
-                               store_mode=1, dst_bound=cat_bound)
+                               store_mode=1, src_bound=cur_bound, dst_bound=cat_bound)
             a, sv, _, _, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save, pool=pool, x_bound=cat_bound)
             saved.append((cur, cat, cs, sv))
             cur = a
@@ -813,10 +821,11 @@ class DecoderFn(torch.autograd.Function):
                 hh, ww = 2 * hc, 2 * wc
             else:
                 g_up = nhwc(g_cat, cs, cto)
-            # ConvT data grad: 4-tap stride-2 gather of g_cat's up half
+            # ConvT data grad: 4-tap stride-2 gather of g_cat's up half (h2: through g_cat's bound, raised by the
+            # DoubleConv data grad that wrote it)
             g_cur = torch.empty_like(cur)
             hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, hip.pack_convT2x2(convT.weight.detach(), 1), cu, None,
-                           nhwc(g_cur))
+                           nhwc(g_cur), src_bound=_bound_of(g_cat, pool))
             # ConvT weight grad: rows = convT input, src = g_up gathered with stride 2
             d, nsplit, nbytes = hip.wgrad_plan(nhwc(cur), g_up, 2, TAPS_2X2)
             slabs = _empty((nbytes // 4,), cur)

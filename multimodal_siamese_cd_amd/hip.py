@@ -274,7 +274,7 @@ def pack_conv3x3(w: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch
     out = torch.empty((co * 9 * ci_pad) if mode == 0 else (ci * 9 * co), device=w.device, dtype=torch.float32)
     _check(lib().scd_pack_conv3x3(w.contiguous().data_ptr(), co, ci, ci_pad, mode, out.data_ptr(), _stream()),
            "scd_pack_conv3x3")
-    return _attach_split(out, co, 9 * ci_pad, True) if mode == 0 else _attach_split(out, ci, 9 * co, True)
+    return _attach_split(out, co, 9 * ci_pad, 9) if mode == 0 else _attach_split(out, ci, 9 * co, 9)
 
 
 class PACKJOB(ctypes.Structure):
@@ -310,7 +310,7 @@ def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:
     out = torch.empty(ci * co * 4, device=w.device, dtype=torch.float32)
     _check(lib().scd_pack_convT2x2(w.contiguous().data_ptr(), ci, co, mode, out.data_ptr(), _stream()),
            "scd_pack_convT2x2")
-    return _attach_split(out, 4 * co, ci) if mode == 0 else _attach_split(out, ci, 4 * co)
+    return _attach_split(out, 4 * co, ci, 1) if mode == 0 else _attach_split(out, ci, 4 * co, 4)
 
 
 def split_bf16x3(src: torch.Tensor) -> torch.Tensor:
@@ -338,16 +338,16 @@ def split_bf16x3_frag(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
     return dst
 
 
-def h2_weight_format(K: int, conv3x3: bool) -> bool:
+def h2_weight_format(K: int, ntaps: int) -> bool:
     """Whether the library expects the h2 split for a conv of this contraction (mirrors h2_weight_format in
-    conv_common.h: 3x3 convs whose source channels are a multiple of 32, under SCD_MATH_H2)."""
-    return conv3x3 and K % 9 == 0 and (K // 9) % 32 == 0 and conv_math() == 'h2'
+    conv_common.h: 3x3, 1-tap and 4-tap convs whose source channels are a multiple of 32, under SCD_MATH_H2)."""
+    return ntaps in (9, 1, 4) and K % ntaps == 0 and (K // ntaps) % 32 == 0 and conv_math() == 'h2'
 
 
-def _attach_split(wpk: torch.Tensor, n_out: int, K: int, conv3x3: bool = False) -> torch.Tensor:
+def _attach_split(wpk: torch.Tensor, n_out: int, K: int, ntaps: int) -> torch.Tensor:
     """Under the split conv arithmetics, pre-split packed weights once so every workgroup stages them by copy."""
     if K % 16 == 0 and conv_math() != 'f32':  # x3, x5, bf16 and h2 all read split planes
-        wpk._x3 = split_h2_frag(wpk, n_out, K) if h2_weight_format(K, conv3x3) else split_bf16x3_frag(wpk, n_out, K)
+        wpk._x3 = split_h2_frag(wpk, n_out, K) if h2_weight_format(K, ntaps) else split_bf16x3_frag(wpk, n_out, K)
     return wpk
 
 

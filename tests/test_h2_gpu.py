@@ -453,3 +453,62 @@ def test_convT_dst_bound(dev, h2, n, h, w, ci, co):
     with pytest.raises(RuntimeError, match='dst_bound'):
         hip.conv_igemm(hip.nhwc(y), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(torch.randn(co, co, 3, 3, device=dev), 0),
                        co, None, hip.nhwc(torch.empty_like(y)), dst_bound=bound)
+
+
+@pytest.mark.parametrize('n,h,w,ci,co', [(2, 8, 8, 64, 64), (3, 5, 7, 128, 64), (8, 64, 64, 64, 64),
+                                         (2, 16, 16, 256, 128), (1, 4, 4, 512, 512)])
+def test_convT_gather16(dev, h2, n, h, w, ci, co):
+    """The ConvTranspose forward (1 tap, pixel-shuffle store) and data grad (4 taps, stride-2 gather) with a source
+    bound take the h2 gather16 kernel: fp32-accurate against fp64 (tiles 128x128 / 128x64 / 64x128, ragged pixel
+    counts), dst_bound raised to exactly max |up|; without a bound they stay on x3 and agree."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * h * w + ci)
+    x = torch.randn(n, h, w, ci, generator=g).to(dev)
+    wt = (torch.randn(ci, co, 2, 2, generator=g) / 8).to(dev)
+    b = torch.randn(co, generator=g).to(dev)
+    wf, wb = hip.pack_convT2x2(wt, 0), hip.pack_convT2x2(wt, 1)
+    cat = torch.zeros(n, 2 * h, 2 * w, co + 32, device=dev)
+    xb = absmax(x, dev, 3.0)  # a loose bound is as good (only the absolute floor moves)
+    assert hip.igemm_arith(hip.nhwc(x), h, w, 1, hip.TAPS_1, wf, 4 * co, hip.nhwc(cat, 32, co), store_mode=1,
+                           src_bound=xb) == 'h2'
+    bound = torch.zeros(1, device=dev)
+    hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_1, wf, 4 * co, b, hip.nhwc(cat, 32, co), store_mode=1,
+                   src_bound=xb, dst_bound=bound)
+    up = cat[..., 32:]
+    ref = F.conv_transpose2d(nchw(x).cpu().double(), wt.cpu().double(), b.cpu().double(), stride=2)
+    assert rel(nchw(up), ref) < 2e-6
+    assert torch.equal(cat[..., :32], torch.zeros_like(cat[..., :32]))
+    assert bound.item() == up.abs().max().item()
+    # data grad: g_up read from a channel slice of a wider buffer (the decoder's g_cat)
+    gcat = torch.randn(n, 2 * h, 2 * w, co + 32, generator=g).to(dev)
+    gub = absmax(gcat, dev)
+    assert hip.igemm_arith(hip.nhwc(gcat, 32, co), h, w, 2, hip.TAPS_2X2, wb, ci, hip.nhwc(x), src_bound=gub) == 'h2'
+    gx = torch.empty(n, h, w, ci, device=dev)
+    hip.conv_igemm(hip.nhwc(gcat, 32, co), h, w, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx), src_bound=gub)
+    xr = nchw(x).cpu().double().requires_grad_()
+    F.conv_transpose2d(xr, wt.cpu().double(), None, stride=2).backward(nchw(gcat[..., 32:]).cpu().double())
+    assert rel(nchw(gx), xr.grad) < 2e-6
+    gx3 = torch.empty_like(gx)  # no bound: the x3 kernel, same values to fp32 rounding
+    hip.conv_igemm(hip.nhwc(gcat, 32, co), h, w, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx3))
+    assert rel(gx3, gx) < 2e-6
+
+
+def test_halo16_dst_bound(dev, h2):
+    """A bounded h2 3x3 conv raises dst_bound to exactly max |stored output| (the decoder's concat-gradient data
+    grad hands it to the ConvTranspose data grad); without the halo16 kernel the request is refused."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(5)
+    n, h, w, ci, co = 2, 32, 32, 64, 128
+    x = torch.randn(n, h, w, ci, generator=g).to(dev)
+    wt = (torch.randn(co, ci, 3, 3, generator=g) / 24).to(dev)
+    wpk = hip.pack_conv3x3(wt, 0)
+    y = torch.empty(n, h, w, co, device=dev)
+    bound = torch.zeros(1, device=dev)
+    assert hip.igemm_arith(hip.nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y), src_bound=absmax(x, dev)) == 'h2'
+    hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, None, hip.nhwc(y), src_bound=absmax(x, dev),
+                   dst_bound=bound)
+    assert bound.item() == y.abs().max().item()
+    ref = F.conv2d(nchw(x).cpu().double(), wt.cpu().double(), padding=1)
+    assert rel(nchw(y), ref) < 2e-6
+    with pytest.raises(RuntimeError, match='dst_bound'):
+        hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, None, hip.nhwc(y), dst_bound=bound)

@@ -1,7 +1,8 @@
 """Per-level timing of the decoder's ConvTranspose2d(2, s2) GEMMs (forward: 1 tap into the pixel-shuffled concat
-slice; data grad: 4 taps, stride 2) on the per-tap x3 kernel, under tile variants (SCD_X3_TILE).
+slice; data grad: 4 taps, stride 2): the per-tap x3 kernel under tile variants (SCD_X3_TILE), or with --math h2 the
+gather16 kernel (source bounds given; --dst-bound also raises the concat bound in the forward, as the engine does).
 
-    python tools/perf_convT.py [--batch 32] [--reps 10] [--tiles 0,1,2,4,5]
+    python tools/perf_convT.py [--batch 32] [--reps 10] [--tiles 0,1,2,4,5] [--math h2] [--dst-bound] [--plain]
 
 Tile 0 is the library's own choice.  HIP events, interleaved per level.
 """
@@ -34,9 +35,11 @@ def main():
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--tiles', default='0,1,2,4,5')
     ap.add_argument('--plain', action='store_true', help='also time the forward GEMM with plain stores')
+    ap.add_argument('--math', default='x3', choices=['x3', 'h2'])
+    ap.add_argument('--dst-bound', action='store_true', help='forward raises a dst bound (h2 engine path)')
     args = ap.parse_args()
     hip.load_library()
-    hip.set_conv_math('x3')
+    hip.set_conv_math(args.math)
     dev = torch.device('cuda:0')
     tiles = args.tiles.split(',')
     # (level, input size, ConvT channels (in == out, networks.py Up), skip channels) of SiameseUNet [64,128,256,512]
@@ -53,18 +56,27 @@ def main():
         gx = torch.empty(b, hc, hc, ci, device=dev)
         wf, wb = hip.pack_convT2x2(wt, 0), hip.pack_convT2x2(wt, 1)
         gup = hip.nhwc(cat, cs, co)
+        xb = gb = db = None
+        if args.math == 'h2':
+            cat.normal_()
+            xb, gb = torch.zeros(1, device=dev), torch.zeros(1, device=dev)
+            hip.absmax_bound(hip.nhwc(x), xb)
+            hip.absmax_bound(hip.nhwc(cat), gb)
+            if args.dst_bound:
+                db = torch.zeros(1, device=dev)
         for t in tiles:
             if t == '0':
                 os.environ.pop('SCD_X3_TILE', None)
             else:
                 os.environ['SCD_X3_TILE'] = t
             f = timeit(lambda: hip.conv_igemm(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, bias, gup,
-                                              store_mode=1), args.reps)
-            d = timeit(lambda: hip.conv_igemm(gup, hc, hc, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx)), args.reps)
+                                              store_mode=1, src_bound=xb, dst_bound=db), args.reps)
+            d = timeit(lambda: hip.conv_igemm(gup, hc, hc, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx), src_bound=gb),
+                       args.reps)
             if args.plain:  # same GEMM, plain row-major stores (no pixel shuffle): isolates the epilogue
                 flat = torch.empty(b, hc, hc, 4 * co, device=dev)
                 fp = timeit(lambda: hip.conv_igemm(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, bias,
-                                                   hip.nhwc(flat)), args.reps)
+                                                   hip.nhwc(flat), src_bound=xb), args.reps)
                 print(f'{name} tile {t}: fwd plain-store {fp * 1e3:7.1f} us', flush=True)
             tot[t][0] += f
             tot[t][1] += d
