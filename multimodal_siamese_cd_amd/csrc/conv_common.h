@@ -142,6 +142,9 @@ void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s);
 // x3 weight-grad instantiations, indexed like kWgradTiles (conv_f32.hip).
 const void *wgrad_x3_fn(int tile_id);
 void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
+// h2 variants of the generic weight grad (both operand bounds; tiles wgrad_x3_h2_tile accepts), conv_x3.hip.
+bool wgrad_x3_h2_tile(int tile_id);
+void launch_wgrad_x3_h2(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
 // Halo weight grad (3x3 / stride 1 / same size, R and C multiples of 64, maps in 2x16 patches).
 const void *wgrad_halo_fn(bool bounded, int rblock);
 int wgrad_halo_rblock(int R, bool bounded);  // 64, or wgrad16_rblock under scd_set_wgrad16

@@ -971,6 +971,13 @@ static bool wgrad_c16_ok(const scd_wgrad_t *d) {
 
 // Both operands bounded: the h2 weight grad under SCD_MATH_H2 (x3 otherwise).
 static bool wgrad_bounded(const scd_wgrad_t *d) { return d->rows_bound && d->src_bound; }
+// The generic (non-halo) weight grad in h2: bounded, SCD_MATH_H2, a tile with an h2 instantiation.  SCD_WGRAD_H2=0
+// keeps it on x3 (A/B switch, read at launch).
+static bool wgrad_generic_h2(const scd_wgrad_t *d) {
+    const char *e = getenv("SCD_WGRAD_H2");
+    return wgrad_bounded(d) && conv_math_mode() == SCD_MATH_H2 && !(e && e[0] == '0') &&
+           wgrad_x3_h2_tile(wgrad_tile(d->rows.c, d->ntaps * d->src.c).id);
+}
 
 static int wgrad_halo_resident(bool c16, bool bounded, int rblock) {
     // per halo weight-grad kernel: 32x32x16; 16x16x32 x3 / x5 / bf16 / h2; 16-channel x3 / x5 / bf16; the
@@ -1037,7 +1044,7 @@ extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
     if (wgrad_halo_ok(d) && wgrad16_mode())
         return conv_math_mode() == SCD_MATH_H2 && !wgrad_bounded(d) ? SCD_MATH_X3 : conv_math_mode();
     if (wgrad_c16_ok(d)) return conv_math_mode() == SCD_MATH_H2 ? SCD_MATH_X3 : conv_math_mode();
-    return SCD_MATH_X3;
+    return wgrad_generic_h2(d) ? SCD_MATH_H2 : SCD_MATH_X3;
 }
 
 extern "C" int scd_wgrad_rows_per_block(const scd_wgrad_t *d) {
@@ -1241,7 +1248,10 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     dim3 grid(a.grid_r * a.grid_j * ns);
     dim3 block(t.threads);
     if (conv_math_x3()) {
-        launch_wgrad_x3(a, t.id, grid, block, s);
+        if (wgrad_generic_h2(d))
+            launch_wgrad_x3_h2(a, t.id, grid, block, s);
+        else
+            launch_wgrad_x3(a, t.id, grid, block, s);
         return launch_status("scd_conv_wgrad");
     }
     switch (t.id) {

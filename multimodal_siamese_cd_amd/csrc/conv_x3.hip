@@ -677,8 +677,15 @@ struct TrPlane {
     }
 };
 
-template <int WAVES_M, int WAVES_N, int TM, int TN>
+// NP = 4: the h2 arithmetic (x3_common.h) for convs outside the halo kernels (the ConvTranspose weight grad): both
+// operands scaled by the powers of two of *rows_bound / *src_bound and split into fp16 h and pre-scaled m' planes,
+// three v_mfma_f32_32x32x16_f16 products (a_h 2^-11) b_m' + a_m' (b_h 2^-11) + a_h b_h, scales undone in the
+// epilogue.
+template <int WAVES_M, int WAVES_N, int TM, int TN, int NP = 3>
 __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
+    static_assert(NP == 3 || NP == 4, "x3 or h2");
+    constexpr bool H2 = NP == 4;
+    constexpr int NPL = H2 ? 2 : 3;  // planes per operand
     constexpr int BK = 16;
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int BM = WAVES_M * TM * 32;
@@ -691,8 +698,13 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
     using LA = TrPlane<BM>;
     using LB = TrPlane<BN>;
     constexpr int PA = LA::BYTES, PB = LB::BYTES;  // plane bytes
-    constexpr int STAGE = 3 * (PA + PB);
+    constexpr int STAGE = NPL * (PA + PB);
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+    float rsc = 1.f, rsc_inv = 1.f, ssc = 1.f, ssc_inv = 1.f;  // h2 operand scales
+    if constexpr (H2) {
+        h2_scale(*a.rows_bound, rsc, rsc_inv);
+        h2_scale(*a.src_bound, ssc, ssc_inv);
+    }
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -743,7 +755,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
         b_img[i] = int(img);
         b_oy[i] = int(oy);
         b_ox[i] = int(rr - oy * uint32_t(a.wo));
-        b_off[i] = 3 * PA + LB::off(b_k[i], q * 8);
+        b_off[i] = NPL * PA + LB::off(b_k[i], q * 8);
     }
 
     f32x4 ra[A_PER], rb[B_PER];
@@ -789,19 +801,27 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
         for (int i = 0; i < A_PER; ++i)
             if (A_FULL || a_in[i]) {
                 u32x2 h, m, l;
-                split3(ra[i], h, m, l);
+                if constexpr (H2) {
+                    split2h_pre(ra[i] * rsc, h, m);
+                } else {
+                    split3(ra[i], h, m, l);
+                    *reinterpret_cast<u32x2 *>(S + 2 * PA + a_off[i]) = l;
+                }
                 *reinterpret_cast<u32x2 *>(S + a_off[i]) = h;
                 *reinterpret_cast<u32x2 *>(S + PA + a_off[i]) = m;
-                *reinterpret_cast<u32x2 *>(S + 2 * PA + a_off[i]) = l;
             }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
             if (B_FULL || b_in[i]) {
                 u32x2 h, m, l;
-                split3(rb[i], h, m, l);
+                if constexpr (H2) {
+                    split2h_pre(rb[i] * ssc, h, m);
+                } else {
+                    split3(rb[i], h, m, l);
+                    *reinterpret_cast<u32x2 *>(S + 2 * PB + b_off[i]) = l;
+                }
                 *reinterpret_cast<u32x2 *>(S + b_off[i]) = h;
                 *reinterpret_cast<u32x2 *>(S + PB + b_off[i]) = m;
-                *reinterpret_cast<u32x2 *>(S + 2 * PB + b_off[i]) = l;
             }
     };
 
@@ -825,8 +845,8 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        b_rd[j] = 3 * PA + LB::off(trk, (wn * TN * 32 + j * 32 + trc) * 2);
-        b_rd4[j] = 3 * PA + LB::off(trk + 4, (wn * TN * 32 + j * 32 + trc) * 2);
+        b_rd[j] = NPL * PA + LB::off(trk, (wn * TN * 32 + j * 32 + trc) * 2);
+        b_rd4[j] = NPL * PA + LB::off(trk + 4, (wn * TN * 32 + j * 32 + trc) * 2);
     }
 
     const int nsteps = (kend > kbeg) ? (kend - kbeg + BK - 1) / BK : 0;
@@ -841,9 +861,9 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
                 load_stage(kbeg + (s + 1) * BK);
             }
             const unsigned char *S = smem + (s & 1) * STAGE;
-            bf16x8 av[3][TM], bv[3][TN];
+            bf16x8 av[NPL][TM], bv[NPL][TN];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) {
+            for (int p = 0; p < NPL; ++p) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
                     const s16x4 lo = lds_tr16(S + p * PA + a_rd[i]);
@@ -857,21 +877,39 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
                     bv[p][j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
                 }
             }
-            constexpr int QA[6] = {1, 0, 2, 0, 1, 0};
-            constexpr int QB[6] = {1, 2, 0, 1, 0, 0};
+            if constexpr (H2) {
+                auto f16 = [](u32x4 v) { return __builtin_bit_cast(f16x8, v); };
 #pragma unroll
-            for (int q = 0; q < 6; ++q)
+                for (int i = 0; i < TM; ++i) {
+                    const u32x4 ah = __builtin_bit_cast(u32x4, av[0][i]), am = __builtin_bit_cast(u32x4, av[1][i]);
+                    const u32x4 ahl = f16_down11(ah);
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
+                    for (int j = 0; j < TN; ++j) {
+                        const u32x4 bh = __builtin_bit_cast(u32x4, bv[0][j]), bm = __builtin_bit_cast(u32x4, bv[1][j]);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f16(ahl), f16(bm), acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f16(am), f16(f16_down11(bh)), acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f16(ah), f16(bh), acc[i][j], 0, 0, 0);
+                    }
+                }
+            } else {
+                constexpr int QA[6] = {1, 0, 2, 0, 1, 0};
+                constexpr int QB[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[QA[q]][i], bv[QB[q]][j], acc[i][j], 0, 0, 0);
+                for (int q = 0; q < 6; ++q)
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] =
+                                __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[QA[q]][i], bv[QB[q]][j], acc[i][j], 0, 0, 0);
+            }
             if (more) store_stage((s + 1) & 1);
             __syncthreads();
         }
     }
 
     float *slab = a.slabs + size_t(split) * a.R * a.Ng;
+    const float osc = rsc_inv * ssc_inv;  // h2: both operand scales (powers of two: exact); 1 otherwise
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int col = j0 + wn * TN * 32 + j * 32 + (lane & 31);
@@ -881,7 +919,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = r0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (row < a.R) gstore1(slab + size_t(row) * a.Ng + col, acc[i][j][r]);
+                if (row < a.R) gstore1(slab + size_t(row) * a.Ng + col, H2 ? acc[i][j][r] * osc : acc[i][j][r]);
             }
     }
 }
@@ -1108,6 +1146,15 @@ void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hip
         case 3: hipLaunchKernelGGL((wgrad_x3<2, 1, 1, 3>), grid, block, 0, s, a); break;
         default: hipLaunchKernelGGL((wgrad_x3<1, 4, 1, 1>), grid, block, 0, s, a); break;
     }
+}
+
+// h2 (both operand bounds given, SCD_MATH_H2): the ConvTranspose weight grad's tiles.
+bool wgrad_x3_h2_tile(int tile_id) { return tile_id == 0 || tile_id == 1; }
+void launch_wgrad_x3_h2(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s) {
+    if (tile_id == 0)
+        hipLaunchKernelGGL((wgrad_x3<2, 2, 2, 2, 4>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((wgrad_x3<1, 4, 2, 2, 4>), grid, block, 0, s, a);
 }
 
 // Fragment-major pre-split weights: dst[p][nb][ks][lane][8] (bf16 bits of term p), the B-operand fragment of

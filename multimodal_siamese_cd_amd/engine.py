@@ -787,7 +787,7 @@ class DecoderFn(torch.autograd.Function):
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto),
                                store_mode=1, src_bound=cur_bound, dst_bound=cat_bound)
             a, sv, _, _, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save, pool=pool, x_bound=cat_bound)
-            saved.append((cur, cat, cs, sv))
+            saved.append((cur, cat, cs, sv, cur_bound))
             cur = a
         if meta.save:
             ctx.meta = meta
@@ -807,7 +807,7 @@ class DecoderFn(torch.autograd.Function):
         pool = _bounds(g)
         for k in range(n - 1, -1, -1):
             up = ups[k]
-            cur, cat, cs, sv = saved[k]
+            cur, cat, cs, sv, cur_bound = saved[k]
             g_cat, pg = _dc_backward(g, sv, up.conv, need_dx=True, pool=pool)
             g_skips[k] = g_cat[..., :cs]
             convT = up.up
@@ -824,10 +824,11 @@ class DecoderFn(torch.autograd.Function):
             # ConvT data grad: 4-tap stride-2 gather of g_cat's up half (h2: through g_cat's bound, raised by the
             # DoubleConv data grad that wrote it)
             g_cur = torch.empty_like(cur)
+            gcat_bound = _bound_of(g_cat, pool)
             hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, hip.pack_convT2x2(convT.weight.detach(), 1), cu, None,
-                           nhwc(g_cur), src_bound=_bound_of(g_cat, pool))
-            # ConvT weight grad: rows = convT input, src = g_up gathered with stride 2
-            d, nsplit, nbytes = hip.wgrad_plan(nhwc(cur), g_up, 2, TAPS_2X2)
+                           nhwc(g_cur), src_bound=gcat_bound)
+            # ConvT weight grad: rows = convT input, src = g_up gathered with stride 2 (h2: both bounds)
+            d, nsplit, nbytes = hip.wgrad_plan(nhwc(cur), g_up, 2, TAPS_2X2, None, cur_bound, gcat_bound)
             slabs = _empty((nbytes // 4,), cur)
             hip.conv_wgrad(d, slabs)
             gwT = torch.empty_like(convT.weight)

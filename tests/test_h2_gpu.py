@@ -486,11 +486,21 @@ def test_convT_gather16(dev, h2, n, h, w, ci, co):
     gx = torch.empty(n, h, w, ci, device=dev)
     hip.conv_igemm(hip.nhwc(gcat, 32, co), h, w, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx), src_bound=gub)
     xr = nchw(x).cpu().double().requires_grad_()
-    F.conv_transpose2d(xr, wt.cpu().double(), None, stride=2).backward(nchw(gcat[..., 32:]).cpu().double())
+    wr = wt.cpu().double().requires_grad_()
+    F.conv_transpose2d(xr, wr, None, stride=2).backward(nchw(gcat[..., 32:]).cpu().double())
     assert rel(nchw(gx), xr.grad) < 2e-6
     gx3 = torch.empty_like(gx)  # no bound: the x3 kernel, same values to fp32 rounding
     hip.conv_igemm(hip.nhwc(gcat, 32, co), h, w, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx3))
     assert rel(gx3, gx) < 2e-6
+    # weight grad: rows = the ConvT input, src = g_up gathered with stride 2, both bounded -> generic h2 weight grad
+    for bounds, arith in (((xb, gub), 'h2'), ((None, None), 'x3')):
+        d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(x), hip.nhwc(gcat, 32, co), 2, hip.TAPS_2X2, None, *bounds)
+        assert hip.wgrad_arith(d) == arith
+        slabs = torch.empty(nbytes // 4, device=dev)
+        hip.conv_wgrad(d, slabs)
+        gw = torch.empty(ci, co, 2, 2, device=dev)
+        hip.wgrad_finalize(slabs, nsplit, ci, 4, co, 1, co, gw)
+        assert rel(gw, wr.grad) < 2e-6, arith
 
 
 def test_halo16_dst_bound(dev, h2):
