@@ -60,7 +60,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     constexpr int A_CH = HR * 8;  // 16-byte (4-channel) pieces of one 32-channel chunk
     constexpr int A_PER = (A_CH + NT - 1) / NT;
     constexpr int PA = HR * 64;
-    constexpr int RED = 2 * WAVES_M * BN * 4;
+    // Epilogue reductions run over groups of 4 pixel tiles (64 pixels) per wave, so a 1 x N wave layout (TM = 8) sums
+    // in the order of the 2 x N layout (TM = 4) and both give bit-identical statistics records.
+    constexpr int RG = TM >= 8 ? TM / 4 : 1;  // reduction groups per wave
+    constexpr int TMG = TM / RG;              // pixel tiles per group
+    constexpr int WME = WAVES_M * RG;         // reduction rows of the block
+    constexpr int RED = 2 * WME * BN * 4;
     constexpr int NBUF = DB ? 2 : 1;
     static_assert(NP == 1 || NP == 2 || NP == 3 || NP == 4 || NP == 5, "x3, x5, bf16 or h2");
     constexpr bool H2 = NP == 2 || NP == 4;  // 4: h2 with the activations' low term pre-scaled (x3_common.h)
@@ -315,19 +320,21 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 
     // Fused BatchNorm statistics of this tile (BM pixels of one image) per channel: mean, then M2 about it.
     if (a.stat_rec) {
-        float *red1 = reinterpret_cast<float *>(smem);  // [WAVES_M][BN] sums
-        float *red2 = red1 + WAVES_M * BN;              // [WAVES_M][BN] M2
+        float *red1 = reinterpret_cast<float *>(smem);  // [WME][BN] sums
+        float *red2 = red1 + WME * BN;                  // [WME][BN] M2
         float mean[TN][4];
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float s = 0.f;
+            for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int i = 0; i < TM; ++i) s += acc[j][i][r] + bias4[j][r];
-                s = row16_sum(s);
-                if (l16 == 0) red1[wm * BN + wn * WCH + j * 16 + 4 * g + r] = s;
-            }
+                for (int q = 0; q < RG; ++q) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int i = q * TMG; i < (q + 1) * TMG; ++i) s += acc[j][i][r] + bias4[j][r];
+                    s = row16_sum(s);
+                    if (l16 == 0) red1[(wm * RG + q) * BN + wn * WCH + j * 16 + 4 * g + r] = s;
+                }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < TN; ++j)
@@ -336,23 +343,26 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                 const int nl = wn * WCH + j * 16 + 4 * g + r;
                 float s = 0.f;
 #pragma unroll
-                for (int w = 0; w < WAVES_M; ++w) s += red1[w * BN + nl];
+                for (int w = 0; w < WME; ++w) s += red1[w * BN + nl];
                 mean[j][r] = s * (1.f / float(BM));
-                float q = 0.f;
 #pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const float d = (acc[j][i][r] + bias4[j][r]) - mean[j][r];
-                    q = fmaf(d, d, q);
+                for (int qg = 0; qg < RG; ++qg) {
+                    float q = 0.f;
+#pragma unroll
+                    for (int i = qg * TMG; i < (qg + 1) * TMG; ++i) {
+                        const float d = (acc[j][i][r] + bias4[j][r]) - mean[j][r];
+                        q = fmaf(d, d, q);
+                    }
+                    q = row16_sum(q);
+                    if (l16 == 0) red2[(wm * RG + qg) * BN + nl] = q;
                 }
-                q = row16_sum(q);
-                if (l16 == 0) red2[wm * BN + nl] = q;
             }
         __syncthreads();
         for (int nl = tid; nl < BN; nl += NT) {
             if (n0 + nl >= a.n_out) continue;
             float s = 0.f, m2 = 0.f;
 #pragma unroll
-            for (int w = 0; w < WAVES_M; ++w) {
+            for (int w = 0; w < WME; ++w) {
                 s += red1[w * BN + nl];
                 m2 += red2[w * BN + nl];
             }
@@ -365,8 +375,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     // Fused BatchNorm + ReLU backward partial sums of the stored g over this tile (exclusive with stat_rec):
     // {sum dz, sum dz * xhat} with the expressions of bn_bwd_partial (bn_f32.hip) -> bb_rec[c][tile][2].
     if (a.bb_rec) {
-        float *red1 = reinterpret_cast<float *>(smem);  // [WAVES_M][BN]
-        float *red2 = red1 + WAVES_M * BN;
+        float *red1 = reinterpret_cast<float *>(smem);  // [WME][BN]
+        float *red2 = red1 + WME * BN;
         const int co = (img / a.bb_seg_imgs) * a.n_out;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -375,25 +385,28 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
             const f32x4 mu = nok ? gload4(a.bb_mean + co + n) : z4, iv = nok ? gload4(a.bb_inv + co + n) : z4;
             const f32x4 sc = nok ? gload4(a.bb_scale + co + n) : z4, sf = nok ? gload4(a.bb_shift + co + n) : z4;
-            f32x4 s1 = z4, s2 = z4;
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int p = wm * WPX + i * 16 + l16;
-                const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
-                const f32x4 y4 = nok ? gload4(a.bb_y + pix * a.bb_ldy + n) : z4;
+            for (int qg = 0; qg < RG; ++qg) {
+                f32x4 s1 = z4, s2 = z4;
+#pragma unroll
+                for (int i = qg * TMG; i < (qg + 1) * TMG; ++i) {
+                    const int p = wm * WPX + i * 16 + l16;
+                    const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+                    const f32x4 y4 = nok ? gload4(a.bb_y + pix * a.bb_ldy + n) : z4;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float dz = fmaf(y4[r], sc[r], sf[r]) > 0.f ? acc[j][i][r] : 0.f;
+                        s1[r] += dz;
+                        s2[r] += dz * ((y4[r] - mu[r]) * iv[r]);
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float dz = fmaf(y4[r], sc[r], sf[r]) > 0.f ? acc[j][i][r] : 0.f;
-                    s1[r] += dz;
-                    s2[r] += dz * ((y4[r] - mu[r]) * iv[r]);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float t1 = row16_sum(s1[r]), t2 = row16_sum(s2[r]);
-                if (l16 == 0) {
-                    red1[wm * BN + wn * WCH + j * 16 + 4 * g + r] = t1;
-                    red2[wm * BN + wn * WCH + j * 16 + 4 * g + r] = t2;
+                    const float t1 = row16_sum(s1[r]), t2 = row16_sum(s2[r]);
+                    if (l16 == 0) {
+                        red1[(wm * RG + qg) * BN + wn * WCH + j * 16 + 4 * g + r] = t1;
+                        red2[(wm * RG + qg) * BN + wn * WCH + j * 16 + 4 * g + r] = t2;
+                    }
                 }
             }
         }
@@ -402,7 +415,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             if (n0 + nl >= a.n_out) continue;
             float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-            for (int w = 0; w < WAVES_M; ++w) {
+            for (int w = 0; w < WME; ++w) {
                 t1 += red1[w * BN + nl];
                 t2 += red2[w * BN + nl];
             }
@@ -462,6 +475,13 @@ int h2_prescale() {
 // h2, >= 128 output channels: the 1 x 4 wave layout of the 128 x 128 tile (SCD_H2_TILE=0: 2 x 2; read at launch).
 int h2_wide_tile() {
     const char *e = getenv("SCD_H2_TILE");
+    return !(e && e[0] == '0');
+}
+
+// h2, 64..127 output channels: the 1 x 2 wave layout of the 128 x 64 tile (config 4: no weight fragment loaded by two
+// waves; same-box A/B 31.81 -> 31.49 ms per step); SCD_H2_TILE64=0: 2 x 2 waves (config 1).  Read at launch.
+int h2_tile64() {
+    const char *e = getenv("SCD_H2_TILE64");
     return !(e && e[0] == '0');
 }
 
@@ -527,8 +547,9 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
 //   0: 2x2 waves of 64 px x 64 ch  (128 x 128), 2 waves/SIMD
 //   1: 2x2 waves of 64 px x 32 ch  (128 x 64),  3 waves/SIMD
 //   2: 2x2 waves of 32 px x 64 ch  (64 x 128),  3 waves/SIMD
-//   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 only (experiment: no duplicated weight loads)
-constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}};
+//   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 only (no duplicated weight loads)
+//   4: 1x2 waves of 128 px x 32 ch (128 x 64),  2 waves/SIMD, h2 only (the same wave tile on 64-channel outputs)
+constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}, {4, 128, 64}};
 
 // The h2 arithmetics only (tile experiments that instantiate no x3 / x5 / bf16 variants).
 template <int WM, int WN, int TM, int TN, int OCC>
@@ -558,10 +579,11 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
         // as 1 x 4 waves of 128 px x 32 ch (no weight fragment loaded by two waves; SCD_H2_TILE=0: 2 x 2)
         id = (a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale() && h2_wide_tile()) ? 3 : 0;
     else if (a.n_out >= 64)
-        id = 1;  // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
+        // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
+        id = (a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale() && h2_tile64()) ? 4 : 1;
     else
         return 0;
-    if (id < 0 || id > 3 || (id > 2 && !(a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale()))) return 0;
+    if (id < 0 || id > 4 || (id > 2 && !(a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale()))) return 0;
     *bm = kCfg[id].bm;
     const char *twe = getenv("SCD_HALO16_TW");  // preferred tile width (hip.halo16_tile_width_pref mirrors it)
     const int pref = twe ? atoi(twe) : 16;  // 16: smallest halo per pixel (180 rows for 128 px)
@@ -578,6 +600,7 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
         case 0: launch16<2, 2, 4, 4, 2>(a, tw, s); break;
         case 1: launch16<2, 2, 4, 2, 3>(a, tw, s); break;
         case 3: launch16_h2only<1, 4, 8, 2, 2>(a, tw, s); break;
+        case 4: launch16_h2only<1, 2, 8, 2, 2>(a, tw, s); break;
         default: launch16<2, 2, 2, 4, 3>(a, tw, s); break;
     }
 }

@@ -522,3 +522,48 @@ def test_halo16_dst_bound(dev, h2):
     assert rel(nchw(y), ref) < 2e-6
     with pytest.raises(RuntimeError, match='dst_bound'):
         hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, None, hip.nhwc(y), dst_bound=bound)
+
+
+@pytest.mark.parametrize('env', ['SCD_H2_TILE64=0', 'SCD_H2_TILE=0'])
+@pytest.mark.parametrize('ci,co,mode', [(64, 64, 'stats'), (32, 64, 'bn_bwd'), (64, 64, 'in_bn'), (128, 128, 'stats'),
+                                        (64, 128, 'bn_bwd'), (64, 96, 'plain')])
+def test_h2_tile_layouts_bit_identical(dev, h2, monkeypatch, env, ci, co, mode):
+    """The 1 x N wave layouts of the h2 halo conv (the library's choice) and the 2 x 2 layouts they replace
+    accumulate every output in the same order and reduce the epilogue statistics in groups of 64 pixels in both:
+    outputs, BatchNorm-statistics records and BatchNorm-backward records are bit-identical."""
+    from multimodal_siamese_cd_amd import hip
+    from multimodal_siamese_cd_amd.hip import TAPS_3X3, nhwc
+    key, val = env.split('=')
+    n, h, w, nseg = 4, 32, 32, 2
+    g = torch.Generator(device=dev).manual_seed(ci + co)
+    x = torch.randn(n, h, w, ci, device=dev, generator=g)
+    wpk = hip.pack_conv3x3(torch.randn(co, ci, 3, 3, device=dev, generator=g) / (3 * ci ** 0.5), 0)
+    sc = torch.rand(nseg * ci, device=dev, generator=g) + 0.5
+    sh = torch.randn(nseg * ci, device=dev, generator=g) * 0.1
+    bound = x.abs().max().reshape(1) * (2.0 if mode == 'in_bn' else 1.0)
+    yb = torch.randn(n, h, w, co, device=dev, generator=g)
+    mu, iv = torch.randn(nseg * co, device=dev, generator=g) * 0.1, torch.rand(nseg * co, device=dev, generator=g) + .5
+    bsc, bsh = torch.rand(nseg * co, device=dev, generator=g) + 0.5, torch.randn(nseg * co, device=dev, generator=g)
+    outs = []
+    for setting in (None, val):
+        if setting is None:
+            monkeypatch.delenv(key, raising=False)
+        else:
+            monkeypatch.setenv(key, setting)
+        y = torch.full((n, h, w, co), 7.0, device=dev)
+        extra, rec = {}, None
+        if mode == 'in_bn':
+            extra['in_bn'] = (sc, sh, nseg)
+        elif mode == 'stats':
+            nt, _ = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), src_bound=bound)
+            rec = extra['stat_rec'] = torch.full((nt * co * 2,), 9.0, device=dev)
+        elif mode == 'bn_bwd':
+            nt, _ = hip.igemm_bn_bwd_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), bound)
+            rec = torch.full((co * nt * 2,), 9.0, device=dev)
+            extra['bn_bwd'] = (yb, nseg, mu, iv, bsc, bsh, rec)
+        assert hip.igemm_arith(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), src_bound=bound) == 'h2'
+        hip.conv_igemm(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, None, nhwc(y), src_bound=bound, **extra)
+        outs.append((y.cpu(), None if rec is None else rec.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[1][1])

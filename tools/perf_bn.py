@@ -25,6 +25,14 @@ def main():
     args = ap.parse_args()
     hip.load_library()
     dev = torch.device('cuda:0')
+    # streaming references on the largest map: torch's float4 copy (1 read + 1 write) and add (2 reads + 1 write)
+    big = torch.randn(args.batch * 65536 * 64, device=dev)
+    big2, out = torch.randn_like(big), torch.empty_like(big)
+    t_c = timeit(lambda: out.copy_(big), args.reps)
+    t_add = timeit(lambda: torch.add(big, big2, out=out), args.reps)
+    print(f'torch copy {t_c:.3f} ms {8 * big.numel() / t_c / 1e9:.2f} TB/s | add {t_add:.3f} ms '
+          f'{12 * big.numel() / t_add / 1e9:.2f} TB/s  ({big.numel() / 1e6:.0f} M floats)', flush=True)
+    del big, big2, out
     tot = {'stats': 0.0, 'apply': 0.0, 'bwd': 0.0}
     byt = {'stats': 0.0, 'apply': 0.0, 'bwd': 0.0}
     print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"c":>5s} | {"stats ms":>8s} {"TB/s":>5s} | {"apply ms":>8s} {"TB/s":>5s} | '
