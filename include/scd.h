@@ -340,6 +340,14 @@ int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx,
                                 const float *gamma, const float *scale, const float *shift, float *dgamma,
                                 float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws,
                                 size_t ws_bytes, scd_stream_t stream);
+/* scd_bn_relu_backward whose incoming gradient is the 1x1 head's input gradient, formed on the fly:
+ *   da[p][c] = sum_o gout[img][o][pix] * w_head[o][c]   (gout NCHW [n][n_out][h][w], n_out <= 4)
+ * -- what scd_conv1x1_bwd would write into gx (same fma chain, bit-identical results); y.n * y.h * y.w < 2^31. */
+int scd_bn_relu_backward_head(scd_nhwc_t y, const float *gout, const float *w_head, int32_t n_out, int32_t nseg,
+                              const float *save_mean, const float *save_invstd, const float *gamma,
+                              const float *scale, const float *shift, float *dgamma, float *dbeta,
+                              float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws, size_t ws_bytes,
+                              scd_stream_t stream);
 /* scd_bn_relu_backward with the partial sums taken from conv-epilogue tile records (scd_bn_bwd_tiles_t.rec,
  * ntiles tiles, image-major, split evenly into nseg segments) instead of a pass over (y, da). */
 int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
@@ -404,6 +412,16 @@ size_t scd_conv1x1_workspace_bytes(scd_nhwc_t x, int32_t n_out);
 /* gx (+)= gout . w ; gw = sum gout*x ; gb = sum gout. */
 int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, int32_t n_out, scd_nhwc_t gx,
                     int32_t accumulate, float *gw, float *gb, void *ws, size_t ws_bytes, scd_stream_t stream);
+/* The head fused with the decoder's last BatchNorm + ReLU (networks.py:380-381 then 457): the head's input
+ * x = relu(fma(y, scale[seg], shift[seg])) (per-segment coefficients of scd_bn_train_stats / scd_bn_eval_coeffs,
+ * nseg | y.n; bn_relu_apply's expression, bit-identical) is read from the conv output y and never written.
+ * _fwd_bn: the forward; _bwd_bn: gw = sum gout*x, gb = sum gout (the input gradient goes through
+ * scd_bn_relu_backward_head instead).  Workspace: scd_conv1x1_workspace_bytes(y, n_out). */
+int scd_conv1x1_fwd_bn(scd_nhwc_t y, const float *scale, const float *shift, int32_t nseg, const float *w,
+                       const float *b, int32_t n_out, float *out, scd_stream_t stream);
+int scd_conv1x1_bwd_bn(scd_nhwc_t y, const float *scale, const float *shift, int32_t nseg, const float *w,
+                       const float *gout, int32_t n_out, float *gw, float *gb, void *ws, size_t ws_bytes,
+                       scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * power_jaccard_loss (utils/loss_functions.py:141-150): p = sigmoid(logit); I = sum p*t;

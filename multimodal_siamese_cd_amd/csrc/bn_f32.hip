@@ -367,6 +367,30 @@ struct DaPooled {
     }
 };
 
+// The decoder's last gradient when the 1x1 head reads its output: dL/da = sum_o gout[img][o][pix] * w[o][c], formed on
+// the fly with conv1x1_bwd_dx_kernel's fma chain (misc_f32.hip; bit-identical), so the full-resolution gradient of
+// the head's input is never written or read.
+struct DaHead {
+    const float *g;  // NCHW [n][n_out][hw]
+    const float *w;  // [n_out][C]
+    int n_out, C, hw;
+    FastDiv div_hw;
+    __device__ __forceinline__ f4 operator()(int64_t p, int c) const {
+        const uint32_t img = fdiv(uint32_t(p), div_hw);
+        const int pix = int(uint32_t(p) - img * uint32_t(hw));
+        f4 r = {0.f, 0.f, 0.f, 0.f};
+        for (int o = 0; o < n_out; ++o) {
+            const float gv = g[(int64_t(img) * n_out + o) * hw + pix];
+            const float *wr = w + int64_t(o) * C + c;
+            r.x = fmaf(gv, wr[0], r.x);
+            r.y = fmaf(gv, wr[1], r.y);
+            r.z = fmaf(gv, wr[2], r.z);
+            r.w = fmaf(gv, wr[3], r.w);
+        }
+        return r;
+    }
+};
+
 // The DaPooled gradient over 2x2 cells: cell (img, cy, cx) covers the full-resolution pixels (2cy + i, 2cx + j) that
 // exist (ceil(h/2) x ceil(w/2) cells per image), so the pooled gradient and its argmax bytes are read and decoded once
 // per cell instead of once per pixel, with the cell's four pixels' loads in flight together.
@@ -734,11 +758,16 @@ __global__ __launch_bounds__(BN_THREADS) void sum_records(const float *__restric
 }
 
 // Per-chunk channel sums (ConvTranspose2d bias grad) and weighted sums (1x1 head weight grad):
-//   rec[c][chunk] = sum_p w(p) * x[p][c],  w(p) = 1 or gout[img][o][pix]
+//   rec[c][chunk] = sum_p w(p) * v(p, c),  w(p) = 1 or gout[img][o][pix],
+//   v = x, or (scale given) relu(fma(x, scale[seg][c], shift[seg][c])) -- the head's input read through the last
+//   BatchNorm + ReLU with bn_relu_apply_kernel's expression (pseg pixels per segment).
+// Four pixels' loads in flight per thread on both paths.
 __global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const float *__restrict__ x, int ldx, int C,
                                                                int64_t npix, int chunk, int nrec, int qpb,
                                                                const float *__restrict__ wgt, int hw, int n_out,
-                                                               int o, float *__restrict__ rec) {
+                                                               int o, const float *__restrict__ scale,
+                                                               const float *__restrict__ shift, int64_t pseg,
+                                                               float *__restrict__ rec) {
     __shared__ f4 sh[BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
@@ -746,24 +775,32 @@ __global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const float *__re
     const int64_t pbeg = int64_t(blockIdx.x) * chunk;
     const int64_t pend = min(pbeg + chunk, npix);
     f4 acc = {0.f, 0.f, 0.f, 0.f};
+    auto value = [&](int64_t p, f4 v) {
+        if (scale) {
+            const int64_t sc_off = (p / pseg) * C + c;
+            v = bn_relu4(v, ld4(scale + sc_off), ld4(shift + sc_off));
+        }
+        if (wgt) {
+            const int64_t img = p / hw, pix = p - img * hw;
+            v *= wgt[(img * n_out + o) * hw + pix];
+        }
+        return v;
+    };
     if (c < C) {
         int64_t p = pbeg + pl;
-        if (!wgt) {
-            for (; p + 3 * npl < pend; p += 4 * npl) {
-                f4 v0 = ld4(x + p * ldx + c), v1 = ld4(x + (p + npl) * ldx + c);
-                f4 v2 = ld4(x + (p + 2 * npl) * ldx + c), v3 = ld4(x + (p + 3 * npl) * ldx + c);
-                PIN4(v0, v1, v2, v3);
-                acc += (v0 + v1) + (v2 + v3);
+        for (; p + 3 * npl < pend; p += 4 * npl) {
+            f4 v0 = ld4(x + p * ldx + c), v1 = ld4(x + (p + npl) * ldx + c);
+            f4 v2 = ld4(x + (p + 2 * npl) * ldx + c), v3 = ld4(x + (p + 3 * npl) * ldx + c);
+            PIN4(v0, v1, v2, v3);
+            if (wgt || scale) {
+                v0 = value(p, v0);
+                v1 = value(p + npl, v1);
+                v2 = value(p + 2 * npl, v2);
+                v3 = value(p + 3 * npl, v3);
             }
+            acc += (v0 + v1) + (v2 + v3);
         }
-        for (; p < pend; p += npl) {
-            f4 v = ld4(x + p * ldx + c);
-            if (wgt) {
-                const int64_t img = p / hw, pix = p - img * hw;
-                v *= wgt[(img * n_out + o) * hw + pix];
-            }
-            acc += v;
-        }
+        for (; p < pend; p += npl) acc += value(p, ld4(x + p * ldx + c));
     }
     sh[tid] = acc;
     __syncthreads();
@@ -795,19 +832,25 @@ size_t weighted_channel_sum_bytes(const scd_nhwc_t &x) {
 }
 
 int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o, float *out, void *ws,
-                         size_t ws_bytes, hipStream_t s);
+                         size_t ws_bytes, hipStream_t s, const float *scale = nullptr, const float *shift = nullptr,
+                         int nseg = 1);
 
+// scale / shift (optional, per segment of nseg): sum relu(fma(x, scale, shift)) instead of x.
 int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o, float *out, void *ws,
-                         size_t ws_bytes, hipStream_t s) {
+                         size_t ws_bytes, hipStream_t s, const float *scale, const float *shift, int nseg) {
     const BnGeom g = bn_geom(x, 1);
     if (!ws || ws_bytes < size_t(g.nrec) * x.c * sizeof(float)) {
         set_error("channel_sum: workspace too small");
         return SCD_ERR_WORKSPACE;
     }
+    if ((scale != nullptr) != (shift != nullptr) || nseg < 1 || x.n % nseg) {
+        set_error("channel_sum: scale and shift go together, nseg must divide n");
+        return SCD_ERR_ARG;
+    }
     float *rec = static_cast<float *>(ws);
     hipLaunchKernelGGL(chan_sum_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        static_cast<const float *>(x.data), x.ldc, x.c, pixels(x), g.chunk, g.nrec, g.qpb, wgt, x.h * x.w, n_out,
-                       o, rec);
+                       o, scale, shift, pixels(x) / nseg, rec);
     hipLaunchKernelGGL(sum_records, dim3(x.c), dim3(BN_THREADS), 0, s, rec, g.nrec, out);
     return SCD_OK;
 }
@@ -1005,6 +1048,29 @@ extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, c
     bn_backward_run(y, DaPlain{static_cast<const float *>(da.data), da.ldc}, nseg, save_mean, save_invstd, gamma, scale,
                     shift, dgamma, dbeta, dbias_prev, dy, dy_bound, ws, as_stream(stream));
     return launch_status("scd_bn_relu_backward");
+}
+
+extern "C" int scd_bn_relu_backward_head(scd_nhwc_t y, const float *gout, const float *w_head, int32_t n_out,
+                                         int32_t nseg, const float *save_mean, const float *save_invstd,
+                                         const float *gamma, const float *scale, const float *shift, float *dgamma,
+                                         float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws,
+                                         size_t ws_bytes, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(bn_check(y, nseg));
+    SCD_TRY(check_view(dy, "bn_bwd_head.dy"));
+    if (!gout || !w_head || n_out < 1 || n_out > 4 || dy.n != y.n || dy.h != y.h || dy.w != y.w || dy.c != y.c ||
+        !save_mean || !save_invstd || !scale || !shift || pixels(y) >= (int64_t(1) << 31)) {
+        set_error("bn_relu_backward_head: shape mismatch / null / n_out not in [1,4] / 2^31 pixels or more");
+        return SCD_ERR_ARG;
+    }
+    if (!ws || ws_bytes < scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg)) {
+        set_error("bn_relu_backward_head: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    const DaHead da{gout, w_head, n_out, y.c, y.h * y.w, make_fastdiv(uint32_t(y.h * y.w))};
+    bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy, dy_bound,
+                    ws, as_stream(stream));
+    return launch_status("scd_bn_relu_backward_head");
 }
 
 extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip,

@@ -26,7 +26,8 @@ void clear_error() { g_err.clear(); }
 
 // bn_f32.hip: sum_p w(p) x[p][c] over all pixels (w = 1 or gout[img][o][pix]).
 int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o, float *out, void *ws,
-                         size_t ws_bytes, hipStream_t s);
+                         size_t ws_bytes, hipStream_t s, const float *scale = nullptr, const float *shift = nullptr,
+                         int nseg = 1);
 size_t weighted_channel_sum_bytes(const scd_nhwc_t &x);
 
 // Row-decomposed grid: x covers the quads of one row (256 per block), y walks rows (grid-stride past 65535).
@@ -299,10 +300,14 @@ __global__ void bn_relu_pool_diff_kernel(const float *__restrict__ x, int hx, in
 // Wave-cooperative 1x1 conv: G = pow2 >= C/4 lanes share a pixel (each a channel quad, coalesced 16-byte
 // loads), partial dots are combined with a fixed xor-shuffle tree.  grid-stride over groups of U pixel sets per
 // wave, whose loads are all issued before the arithmetic (U x the bytes in flight of one set per iteration).
+// scale / shift (optional): the input is read through the producing BatchNorm + ReLU, relu(fma(x, scale, shift))
+// per segment of pseg pixels (bn_relu_apply_kernel's expression), so that activation never has to be written.
 template <int U>
 __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restrict__ x, int ldx, int C, int hw,
                                                           int64_t npix, const float *__restrict__ w,
                                                           const float *__restrict__ b, int n_out, int G,
+                                                          const float *__restrict__ scale,
+                                                          const float *__restrict__ shift, int64_t pseg,
                                                           float *__restrict__ out) {
     const int lane = threadIdx.x & 63;
     const int q = lane % G, pp = lane / G, ppw = 64 / G;
@@ -321,6 +326,17 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restric
             for (int u = 0; u < U; ++u) {
                 const int64_t p = p0 + u * ppw + pp;
                 v[u] = p < npix ? *reinterpret_cast<const float4 *>(x + p * ldx + 4 * qq) : make_float4(0, 0, 0, 0);
+            }
+            if (scale) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int64_t p = p0 + u * ppw + pp;
+                    const int64_t so = (p < npix ? p / pseg : 0) * C + 4 * qq;
+                    const float4 sc = *reinterpret_cast<const float4 *>(scale + so);
+                    const float4 sf = *reinterpret_cast<const float4 *>(shift + so);
+                    v[u] = make_float4(fmaxf(fmaf(v[u].x, sc.x, sf.x), 0.f), fmaxf(fmaf(v[u].y, sc.y, sf.y), 0.f),
+                                       fmaxf(fmaf(v[u].z, sc.z, sf.z), 0.f), fmaxf(fmaf(v[u].w, sc.w, sf.w), 0.f));
+                }
             }
 #pragma unroll
             for (int o = 0; o < 4; ++o) {
@@ -661,6 +677,22 @@ extern "C" int scd_bn_relu_siamese_diff(scd_nhwc_t a, const float *scale, const 
     return launch_status("scd_bn_relu_siamese_diff");
 }
 
+namespace scd {
+static int conv1x1_fwd_run(const scd_nhwc_t &x, const float *scale, const float *shift, int nseg, const float *w,
+                           const float *b, int n_out, float *out, hipStream_t s) {
+    const int64_t npix = pixels(x);
+    int G = 1;
+    while (G < x.c / 4 && G < 64) G *= 2;
+    constexpr int U = 4;
+    const int64_t waves = (npix + (64 / G) * U - 1) / ((64 / G) * U);
+    int blocks = int((waves + 3) / 4);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(conv1x1_fwd_kernel<U>, dim3(blocks), dim3(256), 0, s, static_cast<const float *>(x.data), x.ldc,
+                       x.c, x.h * x.w, npix, w, b, n_out, G, scale, shift, npix / nseg, out);
+    return launch_status("scd_conv1x1_fwd");
+}
+}  // namespace scd
+
 extern "C" int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int32_t n_out, float *out,
                                scd_stream_t stream) {
     clear_error();
@@ -669,16 +701,19 @@ extern "C" int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int
         set_error("conv1x1_fwd: bad arguments (n_out in [1,4])");
         return SCD_ERR_ARG;
     }
-    const int64_t npix = pixels(x);
-    int G = 1;
-    while (G < x.c / 4 && G < 64) G *= 2;
-    constexpr int U = 4;
-    const int64_t waves = (npix + (64 / G) * U - 1) / ((64 / G) * U);
-    int blocks = int((waves + 3) / 4);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(conv1x1_fwd_kernel<U>, dim3(blocks), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(x.data), x.ldc, x.c, x.h * x.w, npix, w, b, n_out, G, out);
-    return launch_status("scd_conv1x1_fwd");
+    return conv1x1_fwd_run(x, nullptr, nullptr, 1, w, b, n_out, out, as_stream(stream));
+}
+
+extern "C" int scd_conv1x1_fwd_bn(scd_nhwc_t y, const float *scale, const float *shift, int32_t nseg, const float *w,
+                                  const float *b, int32_t n_out, float *out, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(y, "conv1x1_bn.y"));
+    if (!w || !out || !scale || !shift || n_out < 1 || n_out > 4 || nseg < 1 || y.n % nseg ||
+        !aligned16(scale) || !aligned16(shift)) {
+        set_error("conv1x1_fwd_bn: bad arguments (n_out in [1,4], 16-byte aligned scale/shift, nseg | n)");
+        return SCD_ERR_ARG;
+    }
+    return conv1x1_fwd_run(y, scale, shift, nseg, w, b, n_out, out, as_stream(stream));
 }
 
 extern "C" size_t scd_conv1x1_workspace_bytes(scd_nhwc_t x, int32_t n_out) {
@@ -723,6 +758,37 @@ extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, 
         hipLaunchKernelGGL(sum_rows_block, dim3(n_out), dim3(256), 0, s, brec, nb, gb);
     }
     return launch_status("scd_conv1x1_bwd");
+}
+
+extern "C" int scd_conv1x1_bwd_bn(scd_nhwc_t y, const float *scale, const float *shift, int32_t nseg, const float *w,
+                                  const float *gout, int32_t n_out, float *gw, float *gb, void *ws, size_t ws_bytes,
+                                  scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(y, "conv1x1_bwd_bn.y"));
+    if (!w || !gout || !scale || !shift || n_out < 1 || n_out > 4 || nseg < 1 || y.n % nseg || !aligned16(scale) ||
+        !aligned16(shift)) {
+        set_error("conv1x1_bwd_bn: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    if ((gw || gb) && (!ws || ws_bytes < scd_conv1x1_workspace_bytes(y, n_out))) {
+        set_error("conv1x1_bwd_bn: workspace too small");
+        return SCD_ERR_WORKSPACE;
+    }
+    hipStream_t s = as_stream(stream);
+    const int64_t npix = pixels(y);
+    const int hw = y.h * y.w;
+    float *rec = static_cast<float *>(ws);
+    const size_t wbytes = weighted_channel_sum_bytes(y);
+    if (gw)
+        for (int o = 0; o < n_out; ++o)
+            SCD_TRY(weighted_channel_sum(y, gout, n_out, o, gw + size_t(o) * y.c, ws, wbytes, s, scale, shift, nseg));
+    if (gb) {
+        float *brec = rec + wbytes / sizeof(float);
+        const int nb = 1024;
+        hipLaunchKernelGGL(conv1x1_bwd_db_partial, dim3(nb, n_out), dim3(256), 0, s, gout, n_out, hw, npix, brec);
+        hipLaunchKernelGGL(sum_rows_block, dim3(n_out), dim3(256), 0, s, brec, nb, gb);
+    }
+    return launch_status("scd_conv1x1_bwd_bn");
 }
 
 static constexpr int PJ_BLOCKS = 1024;

@@ -29,7 +29,7 @@ _F32 = torch.float32
 
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
-         'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True, 'defer_bn_bwd': True}
+         'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True, 'defer_bn_bwd': True, 'fuse_head': True}
 
 
 def conv_math_for(cfg) -> str:
@@ -59,7 +59,9 @@ def set_options(**kw) -> dict:
     fuse_siamese_encoder: Siamese streams run SiameseEncoderFn (BN1 + ReLU fused into the next MaxPool and the
     feature difference, differences written into the decoder's concat buffers).
     defer_bn_bwd: the input layer's BatchNorm backward stops at its statistics and the weight grad (its only
-    reader) forms dy while staging, so that gradient is never written.  Returns the previous options."""
+    reader) forms dy while staging, so that gradient is never written.
+    fuse_head: a 1x1 head that is a decoder output's only reader runs inside the decoder stage (run_decoder head=),
+    reading the last BatchNorm + ReLU through its coefficients.  Returns the previous options."""
     prev = dict(_OPTS)
     for k, v in kw.items():
         if k not in _OPTS:
@@ -397,6 +399,16 @@ class _PooledGrad:
     skip_mode: int
 
 
+@dataclass
+class _HeadGrad:
+    """The decoder's last gradient when the 1x1 head reads its output through the BatchNorm + ReLU: dL/da =
+    g . w2 (g: the logits' gradient, NCHW; w2: [n_out][C]), formed inside the BatchNorm backward
+    (scd_bn_relu_backward_head) instead of being written by the head's backward."""
+    g: torch.Tensor
+    w2: torch.Tensor
+    n_out: int
+
+
 def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, dy_bound=None):
     """`tiles` = (records, ntiles) of the partial sums from the conv epilogue that produced g; g may be a
     _PooledGrad.  `dy_bound` (h2): a zeroed device float raised to max |dy|."""
@@ -407,7 +419,10 @@ def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, dy_bo
     dbias = _empty((c,), y) if conv_bias_grad else None
     n, h, w, _ = y.shape
     ws = _ws(hip.bn_workspace_bytes(n, h, w, c, st.nseg), y)
-    if isinstance(g, _PooledGrad):
+    if isinstance(g, _HeadGrad):
+        hip.bn_relu_backward_head(nhwc(y), g.g, g.w2, g.n_out, st.nseg, st.smean, st.sinv, bn.weight, st.scale,
+                                  st.shift, dgamma, dbeta, dbias, nhwc(dy), ws, dy_bound)
+    elif isinstance(g, _PooledGrad):
         hip.bn_relu_backward_pooled(nhwc(y), nhwc(g.gy) if g.gy is not None else hip._NULL, g.idx,
                                     nhwc(g.gskip) if g.gskip is not None else hip._NULL, g.skip_mode, st.nseg,
                                     st.smean, st.sinv, bn.weight, st.scale, st.shift, dgamma, dbeta, dbias, nhwc(dy),
@@ -756,7 +771,9 @@ class DecoderFn(torch.autograd.Function):
         cur = x_deep
         saved = []
         pool = _bounds(x_deep)
+        head = meta.head
         for k, up in enumerate(ups):
+            last_into_head = head is not None and k == len(ups) - 1
             skip = skips[k]
             b, h, w, cs = skip.shape
             _, hc, wc, cu = cur.shape
@@ -786,9 +803,20 @@ class DecoderFn(torch.autograd.Function):
             else:
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto),
                                store_mode=1, src_bound=cur_bound, dst_bound=cat_bound)
-            a, sv, _, _, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save, pool=pool, x_bound=cat_bound)
+            a, sv, y1, st1, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save, materialize=not last_into_head,
+                                            pool=pool, x_bound=cat_bound)
             saved.append((cur, cat, cs, sv, cur_bound))
             cur = a
+            if last_into_head:
+                # OutConv (networks.py:457) reading relu(BN1(y1)) through the coefficients: the decoder's output
+                # activation is never written
+                n, h, w, c = y1.shape
+                hw_, hb_ = rest[-2], rest[-1]
+                n_out = hw_.shape[0]
+                w2 = hw_.detach().reshape(n_out, c).contiguous()
+                cur = _empty((n, n_out, h, w), y1)
+                hip.conv1x1_fwd_bn(nhwc(y1), st1.scale, st1.shift, st1.nseg, w2, hb_, n_out, cur)
+                ctx.head = (y1, st1, w2, n_out, hw_.shape, hb_ is not None)
         if meta.save:
             ctx.meta = meta
             ctx.saved = saved
@@ -801,10 +829,21 @@ class DecoderFn(torch.autograd.Function):
         n = len(ups)
         g_skips = [None] * n
         grads = [None] * (10 * n)
+        head_grads = [None, None] if meta.head is not None else []
         g = g_out
         if g is None:
-            return (None, None, *g_skips, *grads)
+            return (None, None, *g_skips, *grads, *head_grads)
         pool = _bounds(g)
+        if meta.head is not None:
+            y1, st1, w2, n_out, wshape, has_bias = ctx.head
+            g = g.contiguous()
+            gw = _empty(tuple(wshape), y1)
+            gb = _empty((n_out,), y1) if has_bias else None
+            ws = _ws(hip.conv1x1_workspace_bytes(nhwc(y1), n_out), y1)
+            hip.conv1x1_bwd_bn(nhwc(y1), st1.scale, st1.shift, st1.nseg, w2, g, n_out, gw, gb, ws)
+            head_grads = [gw, gb]
+            g = _HeadGrad(g, w2, n_out)
+            ctx.head = None
         for k in range(n - 1, -1, -1):
             up = ups[k]
             cur, cat, cs, sv, cur_bound = saved[k]
@@ -838,7 +877,7 @@ class DecoderFn(torch.autograd.Function):
             grads[10 * k:10 * k + 10] = [gwT, gbT] + pg
             g = g_cur
         ctx.saved = None
-        return (None, g, *g_skips, *grads)
+        return (None, g, *g_skips, *grads, *head_grads)
 
 
 def decoder_cat_channels(decoder, n_levels: int) -> dict:
@@ -848,13 +887,23 @@ def decoder_cat_channels(decoder, n_levels: int) -> dict:
     return {n_levels - 2 - k: up.up.out_channels for k, up in enumerate(ups)}
 
 
-def run_decoder(decoder, features: list, training: bool, cat_buffers: list | None = None) -> torch.Tensor:
+def run_decoder(decoder, features: list, training: bool, cat_buffers: list | None = None, head=None) -> torch.Tensor:
     """`features` in the reference's order: [deepest, ..., level 0] (Encoder.forward's reversed list).
-    `cat_buffers`: per Up (same order as decoder.up_seq), the concat buffer its skip already lives in, or None."""
+    `cat_buffers`: per Up (same order as decoder.up_seq), the concat buffer its skip already lives in, or None.
+    `head` (an OutConv that is the decoder output's only reader): returns the head's logits (NCHW) instead, with
+    the head reading the last BatchNorm + ReLU through its coefficients (scd_conv1x1_fwd_bn) and its backward
+    feeding that BatchNorm's backward directly (scd_bn_relu_backward_head); results are bit-identical to
+    run_head(head, run_decoder(...))."""
+    if head is not None and not _OPTS['fuse_head']:
+        return run_head(head, run_decoder(decoder, features, training, cat_buffers))
     ups = list(decoder.up_seq.values())
     params = [p for up in ups for p in up_params(up)]
+    if head is not None:
+        params += [head.conv.weight, head.conv.bias]
+        if head.conv.bias is None:
+            raise ValueError("run_decoder: the fused head expects OutConv's bias (networks.py:457)")
     save = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or any(f.requires_grad for f in features))
-    meta = _Meta(ups=ups, training=training, save=save, cat_buffers=cat_buffers)
+    meta = _Meta(ups=ups, training=training, save=save, cat_buffers=cat_buffers, head=head)
     try:
         return DecoderFn.apply(meta, features[0], *features[1:1 + len(ups)], *params)
     finally:

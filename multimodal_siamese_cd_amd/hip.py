@@ -137,6 +137,9 @@ _SIGS = {
     "scd_bn_relu_backward_pooled": ([NHWC, NHWC, c_void_p, NHWC, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p,
                                      c_size_t, c_void_p], c_int),
+    "scd_bn_relu_backward_head": ([NHWC, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_size_t,
+                                   c_void_p], c_int),
     "scd_bn_relu_backward_tiles": (
         [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
          c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_size_t, c_void_p],
@@ -155,6 +158,9 @@ _SIGS = {
     "scd_feature_grad": ([NHWC, c_void_p, NHWC, c_int32, NHWC, c_int32, c_void_p], c_int),
     "scd_siamese_diff": ([NHWC, NHWC, c_void_p], c_int),
     "scd_conv1x1_fwd": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p], c_int),
+    "scd_conv1x1_fwd_bn": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p], c_int),
+    "scd_conv1x1_bwd_bn": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                            c_void_p, c_size_t, c_void_p], c_int),
     "scd_conv1x1_workspace_bytes": ([NHWC, c_int32], c_size_t),
     "scd_conv1x1_bwd": (
         [NHWC, c_void_p, c_void_p, c_int32, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
@@ -578,6 +584,18 @@ def bn_relu_backward_pooled(y: NHWC, gy: NHWC, idx, gskip: NHWC, skip_mode: int,
         "scd_bn_relu_backward_pooled")
 
 
+def bn_relu_backward_head(y: NHWC, gout: torch.Tensor, w_head: torch.Tensor, n_out: int, nseg, smean, sinv, gamma,
+                          scale, shift, dgamma, dbeta, dbias, dy: NHWC, ws, dy_bound=None):
+    """bn_relu_backward of da = gout . w_head, the 1x1 head's input gradient (conv1x1_bwd's gx, never materialised);
+    gout NCHW [n][n_out][h][w], w_head [n_out][C]."""
+    _check(
+        lib().scd_bn_relu_backward_head(y, gout.data_ptr(), w_head.data_ptr(), n_out, nseg, smean.data_ptr(),
+                                        sinv.data_ptr(), _ptr(gamma), scale.data_ptr(), shift.data_ptr(), _ptr(dgamma),
+                                        _ptr(dbeta), _ptr(dbias), dy, _ptr(dy_bound), ws.data_ptr(), ws.numel(),
+                                        _stream()),
+        "scd_bn_relu_backward_head")
+
+
 def bn_relu_backward_tiles(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, tile_rec, ntiles, dgamma, dbeta,
                            dbias, dy: NHWC, ws, dy_bound=None):
     """bn_relu_backward with the partial sums from conv-epilogue tile records (conv_igemm(..., bn_bwd=...))."""
@@ -635,6 +653,18 @@ def siamese_diff(a: NHWC, d: NHWC):
 
 def conv1x1_fwd(x: NHWC, w, b, n_out, out: torch.Tensor):
     _check(lib().scd_conv1x1_fwd(x, w.data_ptr(), _ptr(b), n_out, out.data_ptr(), _stream()), "scd_conv1x1_fwd")
+
+
+def conv1x1_fwd_bn(y: NHWC, scale, shift, nseg, w, b, n_out, out: torch.Tensor):
+    """conv1x1_fwd of relu(fma(y, scale, shift)) (the head reading its input through the last BatchNorm + ReLU)."""
+    _check(lib().scd_conv1x1_fwd_bn(y, scale.data_ptr(), shift.data_ptr(), nseg, w.data_ptr(), _ptr(b), n_out,
+                                    out.data_ptr(), _stream()), "scd_conv1x1_fwd_bn")
+
+
+def conv1x1_bwd_bn(y: NHWC, scale, shift, nseg, w, gout, n_out, gw, gb, ws):
+    """The head's weight / bias grads with its input read through the last BatchNorm + ReLU."""
+    _check(lib().scd_conv1x1_bwd_bn(y, scale.data_ptr(), shift.data_ptr(), nseg, w.data_ptr(), gout.data_ptr(), n_out,
+                                    _ptr(gw), _ptr(gb), ws.data_ptr(), ws.numel(), _stream()), "scd_conv1x1_bwd_bn")
 
 
 def conv1x1_workspace_bytes(x: NHWC, n_out) -> int:

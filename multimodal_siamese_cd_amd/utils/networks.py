@@ -90,20 +90,21 @@ def _band_counts(cfg):
     return len(cfg.DATALOADER.S1_BANDS), len(cfg.DATALOADER.S2_BANDS)
 
 
-def _stream(inc, encoder, decoder, x, nseg, training, siamese):
-    """inc + encoder (+ Siamese diff) + decoder of one stream; returns (decoder output, features)."""
+def _stream(inc, encoder, decoder, x, nseg, training, siamese, head=None):
+    """inc + encoder (+ Siamese diff) + decoder of one stream; returns (decoder output, features).  With `head` (the
+    OutConv that is the decoder output's only reader) the first item is the head's logits (engine.run_decoder)."""
     if siamese and engine.option('fuse_siamese_encoder'):  # networks.py:141-150, fused (engine.SiameseEncoderFn)
         n_levels = len(encoder.down_seq) + 1
         diffs, bufs = engine.run_siamese_encoder(inc, encoder, x, training,
                                                  engine.decoder_cat_channels(decoder, n_levels))
         feats = diffs[::-1]  # Encoder.forward returns the reversed list (networks.py:342)
         ups_bufs = [bufs[n_levels - 2 - k] for k in range(len(decoder.up_seq))]
-        return engine.run_decoder(decoder, feats, training, ups_bufs), feats
+        return engine.run_decoder(decoder, feats, training, ups_bufs, head=head), feats
     feats = engine.run_encoder(inc, encoder, x, nseg, training)
     if siamese:
         feats = [engine.siamese_diff(f) for f in feats]
     feats = feats[::-1]
-    return engine.run_decoder(decoder, feats, training), feats
+    return engine.run_decoder(decoder, feats, training, head=head), feats
 
 
 class UNet(nn.Module):
@@ -119,8 +120,8 @@ class UNet(nn.Module):
 
     def forward(self, x_t1, x_t2):
         x = engine.pack_stream(x_t1, x_t2)  # torch.cat((x_t1, x_t2), dim=1) (networks.py:74)
-        dec, _ = _stream(self.inc, self.encoder, self.decoder, x, 1, self.training, siamese=False)
-        return engine.run_head(self.outc, dec)
+        out, _ = _stream(self.inc, self.encoder, self.decoder, x, 1, self.training, siamese=False, head=self.outc)
+        return out  # self.outc(decoder output) (networks.py:77-78), fused into the decoder stage
 
 
 class DualStreamUNet(nn.Module):
@@ -161,8 +162,8 @@ class SiameseUNet(nn.Module):
 
     def forward(self, x_t1, x_t2):
         x = engine.pack_pair(x_t1, x_t2)
-        dec, _ = _stream(self.inc, self.encoder, self.decoder, x, 2, self.training, siamese=True)
-        return engine.run_head(self.outc, dec)
+        out, _ = _stream(self.inc, self.encoder, self.decoder, x, 2, self.training, siamese=True, head=self.outc)
+        return out  # self.outc(decoder output) (networks.py:152-153), fused into the decoder stage
 
 
 class DualTaskSiameseUNet(nn.Module):
@@ -189,11 +190,12 @@ class DualTaskSiameseUNet(nn.Module):
         x = engine.pack_pair(x_t1, x_t2)
         feats = engine.run_encoder(self.inc, self.encoder, x, 2, self.training)
         diffs = [engine.siamese_diff(f) for f in feats][::-1]
-        out_change = engine.run_head(self.outc_change, engine.run_decoder(self.decoder_change, diffs, self.training))
+        # each decoder output feeds one head (networks.py:187-195): the heads run fused into the decoder stages
+        out_change = engine.run_decoder(self.decoder_change, diffs, self.training, head=self.outc_change)
         f_t2 = [f[b:] for f in feats][::-1]
-        out_sem_t2 = engine.run_head(self.outc_sem, engine.run_decoder(self.decoder_sem, f_t2, self.training))
+        out_sem_t2 = engine.run_decoder(self.decoder_sem, f_t2, self.training, head=self.outc_sem)
         f_t1 = [f[:b] for f in feats][::-1]
-        out_sem_t1 = engine.run_head(self.outc_sem, engine.run_decoder(self.decoder_sem, f_t1, self.training))
+        out_sem_t1 = engine.run_decoder(self.decoder_sem, f_t1, self.training, head=self.outc_sem)
         return out_change, out_sem_t1, out_sem_t2
 
 

@@ -289,3 +289,36 @@ def test_fused_siamese_encoder_matches_unfused(dev, name):
     for k in res[0][1]:
         if not _pre_bn_bias(k):
             assert rel_err(res[0][1][k].numpy(), res[1][1][k].numpy()) < 1e-5, k
+
+
+@pytest.mark.parametrize('name', ['siamese_t8-16', 'siamese_t8-16-32_odd', 'unet_t8-16', 'dtsiamese_t8-16'])
+def test_fused_head_bit_identical(dev, name):
+    """The 1x1 head fused into the decoder stage (engine fuse_head: forward through the last BatchNorm's
+    coefficients, backward through scd_bn_relu_backward_head) vs the materialised decoder output + HeadFn:
+    logits, loss and every gradient bit-identical, in train and eval mode."""
+    from multimodal_siamese_cd_amd import engine, trainers
+    fx = Fixture(name)
+    res = []
+    for fused in (True, False):
+        prev = engine.set_options(fuse_head=fused)
+        try:
+            cfg, net = _build(fx, dev)
+            net.train()
+            batch = {k: v.to(dev) for k, v in fx.batch().items()}
+            out = net(batch['x_t1'], batch['x_t2'])
+            loss = trainers.step_loss(cfg, out, batch)
+            loss.backward()
+            net.eval()
+            with torch.no_grad():
+                ev = net(batch['x_t1'], batch['x_t2'])
+            res.append(([o.detach().cpu() for o in _outs(out)], loss.item(), [o.cpu() for o in _outs(ev)],
+                        {k: p.grad.cpu() for k, p in net.module.named_parameters() if p.grad is not None}))
+        finally:
+            engine.set_options(**prev)
+    (o1, l1, e1, g1), (o0, l0, e0, g0) = res
+    assert l1 == l0
+    for a, b in zip(o1 + e1, o0 + e0):
+        assert torch.equal(a, b)
+    assert g1.keys() == g0.keys()
+    for k in g0:
+        assert torch.equal(g1[k], g0[k]), k

@@ -12,6 +12,7 @@ A variant is a comma list of knob=value with knobs:
   pool_diff  encoder difference + next-level pooling in one pass (engine.set_options(pool_diff=...))
   pooled_bn_bwd  encoder BN backward forms maxpool_bwd -/+ diff grad on the fly (engine.set_options(...))
   defer_bn_bwd  input layer's BN backward formed inside its weight grad (engine.set_options(defer_bn_bwd=...))
+  <engine option>=0|1  any other engine.set_options switch by name (e.g. fuse_head=0)
   SCD_* library environment switches read at launch (e.g. SCD_HALO16_TW=64)
 Prints per-variant median / min ms per step over the rounds.
 """
@@ -60,6 +61,8 @@ def apply(variant: str):
             engine.set_options(defer_bn_bwd=bool(int(v)))
         elif k == 'fuse_enc':
             engine.set_options(fuse_siamese_encoder=bool(int(v)))
+        elif k in engine._OPTS:  # any other engine option by name (e.g. fuse_head=0)
+            engine.set_options(**{k: bool(int(v))})
         elif k.startswith('SCD_'):  # library environment switch (read at launch)
             os.environ[k] = v
         else:
