@@ -439,6 +439,124 @@ __device__ __forceinline__ void cell_grads(const PooledCells &P, uint32_t cell, 
     }
 }
 
+// cell_grads for a Siamese pair (skip_mode 1, two segments of gsn images): `cell` lies in a t1 image, its partner
+// cell (same place) in image img + gsn.  The difference gradient is read once for both (t1 subtracts it, t2 adds
+// it, with cell_grads' expressions: bit-identical).  pix[k] is the t1 pixel; its t2 partner is pix[k] + gsn*hx*wx.
+__device__ __forceinline__ void cell_grads_pair(const PooledCells &P, uint32_t cell, int c, f4 (&g0)[4], f4 (&g1)[4],
+                                                int64_t (&pix)[4], bool (&ok)[4]) {
+    const DaPooled &d = P.da;
+    const uint32_t img = fdiv(cell, P.div_cimg);
+    const uint32_t r = cell - img * uint32_t(P.ch * P.cw);
+    const int cy = int(fdiv(r, P.div_cw)), cx = int(r) - cy * P.cw;
+    f4 gp0 = {0.f, 0.f, 0.f, 0.f}, gp1 = gp0;
+    uint32_t pk0 = 0xffffffffu, pk1 = 0xffffffffu;
+    if (d.gy && cy < d.hy && cx < d.wy) {
+        const int64_t q0 = (int64_t(img) * d.hy + cy) * d.wy + cx;
+        const int64_t q1 = q0 + int64_t(d.gsn) * d.hy * d.wy;
+        pk0 = *reinterpret_cast<const uint32_t *>(d.idx + q0 * d.C + c);
+        pk1 = *reinterpret_cast<const uint32_t *>(d.idx + q1 * d.C + c);
+        gp0 = ld4(d.gy + q0 * d.ldgy + c);
+        gp1 = ld4(d.gy + q1 * d.ldgy + c);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int yy = 2 * cy + (k >> 1), xx = 2 * cx + (k & 1);
+        ok[k] = yy < d.hx && xx < d.wx;
+        pix[k] = (int64_t(img) * d.hx + yy) * d.wx + xx;
+        const uint32_t want = uint32_t(k);
+        f4 v0 = {((pk0 >> 0) & 0xff) == want ? gp0.x : 0.f, ((pk0 >> 8) & 0xff) == want ? gp0.y : 0.f,
+                 ((pk0 >> 16) & 0xff) == want ? gp0.z : 0.f, ((pk0 >> 24) & 0xff) == want ? gp0.w : 0.f};
+        f4 v1 = {((pk1 >> 0) & 0xff) == want ? gp1.x : 0.f, ((pk1 >> 8) & 0xff) == want ? gp1.y : 0.f,
+                 ((pk1 >> 16) & 0xff) == want ? gp1.z : 0.f, ((pk1 >> 24) & 0xff) == want ? gp1.w : 0.f};
+        if (ok[k]) {
+            const f4 sv = ld4(d.gs + pix[k] * d.ldgs + c);
+            const float m = -1.f, p1 = 1.f;
+            v0.x += m * sv.x;
+            v0.y += m * sv.y;
+            v0.z += m * sv.z;
+            v0.w += m * sv.w;
+            v1.x += p1 * sv.x;
+            v1.y += p1 * sv.y;
+            v1.z += p1 * sv.z;
+            v1.w += p1 * sv.w;
+        }
+        g0[k] = v0;
+        g1[k] = v1;
+    }
+}
+
+// Block-wide tree sum of (a, b) per channel quad into rec[c][rec_idx][2] (bn_bwd_pooled_partial's tree and layout).
+__device__ __forceinline__ void pooled_rec2(f4 (&sh1)[BN_THREADS], f4 (&sh2)[BN_THREADS], f4 a, f4 b, int tid, int pl,
+                                            int npl, int qpb, int c, int C, int nrec, int rec_idx,
+                                            float *__restrict__ rec) {
+    sh1[tid] = a;
+    sh2[tid] = b;
+    __syncthreads();
+    for (int off = npl / 2; off > 0; off >>= 1) {
+        if (pl < off) {
+            sh1[tid] += sh1[tid + off * qpb];
+            sh2[tid] += sh2[tid + off * qpb];
+        }
+        __syncthreads();
+    }
+    if (pl == 0 && c < C) {
+        const f4 x = sh1[tid], y = sh2[tid];
+        const float xv[4] = {x.x, x.y, x.z, x.w}, yv[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float *r = rec + (size_t(c + k) * nrec + rec_idx) * 2;
+            r[0] = xv[k];
+            r[1] = yv[k];
+        }
+    }
+    __syncthreads();
+}
+
+// bn_bwd_pooled_partial for a Siamese pair: block k covers chunk k of the t1 segment and chunk k of the t2 segment
+// (same cells), reading the shared difference gradient once; same per-chunk records, bit-identical.
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial_pair(const float *__restrict__ y, int ldy,
+                                                                         PooledCells P, int C, int64_t cseg, int ncps,
+                                                                         int chunk, int nrec, int qpb,
+                                                                         const float *smean, const float *sinv,
+                                                                         const float *scale, const float *shift,
+                                                                         float *__restrict__ rec) {
+    __shared__ f4 sh1[BN_THREADS], sh2[BN_THREADS];
+    const int tid = threadIdx.x;
+    const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
+    const int c = (blockIdx.y * qpb + q) * 4;
+    const Chunk ch = chunk_of(cseg, ncps, chunk);  // blockIdx.x < ncps: the t1 segment's chunk
+    const int64_t poff = int64_t(P.da.gsn) * P.da.hx * P.da.wx;
+    f4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = a1, b1 = a1, b2 = a1;
+    if (c < C) {
+        const f4 mu0 = ld4(smean + c), iv0 = ld4(sinv + c), sc0 = ld4(scale + c), sf0 = ld4(shift + c);
+        const f4 mu1 = ld4(smean + C + c), iv1 = ld4(sinv + C + c), sc1 = ld4(scale + C + c), sf1 = ld4(shift + C + c);
+        for (int64_t cell = ch.beg + pl; cell < ch.end; cell += npl) {
+            f4 g0[4], g1[4];
+            int64_t pix[4];
+            bool ok[4];
+            cell_grads_pair(P, uint32_t(cell), c, g0, g1, pix, ok);
+            f4 y0[4], y1[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                y0[k] = ok[k] ? ld4(y + pix[k] * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+                y1[k] = ok[k] ? ld4(y + (pix[k] + poff) * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) {
+                    const f4 z0 = relu_mask(y0[k], sc0, sf0, g0[k]);
+                    a1 += z0;
+                    a2 += z0 * ((y0[k] - mu0) * iv0);
+                    const f4 z1 = relu_mask(y1[k], sc1, sf1, g1[k]);
+                    b1 += z1;
+                    b2 += z1 * ((y1[k] - mu1) * iv1);
+                }
+        }
+    }
+    pooled_rec2(sh1, sh2, a1, a2, tid, pl, npl, qpb, c, C, nrec, blockIdx.x, rec);
+    pooled_rec2(sh1, sh2, b1, b2, tid, pl, npl, qpb, c, C, nrec, ncps + blockIdx.x, rec);
+}
+
 // bn_bwd_partial over cells: rec[c][chunk][2] = {sum dz, sum dz*xhat} of the chunk's cells' pixels.
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const float *__restrict__ y, int ldy, PooledCells P,
                                                                     int C, int64_t cseg, int ncps, int chunk, int nrec,
@@ -547,6 +665,72 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const float *_
         const float av[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) brec[size_t(c + k) * nrec + blockIdx.x] = av[k];
+    }
+}
+
+// bn_bwd_pooled_apply for a Siamese pair (see bn_bwd_pooled_partial_pair): both segments' dy per cell, the conv-bias
+// records of chunk k of each segment, bit-identical.
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply_pair(
+    const float *__restrict__ y, int ldy, PooledCells P, float *__restrict__ dy, int lddy, int C, int64_t cseg, int ncps,
+    int chunk, int nrec, int qpb, const float *smean, const float *sinv, const float *gamma, const float *scale,
+    const float *shift, const float *coef, float *__restrict__ brec, float *dy_bound) {
+    __shared__ f4 sh[BN_THREADS];
+    const int tid = threadIdx.x;
+    const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
+    const int c = (blockIdx.y * qpb + q) * 4;
+    const Chunk ch = chunk_of(cseg, ncps, chunk);
+    const int64_t poff = int64_t(P.da.gsn) * P.da.hx * P.da.wx;
+    f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    f4 amax = acc0;
+    if (c < C) {
+        const f4 gm = gamma ? ld4(gamma + c) : f4{1.f, 1.f, 1.f, 1.f};
+        const f4 mu0 = ld4(smean + c), iv0 = ld4(sinv + c), sc0 = ld4(scale + c), sf0 = ld4(shift + c);
+        const f4 mu1 = ld4(smean + C + c), iv1 = ld4(sinv + C + c), sc1 = ld4(scale + C + c), sf1 = ld4(shift + C + c);
+        const float *cf0 = coef + size_t(c) * 2, *cf1 = coef + size_t(C + c) * 2;
+        const f4 k10 = {cf0[0], cf0[2], cf0[4], cf0[6]}, k20 = {cf0[1], cf0[3], cf0[5], cf0[7]};
+        const f4 k11 = {cf1[0], cf1[2], cf1[4], cf1[6]}, k21 = {cf1[1], cf1[3], cf1[5], cf1[7]};
+        const f4 mul0 = gm * iv0, mul1 = gm * iv1;
+        for (int64_t cell = ch.beg + pl; cell < ch.end; cell += npl) {
+            f4 g0[4], g1[4];
+            int64_t pix[4];
+            bool ok[4];
+            cell_grads_pair(P, uint32_t(cell), c, g0, g1, pix, ok);
+            f4 y0[4], y1[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                y0[k] = ok[k] ? ld4(y + pix[k] * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+                y1[k] = ok[k] ? ld4(y + (pix[k] + poff) * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) {
+                    const f4 o0 = bn_bwd_dy4(y0[k], g0[k], mu0, iv0, sc0, sf0, k10, k20, mul0);
+                    const f4 o1 = bn_bwd_dy4(y1[k], g1[k], mu1, iv1, sc1, sf1, k11, k21, mul1);
+                    st4(dy + pix[k] * lddy + c, o0);
+                    st4(dy + (pix[k] + poff) * lddy + c, o1);
+                    acc0 += o0;
+                    acc1 += o1;
+                    amax = fmax4(amax, fmax4(fabs4(o0), fabs4(o1)));
+                }
+        }
+    }
+    if (dy_bound) wave_max_bound(dy_bound, fmaxf(fmaxf(amax.x, amax.y), fmaxf(amax.z, amax.w)));
+    if (!brec) return;  // uniform
+#pragma unroll
+    for (int sgm = 0; sgm < 2; ++sgm) {
+        sh[tid] = sgm ? acc1 : acc0;
+        __syncthreads();
+        for (int off = npl / 2; off > 0; off >>= 1) {
+            if (pl < off) sh[tid] += sh[tid + off * qpb];
+            __syncthreads();
+        }
+        if (pl == 0 && c < C) {
+            const f4 a = sh[tid];
+            const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) brec[size_t(c + k) * nrec + sgm * ncps + blockIdx.x] = av[k];
+        }
+        __syncthreads();
     }
 }
 
@@ -1015,6 +1199,22 @@ static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled &da, int 
     float *rec = static_cast<float *>(ws);
     float *brec = rec + size_t(g.nrec) * y.c * 2;
     float *coef = brec + size_t(g.nrec) * y.c;
+    // Siamese pairs (SCD_BN_POOLED_PAIR=0: one image per cell walk): the t1 and t2 cells at one place in one block,
+    // the shared difference gradient read once instead of once per branch
+    const char *pe = getenv("SCD_BN_POOLED_PAIR");
+    if (!(pe && pe[0] == '0') && nseg == 2 && da.gs && da.skip_mode == 1 && 2 * da.gsn == y.n) {
+        hipLaunchKernelGGL(bn_bwd_pooled_partial_pair, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
+                           static_cast<const float *>(y.data), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
+                           save_invstd, scale, shift, rec);
+        hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, ncps, nrec, g.pseg,
+                           coef, dgamma, dbeta);
+        hipLaunchKernelGGL(bn_bwd_pooled_apply_pair, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
+                           static_cast<const float *>(y.data), y.ldc, P, static_cast<float *>(dy.data), dy.ldc, y.c,
+                           cseg, ncps, chunk, nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
+                           dbias_prev ? brec : nullptr, dy_bound);
+        if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, nrec, dbias_prev);
+        return;
+    }
     hipLaunchKernelGGL(bn_bwd_pooled_partial, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        static_cast<const float *>(y.data), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
                        save_invstd, scale, shift, rec);

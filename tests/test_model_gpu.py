@@ -322,3 +322,22 @@ def test_fused_head_bit_identical(dev, name):
     assert g1.keys() == g0.keys()
     for k in g0:
         assert torch.equal(g1[k], g0[k]), k
+
+
+@pytest.mark.parametrize('name', ['siamese_t8-16', 'siamese_t8-16-32_odd', 'whatevernet_t8-16'])
+def test_pooled_bn_backward_pairs_bit_identical(dev, monkeypatch, name):
+    """The encoder BatchNorm backward over Siamese pairs (t1 and t2 cells in one block, the difference gradient read
+    once) vs one image per cell walk (SCD_BN_POOLED_PAIR=0): every gradient bit-identical."""
+    from multimodal_siamese_cd_amd import trainers
+    fx = Fixture(name)
+    res = []
+    for pair in ('1', '0'):
+        monkeypatch.setenv('SCD_BN_POOLED_PAIR', pair)
+        cfg, net = _build(fx, dev)
+        net.train()
+        batch = {k: v.to(dev) for k, v in fx.batch().items()}
+        loss = trainers.step_loss(cfg, net(batch['x_t1'], batch['x_t2']), batch)
+        loss.backward()
+        res.append({k: p.grad.cpu() for k, p in net.module.named_parameters() if p.grad is not None})
+    for k in res[1]:
+        assert torch.equal(res[0][k], res[1][k]), k
