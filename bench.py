@@ -185,8 +185,9 @@ def main():
     hip.load_library()
 
     cfg = experiment_manager.load_cfg(args.config)
-    math = args.math or engine.conv_math_for(cfg)
-    hip.set_conv_math(math)
+    if args.math:
+        cfg.MODEL.CONV_MATH = args.math
+    math = engine.conv_math_for(cfg)  # create_network gives the model this arithmetic (hip.conv_scope per forward)
     dtype = 'bf16' if math == 'bf16' else 'f32'
     batch = args.batch or int(cfg.TRAINER.BATCH_SIZE)
     size = args.size or int(cfg.AUGMENTATION.CROP_SIZE)

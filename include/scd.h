@@ -15,7 +15,8 @@
  *  - The library never allocates, frees or synchronises.  Workspaces are caller-owned (torch caching
  *    allocator); size them with the *_workspace_bytes() queries.  All launches are asynchronous on the
  *    caller's stream (a hipStream_t passed as void*; NULL = legacy default stream).
- *  - Stateless and re-entrant; one GPU per process.
+ *  - Stateless and re-entrant: no process-wide modes and no environment switches; the arithmetic and kernel
+ *    variant of a conv are fields of its descriptor.  One GPU per process.
  */
 #ifndef SCD_H_
 #define SCD_H_
@@ -68,13 +69,14 @@ int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, int32_t w, 
  * replaces: nn.Conv2d(in,out,3,padding=1) parameter layout (networks.py:392,395). */
 /* Batched form for one training step's weights: per job the packed layout above into `out` and, when
  * `split` != NULL, its fragment-major bf16x3 split (the scd_split_bf16x3_frag layout of `out`; its K, 9*ci_pad or
- * 9*co, a multiple of 16).
+ * 9*co, a multiple of 16) -- or, for job.math == SCD_MATH_H2 and K / 9 a multiple of 32, the scd_split_h2_frag format.
  * Any number of jobs; one launch per 48. */
 typedef struct scd_pack_job {
     const float *w;
     float *out;
     uint16_t *split;
     int32_t co, ci, ci_pad, mode;
+    int32_t math; /* arithmetic of the convs reading `split`: SCD_MATH_H2 writes the h2 format where it applies */
 } scd_pack_job_t;
 int scd_pack_conv3x3_multi(const scd_pack_job_t *jobs, int32_t n, scd_stream_t stream);
 int scd_pack_conv3x3(const float *w, int32_t co, int32_t ci, int32_t ci_pad, int32_t mode, float *out,
@@ -87,8 +89,11 @@ int scd_pack_conv3x3(const float *w, int32_t co, int32_t ci, int32_t ci_pad, int
 int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, float *out, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Conv arithmetic.  Both modes compute an fp32 GEMM with fp32 accumulation:
- *   SCD_MATH_F32  v_mfma_f32_32x32x2_f32: exact fp32 products (a k-ordered fmaf chain per MFMA).
+ * Conv arithmetic, chosen per launch by scd_igemm_t.math / scd_wgrad_t.math (and scd_pack_job_t.math for the
+ * weight split it feeds).  The library keeps no arithmetic state: two models with different arithmetic can run
+ * in one process, on one stream or several.  Every mode computes an fp32 GEMM with fp32 accumulation:
+ *   SCD_MATH_F32  v_mfma_f32_32x32x2_f32: exact fp32 products (a k-ordered fmaf chain per MFMA).  The value of a
+ *                 zero-initialised descriptor.
  *   SCD_MATH_X3   v_mfma_f32_32x32x16_bf16 on an exact 3-way bf16 split of each fp32 operand
  *                 (x = h + m + l, each term rounded to nearest), accumulating the six terms
  *                 hh+hm+mh+mm+hl+lh.  The dropped terms are <= ~2^-26 relative, so the rounding error is
@@ -103,29 +108,50 @@ int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, floa
  *   SCD_MATH_X5   SCD_MATH_X3 less one of its three second-order products (w_l*x_h in the fwd/data-grad halo
  *                 kernel, x_l*dy_h in the halo weight grad; each <= 2^-18 relative, below fp32 accumulation noise
  *                 over the contraction lengths here): five products, two weight / X planes.  Halo kernels only.
- * Default: SCD_MATH_X3, or the SCD_CONV_MATH=f32|x3|x5|bf16 environment variable at first use.  Returns the
- * previous mode; SCD_MATH_QUERY only queries.  Process-wide (not per stream).
+ *   SCD_MATH_H2   two-term fp16 split with power-of-two operand scaling (see scd_igemm_t.src_bound): three
+ *                 v_mfma_f32_16x16x32_f16 products per fp32 product, 22 significant bits per operand.  Convs
+ *                 without operand bounds, and shapes the h2 kernels do not take, run SCD_MATH_X3.
  * ------------------------------------------------------------------------------------------- */
 enum scd_conv_math {
-    SCD_MATH_QUERY = -1,
     SCD_MATH_F32 = 0,
     SCD_MATH_X3 = 1,
     SCD_MATH_BF16 = 2,
     SCD_MATH_X5 = 3,
     SCD_MATH_H2 = 4
 };
-int scd_set_conv_math(int32_t mode);
-/* The arithmetic scd_conv_igemm / scd_conv_wgrad would use for this descriptor under the current mode:
- * SCD_MATH_F32, SCD_MATH_X3 or SCD_MATH_BF16; negative = invalid descriptor.  (Declared with the descriptors
- * below.) */
-/* Tile selection of the 16x16x32-MFMA halo conv kernel (SCD_MATH_X3, 3x3 / stride 1, C % 32 == 0):
- * 0 = off (32x32x16 halo kernel), 1 = automatic, 2 + id = force tile id (0: 128 px x 128 ch, 1: 128 x 64,
- * 2: 64 x 128, 3: 128 x 128 as 1 x 4 waves, h2 only).  Returns the previous mode; -1 only queries.
- * Process-wide; results are identical up to summation order. */
-int scd_set_halo16(int32_t mode);
-/* Halo weight-grad kernel selection (SCD_MATH_X3, 3x3 / stride 1, R and C multiples of 64): 0 = 32x32x16
- * MFMA kernel, 1 = 16x16x32 MFMA kernel (default).  Returns the previous mode; -1 only queries. */
-int scd_set_wgrad16(int32_t mode);
+/* ABI revision of this header (struct layouts and signatures); a binding checks it at load time.
+ *   3: scd_igemm_t / scd_wgrad_t / scd_pack_job_t carry `math` (and `tune`); the process-wide mode setters
+ *      (scd_set_conv_math, scd_set_halo16, scd_set_wgrad16) and every launch-time environment switch are gone. */
+#define SCD_ABI_VERSION 3
+int scd_abi_version(void);
+/* The arithmetic scd_conv_igemm / scd_conv_wgrad will use for a descriptor (its `math`, or SCD_MATH_X3 / F32 where
+ * the shape or the missing operand bounds keep the conv off the requested kernels); negative = invalid descriptor.
+ * (Declared with the descriptors below.) */
+/* Kernel-variant selection, scd_igemm_t.tune / scd_wgrad_t.tune.  0 = the library's measured defaults; the other
+ * values select variants kept for bit-identity tests and A/B measurements.  Every variant computes the same
+ * outputs (bit-identical where the tests say so, else equal up to fp32 summation order). */
+#define SCD_TUNE_HALO16_CFG(id)   ((uint32_t)((id) + 1))  /* force 16x16x32 halo tile id 0..4 (id 3, 4: h2 only) */
+#define SCD_TUNE_HALO16_OFF       0xFu                    /* the 32x32x16 halo kernel instead                     */
+#define SCD_TUNE_HALO16_MASK      0xFu
+#define SCD_TUNE_H2_TILE_2X2      (1u << 4)   /* h2, >= 128 outputs: 2x2 waves instead of 1x4                     */
+#define SCD_TUNE_H2_TILE64_2X2    (1u << 5)   /* h2, 64..127 outputs: 2x2 waves instead of 1x2                    */
+#define SCD_TUNE_H2_NO_PRESCALE   (1u << 6)   /* h2 without the 2^11 pre-scaled low term (narrower range)         */
+#define SCD_TUNE_NO_XCD_REMAP     (1u << 7)   /* plain block order instead of the XCD swizzle                     */
+#define SCD_TUNE_HALO_ORDER_M     (1u << 8)   /* halo kernels: N-fastest block order                              */
+#define SCD_TUNE_W16_LAYOUT_2X2   (1u << 9)   /* halo weight grad (h2 / bf16): 2x2 waves instead of along c       */
+#define SCD_TUNE_WGRAD_R64        (1u << 10)  /* halo weight grad: 64-row blocks instead of 128                   */
+#define SCD_TUNE_X3_TILE(t)       ((uint32_t)(t) << 12)   /* per-tap x3 igemm tile 1..5 (0 = automatic)          */
+#define SCD_TUNE_X3_TILE_MASK     (0xFu << 12)
+#define SCD_TUNE_C16_TILES(k)     ((uint32_t)(k) << 16)   /* input-layer forward: tiles per block (0 = 4; 15 =
+                                                             one resident round)                                 */
+#define SCD_TUNE_C16_TILES_MASK   (0xFu << 16)
+#define SCD_TUNE_HALO16_DB_OFF    (1u << 20)  /* halo16 forward: single-buffered halo                             */
+#define SCD_TUNE_HALO16_DB_ON     (1u << 21)  /* halo16 forward: double-buffered halo where it fits (h2 too)     */
+#define SCD_TUNE_NO_GATHER16      (1u << 22)  /* ConvTranspose fwd / data grad on the x3 per-tap kernel           */
+#define SCD_TUNE_NO_WGRAD_C16     (1u << 23)  /* input-layer weight grad on the generic x3 kernel                 */
+#define SCD_TUNE_NO_WGRAD_H2      (1u << 24)  /* ConvTranspose weight grad on x3 instead of h2                    */
+#define SCD_TUNE_NO_HALO16_C16    (1u << 25)  /* input-layer forward on the per-tap x3 kernel                     */
+#define SCD_TUNE_NO_HALO          (1u << 26)  /* no halo kernels at all (per-tap kernels)                         */
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);
@@ -138,11 +164,11 @@ int scd_split_bf16x3_frag(const float *w, int32_t n_out, int32_t K, uint16_t *ds
  * row r the power-of-two scale s_r that brings max_k |w[r][k]| below 2^15, the fp16 h and m planes of w * s_r in
  * the fragment order above (planes 0 and 1), then float inv[NB * 32] = 1 / s_r after the planes (1 for padding
  * rows).  scd_pack_conv3x3_multi writes this format instead of the bf16x3 split for 3x3 jobs whose K / 9 is a
- * multiple of 32 while the mode is SCD_MATH_H2 (including the per-row scales of the data-grad layout). */
+ * multiple of 32 and whose math is SCD_MATH_H2 (including the per-row scales of the data-grad layout). */
 int scd_split_h2_frag(const float *w, int32_t n_out, int32_t K, uint16_t *dst, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Implicit-GEMM convolution on MFMA (arithmetic: scd_set_conv_math).
+ * Implicit-GEMM convolution on MFMA (arithmetic: scd_igemm_t.math).
  *   out[m, o] = bias[o] + sum_{t<ntaps, c<src.c} src[img, oy*stride+dy[t], ox*stride+dx[t], c] * wpk[o][t*src.c + c]
  *   m = (img, oy, ox) over src.n x out_h x out_w; out-of-range source pixels read as 0 (zero padding).
  * store_mode 0: dst[img, oy, ox, o]                            (dst.h == out_h, dst.w == out_w)
@@ -177,7 +203,7 @@ typedef struct scd_igemm {
     const float *bias;  /* [n_out] (store_mode 0) or [n_out/4] (store_mode 1) or NULL */
     scd_nhwc_t dst;
     int32_t store_mode;
-    /* Optional (SCD_MATH_X3 only): wpk pre-split by scd_split_bf16x3_frag (fragment order).
+    /* Optional (split arithmetics): wpk pre-split by scd_split_bf16x3_frag / scd_split_h2_frag (fragment order).
      * The weights are then staged by copy instead of being split in every workgroup.  NULL = split on
      * the fly.  Must describe the same values as wpk. */
     const uint16_t *wsplit;
@@ -197,7 +223,7 @@ typedef struct scd_igemm {
     /* Optional fused BatchNorm backward partial sums of the stored output (see scd_bn_bwd_tiles_t); only
      * where scd_igemm_bn_bwd_tiles() reports > 0 tiles.  NULL = off. */
     const scd_bn_bwd_tiles_t *bn_bwd;
-    /* SCD_MATH_H2 only: device float holding an upper bound U >= |every src element as read| (after the input
+    /* math == SCD_MATH_H2 only: device float holding an upper bound U >= |every src element as read| (after the input
      * transform).  A 3x3 conv with src.c % 32 == 0 (halo16 kernel), or a 1- / 4-tap conv with src.c % 32 == 0 and
      * n_out % 64 == 0 (the ConvTranspose forward and data grad: gather16 kernel), then runs the two-term fp16 split:
      * src scaled by the power of two that brings U below 2^15, weights from the h2 split of wsplit
@@ -211,10 +237,12 @@ typedef struct scd_igemm {
      * convs where scd_igemm_arith reports the halo16 / gather16 h2 path (the decoder's concat-gradient data grad).
      * NULL = off. */
     float *dst_bound;
+    int32_t math;  /* enum scd_conv_math: the arithmetic of this launch */
+    uint32_t tune; /* SCD_TUNE_* kernel-variant bits, 0 = defaults */
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);
-int scd_igemm_arith(const scd_igemm_t *d); /* see scd_set_conv_math */
+int scd_igemm_arith(const scd_igemm_t *d); /* see enum scd_conv_math */
 /* Tiles (and *tile_pixels) of the fused BatchNorm-backward partial sums for `d`, 0 if not available. */
 int scd_igemm_bn_bwd_tiles(const scd_igemm_t *d, int32_t *tile_pixels);
 /* 1 if the kernel scd_conv_igemm would run for `d` applies the in_scale/in_shift input transform, else 0. */
@@ -244,7 +272,7 @@ typedef struct scd_wgrad {
     const float *src_scale;
     const float *src_shift;
     int32_t src_nseg;
-    /* SCD_MATH_H2 only: device floats bounding |rows| and |src| (as read, after the src transform), as
+    /* math == SCD_MATH_H2 only: device floats bounding |rows| and |src| (as read, after the src transform), as
      * scd_igemm_t.src_bound.  With both set the 16x16x32 halo weight grad runs the fp16 two-term split; else x3. */
     const float *rows_bound;
     const float *src_bound;
@@ -258,13 +286,15 @@ typedef struct scd_wgrad {
     scd_nhwc_t rows_y;
     int32_t rows_nseg;
     const float *rows_mean, *rows_invstd, *rows_gamma, *rows_scale, *rows_shift, *rows_coef;
+    int32_t math;  /* enum scd_conv_math: the arithmetic of this launch */
+    uint32_t tune; /* SCD_TUNE_* kernel-variant bits, 0 = defaults */
 } scd_wgrad_t;
 
 /* Number of K-splits the library will use and the slab bytes it needs. */
 int scd_wgrad_plan(const scd_wgrad_t *d, int32_t *nsplit, size_t *slab_bytes);
-int scd_wgrad_arith(const scd_wgrad_t *d); /* see scd_set_conv_math */
+int scd_wgrad_arith(const scd_wgrad_t *d); /* see enum scd_conv_math */
 /* Rows of dY (output channels) per workgroup of the halo weight-grad kernel scd_conv_wgrad would run for `d`:
- * 64 or 128 (SCD_W16_R128=0 keeps 64); 0 when `d` takes another weight-grad kernel.  Diagnostic. */
+ * 64 or 128 (SCD_TUNE_WGRAD_R64 keeps 64); 0 when `d` takes another weight-grad kernel.  Diagnostic. */
 int scd_wgrad_rows_per_block(const scd_wgrad_t *d);
 int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream);
 /* 1 if the weight-grad kernel scd_conv_wgrad would run for `d` applies the src_scale/src_shift transform. */

@@ -1174,13 +1174,18 @@ static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *s
 }
 // The encoder levels' BatchNorm backward with the pooled gradient (DaPooled) over 2x2 cells.  The chunks partition
 // each segment's cells into at most bn_geom's chunk count, so the records fit the same workspace.
-// SCD_BN_POOLED_CELLS=0 runs the per-pixel kernels instead (A/B switch, read at launch).
+// Building with -DSCD_BN_POOLED_CELLS=0 runs the per-pixel kernels instead (A/B experiments; bit-identical).
+#ifndef SCD_BN_POOLED_CELLS
+#define SCD_BN_POOLED_CELLS 1
+#endif
+#ifndef SCD_BN_POOLED_PAIR
+#define SCD_BN_POOLED_PAIR 1
+#endif
 static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled &da, int nseg, const float *save_mean,
                                    const float *save_invstd, const float *gamma, const float *scale, const float *shift,
                                    float *dgamma, float *dbeta, float *dbias_prev, const scd_nhwc_t &dy,
                                    float *dy_bound, void *ws, hipStream_t s) {
-    const char *e = getenv("SCD_BN_POOLED_CELLS");
-    if (e && e[0] == '0') {
+    if (!SCD_BN_POOLED_CELLS) {
         bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy,
                         dy_bound, ws, s);
         return;
@@ -1199,10 +1204,9 @@ static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled &da, int 
     float *rec = static_cast<float *>(ws);
     float *brec = rec + size_t(g.nrec) * y.c * 2;
     float *coef = brec + size_t(g.nrec) * y.c;
-    // Siamese pairs (SCD_BN_POOLED_PAIR=0: one image per cell walk): the t1 and t2 cells at one place in one block,
+    // Siamese pairs (-DSCD_BN_POOLED_PAIR=0: one image per cell walk): the t1 and t2 cells at one place in one block,
     // the shared difference gradient read once instead of once per branch
-    const char *pe = getenv("SCD_BN_POOLED_PAIR");
-    if (!(pe && pe[0] == '0') && nseg == 2 && da.gs && da.skip_mode == 1 && 2 * da.gsn == y.n) {
+    if (SCD_BN_POOLED_PAIR && nseg == 2 && da.gs && da.skip_mode == 1 && 2 * da.gsn == y.n) {
         hipLaunchKernelGGL(bn_bwd_pooled_partial_pair, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
                            static_cast<const float *>(y.data), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
                            save_invstd, scale, shift, rec);

@@ -32,23 +32,13 @@ __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t nwg) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
 }
 
-inline int xcd_remap_enabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("SCD_XCD_REMAP");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v;
-}
-
-// Halo-tiled igemm for 3x3 convs (x3 math); SCD_HALO=0 disables it (A/B experiments).
-inline int halo_enabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("SCD_HALO");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v;
+// Kernel-variant bits of a launch (scd_igemm_t.tune / scd_wgrad_t.tune, SCD_TUNE_* in scd.h; 0 = defaults).
+inline int xcd_remap_enabled(uint32_t tune) { return (tune & SCD_TUNE_NO_XCD_REMAP) ? 0 : 1; }
+// Halo-tiled kernels for 3x3 convs (split arithmetics); SCD_TUNE_NO_HALO keeps the per-tap kernels.
+inline int halo_enabled(uint32_t tune) { return (tune & SCD_TUNE_NO_HALO) ? 0 : 1; }
+// Block order of the halo kernels: N-slowest XCD order (2) unless SCD_TUNE_HALO_ORDER_M / SCD_TUNE_NO_XCD_REMAP.
+inline int halo_remap(uint32_t tune) {
+    return !xcd_remap_enabled(tune) ? 0 : (tune & SCD_TUNE_HALO_ORDER_M) ? 1 : 2;
 }
 
 inline uint64_t pack_taps(const int8_t *v, int n) {
@@ -88,6 +78,8 @@ struct IgemmArgs {
     // the weight planes in wsplit are then the fp16 two-term split with per-row inverse scales (h2_wsplit_bytes)
     const float *src_bound;
     float *dst_bound;  // optional: raised to max |stored output| (x3 / halo16 / gather16 kernels; scd_igemm_t.dst_bound)
+    int math;          // SCD_MATH_* of this launch (scd_igemm_t.math)
+    uint32_t tune;     // SCD_TUNE_* bits (scd_igemm_t.tune)
 };
 
 struct WgradArgs {
@@ -113,6 +105,8 @@ struct WgradArgs {
     uint32_t y_bytes;
     const float *rbn_mean, *rbn_inv, *rbn_gamma, *rbn_scale, *rbn_shift, *rbn_coef;
     int rows_seg_imgs;
+    int math;       // SCD_MATH_* of this launch (scd_wgrad_t.math)
+    uint32_t tune;  // SCD_TUNE_* bits (scd_wgrad_t.tune)
 };
 
 // Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels
@@ -130,38 +124,38 @@ bool igemm_takes_halo16(const IgemmArgs &a);
 bool igemm_takes_c16(const IgemmArgs &a);  // igemm_halo16_c16 (16-channel source)
 bool igemm_takes_gather16(const IgemmArgs &a);  // igemm_gather16_h2 (ConvTranspose forward / data grad)
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
-// 16x16x32-MFMA halo weight grad (conv_halo16.hip), selected by wgrad16_mode() (scd_set_wgrad16).
-int wgrad16_mode();
-const void *wgrad_halo16_fn(bool bounded, int rblock);  // bounded: h2 under SCD_MATH_H2
+// 16x16x32-MFMA halo weight grad (conv_halo16.hip).
+const void *wgrad_halo16_fn(int math, uint32_t tune, bool bounded, int rblock);  // bounded: h2 under SCD_MATH_H2
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
 // dY rows per block of the halo weight grad (64 or 128; threads = 4 * rows): plan and launch use the same value.
-int wgrad16_rblock(int R, bool bounded);
+int wgrad16_rblock(int math, uint32_t tune, int R, bool bounded);
 // 16-channel-source variant (the input layer), same eligibility otherwise (conv_halo16.hip).
-const void *wgrad_halo16_c16_fn();
+const void *wgrad_halo16_c16_fn(int math);
 void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s);
+// Halo weight grad (3x3 / stride 1 / same size, R and C multiples of 64, maps in 2x16 patches).
+inline const void *wgrad_halo_fn(int math, uint32_t tune, bool bounded, int rblock) {
+    return wgrad_halo16_fn(math, tune, bounded, rblock);
+}
+inline int wgrad_halo_rblock(int math, uint32_t tune, int R, bool bounded) {
+    return wgrad16_rblock(math, tune, R, bounded);
+}
 // x3 weight-grad instantiations, indexed like kWgradTiles (conv_f32.hip).
 const void *wgrad_x3_fn(int tile_id);
 void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
 // h2 variants of the generic weight grad (both operand bounds; tiles wgrad_x3_h2_tile accepts), conv_x3.hip.
 bool wgrad_x3_h2_tile(int tile_id);
 void launch_wgrad_x3_h2(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
-// Halo weight grad (3x3 / stride 1 / same size, R and C multiples of 64, maps in 2x16 patches).
-const void *wgrad_halo_fn(bool bounded, int rblock);
-int wgrad_halo_rblock(int R, bool bounded);  // 64, or wgrad16_rblock under scd_set_wgrad16
-void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
-
-// Conv math selection (scd_set_conv_math): SCD_MATH_X3 = split-bf16 MFMA where the shape allows it,
-// SCD_MATH_F32 = fp32 MFMA everywhere, SCD_MATH_BF16 = the x3 pipeline with one bf16 term per operand in the
-// 16x16x32 halo kernels.  Initial value from SCD_CONV_MATH=f32|x3|bf16 (default x3).
-int conv_math_x3();      // split-weight (x3, x5, bf16 or h2) pipeline
-int conv_math_mode();    // the SCD_MATH_* mode
+// Conv arithmetic of a launch (scd_igemm_t.math / scd_wgrad_t.math; enum scd_conv_math in scd.h).
+inline bool math_valid(int m) { return m >= SCD_MATH_F32 && m <= SCD_MATH_H2; }
+inline int math_split(int m) { return m != SCD_MATH_F32; }  // split-weight (x3, x5, bf16 or h2) pipeline
 // halo16 kernel arithmetic: 3 (x3), 5 (x5: x3 less one product), 1 (bf16), 2 (h2: two-term fp16 split)
-int conv_math_planes();
+inline int math_planes(int m) { return m == SCD_MATH_BF16 ? 1 : m == SCD_MATH_X5 ? 5 : m == SCD_MATH_H2 ? 2 : 3; }
+inline int h2_prescale(uint32_t tune) { return (tune & SCD_TUNE_H2_NO_PRESCALE) ? 0 : 1; }
 // SCD_MATH_H2 weight splits exist for 3x3 convs (the halo16 kernels) and 1- / 4-tap convs (the ConvTranspose forward
 // and data grad, the gather16 kernel) whose source channels are a multiple of 32; every other conv keeps the x3
 // split.  wsplit of such a conv is in the h2 format.
-inline bool h2_weight_format(int ntaps, int c) {
-    return conv_math_mode() == SCD_MATH_H2 && (ntaps == 9 || ntaps == 1 || ntaps == 4) && c % 32 == 0;
+inline bool h2_weight_format(int math, int ntaps, int c) {
+    return math == SCD_MATH_H2 && (ntaps == 9 || ntaps == 1 || ntaps == 4) && c % 32 == 0;
 }
 // h2 gather igemm (conv_gather16.hip): 0 when `a` does not take it, else 1 + tile id; launcher.
 int gather16_pick(const IgemmArgs &a);

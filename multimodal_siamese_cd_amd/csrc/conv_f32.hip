@@ -482,7 +482,7 @@ static void launch_igemm(const IgemmArgs &a, hipStream_t s) {
     IgemmArgs b = a;
     b.grid_m = (a.M + BM - 1) / BM;
     b.grid_n = (a.n_out + BN - 1) / BN;
-    b.remap = xcd_remap_enabled();
+    b.remap = xcd_remap_enabled(a.tune);
     hipLaunchKernelGGL((igemm_f32<WM, WN, TM, TN, BK>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN), 0, s, b);
 }
 
@@ -507,47 +507,21 @@ static int check_taps(int ntaps, const int8_t *dy, const int8_t *dx) {
     return SCD_OK;
 }
 
-static int g_conv_math = -1;
-
-int conv_math_mode() {
-    if (g_conv_math < 0) {
-        const char *e = getenv("SCD_CONV_MATH");
-        g_conv_math = (e && e[0] == 'f')                   ? SCD_MATH_F32
-                      : (e && e[0] == 'b')                 ? SCD_MATH_BF16
-                      : (e && e[0] == 'x' && e[1] == '5') ? SCD_MATH_X5
-                      : (e && e[0] == 'h' && e[1] == '2') ? SCD_MATH_H2
-                                                           : SCD_MATH_X3;
-    }
-    return g_conv_math;
-}
-int conv_math_x3() { return conv_math_mode() != SCD_MATH_F32; }
-int conv_math_planes() {
-    const int m = conv_math_mode();
-    return m == SCD_MATH_BF16 ? 1 : m == SCD_MATH_X5 ? 5 : m == SCD_MATH_H2 ? 2 : 3;
-}
-
 }  // namespace scd
 
 using namespace scd;
 
-extern "C" int scd_set_conv_math(int32_t mode) {
-    clear_error();
-    const int prev = conv_math_mode();
-    if (mode == SCD_MATH_F32 || mode == SCD_MATH_X3 || mode == SCD_MATH_BF16 || mode == SCD_MATH_X5 ||
-        mode == SCD_MATH_H2) {
-        g_conv_math = mode;
-    } else if (mode != SCD_MATH_QUERY) {
-        set_error("scd_set_conv_math: mode %d", mode);
-        return SCD_ERR_ARG;
-    }
-    return prev;
-}
+extern "C" int scd_abi_version(void) { return SCD_ABI_VERSION; }
 
 namespace scd {
 // Validate a descriptor and fill the kernel arguments.
 static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     if (!d) {
         set_error("scd_conv_igemm: null descriptor");
+        return SCD_ERR_ARG;
+    }
+    if (!math_valid(d->math)) {
+        set_error("igemm: math %d is not an scd_conv_math value", d->math);
         return SCD_ERR_ARG;
     }
     SCD_TRY(check_view(d->src, "igemm.src"));
@@ -651,6 +625,8 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     }
     a.src_bound = d->src_bound;
     a.dst_bound = d->dst_bound;
+    a.math = d->math;
+    a.tune = d->tune;
     if (d->wsplit && !aligned16(d->wsplit)) {
         set_error("igemm: wsplit must be 16-byte aligned");
         return SCD_ERR_ALIGN;
@@ -770,10 +746,10 @@ extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
     clear_error();
     IgemmArgs a;
     SCD_TRY(igemm_query_prepare(d, a));
-    if (!conv_math_x3()) return SCD_MATH_F32;
-    if (igemm_takes_halo16(a)) return conv_math_mode();  // under SCD_MATH_H2 only bounded h2-split convs take it
+    if (!math_split(a.math)) return SCD_MATH_F32;
+    if (igemm_takes_halo16(a)) return a.math;  // under SCD_MATH_H2 only bounded h2-split convs take it
     if (igemm_takes_gather16(a)) return SCD_MATH_H2;
-    if (igemm_takes_c16(a)) return conv_math_mode() == SCD_MATH_H2 ? SCD_MATH_X3 : conv_math_mode();
+    if (igemm_takes_c16(a)) return a.math == SCD_MATH_H2 ? SCD_MATH_X3 : a.math;
     return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
 }
 
@@ -832,9 +808,9 @@ static int conv_igemm_run(const scd_igemm_t *d, hipStream_t s, int bb_ntiles_tot
                   "(ConvTranspose store_mode 1 convs take it on every split-bf16 kernel)");
         return SCD_ERR_ARG;
     }
-    if (conv_math_x3() && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");
+    if (math_split(a.math) && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");
     if (a.dst_bound) {
-        set_error("igemm: dst_bound needs the split-bf16 kernels (conv math x3 / h2 and src.c %% 16 == 0)");
+        set_error("igemm: dst_bound needs the split-bf16 kernels (math x3 / h2 and src.c %% 16 == 0)");
         return SCD_ERR_ARG;
     }
     if (d->n_out >= 128)
@@ -880,6 +856,10 @@ static int wgrad_validate(const scd_wgrad_t *d) {
     SCD_TRY(check_view(d->rows, "wgrad.rows"));
     SCD_TRY(check_view(d->src, "wgrad.src"));
     SCD_TRY(check_taps(d->ntaps, d->dy, d->dx));
+    if (!math_valid(d->math)) {
+        set_error("wgrad: math %d is not an scd_conv_math value", d->math);
+        return SCD_ERR_ARG;
+    }
     if (d->rows.n != d->src.n || d->stride < 1) {
         set_error("wgrad: rows.n=%d src.n=%d stride=%d", d->rows.n, d->src.n, d->stride);
         return SCD_ERR_ARG;
@@ -891,8 +871,8 @@ static int wgrad_validate(const scd_wgrad_t *d) {
     return SCD_OK;
 }
 // Workgroups of one wgrad instantiation that the whole chip holds at once (occupancy API x CUs), cached.
-static int wgrad_resident_blocks(const WgradTile &t) {
-    const int x3 = conv_math_x3();
+static int wgrad_resident_blocks(const WgradTile &t, int math) {
+    const int x3 = math_split(math);
     static int cache[2][8] = {{0}};
     if (cache[x3][t.id] > 0) return cache[x3][t.id];
     int per_cu = 0, cus = 0, dev = 0;
@@ -955,44 +935,44 @@ static void split_units(int64_t M, int64_t tiles, int64_t cap, int64_t min_units
 // Halo weight grad eligibility: x3 math, 3x3 taps in standard order, stride 1, same-size maps,
 // R and C multiples of 64, maps tiled by 2x16 patches.
 static bool wgrad_halo_shape(const scd_wgrad_t *d) {
-    if (!conv_math_x3() || d->stride != 1 || d->ntaps != 9) return false;
+    if (!math_split(d->math) || d->stride != 1 || d->ntaps != 9) return false;
     for (int t = 0; t < 9; ++t)
         if (d->dy[t] != t / 3 - 1 || d->dx[t] != t % 3 - 1) return false;
     return d->rows.h == d->src.h && d->rows.w == d->src.w && d->rows.c % 64 == 0 && d->rows.h % 2 == 0 &&
-           d->rows.w % 16 == 0 && halo_enabled();
+           d->rows.w % 16 == 0 && halo_enabled(d->tune);
 }
 static bool wgrad_halo_ok(const scd_wgrad_t *d) { return wgrad_halo_shape(d) && d->src.c % 64 == 0; }
-// The 16-channel-source halo kernel (the padded input layer): 16x16x32 MFMA only (scd_set_wgrad16 on).
-// SCD_WGRAD_C16=0 sends it back to the generic x3 weight grad (A/B switch, read at launch).
+// The 16-channel-source halo kernel (the padded input layer).  SCD_TUNE_NO_WGRAD_C16 sends it back to the generic x3
+// weight grad (A/B).
 static bool wgrad_c16_ok(const scd_wgrad_t *d) {
-    const char *e = getenv("SCD_WGRAD_C16");
-    return wgrad_halo_shape(d) && d->src.c == 16 && wgrad16_mode() && !(e && e[0] == '0');
+    return wgrad_halo_shape(d) && d->src.c == 16 && !(d->tune & SCD_TUNE_NO_WGRAD_C16);
 }
 
 // Both operands bounded: the h2 weight grad under SCD_MATH_H2 (x3 otherwise).
 static bool wgrad_bounded(const scd_wgrad_t *d) { return d->rows_bound && d->src_bound; }
-// The generic (non-halo) weight grad in h2: bounded, SCD_MATH_H2, a tile with an h2 instantiation.  SCD_WGRAD_H2=0
-// keeps it on x3 (A/B switch, read at launch).
+// The generic (non-halo) weight grad in h2: bounded, SCD_MATH_H2, a tile with an h2 instantiation.
+// SCD_TUNE_NO_WGRAD_H2 keeps it on x3 (A/B).
 static bool wgrad_generic_h2(const scd_wgrad_t *d) {
-    const char *e = getenv("SCD_WGRAD_H2");
-    return wgrad_bounded(d) && conv_math_mode() == SCD_MATH_H2 && !(e && e[0] == '0') &&
+    return wgrad_bounded(d) && d->math == SCD_MATH_H2 && !(d->tune & SCD_TUNE_NO_WGRAD_H2) &&
            wgrad_x3_h2_tile(wgrad_tile(d->rows.c, d->ntaps * d->src.c).id);
 }
 
-static int wgrad_halo_resident(bool c16, bool bounded, int rblock) {
-    // per halo weight-grad kernel: 32x32x16; 16x16x32 x3 / x5 / bf16 / h2; 16-channel x3 / x5 / bf16; the
-    // 128-row bf16 / h2 blocks
-    static int caches[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const int m = conv_math_planes();
+static int wgrad_halo_resident(const scd_wgrad_t *d, bool c16, bool bounded, int rblock) {
+    // per halo weight-grad kernel: 16x16x32 x3 / x5 / bf16 / h2 (x layout); 16-channel x3 / x5 / bf16; the 128-row
+    // bf16 / h2 blocks
+    static int caches[2][12] = {{0}};
+    const int m = math_planes(d->math);
     const int planes = m == 1 ? 0 : m == 5 ? 1 : (m == 2 && bounded && !c16) ? 3 : 2;
     const bool r128 = !c16 && rblock == 128;
-    int &cache = caches[r128 ? 9 + (planes == 3) : c16 ? 5 + planes : wgrad16_mode() ? 1 + planes : 0];
+    const int lay = (d->tune & SCD_TUNE_W16_LAYOUT_2X2) ? 1 : 0;
+    int &cache = caches[lay][r128 ? 9 + (planes == 3) : c16 ? 5 + planes : 1 + planes];
     if (cache > 0) return cache;
     int per_cu = 0, cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu,
-                                                     c16 ? wgrad_halo16_c16_fn() : wgrad_halo_fn(bounded, rblock),
+                                                     c16 ? wgrad_halo16_c16_fn(d->math)
+                                                         : wgrad_halo_fn(d->math, d->tune, bounded, rblock),
                                                      r128 ? 512 : 256, 0) !=
             hipSuccess ||
         per_cu < 1 ||
@@ -1008,21 +988,21 @@ static int wgrad_halo_resident(bool c16, bool bounded, int rblock) {
 static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
     if (wgrad_halo_ok(d) || wgrad_c16_ok(d)) {
         const bool c16 = !wgrad_halo_ok(d);
-        const int rb = c16 ? 64 : wgrad_halo_rblock(d->rows.c, wgrad_bounded(d));
+        const int rb = c16 ? 64 : wgrad_halo_rblock(d->math, d->tune, d->rows.c, wgrad_bounded(d));
         const int64_t patches = pixels(d->rows) / 32;
         const int64_t tiles = int64_t(d->rows.c / rb) * (c16 ? 1 : d->src.c / 64);
-        split_units(patches, tiles, wgrad_halo_resident(c16, wgrad_bounded(d), rb), 8, 1, nsplit, kchunk);
+        split_units(patches, tiles, wgrad_halo_resident(d, c16, wgrad_bounded(d), rb), 8, 1, nsplit, kchunk);
         return;
     }
     const int Ng = d->ntaps * d->src.c;
     const WgradTile t = wgrad_tile(d->rows.c, Ng);
     const int64_t tiles = int64_t((d->rows.c + t.bm - 1) / t.bm) * ((Ng + t.bn - 1) / t.bn);
-    split_units(pixels(d->rows), tiles, wgrad_resident_blocks(t), 256, 16, nsplit, kchunk);
+    split_units(pixels(d->rows), tiles, wgrad_resident_blocks(t, d->math), 256, 16, nsplit, kchunk);
 }
 }  // namespace scd
 
 namespace scd {
-static bool wgrad_src_bn_ok(const scd_wgrad_t *d) { return (wgrad_halo_ok(d) && wgrad16_mode()) || wgrad_c16_ok(d); }
+static bool wgrad_src_bn_ok(const scd_wgrad_t *d) { return wgrad_halo_ok(d) || wgrad_c16_ok(d); }
 }  // namespace scd
 
 extern "C" int scd_wgrad_src_bn_supported(const scd_wgrad_t *d) {
@@ -1040,17 +1020,16 @@ extern "C" int scd_wgrad_rows_bn_supported(const scd_wgrad_t *d) {
 extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
-    if (!conv_math_x3()) return SCD_MATH_F32;
-    if (wgrad_halo_ok(d) && wgrad16_mode())
-        return conv_math_mode() == SCD_MATH_H2 && !wgrad_bounded(d) ? SCD_MATH_X3 : conv_math_mode();
-    if (wgrad_c16_ok(d)) return conv_math_mode() == SCD_MATH_H2 ? SCD_MATH_X3 : conv_math_mode();
+    if (!math_split(d->math)) return SCD_MATH_F32;
+    if (wgrad_halo_ok(d)) return d->math == SCD_MATH_H2 && !wgrad_bounded(d) ? SCD_MATH_X3 : d->math;
+    if (wgrad_c16_ok(d)) return d->math == SCD_MATH_H2 ? SCD_MATH_X3 : d->math;
     return wgrad_generic_h2(d) ? SCD_MATH_H2 : SCD_MATH_X3;
 }
 
 extern "C" int scd_wgrad_rows_per_block(const scd_wgrad_t *d) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
-    if (wgrad_halo_ok(d)) return wgrad_halo_rblock(d->rows.c, wgrad_bounded(d));
+    if (wgrad_halo_ok(d)) return wgrad_halo_rblock(d->math, d->tune, d->rows.c, wgrad_bounded(d));
     return wgrad_c16_ok(d) ? 64 : 0;
 }
 
@@ -1187,6 +1166,8 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     a.src_seg_imgs = d->src.n;
     a.rows_bound = d->rows_bound;
     a.src_bound = d->src_bound;
+    a.math = d->math;
+    a.tune = d->tune;
     a.rows_y = nullptr;
     a.ldc_y = 0;
     a.y_bytes = 0;
@@ -1227,27 +1208,27 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     }
     if (wgrad_halo_ok(d)) {
         a.n_img_w = d->rows.n;
-        a.grid_r = a.R / wgrad_halo_rblock(a.R, wgrad_bounded(d));
+        a.grid_r = a.R / wgrad_halo_rblock(a.math, a.tune, a.R, wgrad_bounded(d));
         a.grid_j = a.C / 64;
-        a.remap = xcd_remap_enabled();
-        launch_wgrad_halo_x3(a, dim3(a.grid_r * a.grid_j * ns), s);
+        a.remap = xcd_remap_enabled(a.tune);
+        launch_wgrad_halo16_x3(a, dim3(a.grid_r * a.grid_j * ns), s);
         return launch_status("scd_conv_wgrad");
     }
     if (wgrad_c16_ok(d)) {
         a.n_img_w = d->rows.n;
         a.grid_r = a.R / 64;
         a.grid_j = 1;
-        a.remap = xcd_remap_enabled();
+        a.remap = xcd_remap_enabled(a.tune);
         launch_wgrad_halo16_c16(a, dim3(a.grid_r * ns), s);
         return launch_status("scd_conv_wgrad");
     }
     const WgradTile t = wgrad_tile(a.R, Ng);
     a.grid_r = (a.R + t.bm - 1) / t.bm;
     a.grid_j = (Ng + t.bn - 1) / t.bn;
-    a.remap = xcd_remap_enabled();
+    a.remap = xcd_remap_enabled(a.tune);
     dim3 grid(a.grid_r * a.grid_j * ns);
     dim3 block(t.threads);
-    if (conv_math_x3()) {
+    if (math_split(a.math)) {
         if (wgrad_generic_h2(d))
             launch_wgrad_x3_h2(a, t.id, grid, block, s);
         else

@@ -204,10 +204,7 @@ namespace {
 // Tiles: 0 = 128 px x 128 ch (2x2 waves of 64 x 64), 1 = 128 x 64 (2x2 of 64 x 32), 2 = 64 x 128 (2x2 of 32 x 64)
 constexpr int kSK = 2;  // 32-channel k-steps per stage
 
-int gather16_enabled() {
-    const char *e = getenv("SCD_GATHER16");  // A/B switch, read at launch
-    return !(e && e[0] == '0');
-}
+int gather16_enabled(uint32_t tune) { return (tune & SCD_TUNE_NO_GATHER16) ? 0 : 1; }
 
 template <int WM, int WN, int TM, int TN, int OCC>
 void launch_g16(const IgemmArgs &a, hipStream_t s) {
@@ -215,7 +212,7 @@ void launch_g16(const IgemmArgs &a, hipStream_t s) {
     IgemmArgs b = a;
     b.grid_m = (a.M + BM - 1) / BM;
     b.grid_n = (a.n_out + BN - 1) / BN;
-    b.remap = xcd_remap_enabled();
+    b.remap = xcd_remap_enabled(a.tune);
     hipLaunchKernelGGL((igemm_gather16_h2<WM, WN, TM, TN, kSK, OCC>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN), 0,
                        s, b);
 }
@@ -224,7 +221,8 @@ void launch_g16(const IgemmArgs &a, hipStream_t s) {
 // 1 + tile id when `a` takes the gather kernel (h2-split weights, a bound of the source, the shape constraints
 // below), else 0.  Convs with 9 taps go to the halo kernels instead.
 int gather16_pick(const IgemmArgs &a) {
-    if (!a.wsplit || !a.src_bound || a.ntaps == 9 || !h2_weight_format(a.ntaps, a.c) || !gather16_enabled())
+    if (!a.wsplit || !a.src_bound || a.ntaps == 9 || !h2_weight_format(a.math, a.ntaps, a.c) ||
+        !gather16_enabled(a.tune))
         return 0;
     if (a.c % 32 || (a.ntaps * (a.c / 32)) % kSK || a.n_out % 64 || a.ldc_s % 4 || a.ldc_d % 4 || a.K != a.ntaps * a.c ||
         (reinterpret_cast<uintptr_t>(a.src) & 15) || (reinterpret_cast<uintptr_t>(a.dst) & 15) ||

@@ -432,17 +432,11 @@ struct H16Cfg {
     int id, bm, bn;
 };
 
-// 0 = off, 1 = automatic tile choice, 2 + id = force tile config id (scd_set_halo16; initial value from
-// SCD_HALO16=0 and SCD_HALO16_CFG=<id>).
-int g_halo16 = -2;
-int halo16_mode() {
-    if (g_halo16 == -2) {
-        const char *e = getenv("SCD_HALO16");
-        g_halo16 = (e && e[0] == '0') ? 0 : 1;
-        const char *c = getenv("SCD_HALO16_CFG");
-        if (g_halo16 && c) g_halo16 = 2 + atoi(c);
-    }
-    return g_halo16;
+// 0 = off (the 32x32x16 halo kernel), 1 = automatic tile choice, 2 + id = force tile config id
+// (SCD_TUNE_HALO16_* bits of the launch).
+int halo16_mode(uint32_t tune) {
+    const uint32_t v = tune & SCD_TUNE_HALO16_MASK;
+    return v == SCD_TUNE_HALO16_OFF ? 0 : v == 0 ? 1 : int(v) + 1;
 }
 
 template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN, bool DB, int NP>
@@ -451,11 +445,7 @@ void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     IgemmArgs b = a;
     b.grid_m = a.n_img * (a.ho / (BM / tw)) * (a.wo / tw);
     b.grid_n = (a.n_out + BN - 1) / BN;
-    b.remap = xcd_remap_enabled();
-    {
-        const char *o = getenv("SCD_HALO_ORDER");
-        if (b.remap && !(o && o[0] == 'm')) b.remap = 2;
-    }
+    b.remap = halo_remap(a.tune);
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
     if (tw == 64)
         hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN, DB, NP>), grid, block, 0, s, b);
@@ -466,30 +456,21 @@ void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
 }
 
 // h2: the activation / gradient operand's low term pre-scaled by 2^11 (x3_common.h; floor 2^-36 instead of 2^-25
-// of the scaled bound).  SCD_H2_PRESCALE=0 drops it (A/B switch, read at launch).
-int h2_prescale() {
-    const char *e = getenv("SCD_H2_PRESCALE");
-    return !(e && e[0] == '0');
-}
+// of the scaled bound): h2_prescale(tune), conv_common.h (SCD_TUNE_H2_NO_PRESCALE drops it).
 
-// h2, >= 128 output channels: the 1 x 4 wave layout of the 128 x 128 tile (SCD_H2_TILE=0: 2 x 2; read at launch).
-int h2_wide_tile() {
-    const char *e = getenv("SCD_H2_TILE");
-    return !(e && e[0] == '0');
-}
+// h2, >= 128 output channels: the 1 x 4 wave layout of the 128 x 128 tile (SCD_TUNE_H2_TILE_2X2: 2 x 2).
+int h2_wide_tile(uint32_t tune) { return (tune & SCD_TUNE_H2_TILE_2X2) ? 0 : 1; }
 
 // h2, 64..127 output channels: the 1 x 2 wave layout of the 128 x 64 tile (config 4: no weight fragment loaded by two
-// waves; same-box A/B 31.81 -> 31.49 ms per step); SCD_H2_TILE64=0: 2 x 2 waves (config 1).  Read at launch.
-int h2_tile64() {
-    const char *e = getenv("SCD_H2_TILE64");
-    return !(e && e[0] == '0');
-}
+// waves; same-box A/B 31.81 -> 31.49 ms per step); SCD_TUNE_H2_TILE64_2X2: 2 x 2 waves (config 1).
+int h2_tile64(uint32_t tune) { return (tune & SCD_TUNE_H2_TILE64_2X2) ? 0 : 1; }
 
 // Double buffering where two halo buffers of every resident block still fit the CU's 160 KB of LDS: for x3 / x5 /
-// bf16; h2 runs single-buffered (same-box A/B: data grad -2.3%, step +0.5%).  SCD_HALO16_DB=0|1 forces it.
-int halo16_db(bool h2) {
-    const char *e = getenv("SCD_HALO16_DB");  // experiment switch
-    return e ? atoi(e) : (h2 ? 0 : 1);
+// bf16; h2 runs single-buffered (same-box A/B: data grad -2.3%, step +0.5%).  SCD_TUNE_HALO16_DB_ON / _OFF force it.
+int halo16_db(uint32_t tune, bool h2) {
+    if (tune & SCD_TUNE_HALO16_DB_OFF) return 0;
+    if (tune & SCD_TUNE_HALO16_DB_ON) return 1;
+    return h2 ? 0 : 1;
 }
 
 template <int WM, int WN, int TM, int TN, int OCC, bool DB, int NP>
@@ -504,15 +485,15 @@ template <int WM, int WN, int TM, int TN, int OCC>
 void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
-    const bool db3 = tw != 64 && halo16_db(false) && OCC * 2 * 3 * hr * 64 <= 160 * 1024;
-    const bool db_h2 = tw != 64 && halo16_db(true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
+    const bool db3 = tw != 64 && halo16_db(a.tune, false) && OCC * 2 * 3 * hr * 64 <= 160 * 1024;
+    const bool db_h2 = tw != 64 && halo16_db(a.tune, true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
     // h2 needs the h2 weight split and a bound (igemm_takes_halo16); otherwise x3 (h2 mode: other shapes)
-    const int planes = a.src_bound && h2_weight_format(a.ntaps, a.c) ? (h2_prescale() ? 4 : 2)
-                       : conv_math_planes() == 2                      ? 3
-                                                                      : conv_math_planes();
+    const int planes = a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) ? (h2_prescale(a.tune) ? 4 : 2)
+                       : math_planes(a.math) == 2                            ? 3
+                                                                             : math_planes(a.math);
     switch (planes) {
         case 1:  // one plane: double buffering always fits
-            if (halo16_db(false))
+            if (halo16_db(a.tune, false))
                 launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
             else
                 launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
@@ -556,7 +537,7 @@ template <int WM, int WN, int TM, int TN, int OCC>
 void launch16_h2only(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
-    const bool db2 = tw != 64 && halo16_db(true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
+    const bool db2 = tw != 64 && halo16_db(a.tune, true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
     if (db2)
         launch16c<WM, WN, TM, TN, OCC, true, 4>(a, tw, s);
     else
@@ -567,7 +548,7 @@ void launch16_h2only(const IgemmArgs &a, int tw, hipStream_t s) {
 
 // 0 when `a` does not take this kernel, else 1 + config id; *bm = pixels per tile, *tw = tile width.
 int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
-    const int mode = halo16_mode();
+    const int mode = halo16_mode(a.tune);
     if (!mode || !eligible || a.c % 32 || a.n_out % 4 || a.ldc_d % 4 || (reinterpret_cast<uintptr_t>(a.dst) & 15) ||
         (a.bias && (reinterpret_cast<uintptr_t>(a.bias) & 15)))
         return 0;
@@ -577,16 +558,20 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     else if (a.n_out >= 128)
         // 128 x 128 at 2 waves/SIMD: +4..17% over the 32x32x16 halo kernel on the 128..512-channel layers; under h2
         // as 1 x 4 waves of 128 px x 32 ch (no weight fragment loaded by two waves; SCD_H2_TILE=0: 2 x 2)
-        id = (a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale() && h2_wide_tile()) ? 3 : 0;
+        id = (a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune) && h2_wide_tile(a.tune))
+                 ? 3
+                 : 0;
     else if (a.n_out >= 64)
         // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
-        id = (a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale() && h2_tile64()) ? 4 : 1;
+        id = (a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune) && h2_tile64(a.tune)) ? 4
+                                                                                                              : 1;
     else
         return 0;
-    if (id < 0 || id > 4 || (id > 2 && !(a.src_bound && h2_weight_format(a.ntaps, a.c) && h2_prescale()))) return 0;
+    if (id < 0 || id > 4 ||
+        (id > 2 && !(a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune))))
+        return 0;
     *bm = kCfg[id].bm;
-    const char *twe = getenv("SCD_HALO16_TW");  // preferred tile width (hip.halo16_tile_width_pref mirrors it)
-    const int pref = twe ? atoi(twe) : 16;  // 16: smallest halo per pixel (180 rows for 128 px)
+    const int pref = 16;  // preferred tile width, the smallest halo per pixel (180 rows for 128 px)
     for (int cand : {pref, 64, 32, 16})
         if (a.wo % cand == 0 && a.ho % (*bm / cand) == 0 && *bm / cand >= 1 && *bm % cand == 0) {
             *tw = cand;
@@ -838,10 +823,10 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
 }
 
 // 0 when `a` does not take igemm_halo16_c16, else 1; *bm = 128 pixels per tile, *tw = tile width.
-// SCD_HALO16_C16=0 switches it off (A/B).
+// SCD_TUNE_NO_HALO16_C16 switches it off (A/B).
 int halo16_c16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
-    const char *e = getenv("SCD_HALO16_C16");
-    if (!halo16_mode() || !eligible || (e && e[0] == '0') || a.c != 16 || a.K != 144 || a.in_scale || a.bb_rec ||
+    if (!halo16_mode(a.tune) || !eligible || (a.tune & SCD_TUNE_NO_HALO16_C16) || a.c != 16 || a.K != 144 ||
+        a.in_scale || a.bb_rec ||
         a.n_out % 4 || a.ldc_d % 4 || (reinterpret_cast<uintptr_t>(a.dst) & 15) ||
         (a.bias && (reinterpret_cast<uintptr_t>(a.bias) & 15)))
         return 0;
@@ -856,11 +841,11 @@ int halo16_c16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
 
 // Arithmetic of the kernels that keep the split-bf16 planes under every mode (the 16-channel input layer): the
 // mode's own, except h2 (whose fp16 weight split exists only for 32-channel multiples), which runs x3 here.
-static int bf16_planes() { return conv_math_planes() == 2 ? 3 : conv_math_planes(); }
+static int bf16_planes(int math) { return math_planes(math) == 2 ? 3 : math_planes(math); }
 
 template <int TW>
 static void launch_c16_tw(const IgemmArgs &b, dim3 grid, hipStream_t s) {
-    switch (bf16_planes()) {
+    switch (bf16_planes(b.math)) {
         case 1: hipLaunchKernelGGL((igemm_halo16_c16<TW, 1>), grid, dim3(256), 0, s, b); break;
         case 5: hipLaunchKernelGGL((igemm_halo16_c16<TW, 5>), grid, dim3(256), 0, s, b); break;
         default: hipLaunchKernelGGL((igemm_halo16_c16<TW, 3>), grid, dim3(256), 0, s, b);
@@ -868,9 +853,9 @@ static void launch_c16_tw(const IgemmArgs &b, dim3 grid, hipStream_t s) {
 }
 
 template <int TW>
-static int c16_resident() {
+static int c16_resident(int math) {
     static int cache[3] = {0, 0, 0};  // per arithmetic: bf16, x5, x3
-    const int k = bf16_planes() == 1 ? 0 : bf16_planes() == 5 ? 1 : 2;
+    const int k = bf16_planes(math) == 1 ? 0 : bf16_planes(math) == 5 ? 1 : 2;
     if (cache[k] > 0) return cache[k];
     const void *fn = k == 0   ? reinterpret_cast<const void *>(&igemm_halo16_c16<TW, 1>)
                      : k == 1 ? reinterpret_cast<const void *>(&igemm_halo16_c16<TW, 5>)
@@ -888,17 +873,17 @@ static int c16_resident() {
 }
 
 // Each block walks 4 tiles (measured on the 256^2 input layer, x3 / bf16: 1 tile 0.62 / 0.35 ms, 4 tiles 0.50 /
-// 0.31, as many as the resident capacity allows 0.53 / 0.32); SCD_C16_TILES_PER_BLOCK=<k> overrides, 0 = one
-// resident round.
+// 0.31, as many as the resident capacity allows 0.53 / 0.32); SCD_TUNE_C16_TILES(k) overrides, 15 = one resident
+// round.
 void launch_halo16_c16(const IgemmArgs &a, int tw, hipStream_t s) {
     IgemmArgs b = a;
     b.grid_m = a.n_img * (a.ho / (128 / tw)) * (a.wo / tw);
     b.grid_n = (a.n_out + 63) / 64;
     b.remap = 0;
     const int64_t ntile = int64_t(b.grid_m) * b.grid_n;
-    const int cap = tw == 64 ? c16_resident<64>() : tw == 32 ? c16_resident<32>() : c16_resident<16>();
-    const char *e = getenv("SCD_C16_TILES_PER_BLOCK");
-    const int k = e ? atoi(e) : 4;
+    const int cap = tw == 64 ? c16_resident<64>(a.math) : tw == 32 ? c16_resident<32>(a.math) : c16_resident<16>(a.math);
+    const int kt = int((a.tune & SCD_TUNE_C16_TILES_MASK) >> 16);
+    const int k = kt == 0 ? 4 : kt == 15 ? 0 : kt;
     const int64_t blocks = k >= 1 ? (ntile + k - 1) / k : (ntile < cap ? ntile : cap);
     const dim3 grid(static_cast<unsigned>(blocks));
     if (tw == 64)
@@ -1442,8 +1427,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
     for (int t = 0; t < 9; ++t) gstore4(slab + size_t(row) * a.Ng + t * 16 + 4 * g, acc[t]);
 }
 
-const void *wgrad_halo16_c16_fn() {
-    switch (bf16_planes()) {
+const void *wgrad_halo16_c16_fn(int math) {
+    switch (bf16_planes(math)) {
         case 1: return reinterpret_cast<const void *>(&wgrad_halo16_c16<1, false>);
         case 5: return reinterpret_cast<const void *>(&wgrad_halo16_c16<5, false>);
         default: return reinterpret_cast<const void *>(&wgrad_halo16_c16<3, false>);
@@ -1451,7 +1436,7 @@ const void *wgrad_halo16_c16_fn() {
 }
 template <bool RBN>
 static void launch_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    switch (bf16_planes()) {
+    switch (bf16_planes(a.math)) {
         case 1: hipLaunchKernelGGL((wgrad_halo16_c16<1, RBN>), grid, dim3(256), 0, s, a); break;
         case 5: hipLaunchKernelGGL((wgrad_halo16_c16<5, RBN>), grid, dim3(256), 0, s, a); break;
         default: hipLaunchKernelGGL((wgrad_halo16_c16<3, RBN>), grid, dim3(256), 0, s, a);
@@ -1464,32 +1449,19 @@ void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
         launch_c16<false>(a, grid, s);
 }
 
-// 0 = the 32x32x16 halo weight-grad kernel, 1 = this one (scd_set_wgrad16; initial value from SCD_WGRAD16).
-int g_wgrad16 = -1;
-int wgrad16_mode() {
-    if (g_wgrad16 < 0) {
-        const char *e = getenv("SCD_WGRAD16");
-        g_wgrad16 = (e && e[0] == '0') ? 0 : 1;
-    }
-    return g_wgrad16;
-}
 // h2 runs where both operands are bounded, x3 otherwise.
-static int wgrad16_planes(bool bounded) {
-    return conv_math_planes() == 2 ? (bounded ? (h2_prescale() ? 4 : 2) : 3) : conv_math_planes();
+static int wgrad16_planes(int math, uint32_t tune, bool bounded) {
+    return math_planes(math) == 2 ? (bounded ? (h2_prescale(tune) ? 4 : 2) : 3) : math_planes(math);
 }
-// Wave layout of the h2 and bf16 variants (W16L): SCD_W16_LAYOUT=0 keeps the 2x2 layout, default 1 (along c).
+// Wave layout of the h2 and bf16 variants (W16L): SCD_TUNE_W16_LAYOUT_2X2 keeps the 2x2 layout, default along c.
 // x3 / x5 keep 2x2: their third dY plane does not fit four r blocks in registers.
-static int w16_layout() {  // read at launch, like the other A/B switches
-    const char *e = getenv("SCD_W16_LAYOUT");
-    return (e && e[0] == '0') ? 0 : 1;
-}
+static int w16_layout(uint32_t tune) { return (tune & SCD_TUNE_W16_LAYOUT_2X2) ? 0 : 1; }
 // Rows of dY per block: 128 (RG 2) for the h2 / bf16 variants in the along-c layout when R % 128 == 0, else 64
-// (SCD_W16_R128=0: always 64; read at plan and launch time alike).
-int wgrad16_rblock(int R, bool bounded) {
-    const int np = wgrad16_planes(bounded);
-    if (!(np == 1 || np == 2 || np == 4) || !w16_layout() || R % 128) return 64;
-    const char *e = getenv("SCD_W16_R128");
-    return (e && e[0] == '0') ? 64 : 128;
+// (SCD_TUNE_WGRAD_R64: always 64; plan and launch see the same descriptor bits).
+int wgrad16_rblock(int math, uint32_t tune, int R, bool bounded) {
+    const int np = wgrad16_planes(math, tune, bounded);
+    if (!(np == 1 || np == 2 || np == 4) || !w16_layout(tune) || R % 128) return 64;
+    return (tune & SCD_TUNE_WGRAD_R64) ? 64 : 128;
 }
 template <int NP>
 static const void *w16_kernel(int lc, int rb) {
@@ -1506,20 +1478,20 @@ static void w16_launch(int lc, int rb, const WgradArgs &a, dim3 grid, hipStream_
     else
         hipLaunchKernelGGL((wgrad_halo16_x3<NP, 0, 1>), grid, dim3(256), 0, s, a);
 }
-const void *wgrad_halo16_fn(bool bounded, int rblock) {
-    switch (wgrad16_planes(bounded)) {
-        case 1: return w16_kernel<1>(w16_layout(), rblock);
-        case 2: return w16_kernel<2>(w16_layout(), rblock);
-        case 4: return w16_kernel<4>(w16_layout(), rblock);
+const void *wgrad_halo16_fn(int math, uint32_t tune, bool bounded, int rblock) {
+    switch (wgrad16_planes(math, tune, bounded)) {
+        case 1: return w16_kernel<1>(w16_layout(tune), rblock);
+        case 2: return w16_kernel<2>(w16_layout(tune), rblock);
+        case 4: return w16_kernel<4>(w16_layout(tune), rblock);
         case 5: return reinterpret_cast<const void *>(&wgrad_halo16_x3<5, 0, 1>);
         default: return reinterpret_cast<const void *>(&wgrad_halo16_x3<3, 0, 1>);
     }
 }
-// a.grid_r = R / wgrad16_rblock(R, bounded) (the caller plans with the same choice).
+// a.grid_r = R / wgrad16_rblock(...) (the caller plans with the same choice).
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
     const bool bounded = a.rows_bound && a.src_bound;
-    const int lc = w16_layout(), rb = wgrad16_rblock(a.R, bounded);
-    switch (wgrad16_planes(bounded)) {
+    const int lc = w16_layout(a.tune), rb = wgrad16_rblock(a.math, a.tune, a.R, bounded);
+    switch (wgrad16_planes(a.math, a.tune, bounded)) {
         case 1: w16_launch<1>(lc, rb, a, grid, s); break;
         case 2: w16_launch<2>(lc, rb, a, grid, s); break;
         case 4: w16_launch<4>(lc, rb, a, grid, s); break;
@@ -1531,28 +1503,3 @@ void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
 }  // namespace scd
 
 using namespace scd;
-
-extern "C" int scd_set_wgrad16(int32_t mode) {
-    clear_error();
-    const int prev = wgrad16_mode();
-    if (mode == 0 || mode == 1) {
-        g_wgrad16 = mode;
-    } else if (mode != -1) {
-        set_error("scd_set_wgrad16: mode %d", mode);
-        return SCD_ERR_ARG;
-    }
-    return prev;
-}
-
-
-extern "C" int scd_set_halo16(int32_t mode) {
-    clear_error();
-    const int prev = scd::halo16_mode();
-    if (mode >= 0 && mode <= 5) {
-        scd::g_halo16 = mode;
-    } else if (mode != -1) {
-        set_error("scd_set_halo16: mode %d", mode);
-        return SCD_ERR_ARG;
-    }
-    return prev;
-}

@@ -277,7 +277,7 @@ static void launch_x3(const IgemmArgs &a, hipStream_t s) {
     IgemmArgs b = a;
     b.grid_m = (a.M + BM - 1) / BM;
     b.grid_n = (a.n_out + BN - 1) / BN;
-    b.remap = xcd_remap_enabled();
+    b.remap = xcd_remap_enabled(a.tune);
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
     if (a.wsplit)
         hipLaunchKernelGGL((igemm_x3<WM, WN, TM, TN, true>), grid, block, 0, s, b);
@@ -533,12 +533,8 @@ static void launch_halo(const IgemmArgs &a, int tw, hipStream_t s) {
     b.grid_m = a.n_img * (a.ho / (BM / tw)) * (a.wo / tw);
     b.grid_n = (a.n_out + BN - 1) / BN;
     // N-slowest XCD order by default (keeps one n-tile of weights per XCD L2: -4..13% on the 512/1024-channel
-    // layers, neutral elsewhere); SCD_HALO_ORDER=m selects the N-fastest order.
-    b.remap = xcd_remap_enabled();
-    {
-        const char *o = getenv("SCD_HALO_ORDER");
-        if (b.remap && !(o && o[0] == 'm')) b.remap = 2;
-    }
+    // layers, neutral elsewhere); SCD_TUNE_HALO_ORDER_M selects the N-fastest order.
+    b.remap = halo_remap(a.tune);
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
     if (tw == 64)
         hipLaunchKernelGGL((igemm_halo_x3<WM, WN, TM, TN, 64>), grid, block, 0, s, b);
@@ -558,7 +554,7 @@ static bool halo_eligible(const IgemmArgs &a) {
         const int sdy = dy >= 8 ? dy - 16 : dy, sdx = dx >= 8 ? dx - 16 : dx;
         if (sdy < -1 || sdy > 1 || sdx < -1 || sdx > 1) return false;
     }
-    return halo_enabled();
+    return halo_enabled(a.tune);
 }
 
 // Halo configuration of `a`: 0 = not eligible, 1 = <2,2,2,2> (128 px x 128), 2 = <4,1,2,2> (256 x 64),
@@ -581,30 +577,30 @@ static int halo_pick(const IgemmArgs &a, int *bm, int *tw) {
 static IgemmArgs x3_view(const IgemmArgs &a) {
     IgemmArgs b = a;
     int bm = 0, tw = 0;
-    if (h2_weight_format(a.ntaps, a.c) &&
+    if (h2_weight_format(a.math, a.ntaps, a.c) &&
         (!a.src_bound || (a.ntaps == 9 ? !halo16_pick(a, halo_eligible(a), &bm, &tw) : !gather16_pick(a))))
         b.wsplit = nullptr;
     return b;
 }
 
-bool igemm_takes_gather16(const IgemmArgs &a) { return conv_math_x3() && a.c % 16 == 0 && gather16_pick(a) != 0; }
+bool igemm_takes_gather16(const IgemmArgs &a) { return math_split(a.math) && a.c % 16 == 0 && gather16_pick(a) != 0; }
 
 bool igemm_takes_halo16(const IgemmArgs &a0) {
     int bm = 0, tw = 0;
     const IgemmArgs a = x3_view(a0);
-    return conv_math_x3() && a.c % 16 == 0 && halo16_pick(a, halo_eligible(a), &bm, &tw) != 0;
+    return math_split(a.math) && a.c % 16 == 0 && halo16_pick(a, halo_eligible(a), &bm, &tw) != 0;
 }
 
 bool igemm_takes_c16(const IgemmArgs &a0) {
     int bm = 0, tw = 0;
     const IgemmArgs a = x3_view(a0);
-    return conv_math_x3() && halo16_c16_pick(a, halo_eligible(a), &bm, &tw) != 0;
+    return math_split(a.math) && halo16_c16_pick(a, halo_eligible(a), &bm, &tw) != 0;
 }
 
 int halo_stat_tiles(const IgemmArgs &a0, int *tile_pixels) {
     int bm = 0, tw = 0;
     const IgemmArgs a = x3_view(a0);
-    if (!conv_math_x3()) return 0;
+    if (!math_split(a.math)) return 0;
     if (!halo16_pick(a, halo_eligible(a), &bm, &tw) && !halo16_c16_pick(a, halo_eligible(a), &bm, &tw) &&
         !halo_pick(a, &bm, &tw))
         return 0;
@@ -634,16 +630,14 @@ bool launch_igemm_x3(const IgemmArgs &a0, hipStream_t s) {
         case 3: launch_halo<4, 1, 2, 1>(a, tw, s); return true;
         default: break;
     }
-    // SCD_X3_TILE (tile study, tools/perf_convT.py): 1 128x128, 2 256x64, 3 256x32, 4 128x64, 5 256x128
-    if (const char *t = getenv("SCD_X3_TILE")) {
-        switch (t[0]) {
-            case '1': launch_x3<2, 2, 2, 2>(a, s); return true;
-            case '2': launch_x3<4, 1, 2, 2>(a, s); return true;
-            case '3': launch_x3<4, 1, 2, 1>(a, s); return true;
-            case '4': launch_x3<2, 2, 2, 1>(a, s); return true;
-            case '5': launch_x3<4, 2, 2, 2>(a, s); return true;
-            default: break;
-        }
+    // SCD_TUNE_X3_TILE (tile study, tools/perf_convT.py): 1 128x128, 2 256x64, 3 256x32, 4 128x64, 5 256x128
+    switch ((a.tune & SCD_TUNE_X3_TILE_MASK) >> 12) {
+        case 1: launch_x3<2, 2, 2, 2>(a, s); return true;
+        case 2: launch_x3<4, 1, 2, 2>(a, s); return true;
+        case 3: launch_x3<4, 1, 2, 1>(a, s); return true;
+        case 4: launch_x3<2, 2, 2, 1>(a, s); return true;
+        case 5: launch_x3<4, 2, 2, 2>(a, s); return true;
+        default: break;
     }
     if (a.n_out >= 128)
         launch_x3<2, 2, 2, 2>(a, s);  // 128 x 128
@@ -924,209 +918,6 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
     }
 }
 
-template <int S, int T, int RS, int PA, int PB, int HW_>
-__device__ __forceinline__ void halo_read_b(s16x4 (&f)[6], uint32_t bbase) {
-    constexpr int hr = (S + 1 + (T / 3 - 1)) * HW_ + 1 + (T % 3 - 1);
-    tr_read<0 * PB + hr * RS>(f[0], bbase);
-    tr_read<0 * PB + (hr + 4) * RS>(f[1], bbase);
-    tr_read<1 * PB + hr * RS>(f[2], bbase);
-    tr_read<1 * PB + (hr + 4) * RS>(f[3], bbase);
-    tr_read<2 * PB + hr * RS>(f[4], bbase);
-    tr_read<2 * PB + (hr + 4) * RS>(f[5], bbase);
-}
-
-
-// One tap: wait for its fragments (older reads retire first), then the six split products.
-template <int T, int WAIT>
-__device__ __forceinline__ void halo_tap(f32x16 (&acc)[9], bf16x8 (&av)[3], s16x4 (&f)[6]) {
-    bf16x8 b0 = cat8(f[0], f[1]), b1 = cat8(f[2], f[3]), b2 = cat8(f[4], f[5]);
-    lds_wait<WAIT>(b0, b1, b2);
-    if (T == 0) lds_wait<WAIT>(av[0], av[1], av[2]);
-    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], b1, acc[T], 0, 0, 0);
-    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], b2, acc[T], 0, 0, 0);
-    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], b0, acc[T], 0, 0, 0);
-    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], b1, acc[T], 0, 0, 0);
-    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], b0, acc[T], 0, 0, 0);
-    acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], b0, acc[T], 0, 0, 0);
-}
-
-template <int S, int RS, int PA, int PB, int HW_>
-__device__ __forceinline__ void halo_substep(f32x16 (&acc)[9], uint32_t abase, uint32_t bbase) {
-    s16x4 fa[6];
-    tr_read<0 * PA + (S * 16) * RS>(fa[0], abase);
-    tr_read<0 * PA + (S * 16 + 4) * RS>(fa[1], abase);
-    tr_read<1 * PA + (S * 16) * RS>(fa[2], abase);
-    tr_read<1 * PA + (S * 16 + 4) * RS>(fa[3], abase);
-    tr_read<2 * PA + (S * 16) * RS>(fa[4], abase);
-    tr_read<2 * PA + (S * 16 + 4) * RS>(fa[5], abase);
-    bf16x8 av[3] = {cat8(fa[0], fa[1]), cat8(fa[2], fa[3]), cat8(fa[4], fa[5])};
-    // B fragments one tap ahead: while tap t's MFMAs run, tap t+1's six reads are in flight
-    s16x4 f0[6], f1[6];
-    halo_read_b<S, 0, RS, PA, PB, HW_>(f0, bbase);
-    halo_read_b<S, 1, RS, PA, PB, HW_>(f1, bbase);
-    halo_tap<0, 6>(acc, av, f0);
-    halo_read_b<S, 2, RS, PA, PB, HW_>(f0, bbase);
-    halo_tap<1, 6>(acc, av, f1);
-    halo_read_b<S, 3, RS, PA, PB, HW_>(f1, bbase);
-    halo_tap<2, 6>(acc, av, f0);
-    halo_read_b<S, 4, RS, PA, PB, HW_>(f0, bbase);
-    halo_tap<3, 6>(acc, av, f1);
-    halo_read_b<S, 5, RS, PA, PB, HW_>(f1, bbase);
-    halo_tap<4, 6>(acc, av, f0);
-    halo_read_b<S, 6, RS, PA, PB, HW_>(f0, bbase);
-    halo_tap<5, 6>(acc, av, f1);
-    halo_read_b<S, 7, RS, PA, PB, HW_>(f1, bbase);
-    halo_tap<6, 6>(acc, av, f0);
-    halo_read_b<S, 8, RS, PA, PB, HW_>(f0, bbase);
-    halo_tap<7, 6>(acc, av, f1);
-    halo_tap<8, 0>(acc, av, f0);
-}
-
-template <int RS, int PA, int PB, int HW_>
-__device__ __forceinline__ void wgrad_halo_patch(f32x16 (&acc)[9], uint32_t abase, uint32_t bbase) {
-    halo_substep<0, RS, PA, PB, HW_>(acc, abase, bbase);
-    halo_substep<1, RS, PA, PB, HW_>(acc, abase, bbase);
-}
-
-
-// ------------------------------------------------------------------------------------------------
-// Halo weight gradient for 3x3 / stride 1 / same-size convs.
-//   dW[r][t][c] = sum_p dY[p][r] * X[p + off_t][c]
-// A block owns 64 rows r x 64 channels c x all 9 taps (36 tiles of 32x32; wave w keeps rows
-// 32*(w>>1) and channels 32*(w&1), 9 taps = 144 accumulator registers).  It walks a range of 2x16-pixel
-// patches of the image batch (split-K over patches).  Per patch it stages two things once, split into
-// their three bf16 planes:
-//   - the dY patch, 32 px x 64 rows;
-//   - the X halo, 4 x 18 px x 64 channels.
-// All 9 taps then read shifted halo rows with ds_read_b64_tr_b16 (every lane supplies its own row
-// address, so the shift is free).  The per-tap path stages and splits X once per tap column tile.
-// LDS is single-buffered: the next patch is prefetched into registers during the MFMAs and stored between
-// two barriers.  Slab layout and reduction are those of wgrad_x3.
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void wgrad_halo_x3(WgradArgs a) {
-    constexpr int BR = 64, BC = 64, PH = 2, PW = 16, P = PH * PW;
-    constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
-    constexpr int RS = tr_stride(64);                  // 192-byte rows (= 64 mod 128: conflict-free tr reads)
-    constexpr int PA = P * RS, PB = HP * RS;           // plane bytes
-    constexpr int A_CH = P * 16, B_CH = HP * 16;       // 4-channel chunks
-    constexpr int A_PER = A_CH / 256, B_PER = (B_CH + 255) / 256;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[3 * PA + 3 * PB];
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wi = wid >> 1, wj = wid & 1;
-    const uint32_t per_split = uint32_t(a.grid_r * a.grid_j);
-    const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int split = int(L / per_split);
-    const int rem = int(L - uint32_t(split) * per_split);
-    const int ct = rem / a.grid_r;
-    const int r0 = (rem - ct * a.grid_r) * BR, c0 = ct * BC;
-    const int pw_n = a.wo / PW, ph_n = a.ho / PH, pimg = pw_n * ph_n;
-    const int npatch = a.n_img_w * pimg;
-    const int pbeg = split * a.kchunk, pend = min(npatch, pbeg + a.kchunk);
-
-    const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
-    const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
-
-    // staging roles are recomputed from tid where used (cheap shifts / constant divisions) to keep the
-    // register budget for the 144 accumulators; R and C are host-checked multiples of 64.
-    f32x4 ra[A_PER], rb[B_PER];
-    auto load_patch = [&](int pi) {
-        const int img = pi / pimg, pr = pi - img * pimg;
-        const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
-#pragma unroll
-        for (int i = 0; i < A_PER; ++i) {
-            const int e = tid + i * 256, q = e >> 4, cq = e & 15;
-            const int py = q >> 4, px = q & 15;
-            const uint32_t off = uint32_t(((img * a.ho + y0 + py) * a.wo + x0 + px) * a.ldc_r + r0 + cq * 4) * 4u;
-            ra[i] = bload4(rs_rows, off);
-        }
-#pragma unroll
-        for (int i = 0; i < B_PER; ++i) {
-            const int e = tid + i * 256, hp = e >> 4, cq = e & 15;
-            const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
-            const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
-            const bool v = e < B_CH && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
-            rb[i] = bload4(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + cq * 4) * 4u
-                                     : kOOB);
-        }
-    };
-    auto store_patch = [&]() {
-#pragma unroll
-        for (int i = 0; i < A_PER; ++i) {
-            u32x2 h, m, l;
-            split3(ra[i], h, m, l);
-            const int e = tid + i * 256;
-            const int o = (e >> 4) * RS + (e & 15) * 8;
-            *reinterpret_cast<u32x2 *>(smem + o) = h;
-            *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
-            *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
-        }
-#pragma unroll
-        for (int i = 0; i < B_PER; ++i)
-            if (tid + i * 256 < B_CH) {
-                u32x2 h, m, l;
-                split3(rb[i], h, m, l);
-                const int e = tid + i * 256;
-                const int o = 3 * PA + (e >> 4) * RS + (e & 15) * 8;
-                *reinterpret_cast<u32x2 *>(smem + o) = h;
-                *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
-                *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
-            }
-    };
-
-    f32x16 acc[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-    // transposed-read lane roles: 16-lane group g reads pixel rows trk (+4), channel columns trc..trc+3
-    const int g = lane >> 4, w16 = lane & 15;
-    const int trk = 8 * (g >> 1) + (w16 >> 2);
-    const int trc = 16 * (g & 1) + 4 * (w16 & 3);
-    // one base address per operand; every (sub-step, tap, plane, +4 rows) read is an immediate offset from it
-    // (taps are the standard 3x3 order t = 3*(dy+1) + (dx+1), host-checked)
-    const uint32_t abase = lds_addr(smem) + trk * RS + (32 * wi + trc) * 2;
-    const uint32_t bbase = lds_addr(smem) + 3 * PA + trk * RS + (32 * wj + trc) * 2;
-
-    if (pbeg < pend) {
-        load_patch(pbeg);
-        store_patch();
-        __syncthreads();
-        for (int pi = pbeg; pi < pend; ++pi) {
-            const bool more = pi + 1 < pend;
-            if (more) load_patch(pi + 1);
-            wgrad_halo_patch<RS, PA, PB, HW_>(acc, abase, bbase);
-            if (more) {
-                __syncthreads();  // every wave is done with this patch
-                store_patch();
-                __syncthreads();
-            }
-        }
-    }
-
-    float *slab = a.slabs + size_t(split) * a.R * a.Ng;
-    const int col = c0 + 32 * wj + (lane & 31);
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = r0 + 32 * wi + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            gstore1(slab + size_t(row) * a.Ng + t * a.C + col, acc[t][r]);
-        }
-}
-
-const void *wgrad_halo_fn(bool bounded, int rblock) {
-    return wgrad16_mode() ? wgrad_halo16_fn(bounded, rblock) : reinterpret_cast<const void *>(&wgrad_halo_x3);
-}
-int wgrad_halo_rblock(int R, bool bounded) { return wgrad16_mode() ? wgrad16_rblock(R, bounded) : 64; }
-
-void launch_wgrad_halo_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    if (wgrad16_mode())
-        launch_wgrad_halo16_x3(a, grid, s);
-    else
-        hipLaunchKernelGGL(wgrad_halo_x3, grid, dim3(256), 0, s, a);
-}
 
 const void *wgrad_x3_fn(int tile_id) {
     switch (tile_id) {
@@ -1323,7 +1114,7 @@ extern "C" int scd_pack_conv3x3_multi(const scd_pack_job_t *jobs, int32_t n, scd
         for (int i = 0; i < pj.n; ++i) {
             const scd_pack_job_t &J = jobs[base + i];
             const int rows = J.mode == 0 ? J.co : J.ci, K = 9 * (J.mode == 0 ? J.ci_pad : J.co);
-            pj.h2[i] = J.split && h2_weight_format(9, K / 9);
+            pj.h2[i] = J.split && h2_weight_format(J.math, 9, K / 9);
             pj.first_row[i + 1] = pj.first_row[i] + (pj.h2[i] ? (rows + 31) / 32 * 32 : 0);
             if (!J.w || !J.out || J.co < 1 || J.ci < 1 || J.ci_pad < J.ci || (J.mode != 0 && J.mode != 1) ||
                 (J.split && (K % 16 || !aligned16(J.split)))) {

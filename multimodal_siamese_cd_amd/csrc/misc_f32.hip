@@ -510,7 +510,7 @@ __global__ void pjaccard_bwd_kernel(const float *__restrict__ logits, const floa
 using namespace scd;
 
 // ------------------------------------------------------------------------------------------------
-extern "C" const char *scd_version(void) { return "libscd 0.1.0 (gfx950, fp32 MFMA implicit-GEMM)"; }
+extern "C" const char *scd_version(void) { return "libscd 0.3.0 (gfx950, ABI 3: per-descriptor conv arithmetic)"; }
 extern "C" const char *scd_last_error(void) { return g_err.c_str(); }
 
 extern "C" int scd_device_check(int device) {

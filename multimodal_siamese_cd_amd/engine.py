@@ -570,6 +570,7 @@ class EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, meta, *params):
         ctx.set_materialize_grads(False)
+        meta.scope = (hip.conv_math(), hip.conv_tune())
         blocks = meta.blocks
         feats, saved = [], []
         cur = x
@@ -593,6 +594,11 @@ class EncoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *g_feats):
+        with hip.conv_scope(*ctx.meta.scope):
+            return EncoderFn._backward(ctx, *g_feats)
+
+    @staticmethod
+    def _backward(ctx, *g_feats):
         meta, saved = ctx.meta, ctx.saved
         blocks = meta.blocks
         L = len(blocks) - 1
@@ -650,6 +656,7 @@ class SiameseEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, meta, *params):
         ctx.set_materialize_grads(False)
+        meta.scope = (hip.conv_math(), hip.conv_tune())
         blocks = meta.blocks
         diffs, saved, bufs = [], [], []
         cur = x
@@ -694,6 +701,11 @@ class SiameseEncoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *g_diffs):
+        with hip.conv_scope(*ctx.meta.scope):
+            return SiameseEncoderFn._backward(ctx, *g_diffs)
+
+    @staticmethod
+    def _backward(ctx, *g_diffs):
         meta, saved = ctx.meta, ctx.saved
         blocks = meta.blocks
         L = len(blocks) - 1
@@ -766,6 +778,7 @@ class DecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, x_deep, *rest):
         ctx.set_materialize_grads(False)
+        meta.scope = (hip.conv_math(), hip.conv_tune())
         ups = meta.ups
         skips = rest[:len(ups)]
         cur = x_deep
@@ -790,19 +803,27 @@ class DecoderFn(torch.autograd.Function):
                 cat = _empty((b, h, w, cs + cto), skip)
                 hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
             wT = hip.pack_convT2x2(convT.weight.detach(), 0)
-            # h2: the concat's bound is the skip's, raised in place by the ConvT epilogue to max |up| (still a
-            # bound of the skip; F.pad's zero border adds nothing); the ConvT reads cur through cur's bound
+            # h2: the concat's own bound, seeded with the skip's and raised by the ConvT epilogue to max |up| (F.pad's
+            # zero border adds nothing); the skip's bound, also read by the encoder's weight grads, stays as it is.
+            # The ConvT reads cur through cur's bound.
             cur_bound = _bound_of(cur, pool)
-            cat_bound = _bound_of(skip, pool) if pool is not None else None
+            cat_bound = None
+            if pool is not None:
+                cat_bound = pool.take()
+                cat_bound.copy_(_bound_of(skip, pool))
+            # the ConvT epilogue raises a bound on the split kernels only (src.c % 16 == 0); else one absmax pass
+            epi_bound = cat_bound if hip.conv_math() != 'f32' and cu % 16 == 0 else None
             if pad_y or pad_x:
                 # ConvT into its own map, then F.pad's zero border and placement in one window copy
                 upm = _empty((b, 2 * hc, 2 * wc, cto), skip)
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(upm), store_mode=1,
-                               src_bound=cur_bound, dst_bound=cat_bound)
+                               src_bound=cur_bound, dst_bound=epi_bound)
                 hip.window_copy(nhwc(upm), nhwc(cat, cs, cto), -(pad_y // 2), -(pad_x // 2))
             else:
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto),
-                               store_mode=1, src_bound=cur_bound, dst_bound=cat_bound)
+                               store_mode=1, src_bound=cur_bound, dst_bound=epi_bound)
+            if cat_bound is not None and epi_bound is None:
+                hip.absmax_bound(nhwc(cat, cs, cto), cat_bound)
             a, sv, y1, st1, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save, materialize=not last_into_head,
                                             pool=pool, x_bound=cat_bound)
             saved.append((cur, cat, cs, sv, cur_bound))
@@ -824,6 +845,11 @@ class DecoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_out):
+        with hip.conv_scope(*ctx.meta.scope):
+            return DecoderFn._backward(ctx, g_out)
+
+    @staticmethod
+    def _backward(ctx, g_out):
         meta, saved = ctx.meta, ctx.saved
         ups = meta.ups
         n = len(ups)
@@ -894,9 +920,14 @@ def run_decoder(decoder, features: list, training: bool, cat_buffers: list | Non
     the head reading the last BatchNorm + ReLU through its coefficients (scd_conv1x1_fwd_bn) and its backward
     feeding that BatchNorm's backward directly (scd_bn_relu_backward_head); results are bit-identical to
     run_head(head, run_decoder(...))."""
-    if head is not None and not _OPTS['fuse_head']:
-        return run_head(head, run_decoder(decoder, features, training, cat_buffers))
-    ups = list(decoder.up_seq.values())
+    return run_ups(list(decoder.up_seq.values()), features, training, cat_buffers, head)
+
+
+def run_ups(ups: list, features: list, training: bool, cat_buffers: list | None = None, head=None) -> torch.Tensor:
+    """Up blocks in sequence (Decoder.forward, networks.py:375-382): features[0] is the deepest map, features[1 + k]
+    the skip of ups[k]."""
+    if head is not None and (not _OPTS['fuse_head'] or head.conv.out_channels > 4):
+        return run_head(head, run_ups(ups, features, training, cat_buffers))
     params = [p for up in ups for p in up_params(up)]
     if head is not None:
         params += [head.conv.weight, head.conv.bias]
@@ -940,7 +971,89 @@ class HeadFn(torch.autograd.Function):
 
 
 def run_head(outc, x: torch.Tensor) -> torch.Tensor:
-    return HeadFn.apply(x, outc.conv.weight, outc.conv.bias)
+    """OutConv (networks.py:454-461) of an NHWC activation -> NCHW logits.  The 1x1 kernel takes up to 4 output
+    channels per launch and channel counts in multiples of 4: wider heads run in groups of 4 outputs, and a source
+    whose channels are not a multiple of 4 is zero-padded with its weight (both differentiable: the padding's
+    gradient is dropped)."""
+    w, b = outc.conv.weight, outc.conv.bias
+    c = x.shape[3]
+    if c % 4:
+        cp = (c + 3) // 4 * 4
+        x = torch.nn.functional.pad(x, (0, cp - c))
+        w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, cp - c))
+    n_out = w.shape[0]
+    if n_out <= 4:
+        return HeadFn.apply(x, w, b)
+    outs = [HeadFn.apply(x, w[i:i + 4], None if b is None else b[i:i + 4]) for i in range(0, n_out, 4)]
+    return torch.cat(outs, dim=1)
+
+
+# ------------------------------------------------------------------------------------------------
+# Standalone building blocks (DoubleConv / InConv / Down, networks.py:386-426) for callers that use a block on its
+# own (e.g. assessment_semantics.py:34 calls net.outc_sem_change directly).  The model forwards do not come here:
+# they run whole stages (EncoderFn, SiameseEncoderFn, DecoderFn).
+# ------------------------------------------------------------------------------------------------
+def to_nhwc(x: torch.Tensor, c_pad: int | None = None) -> torch.Tensor:
+    """NCHW -> contiguous NHWC fp32 (zero channels up to c_pad), differentiable."""
+    hip.ensure_device(x)
+    if x.dim() != 4:
+        raise ValueError(f"expected a (B, C, H, W) tensor, got {tuple(x.shape)}")
+    y = x.float().permute(0, 2, 3, 1)
+    if c_pad is not None and c_pad > y.shape[3]:
+        y = torch.nn.functional.pad(y, (0, c_pad - y.shape[3]))
+    return y.contiguous()
+
+
+def to_nchw(y: torch.Tensor) -> torch.Tensor:
+    return y.permute(0, 3, 1, 2).contiguous()
+
+
+class BlockFn(torch.autograd.Function):
+    """One DoubleConv on an NHWC batch (one BatchNorm segment), optionally behind MaxPool2d(2) (Down)."""
+
+    @staticmethod
+    def forward(ctx, x, meta, *params):
+        ctx.set_materialize_grads(False)
+        meta.scope = (hip.conv_math(), hip.conv_tune())
+        pool = _bounds(x)
+        cur, idx = x, None
+        if meta.maxpool:
+            n, h, w, c = x.shape
+            cur = _empty((n, h // 2, w // 2, c), x)
+            idx = _empty((n, h // 2, w // 2, c), x, dtype=torch.uint8)
+            hip.maxpool2_fwd(nhwc(x), nhwc(cur), idx)
+        a, sv, _, _, _ = _dc_forward(cur, meta.dc, 1, meta.training, meta.save, pool=pool)
+        if meta.save:
+            ctx.meta, ctx.saved = meta, (idx, sv, tuple(x.shape))
+        return a
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is None:
+            return (None, None) + (None,) * 8
+        meta = ctx.meta
+        with hip.conv_scope(*meta.scope):
+            idx, sv, xshape = ctx.saved
+            need_dx = ctx.needs_input_grad[0]
+            gx, pg = _dc_backward(g.contiguous(), sv, meta.dc, need_dx=need_dx, pool=_bounds(g))
+            if need_dx and meta.maxpool:  # MaxPool2d backward through the argmax bytes
+                gfull = _empty(xshape, g)
+                hip.feature_grad(nhwc(gx), idx, hip._NULL, 0, nhwc(gfull))
+                gx = gfull
+        ctx.saved = None
+        return (gx, None, *pg)
+
+
+def run_block(dc, x: torch.Tensor, training: bool, maxpool: bool = False) -> torch.Tensor:
+    """DoubleConv `dc` (networks.py:386-402) of an NHWC batch, after MaxPool2d(2) when `maxpool` (Down,
+    networks.py:415-426); NHWC out."""
+    params = dc_params(dc)
+    save = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
+    meta = _Meta(dc=dc, training=training, save=save, maxpool=maxpool)
+    try:
+        return BlockFn.apply(x, meta, *params)
+    finally:
+        flush_bn_counters()
 
 
 # ------------------------------------------------------------------------------------------------

@@ -6,9 +6,11 @@ is no fallback: if the library is missing or the device is not gfx950 the first 
 """
 from __future__ import annotations
 
+import contextlib
+import contextvars
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_float, c_int, c_int8, c_int32, c_int64, c_size_t, c_uint8, c_void_p
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int8, c_int32, c_int64, c_size_t, c_uint8, c_uint32, c_void_p
 
 import torch
 
@@ -50,6 +52,8 @@ class IGEMM(ctypes.Structure):
         ("bn_bwd", POINTER(BNBWD)),
         ("src_bound", c_void_p),
         ("dst_bound", c_void_p),
+        ("math", c_int32),
+        ("tune", c_uint32),
     ]
 
 
@@ -74,6 +78,8 @@ class WGRAD(ctypes.Structure):
         ("rows_scale", c_void_p),
         ("rows_shift", c_void_p),
         ("rows_coef", c_void_p),
+        ("math", c_int32),
+        ("tune", c_uint32),
     ]
 
 
@@ -89,15 +95,13 @@ _dev_checked: set = set()
 
 _SIGS = {
     "scd_version": ([], c_char_p),
+    "scd_abi_version": ([], c_int),
     "scd_last_error": ([], c_char_p),
     "scd_device_check": ([c_int], c_int),
     "scd_pack_nchw": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, NHWC, c_void_p], c_int),
     "scd_pack_conv3x3": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_pack_conv3x3_multi": ([c_void_p, c_int32, c_void_p], c_int),
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
-    "scd_set_conv_math": ([c_int32], c_int),
-    "scd_set_halo16": ([c_int32], c_int),
-    "scd_set_wgrad16": ([c_int32], c_int),
     "scd_split_bf16x3": ([c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "scd_split_frag_bytes": ([c_int32, c_int32], c_size_t),
     "scd_split_bf16x3_frag": ([c_void_p, c_int32, c_int32, c_void_p, c_void_p], c_int),
@@ -183,6 +187,7 @@ _SIGS = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
+ABI_VERSION = 3  # SCD_ABI_VERSION of include/scd.h
 
 
 def load_library(path: str = LIB_PATH):
@@ -196,6 +201,11 @@ def load_library(path: str = LIB_PATH):
             "(hipcc --offload-arch=gfx950). There is no CPU fallback."
         )
     lib = ctypes.CDLL(path)
+    abi = getattr(lib, 'scd_abi_version', None)
+    got = abi() if abi is not None else None
+    if got != ABI_VERSION:
+        raise RuntimeError(f"{path}: libscd ABI {got}, this binding needs ABI {ABI_VERSION} (rebuild: "
+                           "`python -c 'import __graft_entry__ as g; g.build()'`)")
     for name, (argtypes, restype) in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
@@ -285,7 +295,7 @@ def pack_conv3x3(w: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch
 
 class PACKJOB(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("out", c_void_p), ("split", c_void_p), ("co", c_int32), ("ci", c_int32),
-                ("ci_pad", c_int32), ("mode", c_int32)]
+                ("ci_pad", c_int32), ("mode", c_int32), ("math", c_int32)]
 
 
 def pack_conv3x3_multi(jobs) -> list:
@@ -294,6 +304,7 @@ def pack_conv3x3_multi(jobs) -> list:
     if not jobs:
         return []
     split = conv_math() != 'f32'
+    m = _MATH_NAMES[conv_math()]
     outs, keep, arr = [], [], (PACKJOB * len(jobs))()
     for i, (w, mode, ci_pad) in enumerate(jobs):
         co, ci = w.shape[0], w.shape[1]
@@ -305,7 +316,7 @@ def pack_conv3x3_multi(jobs) -> list:
             sp = torch.empty(lib().scd_split_frag_bytes(rows, K) // 2, dtype=torch.int16, device=w.device)
             out._x3 = sp
         keep.append(w)
-        arr[i] = PACKJOB(w.data_ptr(), out.data_ptr(), _ptr(sp), co, ci, ci_pad, mode)
+        arr[i] = PACKJOB(w.data_ptr(), out.data_ptr(), _ptr(sp), co, ci, ci_pad, mode, m)
         outs.append(out)
     _check(lib().scd_pack_conv3x3_multi(ctypes.cast(arr, c_void_p), len(jobs), _stream()), "scd_pack_conv3x3_multi")
     return outs
@@ -359,42 +370,116 @@ def _attach_split(wpk: torch.Tensor, n_out: int, K: int, ntaps: int) -> torch.Te
 
 MATH_F32, MATH_X3, MATH_BF16, MATH_X5, MATH_H2 = 0, 1, 2, 3, 4
 _MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3, 'bf16': MATH_BF16, 'x5': MATH_X5, 'h2': MATH_H2}
+_MATH_BY_ID = {v: k for k, v in _MATH_NAMES.items()}
+
+# SCD_TUNE_* kernel-variant bits (include/scd.h): 0 = the library's measured defaults.
+TUNE_HALO16_OFF = 0xF
+TUNE_H2_TILE_2X2 = 1 << 4
+TUNE_H2_TILE64_2X2 = 1 << 5
+TUNE_H2_NO_PRESCALE = 1 << 6
+TUNE_NO_XCD_REMAP = 1 << 7
+TUNE_HALO_ORDER_M = 1 << 8
+TUNE_W16_LAYOUT_2X2 = 1 << 9
+TUNE_WGRAD_R64 = 1 << 10
+TUNE_HALO16_DB_OFF = 1 << 20
+TUNE_HALO16_DB_ON = 1 << 21
+TUNE_NO_GATHER16 = 1 << 22
+TUNE_NO_WGRAD_C16 = 1 << 23
+TUNE_NO_WGRAD_H2 = 1 << 24
+TUNE_NO_HALO16_C16 = 1 << 25
+TUNE_NO_HALO = 1 << 26
 
 
-def set_conv_math(mode) -> str:
-    """Select the conv arithmetic ('f32' = fp32 MFMA, 'x3' = exact 3-way split-bf16 MFMA, 'bf16' = bf16 operands
-    with fp32 accumulation in the halo kernels); returns the previous."""
-    m = _MATH_NAMES[mode] if isinstance(mode, str) else int(mode)
-    rc = lib().scd_set_conv_math(m)
-    if rc < 0:
-        _check(rc, "scd_set_conv_math")
-    return {v: k for k, v in _MATH_NAMES.items()}[rc]
+def tune_halo16_cfg(tile_id: int) -> int:
+    return tile_id + 1
 
 
-def set_halo16(mode: int) -> int:
-    """Tile selection of the 16x16x32-MFMA halo conv kernel (see scd.h); returns the previous mode."""
-    rc = lib().scd_set_halo16(int(mode))
-    if rc < 0:
-        _check(rc, "scd_set_halo16")
-    return rc
+def tune_x3_tile(t: int) -> int:
+    return (t & 15) << 12
 
 
-def halo16_tile_width_pref() -> int:
-    """The tile width the 16x16x32 halo kernel tries first (mirrors halo16_pick in conv_halo16.hip)."""
-    return int(os.environ.get('SCD_HALO16_TW', '16'))
+def tune_c16_tiles(k: int) -> int:
+    return (k & 15) << 16
 
 
-def set_wgrad16(mode: int) -> int:
-    """Halo weight-grad kernel selection (0 = 32x32x16 MFMA, 1 = 16x16x32 MFMA); returns the previous mode."""
-    rc = lib().scd_set_wgrad16(int(mode))
-    if rc < 0:
-        _check(rc, "scd_set_wgrad16")
-    return rc
+# The arithmetic and kernel-variant bits every conv descriptor is built with.  libscd keeps no mode: these are
+# host-side values stamped into each scd_igemm_t / scd_wgrad_t / scd_pack_job_t.  A model carries its own
+# arithmetic (utils.networks.create_network: MODEL.PRECISION / CONV_MATH) and runs its forward and backward inside
+# conv_scope(model math); code outside any scope (kernel tests, tools) uses the process default.
+_DEFAULT = {'math': MATH_X3, 'tune': 0}
+_SCOPE: contextvars.ContextVar = contextvars.ContextVar('scd_conv_scope', default=None)
+
+
+def _cur():
+    sc = _SCOPE.get()
+    return sc if sc is not None else (_DEFAULT['math'], _DEFAULT['tune'])
+
+
+def _math_id(mode) -> int:
+    if isinstance(mode, str):
+        if mode not in _MATH_NAMES:
+            raise ValueError(f"conv arithmetic {mode!r}: expected one of {sorted(_MATH_NAMES)}")
+        return _MATH_NAMES[mode]
+    m = int(mode)
+    if m not in _MATH_BY_ID:
+        raise ValueError(f"conv arithmetic {mode!r}")
+    return m
 
 
 def conv_math() -> str:
-    rc = lib().scd_set_conv_math(-1)
-    return {v: k for k, v in _MATH_NAMES.items()}[rc]
+    """The arithmetic of descriptors built now: the innermost conv_scope's, else the process default."""
+    return _MATH_BY_ID[_cur()[0]]
+
+
+def conv_tune() -> int:
+    return _cur()[1]
+
+
+@contextlib.contextmanager
+def conv_scope(math=None, tune=None):
+    """Build every conv descriptor inside with this arithmetic ('f32', 'x3', 'x5', 'bf16', 'h2') and tune bits
+    (None: inherit the enclosing value).  Context-local, so models with different arithmetic coexist."""
+    m0, t0 = _cur()
+    tok = _SCOPE.set((m0 if math is None else _math_id(math), t0 if tune is None else int(tune)))
+    try:
+        yield
+    finally:
+        _SCOPE.reset(tok)
+
+
+def set_conv_math(mode) -> str:
+    """Set the process-default arithmetic for descriptors built outside any conv_scope ('f32' = fp32 MFMA, 'x3' =
+    exact 3-way split-bf16 MFMA, 'x5', 'bf16', 'h2'); returns the previous default."""
+    prev = _MATH_BY_ID[_DEFAULT['math']]
+    _DEFAULT['math'] = _math_id(mode)
+    return prev
+
+
+def set_tune(bits: int) -> int:
+    """Set the process-default SCD_TUNE_* bits (kernel variants for tests / A/B); returns the previous default."""
+    prev = _DEFAULT['tune']
+    _DEFAULT['tune'] = int(bits)
+    return prev
+
+
+def get_tune() -> int:
+    return _DEFAULT['tune']
+
+
+def set_halo16(mode: int) -> int:
+    """Tile selection of the 16x16x32-MFMA halo conv kernel through the default tune bits: 0 = off (32x32x16 halo
+    kernel), 1 = automatic, 2 + id = force tile id.  Returns the previous mode."""
+    t = _DEFAULT['tune']
+    v = t & 0xF
+    prev = 0 if v == TUNE_HALO16_OFF else 1 if v == 0 else v + 1
+    new = TUNE_HALO16_OFF if mode == 0 else 0 if mode == 1 else tune_halo16_cfg(int(mode) - 2)
+    _DEFAULT['tune'] = (t & ~0xF) | new
+    return prev
+
+
+def halo16_tile_width_pref() -> int:
+    """The tile width the 16x16x32 halo kernel tries first (halo16_pick in conv_halo16.hip)."""
+    return 16
 
 
 def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None, in_bn=None,
@@ -405,9 +490,10 @@ def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mo
     if bn_bwd is not None:  # (y, nseg, save_mean, save_invstd, scale, shift, rec)
         y, bseg, mu, iv, bsc, bsh, rec = bn_bwd
         bb = ctypes.pointer(BNBWD(nhwc(y), bseg, _ptr(mu), _ptr(iv), _ptr(bsc), _ptr(bsh), _ptr(rec)))
+    m, t = _cur()
     return IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
                  _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg, bb, _ptr(src_bound),
-                 _ptr(dst_bound))
+                 _ptr(dst_bound), m, t)
 
 
 def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
@@ -434,19 +520,19 @@ def igemm_bn_bwd_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk
 
 def igemm_arith(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
                 dst: NHWC, store_mode: int = 0, src_bound=None) -> str:
-    """The arithmetic ('f32', 'x3', 'x5', 'bf16', 'h2') scd_conv_igemm would use for this conv under the current
-    mode."""
+    """The arithmetic ('f32', 'x3', 'x5', 'bf16', 'h2') scd_conv_igemm will use for this conv (descriptor built with
+    the current conv_math())."""
     d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, None, dst, store_mode, src_bound=src_bound)
     rc = lib().scd_igemm_arith(ctypes.byref(d))
     _check(min(rc, 0), "scd_igemm_arith")
-    return {v: k for k, v in _MATH_NAMES.items()}[rc]
+    return _MATH_BY_ID[rc]
 
 
 def wgrad_arith(d: 'WGRAD') -> str:
-    """The arithmetic scd_conv_wgrad would use for this descriptor under the current mode."""
+    """The arithmetic scd_conv_wgrad will use for this descriptor."""
     rc = lib().scd_wgrad_arith(ctypes.byref(d))
     _check(min(rc, 0), "scd_wgrad_arith")
-    return {v: k for k, v in _MATH_NAMES.items()}[rc]
+    return _MATH_BY_ID[rc]
 
 
 def wgrad_rows_per_block(d: 'WGRAD') -> int:
@@ -471,6 +557,15 @@ def igemm_stat_tiles(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: 
     return (n, tp.value) if n > 0 else (0, 0)
 
 
+def wgrad_desc(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None, rows_bound=None, src_bound=None) -> 'WGRAD':
+    """An scd_wgrad_t stamped with the current arithmetic and tune bits."""
+    nt, dy, dx = _taps(taps)
+    sc, sh, nseg = src_bn if src_bn is not None else (None, None, 0)
+    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg, _ptr(rows_bound), _ptr(src_bound))
+    d.math, d.tune = _cur()
+    return d
+
+
 def _rows_bn_fields(d: 'WGRAD', rows_bn):
     """rows_bn = (y NHWC, nseg, save_mean, save_invstd, gamma or None, scale, shift, coef): the rows are dL/da and
     the kernel forms dy through the BatchNorm backward while staging (scd_wgrad_t.rows_y)."""
@@ -486,9 +581,7 @@ def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None, rows_bound
     """`src_bn` = (scale, shift, nseg): read src through its BatchNorm-apply + ReLU (see scd_wgrad_t).
     `rows_bound` / `src_bound`: device floats bounding |rows| and |src as read| (SCD_MATH_H2; both or neither).
     `rows_bn`: see _rows_bn_fields (only where wgrad_rows_bn_supported)."""
-    nt, dy, dx = _taps(taps)
-    sc, sh, nseg = src_bn if src_bn is not None else (None, None, 0)
-    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg, _ptr(rows_bound), _ptr(src_bound))
+    d = wgrad_desc(rows, src, stride, taps, src_bn, rows_bound, src_bound)
     if rows_bn is not None:
         _rows_bn_fields(d, rows_bn)
     d._keep = (rows_bound, src_bound, rows_bn)
@@ -499,16 +592,13 @@ def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None, rows_bound
 
 
 def wgrad_src_bn_supported(rows: NHWC, src: NHWC, stride: int, taps, src_bn) -> bool:
-    nt, dy, dx = _taps(taps)
-    sc, sh, nseg = src_bn
-    d = WGRAD(rows, src, stride, nt, dy, dx, _ptr(sc), _ptr(sh), nseg, None, None)
+    d = wgrad_desc(rows, src, stride, taps, src_bn)
     return lib().scd_wgrad_src_bn_supported(ctypes.byref(d)) == 1
 
 
 def wgrad_rows_bn_supported(rows: NHWC, src: NHWC, stride: int, taps) -> bool:
     """Whether the weight grad for (rows, src) can form its rows through the fused BatchNorm backward."""
-    nt, dy, dx = _taps(taps)
-    d = WGRAD(rows, src, stride, nt, dy, dx, None, None, 0, None, None)
+    d = wgrad_desc(rows, src, stride, taps)
     return lib().scd_wgrad_rows_bn_supported(ctypes.byref(d)) == 1
 
 

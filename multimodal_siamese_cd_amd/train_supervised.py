@@ -17,7 +17,7 @@ import timeit
 import numpy as np
 import torch
 
-from . import engine, hip, parallel, trainers
+from . import engine, hip, parallel, trainers  # noqa: F401
 from .utils import datasets, evaluation, experiment_manager, networks, parsers
 
 
@@ -30,6 +30,17 @@ def _evaluate(net, cfg, device, run_types, epoch_float, step, rank):
     for rt in run_types:
         evaluation.model_evaluation(module, cfg, device, rt, epoch_float, step)
     net.train()
+
+
+def _checked_loss(value: float, cfg, step: int) -> float:
+    """The logged loss (a host sync the loop makes anyway), refused when non-finite.  Under MODEL.PRECISION fp32 the
+    convs run h2 (engine.conv_math_for), whose operand scaling relies on every producer's magnitude bound: an
+    underestimated bound overflows fp16 into inf / NaN, so the error names the arithmetic that was active."""
+    if not np.isfinite(value):
+        raise FloatingPointError(f"non-finite training loss {value} at step {step} (conv arithmetic "
+                                 f"{engine.conv_math_for(cfg)!r}; MODEL.CONV_MATH x3 is the bound-free fp32-class "
+                                 "alternative)")
+    return value
 
 
 def run_training(cfg, device, max_steps: int | None = None):
@@ -74,8 +85,8 @@ def run_training(cfg, device, max_steps: int | None = None):
                 break
             if global_step % int(cfg.LOG_FREQ) == 0 and rank == 0:
                 t = timeit.default_timer() - start
-                print(f'step {global_step} epoch {epoch_float:.2f} '
-                      f'loss {torch.stack(losses).mean().item():.5f} time {t:.1f}s', flush=True)
+                mean_loss = _checked_loss(torch.stack(losses).mean().item(), cfg, global_step)
+                print(f'step {global_step} epoch {epoch_float:.2f} loss {mean_loss:.5f} time {t:.1f}s', flush=True)
                 _evaluate(net, cfg, device, ('training', 'validation'), epoch_float, global_step, rank)
             if max_steps is not None and global_step >= max_steps:
                 break
@@ -83,7 +94,8 @@ def run_training(cfg, device, max_steps: int | None = None):
             _evaluate(net, cfg, device, ('training', 'validation', 'test'), global_step / steps_per_epoch,
                       global_step, rank)
         if rank == 0:
-            print(f'epoch {epoch}: mean loss {torch.stack(losses).mean().item():.5f}', flush=True)
+            print(f'epoch {epoch}: mean loss {_checked_loss(torch.stack(losses).mean().item(), cfg, global_step):.5f}',
+                  flush=True)
             if epoch in list(cfg.SAVE_CHECKPOINTS) and not cfg.DEBUG:
                 networks.save_checkpoint(net, optimizer, epoch, global_step, cfg)
         if cfg.DEBUG or (max_steps is not None and global_step >= max_steps):
@@ -102,7 +114,6 @@ def main(argv=None):
     device = torch.device('cuda', parallel.device_index(local_rank))
     torch.cuda.set_device(device)
     hip.load_library()
-    hip.set_conv_math(engine.conv_math_for(cfg))
     try:
         run_training(cfg, device)
     except KeyboardInterrupt:

@@ -10,8 +10,13 @@ Up (429-451), OutConv (454-461).  Constructor arguments, submodule attribute pat
 
 What differs is the execution: the model-level forward runs every stage through the HIP kernels of
 libscd (via multimodal_siamese_cd_amd.engine) on NHWC fp32 buffers, with the Siamese encoder run as one
-2B-image batch whose BatchNorm statistics are segmented per branch.  torch.nn modules are used only as
-parameter/buffer containers; their own forward is never called on the hot path.
+2B-image batch whose BatchNorm statistics are segmented per branch.  The building blocks (Encoder, Decoder,
+DoubleConv, InConv, Down, Up, OutConv) are callable on their own as in the reference (NCHW in, NCHW out, autograd),
+on the same kernels; the model forwards do not call them but run whole stages.
+
+Every model carries the conv arithmetic its config asks for (`conv_math`, engine.conv_math_for: MODEL.CONV_MATH,
+else MODEL.PRECISION 'fp32' -> h2, 'bf16' -> bf16) and runs its forward and backward in that arithmetic
+(hip.conv_scope), so models of different precision coexist in one process.
 """
 from __future__ import annotations
 
@@ -21,7 +26,7 @@ from pathlib import Path
 import torch
 import torch.nn as nn
 
-from .. import engine
+from .. import engine, hip
 
 
 def _check_topology(cfg):
@@ -29,8 +34,6 @@ def _check_topology(cfg):
     bad = [t for t in topo if t % 8]
     if bad:
         raise ValueError(f"MODEL.TOPOLOGY entries must be multiples of 8 for the MFMA kernels, got {topo}")
-    if cfg.MODEL.OUT_CHANNELS > 4:
-        raise ValueError("OUT_CHANNELS > 4 is not supported by the 1x1 head kernel")
 
 
 class ModelWrapper(nn.Module):
@@ -90,6 +93,21 @@ def _band_counts(cfg):
     return len(cfg.DATALOADER.S1_BANDS), len(cfg.DATALOADER.S2_BANDS)
 
 
+class _HipNet(nn.Module):
+    """The part every model family shares: topology check, config, arithmetic; forward runs in the model's
+    arithmetic (a block called on its own runs in the caller's, hip.conv_scope / the process default)."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        _check_topology(cfg)
+        self.cfg = cfg
+        self.conv_math = engine.conv_math_for(cfg)
+
+    def forward(self, x_t1, x_t2):
+        with hip.conv_scope(self.conv_math):
+            return self._forward(x_t1, x_t2)
+
+
 def _stream(inc, encoder, decoder, x, nseg, training, siamese, head=None):
     """inc + encoder (+ Siamese diff) + decoder of one stream; returns (decoder output, features).  With `head` (the
     OutConv that is the decoder output's only reader) the first item is the head's logits (engine.run_decoder)."""
@@ -107,28 +125,24 @@ def _stream(inc, encoder, decoder, x, nseg, training, siamese, head=None):
     return engine.run_decoder(decoder, feats, training, head=head), feats
 
 
-class UNet(nn.Module):
+class UNet(_HipNet):
     def __init__(self, cfg):
-        super().__init__()
-        _check_topology(cfg)
-        self.cfg = cfg
+        super().__init__(cfg)
         topology = cfg.MODEL.TOPOLOGY
         self.inc = InConv(cfg.MODEL.IN_CHANNELS * 2, topology[0], DoubleConv)
         self.encoder = Encoder(cfg)
         self.decoder = Decoder(cfg)
         self.outc = OutConv(topology[0], cfg.MODEL.OUT_CHANNELS)
 
-    def forward(self, x_t1, x_t2):
+    def _forward(self, x_t1, x_t2):
         x = engine.pack_stream(x_t1, x_t2)  # torch.cat((x_t1, x_t2), dim=1) (networks.py:74)
         out, _ = _stream(self.inc, self.encoder, self.decoder, x, 1, self.training, siamese=False, head=self.outc)
         return out  # self.outc(decoder output) (networks.py:77-78), fused into the decoder stage
 
 
-class DualStreamUNet(nn.Module):
+class DualStreamUNet(_HipNet):
     def __init__(self, cfg):
-        super().__init__()
-        _check_topology(cfg)
-        self.cfg = cfg
+        super().__init__(cfg)
         topology = cfg.MODEL.TOPOLOGY
         n1, n2 = _band_counts(cfg)
         self.inc_stream1 = InConv(2 * n1, topology[0], DoubleConv)
@@ -139,7 +153,7 @@ class DualStreamUNet(nn.Module):
         self.decoder_stream2 = Decoder(cfg)
         self.outc = OutConv(2 * topology[0], cfg.MODEL.OUT_CHANNELS)
 
-    def forward(self, x_t1, x_t2):
+    def _forward(self, x_t1, x_t2):
         n1, _ = _band_counts(self.cfg)
         c = x_t1.shape[1]
         x1 = engine.pack_stream(x_t1, x_t2, 0, n1)
@@ -149,32 +163,28 @@ class DualStreamUNet(nn.Module):
         return engine.run_head(self.outc, engine.cat_channels(d1, d2))
 
 
-class SiameseUNet(nn.Module):
+class SiameseUNet(_HipNet):
     def __init__(self, cfg):
-        super().__init__()
-        _check_topology(cfg)
-        self.cfg = cfg
+        super().__init__(cfg)
         topology = cfg.MODEL.TOPOLOGY
         self.inc = InConv(cfg.MODEL.IN_CHANNELS, topology[0], DoubleConv)
         self.encoder = Encoder(cfg)
         self.decoder = Decoder(cfg)
         self.outc = OutConv(topology[0], cfg.MODEL.OUT_CHANNELS)
 
-    def forward(self, x_t1, x_t2):
+    def _forward(self, x_t1, x_t2):
         x = engine.pack_pair(x_t1, x_t2)
         out, _ = _stream(self.inc, self.encoder, self.decoder, x, 2, self.training, siamese=True, head=self.outc)
         return out  # self.outc(decoder output) (networks.py:152-153), fused into the decoder stage
 
 
-class DualTaskSiameseUNet(nn.Module):
-    # outc_sem_change is built (state_dict keys) but never called (reference networks.py:174, 176-197);
-    # parallel.wrap_ddp turns DDP's unused-parameter search on for it
+class DualTaskSiameseUNet(_HipNet):
+    # outc_sem_change is built (state_dict keys) but never called by forward (reference networks.py:174, 176-197;
+    # assessment_semantics.py:34,117 calls it directly); parallel.wrap_ddp turns DDP's unused-parameter search on
     PARAMS_OUTSIDE_FORWARD = ('outc_sem_change',)
 
     def __init__(self, cfg):
-        super().__init__()
-        _check_topology(cfg)
-        self.cfg = cfg
+        super().__init__(cfg)
         topology = cfg.MODEL.TOPOLOGY
         n_classes = cfg.MODEL.OUT_CHANNELS
         self.inc = InConv(cfg.MODEL.IN_CHANNELS, topology[0], DoubleConv)
@@ -185,7 +195,7 @@ class DualTaskSiameseUNet(nn.Module):
         self.outc_sem = OutConv(topology[0], n_classes)
         self.outc_sem_change = OutConv(2, 1)  # present in the reference, unused by forward (networks.py:174)
 
-    def forward(self, x_t1, x_t2):
+    def _forward(self, x_t1, x_t2):
         b = x_t1.shape[0]
         x = engine.pack_pair(x_t1, x_t2)
         feats = engine.run_encoder(self.inc, self.encoder, x, 2, self.training)
@@ -199,11 +209,9 @@ class DualTaskSiameseUNet(nn.Module):
         return out_change, out_sem_t1, out_sem_t2
 
 
-class WhateverNet(nn.Module):
+class WhateverNet(_HipNet):
     def __init__(self, cfg):
-        super().__init__()
-        _check_topology(cfg)
-        self.cfg = cfg
+        super().__init__(cfg)
         topology = cfg.MODEL.TOPOLOGY
         n_classes = cfg.MODEL.OUT_CHANNELS
         n1, n2 = _band_counts(cfg)
@@ -217,7 +225,7 @@ class WhateverNet(nn.Module):
         self.outc_stream2 = OutConv(topology[0], n_classes)
         self.outc_fusion = OutConv(2 * topology[0], n_classes)
 
-    def forward(self, x_t1, x_t2):
+    def _forward(self, x_t1, x_t2):
         n1, _ = _band_counts(self.cfg)
         c = x_t1.shape[1]
         x1 = engine.pack_pair(x_t1, x_t2, 0, n1)
@@ -232,11 +240,9 @@ class WhateverNet(nn.Module):
         return out_fusion
 
 
-class WhateverNet2(nn.Module):
+class WhateverNet2(_HipNet):
     def __init__(self, cfg):
-        super().__init__()
-        _check_topology(cfg)
-        self.cfg = cfg
+        super().__init__(cfg)
         topology = cfg.MODEL.TOPOLOGY
         n_classes = cfg.MODEL.OUT_CHANNELS
         n1, n2 = _band_counts(cfg)
@@ -250,7 +256,7 @@ class WhateverNet2(nn.Module):
         self.outc_stream2 = OutConv(topology[0], n_classes)
         self.outc_fusion = OutConv(2 * topology[0], n_classes)
 
-    def forward(self, x_t1, x_t2):
+    def _forward(self, x_t1, x_t2):
         n1, _ = _band_counts(self.cfg)
         c = x_t1.shape[1]
         x1 = engine.pack_stream(x_t1, x_t2, 0, n1)
@@ -266,12 +272,8 @@ class WhateverNet2(nn.Module):
 
 
 # ------------------------------------------------------------------------------------------------
-# Building blocks: parameter containers with the reference's attribute paths.
+# Building blocks: the reference's attribute paths and parameters; forwards on the HIP kernels (NCHW in and out).
 # ------------------------------------------------------------------------------------------------
-_STAGE_ONLY = ("{} is executed as part of a model-level stage on the HIP path "
-               "(multimodal_siamese_cd_amd.engine); call the model's forward instead")
-
-
 class Encoder(nn.Module):
     def __init__(self, cfg):
         super().__init__()
@@ -286,7 +288,12 @@ class Encoder(nn.Module):
         self.down_seq = nn.ModuleDict(down_dict)
 
     def forward(self, x1):
-        raise NotImplementedError(_STAGE_ONLY.format("Encoder"))
+        """[x1, down1(x1), down2(...), ...] reversed (networks.py:334-343)."""
+        feats = [x1]
+        for layer in self.down_seq.values():
+            feats.append(layer(feats[-1]))
+        feats.reverse()
+        return feats
 
 
 class Decoder(nn.Module):
@@ -305,7 +312,12 @@ class Decoder(nn.Module):
         self.up_seq = nn.ModuleDict(up_dict)
 
     def forward(self, features):
-        raise NotImplementedError(_STAGE_ONLY.format("Decoder"))
+        """Pops the deepest map off `features` (the caller's list, as the reference does) and runs the Up blocks
+        against the rest (networks.py:375-382)."""
+        x1 = features.pop(0)
+        for idx, layer in enumerate(self.up_seq.values()):
+            x1 = layer(x1, features[idx])
+        return x1
 
 
 class DoubleConv(nn.Module):
@@ -323,7 +335,16 @@ class DoubleConv(nn.Module):
         )
 
     def forward(self, x):
-        raise NotImplementedError(_STAGE_ONLY.format("DoubleConv"))
+        return _block(self, x, maxpool=False)
+
+
+def _block(dc: DoubleConv, x, maxpool: bool):
+    """DoubleConv (networks.py:386-402), behind MaxPool2d(2) for Down (415-426), on the engine's block Function.  A
+    source whose channels are not a multiple of 8 is zero-padded (its input gradient is then not available)."""
+    cin = x.shape[1]
+    cp = engine.pad_in(cin) if cin % 8 else cin
+    y = engine.run_block(dc, engine.to_nhwc(x, cp), dc.training, maxpool=maxpool)
+    return engine.to_nchw(y)
 
 
 class InConv(nn.Module):
@@ -332,7 +353,7 @@ class InConv(nn.Module):
         self.conv = conv_block(in_ch, out_ch)
 
     def forward(self, x):
-        raise NotImplementedError(_STAGE_ONLY.format("InConv"))
+        return self.conv(x)
 
 
 class Down(nn.Module):
@@ -341,7 +362,7 @@ class Down(nn.Module):
         self.mpconv = nn.Sequential(nn.MaxPool2d(2), conv_block(in_ch, out_ch))
 
     def forward(self, x):
-        raise NotImplementedError(_STAGE_ONLY.format("Down"))
+        return _block(self.mpconv[1], x, maxpool=True)
 
 
 class Up(nn.Module):
@@ -351,7 +372,9 @@ class Up(nn.Module):
         self.conv = conv_block(in_ch, out_ch)
 
     def forward(self, x1, x2):
-        raise NotImplementedError(_STAGE_ONLY.format("Up"))
+        """ConvT(x1), F.pad to x2's size, cat([x2, up], 1), DoubleConv (networks.py:436-451)."""
+        y = engine.run_ups([self], [engine.to_nhwc(x1), engine.to_nhwc(x2)], self.training)
+        return engine.to_nchw(y)
 
 
 class OutConv(nn.Module):
@@ -360,4 +383,4 @@ class OutConv(nn.Module):
         self.conv = nn.Conv2d(in_ch, out_ch, 1)
 
     def forward(self, x):
-        raise NotImplementedError(_STAGE_ONLY.format("OutConv"))
+        return engine.run_head(self, engine.to_nhwc(x))

@@ -15,6 +15,7 @@ from the reference's source (SebastianHafner/multimodal_siamese_cd):
   DualStreamUNet  utils/networks.py:82-120    per-modality early fusion, cat of decoders -> head
   DualTaskSiameseUNet utils/networks.py:157-197
   WhateverNet     utils/networks.py:200-263   per-modality Siamese streams + fusion head
+  WhateverNet2    utils/networks.py:266-310   per-modality early-fusion streams, per-stream heads + fusion head
   power_jaccard_loss  utils/loss_functions.py:141-150
 
 Parameters are a flat dict keyed by the reference's state_dict names (without the `module.` prefix);
@@ -151,6 +152,15 @@ def forward(model_type, P, B, x_t1, x_t2, cfg, training=True):
             outs.append(out_conv(d, P, f'outc_stream{s}.'))
         fusion = out_conv(torch.cat(decs, dim=1), P, 'outc_fusion.')
         return (fusion, outs[0], outs[1]) if training else fusion
+    if model_type == 'whatevernet2':  # networks.py:288-310
+        decs, outs = [], []
+        for s, (a, b) in ((1, (x_t1[:, :n1], x_t2[:, :n1])), (2, (x_t1[:, n1:], x_t2[:, n1:]))):
+            f = encoder(torch.cat((a, b), dim=1), P, B, f'inc_stream{s}.', f'encoder_stream{s}.', topo, training)
+            d = decoder(f, P, B, f'decoder_stream{s}.', topo, training)
+            decs.append(d)
+            outs.append(out_conv(d, P, f'outc_stream{s}.'))
+        fusion = out_conv(torch.cat(decs, dim=1), P, 'outc_fusion.')
+        return (fusion, outs[0], outs[1]) if training else fusion
     raise ValueError(f'oracle: unsupported model {model_type}')
 
 
@@ -182,7 +192,7 @@ def step_loss(model_type, outputs, batch, alpha=0.5):
         lc = power_jaccard_loss(out_change, y)
         ls = (power_jaccard_loss(out_sem_t1, batch['y_sem_t1']) + power_jaccard_loss(out_sem_t2, batch['y_sem_t2'])) / 2
         return (lc + ls) / 2
-    if model_type == 'whatevernet':
+    if model_type in ('whatevernet', 'whatevernet2'):
         fusion, s1, s2 = outputs
         lab = batch['is_labeled']
         loss = None
@@ -250,8 +260,9 @@ def param_shapes(model_type, cfg):
         s['outc.conv.weight'] = (nout, 2 * topo[0], 1, 1)
         s['outc.conv.bias'] = (nout,)
         return s
-    if model_type == 'whatevernet':
+    if model_type in ('whatevernet', 'whatevernet2'):
         for k, nb in ((1, n1), (2, n2)):
+            nb = nb if model_type == 'whatevernet' else 2 * nb  # WhateverNet2: early fusion of t1 and t2 bands
             s.update(_stream_shapes(f'inc_stream{k}.', f'encoder_stream{k}.', f'decoder_stream{k}.', nb, topo))
             s[f'outc_stream{k}.conv.weight'] = (nout, topo[0], 1, 1)
             s[f'outc_stream{k}.conv.bias'] = (nout,)

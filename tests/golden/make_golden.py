@@ -41,6 +41,11 @@ CONFIGS = [
     # tiles not divisible by 2**levels: MaxPool floors and Up zero-pads the upsampled map (networks.py:437-443)
     ('siamese_t8-16-32_odd', 'siameseunet', [8, 16, 32], 5, [0, 1], [2, 1, 0], 2, (37, 45), None),
     ('dualstream_t8-16_odd', 'dualstreamunet', [8, 16], 5, [0, 1], [2, 1, 0], 1, (27, 30), None),
+    ('whatevernet2_t8-16', 'whatevernet2', [8, 16], 5, [0, 1], [2, 1, 0], 2, 32, [True, False]),
+    # channel counts that take the production kernels (16x16x32 halo / h2 paths: source channels multiple of 32)
+    ('siamese_t32-64', 'siameseunet', [32, 64], 5, [0, 1], [2, 1, 0], 2, 64, None),
+    ('dtsiamese_t32-64', 'dtsiameseunet', [32, 64], 5, [0, 1], [2, 1, 0], 2, 64, None),
+    ('dualstream_t32-64', 'dualstreamunet', [32, 64], 5, [0, 1], [2, 1, 0], 2, 64, None),
 ]
 LR = 1e-3
 WD = 0.01
@@ -224,7 +229,7 @@ def _ref_step_loss(mtype, out, batch, pj):
     if mtype == 'dtsiameseunet':
         c, s1, s2 = out
         return (pj(c, y) + (pj(s1, batch['y_sem_t1']) + pj(s2, batch['y_sem_t2'])) / 2) / 2
-    if mtype == 'whatevernet':
+    if mtype in ('whatevernet', 'whatevernet2'):
         f, s1, s2 = out
         lab = batch['is_labeled']
         loss = None

@@ -174,18 +174,16 @@ def test_bf16_siamese_model_step(dev):
     batch = O.synthetic_batch(ocfg, 2, 64, 4)
     out32, loss32, g32 = _oracle_step(P, B, batch, ocfg, False)
     out16, loss16, _ = _oracle_step(P, B, batch, ocfg, True)
-    prev = hip.set_conv_math('bf16')
-    try:
-        net = networks.create_network(cfg).to(dev)
-        with torch.no_grad():
-            for k, p in net.module.named_parameters():
-                p.copy_(P[k])
-        net.train()
-        out = net(batch['x_t1'].to(dev), batch['x_t2'].to(dev))
-        loss = loss_functions.get_criterion('PowerJaccardLoss')(out, batch['y_change'].to(dev))
-        loss.backward()
-    finally:
-        hip.set_conv_math(prev)
+    cfg.MODEL.PRECISION = 'bf16'  # create_network gives the model the bf16 arithmetic
+    net = networks.create_network(cfg).to(dev)
+    assert net.module.conv_math == 'bf16'
+    with torch.no_grad():
+        for k, p in net.module.named_parameters():
+            p.copy_(P[k])
+    net.train()
+    out = net(batch['x_t1'].to(dev), batch['x_t2'].to(dev))
+    loss = loss_functions.get_criterion('PowerJaccardLoss')(out, batch['y_change'].to(dev))
+    loss.backward()
     e16, e32 = rel(out, out16), rel(out, out32)
     print(f'bf16 logits rel err vs emulated {e16:.2e}, vs fp32 {e32:.2e}; loss {loss.item():.6f} emulated '
           f'{loss16.item():.6f} fp32 {loss32.item():.6f}')
@@ -223,18 +221,16 @@ def test_split_math_siamese_model_step_meets_the_fp32_bars(dev, math):
     B = O.fresh_buffers(shapes)
     batch = O.synthetic_batch(ocfg, 2, 64, 4)
     out32, loss32, g32 = _oracle_step(P, B, batch, ocfg, False)
-    prev = hip.set_conv_math(math)
-    try:
-        net = networks.create_network(cfg).to(dev)
-        with torch.no_grad():
-            for k, p in net.module.named_parameters():
-                p.copy_(P[k])
-        net.train()
-        out = net(batch['x_t1'].to(dev), batch['x_t2'].to(dev))
-        loss = loss_functions.get_criterion('PowerJaccardLoss')(out, batch['y_change'].to(dev))
-        loss.backward()
-    finally:
-        hip.set_conv_math(prev)
+    cfg.MODEL.CONV_MATH = math
+    net = networks.create_network(cfg).to(dev)
+    assert net.module.conv_math == math
+    with torch.no_grad():
+        for k, p in net.module.named_parameters():
+            p.copy_(P[k])
+    net.train()
+    out = net(batch['x_t1'].to(dev), batch['x_t2'].to(dev))
+    loss = loss_functions.get_criterion('PowerJaccardLoss')(out, batch['y_change'].to(dev))
+    loss.backward()
     e = rel(out, out32)
     cos = {}
     for k, p in net.module.named_parameters():

@@ -109,3 +109,33 @@ def test_synthetic_mode_follows_the_split():
     cfg.DATALOADER.SYNTHETIC = False
     cfg.DATASET.TRAINING_IDS = []
     assert not datasets.uses_synthetic_data(cfg)
+
+
+@pytest.mark.parametrize('config,math', [('baseline_siamese', 'h2'), ('baseline_dualstream', 'bf16'), ('dtsiamese', 'h2'),
+                                         ('siamese_mmcr_alpha0500', 'bf16'), ('debug', 'h2')])
+def test_create_network_takes_the_arithmetic_from_the_config(config, math):
+    """MODEL.PRECISION fp32 -> h2, bf16 -> bf16; MODEL.CONV_MATH overrides; the model carries it (no process mode)."""
+    from multimodal_siamese_cd_amd import hip
+    from multimodal_siamese_cd_amd.utils import networks
+    cfg = em.load_cfg(config)
+    assert networks.create_network(cfg).module.conv_math == math
+    cfg.MODEL.CONV_MATH = 'x3'
+    assert networks.create_network(cfg).module.conv_math == 'x3'
+    with hip.conv_scope('f32'):
+        assert hip.conv_math() == 'f32'
+        with hip.conv_scope(tune=hip.TUNE_WGRAD_R64):
+            assert hip.conv_math() == 'f32' and hip.conv_tune() == hip.TUNE_WGRAD_R64
+    cfg.MODEL.CONV_MATH = None
+    cfg.MODEL.PRECISION = 'fp16'
+    with pytest.raises(ValueError, match='PRECISION'):
+        networks.create_network(cfg)
+
+
+def test_topology_and_head_generality_on_cpu():
+    """Any multiple-of-8 topology and any OUT_CHANNELS build (the 1x1 head runs in groups of 4 outputs)."""
+    from multimodal_siamese_cd_amd.utils import networks
+    cfg = em.load_cfg('debug')
+    cfg.MODEL.TOPOLOGY = [24, 40]
+    cfg.MODEL.OUT_CHANNELS = 7
+    net = networks.create_network(cfg)
+    assert net.module.outc.conv.weight.shape == (7, 24, 1, 1)

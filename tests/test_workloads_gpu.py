@@ -1,0 +1,249 @@
+"""Every shipped BASELINE workload against the oracle on the production kernels (MI355X).
+
+The model is built only through the drop-in surface (utils.networks.create_network with the workload's config), so
+it runs the arithmetic its config selects (MODEL.PRECISION fp32 -> h2, bf16 -> bf16); every conv launch is checked
+to run that arithmetic wherever the library's kernels take it.
+
+fp32 workloads (h2): outputs within 1e-4 of the fp64 oracle (north_star's logits bar), change masks bit-exact
+outside the |logit| < 1e-4 max band, loss within 1e-5, BatchNorm running statistics within 1e-5; gradients within 2x
+of the error the bound-free x3 arithmetic reaches against the same fp64 oracle (+1e-5), with the ReLU-kink handling
+of tests/_parity.py.
+
+bf16 workloads: bf16 roundings amplify through depth, so no bf16 implementation matches another to fp32 precision at
+model level (the kernel tests pin the arithmetic exactly).  Outputs within 3e-2 of the fp32 oracle and closer to an
+oracle with the bf16 conv arithmetic emulated than to the fp32 one; loss within 1e-2; every weight gradient with
+cosine similarity > 0.95 to the fp32 oracle's.
+
+Sizes: the workloads' own tiles and topologies ([64, 128, 256, 512], 256x256; WhateverNet 512x512) at bs=2, and the
+headline baseline_siamese at its bench batch, bs=32 (the BatchNorm-derived h2 bounds grow with the batch).
+"""
+import numpy as np
+import pytest
+import torch
+
+from _parity import bf16_conv_oracle, check_gradients, mask_mismatch, record_arith, record_kinks, rel
+
+pytestmark = pytest.mark.gpu
+
+FULL = [64, 128, 256, 512]
+
+
+@pytest.fixture(scope='module')
+def dev():
+    from multimodal_siamese_cd_amd import hip
+    hip.load_library()
+    d = torch.device('cuda:0')
+    hip.ensure_device(torch.empty(1, device=d))
+    return d
+
+
+def _cfg(config, model, topo, **model_kw):
+    """The shipped config file (configs/<config>.yaml), its model type and topology, plus overrides."""
+    from multimodal_siamese_cd_amd.utils import experiment_manager as em
+    cfg = em.load_cfg(config)
+    cfg.MODEL.TYPE = model
+    cfg.MODEL.TOPOLOGY = list(topo)
+    for k, v in model_kw.items():
+        cfg.MODEL[k] = v
+    return cfg
+
+
+def _ocfg(cfg):
+    return dict(TYPE=cfg.MODEL.TYPE, TOPOLOGY=list(cfg.MODEL.TOPOLOGY), IN_CHANNELS=cfg.MODEL.IN_CHANNELS,
+                OUT_CHANNELS=cfg.MODEL.OUT_CHANNELS, S1_BANDS=list(cfg.DATALOADER.S1_BANDS),
+                S2_BANDS=list(cfg.DATALOADER.S2_BANDS))
+
+
+def _outs(o):
+    return list(o) if isinstance(o, (tuple, list)) else [o]
+
+
+def _gpu_step(cfg, P, batch, dev, monkeypatch):
+    """One training step of the drop-in model on the GPU: (outputs, loss, grads, state_dict, launches)."""
+    from multimodal_siamese_cd_amd import trainers
+    from multimodal_siamese_cd_amd.utils import networks
+    net = networks.create_network(cfg)
+    with torch.no_grad():
+        for k, p in net.module.named_parameters():
+            p.copy_(P[k])
+    net.to(dev).train()
+    seen = record_arith(monkeypatch, dev)
+    b = {k: v.to(dev) for k, v in batch.items()}
+    out = net(b['x_t1'], b['x_t2'])
+    loss = trainers.step_loss(cfg, out, b)
+    loss.backward()
+    monkeypatch.undo()
+    torch.cuda.synchronize()
+    return ([o.detach().cpu() for o in _outs(out)], loss.item(),
+            {k: p.grad.detach().cpu() for k, p in net.module.named_parameters() if p.grad is not None},
+            {k: v.detach().cpu() for k, v in net.module.state_dict().items()}, seen, net.module.conv_math)
+
+
+def _oracle_step(cfg, P, batch, dtype, alpha=0.5):
+    from oracle import siamese_oracle as O
+    ocfg = _ocfg(cfg)
+    model = cfg.MODEL.TYPE
+    shapes = O.param_shapes(model, ocfg)
+    Pr = {k: v.detach().to(dtype).clone().requires_grad_(True) for k, v in P.items()}
+    B = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in O.fresh_buffers(shapes).items()}
+    bt = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in batch.items()}
+    out = O.forward(model, Pr, B, bt['x_t1'], bt['x_t2'], ocfg, True)
+    loss = O.step_loss(model, out, bt, alpha)
+    loss.backward()
+    return ([o.detach() for o in _outs(out)], loss.item(),
+            {k: v.grad for k, v in Pr.items() if v.grad is not None}, B)
+
+
+def _setup(cfg, batch_size, size, labeled=None, seed=7):
+    from oracle import siamese_oracle as O
+    ocfg = _ocfg(cfg)
+    P = O.deterministic_params(O.param_shapes(cfg.MODEL.TYPE, ocfg), seed)
+    batch = O.synthetic_batch(ocfg, batch_size, size, seed + 1, labeled)
+    return P, batch
+
+
+def _check_routing(seen, math):
+    """Every conv launch runs the arithmetic it would run with bounds on every operand (no h2-capable conv left on
+    x3 for want of a bound), and at least one runs `math`."""
+    assert seen, 'no conv launches recorded'
+    assert all(s[4] == s[5] for s in seen), [s for s in seen if s[4] != s[5]]
+    n = sum(s[4] == math for s in seen)
+    print(f'{n} of {len(seen)} conv launches run {math}')
+    assert n > 0
+
+
+FP32_WORKLOADS = [
+    # id, config file, model, topology, tile, batch
+    ('dtsiamese', 'dtsiamese', 'dtsiameseunet', FULL, 256, 2),
+    ('baseline_siamese_bs32', 'baseline_siamese', 'siameseunet', FULL, 256, 32),
+    # ConvTranspose inputs of 24 / 40 channels (c % 16 == 8): no split-kernel epilogue bound, an absmax pass instead
+    ('siamese_t24-32', 'baseline_siamese', 'siameseunet', [24, 32], 32, 2),
+    ('unet_t16-40', 'baseline_siamese', 'unet', [16, 40], 32, 2),
+]
+
+
+@pytest.mark.parametrize('wid,config,model,topo,size,bs', FP32_WORKLOADS, ids=[w[0] for w in FP32_WORKLOADS])
+def test_fp32_workload_matches_oracle(dev, monkeypatch, wid, config, model, topo, size, bs):
+    cfg = _cfg(config, model, topo, PRECISION='fp32')
+    P, batch = _setup(cfg, bs, size)
+    outs, loss, grads, sd, seen, math = _gpu_step(cfg, P, batch, dev, monkeypatch)
+    assert math == 'h2'
+    _check_routing(seen, 'h2')
+    cfg_x3 = _cfg(config, model, topo, PRECISION='fp32', CONV_MATH='x3')
+    outs3, _, grads3, _, _, _ = _gpu_step(cfg_x3, P, batch, dev, monkeypatch)
+    ref_out, ref_loss, ref_g, ref_B = _oracle_step(cfg, P, batch, torch.float64)
+    for i, (o, r) in enumerate(zip(outs, ref_out)):
+        e, e3 = rel(o, r), rel(outs3[i], r)
+        print(f'output {i}: rel err vs fp64 oracle h2 {e:.2e} (x3 {e3:.2e})')
+        assert e < 1e-4
+        assert mask_mismatch(o.numpy(), r.numpy()) == 0
+    assert abs(loss - ref_loss) < 1e-5
+    for k, v in ref_B.items():
+        if k.endswith('running_mean') or k.endswith('running_var'):
+            assert rel(sd[k], v) < 1e-5, k
+        elif k.endswith('num_batches_tracked'):
+            assert int(sd[k]) == int(v), k
+    bars = {}
+    for k, r in ref_g.items():
+        den = r.abs().max().clamp_min(1e-30)
+        bars[k] = 2 * ((grads3[k].double() - r.double()).abs().max() / den).item() + 1e-5
+    from oracle import siamese_oracle as O
+    kinks = record_kinks(model, P, O.fresh_buffers(O.param_shapes(model, _ocfg(cfg))), batch, _ocfg(cfg))
+    bad = check_gradients(grads, ref_g, list(grads), bars, kinks)
+    assert not bad, bad
+
+
+BF16_WORKLOADS = [
+    # id, config file, model, topology, tile, batch, labelled samples
+    ('baseline_dualstream', 'baseline_dualstream', 'dualstreamunet', FULL, 256, 2, None),
+    ('siamese_mmcr_alpha0500', 'siamese_mmcr_alpha0500', 'whatevernet', FULL, 512, 2, [True, False]),
+]
+
+
+@pytest.mark.parametrize('wid,config,model,topo,size,bs,labeled', BF16_WORKLOADS, ids=[w[0] for w in BF16_WORKLOADS])
+def test_bf16_workload_matches_oracle(dev, monkeypatch, wid, config, model, topo, size, bs, labeled):
+    cfg = _cfg(config, model, topo)
+    assert str(cfg.MODEL.PRECISION) == 'bf16'
+    P, batch = _setup(cfg, bs, size, labeled)
+    alpha = float(cfg.CONSISTENCY_TRAINER.LOSS_FACTOR)
+    outs, loss, grads, sd, seen, math = _gpu_step(cfg, P, batch, dev, monkeypatch)
+    assert math == 'bf16'
+    _check_routing(seen, 'bf16')
+    ref32, loss32, g32, _ = _oracle_step(cfg, P, batch, torch.float32, alpha)
+    with bf16_conv_oracle():
+        ref16, loss16, _, _ = _oracle_step(cfg, P, batch, torch.float32, alpha)
+    for i, (o, r32, r16) in enumerate(zip(outs, ref32, ref16)):
+        e32, e16 = rel(o, r32), rel(o, r16)
+        print(f'output {i}: rel err vs fp32 oracle {e32:.2e}, vs bf16-emulating oracle {e16:.2e}')
+        assert e32 < 3e-2
+        assert e16 < e32
+    print(f'loss {loss:.6f} fp32 oracle {loss32:.6f} emulated {loss16:.6f}')
+    assert abs(loss - loss32) < 1e-2
+    worst = 1.0
+    for k, r in g32.items():
+        if k.endswith('conv.0.bias') or k.endswith('conv.3.bias'):
+            continue
+        a, b = grads[k].double().flatten(), r.double().flatten()
+        cs = float(torch.dot(a, b) / (a.norm() * b.norm()).clamp_min(1e-30))
+        worst = min(worst, cs)
+        assert cs > 0.95, (k, cs)
+    print(f'worst gradient cosine similarity {worst:.4f}')
+
+
+@pytest.mark.parametrize('config,math', [('baseline_siamese', 'h2'), ('baseline_dualstream', 'bf16'),
+                                         ('dtsiamese', 'h2'), ('siamese_mmcr_alpha0500', 'bf16'), ('debug', 'h2')])
+def test_create_network_carries_the_config_arithmetic(dev, monkeypatch, config, math):
+    """A model built only through create_network(load_cfg(config)) runs the config's arithmetic, launch by launch
+    (scd_igemm_arith / scd_wgrad_arith), whatever the process default is."""
+    from multimodal_siamese_cd_amd import hip, trainers
+    from multimodal_siamese_cd_amd.utils import datasets, experiment_manager as em, networks
+    cfg = em.load_cfg(config)
+    prev = hip.set_conv_math('f32')  # a different process default must not leak into the model
+    try:
+        net = networks.create_network(cfg).to(dev).train()
+        assert net.module.conv_math == math
+        gen = torch.Generator(device=dev).manual_seed(3)
+        b = datasets.synthetic_batch(cfg, 2, dev, gen, 64)
+        seen = record_arith(monkeypatch, dev)
+        trainers.step_loss(cfg, net(b['x_t1'], b['x_t2']), b).backward()
+        monkeypatch.undo()
+    finally:
+        hip.set_conv_math(prev)
+    _check_routing(seen, math)
+    assert not any(s[4] == 'f32' for s in seen)
+
+
+def test_models_of_different_arithmetic_coexist(dev):
+    """An h2 model and a bf16 model in one process, interleaved: each keeps its own arithmetic and its results equal
+    those of the same model run alone."""
+    from multimodal_siamese_cd_amd import trainers
+    from multimodal_siamese_cd_amd.utils import datasets, experiment_manager as em, networks
+    cfg_a = em.load_cfg('debug')
+    cfg_b = em.load_cfg('debug')
+    cfg_b.MODEL.PRECISION = 'bf16'
+    gen = torch.Generator(device=dev).manual_seed(4)
+    b = datasets.synthetic_batch(cfg_a, 2, dev, gen, 64)
+
+    def make(cfg):
+        torch.manual_seed(0)
+        return networks.create_network(cfg).to(dev).train()
+
+    def run(net, cfg):
+        net.zero_grad(set_to_none=True)
+        out = net(b['x_t1'], b['x_t2'])
+        trainers.step_loss(cfg, out, b).backward()
+        return out.detach().clone(), [p.grad.clone() for p in net.parameters()]
+
+    na, nb = make(cfg_a), make(cfg_b)
+    alone_a, alone_b = run(na, cfg_a), run(nb, cfg_b)
+    na, nb = make(cfg_a), make(cfg_b)
+    out_a = na(b['x_t1'], b['x_t2'])
+    out_b = nb(b['x_t1'], b['x_t2'])  # forward of b between a's forward and a's backward
+    trainers.step_loss(cfg_a, out_a, b).backward()
+    trainers.step_loss(cfg_b, out_b, b).backward()
+    assert torch.equal(out_a.detach(), alone_a[0]) and torch.equal(out_b.detach(), alone_b[0])
+    for p, g in zip(na.parameters(), alone_a[1]):
+        assert torch.equal(p.grad, g)
+    for p, g in zip(nb.parameters(), alone_b[1]):
+        assert torch.equal(p.grad, g)
+    assert rel(out_a.detach(), out_b.detach()) > 1e-4  # really two arithmetics

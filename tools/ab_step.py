@@ -3,17 +3,17 @@
     python tools/ab_step.py --variants "h16=1,w16=0" "h16=1,w16=1" [--rounds 6 --steps 8]
 
 A variant is a comma list of knob=value with knobs:
-  h16   scd_set_halo16 mode        w16   scd_set_wgrad16 mode
+  h16   halo16 tile mode (hip.set_halo16: 0 off, 1 auto, 2 + id forced)
+  tune  SCD_TUNE_* bits of every conv descriptor (hip.set_tune; decimal or 0x hex)
   fuse  engine BN-apply fusion into the consuming conv (engine.set_options(fuse_input_bn=...))
   fuse_bb  BN-backward partial sums in the data-grad epilogue (engine.set_options(fuse_bn_bwd=...))
   fuse_enc  fused Siamese encoder (engine.set_options(fuse_siamese_encoder=...))
-  math  conv arithmetic (hip.set_conv_math: f32 | x3 | bf16)
+  math  the model's conv arithmetic (model.conv_math: f32 | x3 | x5 | bf16 | h2)
   pack  weight packing: 0 per call, 1 cached per weight, 2 batched per model (engine.packed_conv3x3)
   pool_diff  encoder difference + next-level pooling in one pass (engine.set_options(pool_diff=...))
   pooled_bn_bwd  encoder BN backward forms maxpool_bwd -/+ diff grad on the fly (engine.set_options(...))
   defer_bn_bwd  input layer's BN backward formed inside its weight grad (engine.set_options(defer_bn_bwd=...))
   <engine option>=0|1  any other engine.set_options switch by name (e.g. fuse_head=0)
-  SCD_* library environment switches read at launch (e.g. SCD_HALO16_TW=64)
 Prints per-variant median / min ms per step over the rounds.
 """
 import argparse
@@ -33,18 +33,17 @@ from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_f
 _DEFAULT_OPTS = dict(engine._OPTS)
 
 
-def apply(variant: str):
-    """Every variant starts from the defaults: library switches, engine options and x3 math."""
-    for k in [k for k in os.environ if k.startswith('SCD_')]:
-        del os.environ[k]
-    hip.set_conv_math('x3')
+def apply(variant: str, model, math0: str):
+    """Every variant starts from the defaults: tune bits 0, engine options and the config's arithmetic."""
+    hip.set_tune(0)
+    model.conv_math = math0
     engine.set_options(**_DEFAULT_OPTS)
     for kv in filter(None, variant.split(',')):
         k, v = kv.split('=')
         if k == 'h16':
             hip.set_halo16(int(v))
-        elif k == 'w16':
-            hip.set_wgrad16(int(v))
+        elif k == 'tune':
+            hip.set_tune(hip.get_tune() | int(v, 0))
         elif k == 'fuse':
             engine.set_options(fuse_input_bn=bool(int(v)))
         elif k == 'fuse_bb':
@@ -52,7 +51,7 @@ def apply(variant: str):
         elif k == 'pack':  # 0 = per-call packing (no cache), 1 = per-weight cache, 2 = batched group cache
             engine.set_options(pack_cache=int(v) > 0, batch_pack=int(v) > 1)
         elif k == 'math':
-            hip.set_conv_math(v)
+            model.conv_math = v
         elif k == 'pool_diff':
             engine.set_options(pool_diff=bool(int(v)))
         elif k == 'pooled_bn_bwd':
@@ -63,8 +62,6 @@ def apply(variant: str):
             engine.set_options(fuse_siamese_encoder=bool(int(v)))
         elif k in engine._OPTS:  # any other engine option by name (e.g. fuse_head=0)
             engine.set_options(**{k: bool(int(v))})
-        elif k.startswith('SCD_'):  # library environment switch (read at launch)
-            os.environ[k] = v
         else:
             raise SystemExit(f'unknown knob {k}')
 
@@ -95,14 +92,15 @@ def main():
         opt.step()
 
     times = {v: [] for v in args.variants}
+    math0 = net.module.conv_math
     for v in args.variants:  # warm every variant (allocator, occupancy caches, clocks)
-        apply(v)
+        apply(v, net.module, math0)
         for _ in range(3):
             step()
     torch.cuda.synchronize()
     for r in range(args.rounds):
         for v in args.variants:
-            apply(v)
+            apply(v, net.module, math0)
             step()
             torch.cuda.synchronize()
             t0 = time.perf_counter()

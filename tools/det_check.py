@@ -27,7 +27,6 @@ def main():
     args = ap.parse_args()
     hip.load_library()
     dev = torch.device('cuda:0')
-    hip.set_conv_math(args.math)
     topo = [int(t) for t in args.topo.split(',')]
     ocfg = dict(TOPOLOGY=topo, IN_CHANNELS=5, OUT_CHANNELS=1, S1_BANDS=[0, 1], S2_BANDS=[2, 1, 0])
     P = O.deterministic_params(O.param_shapes('siameseunet', ocfg), 7)
@@ -36,6 +35,7 @@ def main():
     cfg.MODEL.TYPE, cfg.MODEL.IN_CHANNELS, cfg.MODEL.OUT_CHANNELS = 'siameseunet', 5, 1
     cfg.MODEL.TOPOLOGY = topo
     cfg.DATALOADER.S1_BANDS, cfg.DATALOADER.S2_BANDS = [0, 1], [2, 1, 0]
+    cfg.MODEL.CONV_MATH = args.math
     crit = loss_functions.get_criterion('PowerJaccardLoss')
     ref = None
     for run in range(args.runs):

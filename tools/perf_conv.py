@@ -60,8 +60,7 @@ def main():
                     help='conv arithmetic (default: library default; h2 gets absmax operand bounds)')
     ap.add_argument('--variants', default=None,
                     help='comma-separated variants, interleaved per layer; a variant is "+"-joined settings '
-                         'h16=<scd_set_halo16 mode>, w16=<scd_set_wgrad16 mode> or ENVVAR=value (read by the '
-                         'library at launch), e.g. h16=1+SCD_HALO16_DB=0,h16=1')
+                         'h16=<hip.set_halo16 mode> or tune=<SCD_TUNE_* bits, OR-ed>, e.g. h16=1+tune=0x100000,h16=1')
     args = ap.parse_args()
     hip.load_library()
     if args.math:
@@ -69,7 +68,6 @@ def main():
     print(f'conv math: {hip.conv_math()}')
     dev = torch.device('cuda:0')
     modes = [None] if args.variants is None else args.variants.split(',')
-    env_set = set()
     tots = {m: {'fwd': [0.0, 0.0], 'dgrad': [0.0, 0.0], 'wgrad': [0.0, 0.0]} for m in modes}
     print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"cin":>5s} {"cout":>5s} | '
           f'{"fwd ms":>8s} {"TF/s":>6s} | {"dgrad ms":>8s} {"TF/s":>6s} | {"wgrad ms":>8s} {"TF/s":>6s}')
@@ -92,20 +90,17 @@ def main():
             hip.absmax_bound(hip.nhwc(x), xb)
             hip.absmax_bound(hip.nhwc(dy), db)
         for mode in modes:
-            if mode is not None:
+            if mode is not None:  # every variant starts from tune 0
+                hip.set_tune(0)
                 for kv in mode.split('+'):
                     k, v = kv.split('=')
                     if k == 'h16':
                         hip.set_halo16(int(v))
-                    elif k == 'w16':
-                        hip.set_wgrad16(int(v))
+                    elif k == 'tune':
+                        hip.set_tune(hip.get_tune() | int(v, 0))
                     else:
-                        os.environ[k] = v
-                        env_set.add(k)
+                        raise SystemExit(f'unknown setting {k}')
             tot = tots[mode]
-            if mode is not None:  # settings not named by this variant go back to their defaults
-                for k in env_set - {kv.split('=')[0] for kv in mode.split('+')}:
-                    os.environ.pop(k, None)
             res = {}
             if args.only in (None, 'fwd'):
                 res['fwd'] = timeit(lambda: hip.conv_igemm(hip.nhwc(x), s, s, 1, hip.TAPS_3X3, wf, co, None,

@@ -1,5 +1,5 @@
 """Per-level timing of the decoder's ConvTranspose2d(2, s2) GEMMs (forward: 1 tap into the pixel-shuffled concat
-slice; data grad: 4 taps, stride 2): the per-tap x3 kernel under tile variants (SCD_X3_TILE), or with --math h2 the
+slice; data grad: 4 taps, stride 2): the per-tap x3 kernel under tile variants (SCD_TUNE_X3_TILE), or with --math h2 the
 gather16 kernel (source bounds given; --dst-bound also raises the concat bound in the forward, as the engine does).
 
     python tools/perf_convT.py [--batch 32] [--reps 10] [--tiles 0,1,2,4,5] [--math h2] [--dst-bound] [--plain]
@@ -65,10 +65,7 @@ def main():
             if args.dst_bound:
                 db = torch.zeros(1, device=dev)
         for t in tiles:
-            if t == '0':
-                os.environ.pop('SCD_X3_TILE', None)
-            else:
-                os.environ['SCD_X3_TILE'] = t
+            hip.set_tune(hip.tune_x3_tile(int(t)))  # 0: automatic
             f = timeit(lambda: hip.conv_igemm(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, bias, gup,
                                               store_mode=1, src_bound=xb, dst_bound=db), args.reps)
             d = timeit(lambda: hip.conv_igemm(gup, hc, hc, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx), src_bound=gb),
@@ -82,7 +79,7 @@ def main():
             tot[t][1] += d
             print(f'{name} hc={hc:4d} ci={ci:4d} co={co:4d} tile {t}: fwd {f * 1e3:7.1f} us  dgrad {d * 1e3:7.1f} us',
                   flush=True)
-    os.environ.pop('SCD_X3_TILE', None)
+    hip.set_tune(0)
     for t, (f, d) in tot.items():
         print(f'tile {t}: fwd {f * 1e3:7.1f} us  dgrad {d * 1e3:7.1f} us  sum {(f + d) * 1e3:7.1f} us')
 
