@@ -152,6 +152,7 @@ int scd_abi_version(void);
 #define SCD_TUNE_NO_WGRAD_H2      (1u << 24)  /* ConvTranspose weight grad on x3 instead of h2                    */
 #define SCD_TUNE_NO_HALO16_C16    (1u << 25)  /* input-layer forward on the per-tap x3 kernel                     */
 #define SCD_TUNE_NO_HALO          (1u << 26)  /* no halo kernels at all (per-tap kernels)                         */
+#define SCD_TUNE_HALO16_LATE_LOAD (1u << 27)  /* single-buffered halo16: next chunk's halo loaded at the last tap  */
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);
@@ -482,9 +483,16 @@ int scd_jaccard_multi_fwd(const scd_jaccard_term_t *terms, int32_t n_terms, cons
                           int64_t pixels, float *sums, float *loss, void *ws, size_t ws_bytes, scd_stream_t stream);
 int scd_jaccard_multi_bwd(const scd_jaccard_term_t *terms, int32_t n_terms, const uint8_t *labeled, int32_t n_samples,
                           int64_t pixels, const float *sums, const float *gloss, scd_stream_t stream);
+/* Exact-DataParallel form (one loss over the batch of all ranks, as nn.DataParallel's gathered-batch loss,
+ * utils/networks.py:27 + train_supervised.py:75): after the fwd call every rank all-reduces `sums` (SUM over ranks,
+ * caller's collective), then these re-form D = sum(p^2 + t^2) - I + 1e-6 and the loss from the global sums in place
+ * of the local ones; the bwd call then takes the global sums.  sums layout as the fwd call writes it. */
+int scd_jaccard_multi_loss_from_sums(const scd_jaccard_term_t *terms, int32_t n_terms, float *sums, float *loss,
+                                     scd_stream_t stream);
 size_t scd_pjaccard_workspace_bytes(int64_t n);
 int scd_pjaccard_fwd(const float *logits, const float *target, int64_t n, float *sums_out, float *loss_out,
                      void *ws, size_t ws_bytes, scd_stream_t stream);
+int scd_pjaccard_loss_from_sums(float *sums, float *loss, scd_stream_t stream);
 /* glogits = gloss * dL/dlogit; if gtarget != NULL also the soft-target grad (MMCR consistency loss,
  * train_semisupervised.py:107, where the target sigma(logits_s2) is not detached). */
 int scd_pjaccard_bwd(const float *logits, const float *target, int64_t n, const float *sums,

@@ -204,6 +204,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 
     const int nsteps = cpk * a.ntaps;
     constexpr int T_STORE = 4;  // DB: tap at which the prefetched halo is written to the other buffer
+    // single buffer: the tap at which the next chunk's halo loads are issued into registers (stored at the chunk end),
+    // 4 taps ahead so HBM latency hides behind 4 taps of MFMAs; SCD_TUNE_HALO16_LATE_LOAD: the last tap (A/B)
+    const int t_load = (a.tune & SCD_TUNE_HALO16_LATE_LOAD) || a.ntaps < 5 ? a.ntaps - 1 : a.ntaps - 5;
     u32x4 wq[WP][TN];
     load_A(0);
     load_W(0, 0, wq);
@@ -220,7 +223,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         if constexpr (DB) {
             if (t == 0 && cc + 1 < cpk) load_A(cc + 1);
         } else {
-            if (more && t1 == 0) load_A(cc1);
+            if (t == t_load && cc + 1 < cpk) load_A(cc + 1);
         }
         const unsigned char *const sbuf = smem + (DB ? (cc & 1) * (XP * PA) : 0);
         const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);

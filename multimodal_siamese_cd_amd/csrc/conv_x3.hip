@@ -939,13 +939,17 @@ void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hip
     }
 }
 
-// h2 (both operand bounds given, SCD_MATH_H2): the ConvTranspose weight grad's tiles.
-bool wgrad_x3_h2_tile(int tile_id) { return tile_id == 0 || tile_id == 1; }
+// h2 (both operand bounds given, SCD_MATH_H2): every tile of the generic weight grad (the ConvTranspose weight grads
+// and the 3x3 weight grads outside the halo kernels, e.g. a 32-channel source).
+bool wgrad_x3_h2_tile(int tile_id) { return tile_id >= 0 && tile_id <= 4; }
 void launch_wgrad_x3_h2(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s) {
-    if (tile_id == 0)
-        hipLaunchKernelGGL((wgrad_x3<2, 2, 2, 2, 4>), grid, block, 0, s, a);
-    else
-        hipLaunchKernelGGL((wgrad_x3<1, 4, 2, 2, 4>), grid, block, 0, s, a);
+    switch (tile_id) {
+        case 0: hipLaunchKernelGGL((wgrad_x3<2, 2, 2, 2, 4>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((wgrad_x3<1, 4, 2, 2, 4>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((wgrad_x3<2, 2, 1, 3, 4>), grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((wgrad_x3<2, 1, 1, 3, 4>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((wgrad_x3<1, 4, 1, 1, 4>), grid, block, 0, s, a); break;
+    }
 }
 
 // Fragment-major pre-split weights: dst[p][nb][ks][lane][8] (bf16 bits of term p), the B-operand fragment of

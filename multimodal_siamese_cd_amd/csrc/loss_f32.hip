@@ -120,6 +120,23 @@ __global__ void jaccard_multi_bwd_kernel(JTerms terms, const uint8_t *__restrict
     }
 }
 
+// The exact-DataParallel loss (utils/networks.py:27 with train_supervised.py:75: ONE loss over the gathered batch):
+// each rank's per-term records {I, S = sum(p^2 + t^2), D, count} (stride 4; the single-term form: {I, S, D}, stride
+// 3) are summed over the ranks, then D = S - I + 1e-6 and the loss are re-formed from the global sums exactly as
+// the finalize kernels form them from one device's partial sums.
+__global__ void jaccard_loss_from_sums(JTerms terms, int stride, float *sums, float *loss) {
+    if (threadIdx.x != 0) return;
+    float total = 0.f;
+    for (int k = 0; k < terms.n; ++k) {
+        float *r = sums + k * stride;
+        const float If = r[0];
+        const float Df = r[1] - If + 1e-6f;
+        r[2] = Df;
+        if (stride < 4 || r[3] > 0.f) total += terms.t[k].coef * (1.f - If / Df);
+    }
+    loss[0] = total;
+}
+
 static int jt_load(const scd_jaccard_term_t *terms, int n_terms, JTerms &jt, const char *what) {
     if (!terms || n_terms < 1 || n_terms > JT_MAX) {
         set_error("%s: 1..%d terms", what, JT_MAX);
@@ -184,4 +201,31 @@ extern "C" int scd_jaccard_multi_bwd(const scd_jaccard_term_t *terms, int32_t n_
     hipLaunchKernelGGL(jaccard_multi_bwd_kernel, dim3(unsigned(blocks), n_terms), dim3(256), 0, as_stream(stream), jt,
                        labeled, n_samples, pixels, sums, gloss);
     return launch_status("scd_jaccard_multi_bwd");
+}
+
+extern "C" int scd_jaccard_multi_loss_from_sums(const scd_jaccard_term_t *terms, int32_t n_terms, float *sums,
+                                                float *loss, scd_stream_t stream) {
+    clear_error();
+    JTerms jt;
+    SCD_TRY(jt_load(terms, n_terms, jt, "jaccard_multi_loss_from_sums"));
+    if (!sums || !loss) {
+        set_error("jaccard_multi_loss_from_sums: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    hipLaunchKernelGGL(jaccard_loss_from_sums, dim3(1), dim3(64), 0, as_stream(stream), jt, 4, sums, loss);
+    return launch_status("scd_jaccard_multi_loss_from_sums");
+}
+
+extern "C" int scd_pjaccard_loss_from_sums(float *sums, float *loss, scd_stream_t stream) {
+    clear_error();
+    if (!sums || !loss) {
+        set_error("pjaccard_loss_from_sums: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    JTerms jt;
+    jt.n = 1;
+    jt.t[0] = scd_jaccard_term_t{};
+    jt.t[0].coef = 1.f;
+    hipLaunchKernelGGL(jaccard_loss_from_sums, dim3(1), dim3(64), 0, as_stream(stream), jt, 3, sums, loss);
+    return launch_status("scd_pjaccard_loss_from_sums");
 }

@@ -4,7 +4,8 @@ Each Function runs a whole stage of the reference's forward (utils/networks.py) 
 calls on NHWC fp32 device buffers, and its backward as the reverse sequence:
 
   pack_pair / pack_stream  input NCHW -> NHWC (+ channel padding)        train_supervised.py:68-69
-  EncoderFn                InConv + Encoder (Down x L)                    networks.py:313-343, 405-426
+  EncoderLevelFn           one level of InConv + Encoder (Down x L)       networks.py:313-343, 405-426
+  SiameseLevelFn           the same on the t1/t2 pair batch, + f_t2 - f_t1 networks.py:141-150
   SiameseDiffFn            f_t2 - f_t1                                     networks.py:147-150
   DecoderFn                Up x L (ConvT -> cat -> DoubleConv)             networks.py:346-382, 429-451
   HeadFn                   OutConv 1x1                                     networks.py:454-461
@@ -17,6 +18,7 @@ exactly: per-branch batch statistics, two running-stat updates (t1 first), summe
 """
 from __future__ import annotations
 
+import contextlib
 import weakref
 from dataclasses import dataclass
 
@@ -56,7 +58,7 @@ def set_options(**kw) -> dict:
     (forward and weight-grad) instead of materialising the activation.
     fuse_bn_bwd: compute the first BatchNorm's backward partial sums in the epilogue of the data-grad conv that
     produces its incoming gradient, instead of a separate pass.
-    fuse_siamese_encoder: Siamese streams run SiameseEncoderFn (BN1 + ReLU fused into the next MaxPool and the
+    fuse_siamese_encoder: Siamese streams run SiameseLevelFn (BN1 + ReLU fused into the next MaxPool and the
     feature difference, differences written into the decoder's concat buffers).
     defer_bn_bwd: the input layer's BatchNorm backward stops at its statistics and the weight grad (its only
     reader) forms dy while staging, so that gradient is never written.
@@ -262,6 +264,28 @@ def flush_bn_counters() -> None:
         torch._foreach_add_(ts, inc)
 
 
+# Instrumentation for the parity tests (tests/_parity.py BranchMatch): while trace_bn() is open, every BatchNorm
+# forward appends (module, conv output y, scale, shift, nseg) -- the values the ReLU decisions fma(y, scale, shift)
+# > 0 and the MaxPool2d argmaxes of this forward are taken from, so a CPU oracle can follow the same branches.
+_BN_TRACE: list | None = None
+
+
+@contextlib.contextmanager
+def trace_bn():
+    global _BN_TRACE
+    prev, _BN_TRACE = _BN_TRACE, []
+    try:
+        yield _BN_TRACE
+    finally:
+        _BN_TRACE = prev
+
+
+def _traced(bn, y: torch.Tensor, st: '_BNSaved') -> '_BNSaved':
+    if _BN_TRACE is not None:
+        _BN_TRACE.append((bn, y.detach().clone(), st.scale.clone(), st.shift.clone(), st.nseg))
+    return st
+
+
 def _bn_uses_batch_stats(bn: torch.nn.BatchNorm2d, training: bool) -> bool:
     return training or not bn.track_running_stats or bn.running_mean is None
 
@@ -292,12 +316,12 @@ def _bn_forward(y: torch.Tensor, bn: torch.nn.BatchNorm2d, nseg: int, training: 
                                bn.running_var, smean, sinv, scale, shift, ws, act_bound=bound)
         if update:
             _NBT_PENDING.append((bn.num_batches_tracked, nseg))
-        return _BNSaved(smean, sinv, scale, shift, nseg)
+        return _traced(bn, y, _BNSaved(smean, sinv, scale, shift, nseg))
     scale, shift = _empty((c,), y), _empty((c,), y)
     hip.bn_eval_coeffs(c, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, scale, shift)
     if bound is not None:
         hip.absmax_bound(nhwc(y), bound, 1, scale, shift)
-    return _BNSaved(None, None, scale, shift, 1)
+    return _traced(bn, y, _BNSaved(None, None, scale, shift, 1))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -566,73 +590,76 @@ def encoder_blocks(inc, encoder) -> list:
     return [inc.conv] + [down.mpconv[1] for down in encoder.down_seq.values()]
 
 
-class EncoderFn(torch.autograd.Function):
+# One autograd Function per encoder level (InConv = level 0, Down{k} = level k).  A level's parameter gradients are
+# therefore final as soon as that level's backward returns -- the deepest level first -- and DDP can all-reduce them
+# while the shallower levels' backward still runs (one Function for the whole encoder would hand every encoder
+# gradient, 64% of the model's, to DDP only at the very end of the backward).  Each level also produces the next
+# level's pooled input, so its backward receives the pooled gradient and the skip / difference gradient together and
+# forms dL/da = maxpool_bwd(g_pool) +/- g_skip inside its BatchNorm backward (scd_bn_relu_backward_pooled).
+def _level_grad(g_pool, idx, g_skip, skip_mode: int, like: torch.Tensor):
+    """The incoming gradient of a level's output activation: a _PooledGrad formed inside the BatchNorm backward, or
+    (engine option pooled_bn_bwd off) materialised by scd_feature_grad."""
+    if _OPTS['pooled_bn_bwd'] and (g_pool is not None or g_skip is not None):
+        return _PooledGrad(g_pool, idx if g_pool is not None else None, g_skip, skip_mode)
+    ga = torch.empty_like(like)
+    hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL, idx if g_pool is not None else None,
+                     nhwc(g_skip) if g_skip is not None else hip._NULL, skip_mode, nhwc(ga))
+    return ga
+
+
+class EncoderLevelFn(torch.autograd.Function):
+    """One level of InConv + Encoder (networks.py:313-343, 405-426) on one BatchNorm-segmented batch: the level's
+    DoubleConv output activation a (materialised: it is a decoder skip) and, below the deepest level, the next level's
+    input MaxPool2d(a) with its argmax bytes.  meta.x_bound (h2) bounds the input; meta.out_bound receives a's."""
+
     @staticmethod
     def forward(ctx, x, meta, *params):
         ctx.set_materialize_grads(False)
         meta.scope = (hip.conv_math(), hip.conv_tune())
-        blocks = meta.blocks
-        feats, saved = [], []
-        cur = x
-        pool, bound = _bounds(x), None
-        for level, dc in enumerate(blocks):
-            idx = None
-            if level > 0:
-                prev = feats[-1]
-                n, h, w, c = prev.shape
-                cur = _empty((n, h // 2, w // 2, c), prev)
-                idx = _empty((n, h // 2, w // 2, c), prev, dtype=torch.uint8)
-                hip.maxpool2_fwd(nhwc(prev), nhwc(cur), idx)  # the pooled map keeps the level's bound
-            a, sv, _, _, bound = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save, pool=pool, x_bound=bound)
-            feats.append(a)
-            saved.append((idx, sv))
+        a, sv, _, _, bound = _dc_forward(x, meta.dc, meta.nseg, meta.training, meta.save, pool=meta.pool,
+                                         x_bound=meta.x_bound)
+        meta.out_bound = bound
+        outs, idx = (a,), None
+        if not meta.last:
+            n, h, w, c = a.shape
+            nxt = _empty((n, h // 2, w // 2, c), a)
+            idx = _empty((n, h // 2, w // 2, c), a, dtype=torch.uint8)
+            hip.maxpool2_fwd(nhwc(a), nhwc(nxt), idx)  # the pooled map keeps the level's bound
+            outs = (a, nxt)
         if meta.save:
-            ctx.meta = meta
-            ctx.saved = saved
-            ctx.feat_shapes = [f.shape for f in feats]
-        return tuple(feats)
+            ctx.meta, ctx.saved = meta, (sv, idx)
+        return outs
 
     @staticmethod
-    def backward(ctx, *g_feats):
-        with hip.conv_scope(*ctx.meta.scope):
-            return EncoderFn._backward(ctx, *g_feats)
-
-    @staticmethod
-    def _backward(ctx, *g_feats):
-        meta, saved = ctx.meta, ctx.saved
-        blocks = meta.blocks
-        L = len(blocks) - 1
-        grads = [None] * (8 * len(blocks))
-        g_pool = None
-        dev_like = saved[0][1][1]
-        pool = _bounds(dev_like)
-        for level in range(L, -1, -1):
-            shape = ctx.feat_shapes[level]
-            idx_next = saved[level + 1][0] if level < L else None
-            gf = g_feats[level]
-            if _OPTS['pooled_bn_bwd'] and (g_pool is not None or gf is not None):
-                ga = _PooledGrad(g_pool, idx_next if g_pool is not None else None, gf, 0)
-            else:
-                ga = _empty(tuple(shape), dev_like)
-                hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL,
-                                 idx_next if g_pool is not None else None, nhwc(gf) if gf is not None else hip._NULL,
-                                 0, nhwc(ga))
-            gx, pg = _dc_backward(ga, saved[level][1], blocks[level], need_dx=level > 0, pool=pool)
-            grads[8 * level:8 * level + 8] = pg
-            g_pool = gx
+    def backward(ctx, g_a, g_next=None):
+        meta = ctx.meta
+        with hip.conv_scope(*meta.scope):
+            sv, idx = ctx.saved
+            ga = _level_grad(g_next, idx, g_a, 0, sv[4])
+            gx, pg = _dc_backward(ga, sv, meta.dc, need_dx=ctx.needs_input_grad[0], pool=_bounds(sv[4]))
         ctx.saved = None
-        return (None, None, *grads)
+        return (gx, None, *pg)
 
 
 def run_encoder(inc, encoder, x: torch.Tensor, nseg: int, training: bool) -> list:
+    """InConv + Encoder: the level activations, level 0 first (Encoder.forward returns them reversed)."""
     blocks = encoder_blocks(inc, encoder)
-    params = [p for dc in blocks for p in dc_params(dc)]
-    save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
-    meta = _Meta(blocks=blocks, nseg=nseg, training=training, save=save)
+    pool, bound = _bounds(x), None
+    feats, cur = [], x
     try:
-        return list(EncoderFn.apply(x, meta, *params))
+        for level, dc in enumerate(blocks):
+            params = dc_params(dc)
+            save = torch.is_grad_enabled() and (cur.requires_grad or any(p.requires_grad for p in params))
+            meta = _Meta(dc=dc, nseg=nseg, training=training, save=save, last=level == len(blocks) - 1, pool=pool,
+                         x_bound=bound)
+            outs = EncoderLevelFn.apply(cur, meta, *params)
+            feats.append(outs[0])
+            bound = meta.out_bound
+            if not meta.last:
+                cur = outs[1]
     finally:
         flush_bn_counters()
+    return feats
 
 
 # ------------------------------------------------------------------------------------------------
@@ -645,103 +672,74 @@ def _two_seg(st: _BNSaved):
     return torch.cat([st.scale, st.scale]), torch.cat([st.shift, st.shift])
 
 
-class SiameseEncoderFn(torch.autograd.Function):
-    """InConv + Encoder on the 2B-image pair batch, returning f_t2 - f_t1 per level (networks.py:141-150).
+class SiameseLevelFn(torch.autograd.Function):
+    """One level of InConv + Encoder on the 2B-image pair batch, returning f_t2 - f_t1 (networks.py:141-150) and,
+    below the deepest level, the next level's pooled input.
 
-    Each level's output activation relu(BN1(y1)) is never materialised: the next level's MaxPool2d and the
-    difference read y1 through BN1 + ReLU.  A level's difference is written into channels [0, C) of the
-    decoder's concat buffer when `meta.extra[level]` names its ConvT channels (zero-copy cat, networks.py:449).
-    Backward: one pass per level forms dL/da1 = maxpool_bwd(g_pool) -/+ g_diff (t1/t2)."""
+    The level's output activation relu(BN1(y1)) is never materialised: the difference and the next level's
+    MaxPool2d read y1 through BN1 + ReLU (one pass, scd_bn_relu_pool_diff, for even maps).  The difference is written
+    into channels [0, C) of the decoder's concat buffer when meta.extra names its ConvT channels (zero-copy cat,
+    networks.py:449).  Backward: dL/da1 = maxpool_bwd(g_pool) -/+ g_diff (t1/t2), formed in the BatchNorm backward."""
 
     @staticmethod
     def forward(ctx, x, meta, *params):
         ctx.set_materialize_grads(False)
         meta.scope = (hip.conv_math(), hip.conv_tune())
-        blocks = meta.blocks
-        diffs, saved, bufs = [], [], []
-        cur = x
-        prev = None  # (y1, st1) of the previous level
-        pooled = None  # (pooled input, idx) of this level when the previous level's fused pass produced them
-        pool, bound = _bounds(x), None  # h2: bound of the previous level's activation = of this level's input
-        for level, dc in enumerate(blocks):
-            idx = None
-            if pooled is not None:
-                cur, idx = pooled
-            elif level > 0:
-                y1p, st1p = prev
-                n, h, w, c = y1p.shape
-                cur = _empty((n, h // 2, w // 2, c), y1p)
-                idx = _empty((n, h // 2, w // 2, c), y1p, dtype=torch.uint8)
-                hip.bn_relu_maxpool2_fwd(nhwc(y1p), st1p.nseg, st1p.scale, st1p.shift, nhwc(cur), idx)
-            _, sv, y1, st1, bound = _dc_forward(cur, dc, meta.nseg, meta.training, meta.save, materialize=False,
-                                                pool=pool, x_bound=bound)
-            n2, h, w, c = y1.shape
-            extra = meta.extra.get(level, 0)
-            buf = _empty((n2 // 2, h, w, c + extra), y1)
-            d = buf[..., :c] if extra else buf
-            sc, sh = _two_seg(st1)
-            pooled = None
-            if level + 1 < len(blocks) and h % 2 == 0 and w % 2 == 0 and _OPTS['pool_diff']:
-                # the difference and the next level's pooling in one read of y1
-                nxt = _empty((n2, h // 2, w // 2, c), y1)
-                nidx = _empty((n2, h // 2, w // 2, c), y1, dtype=torch.uint8)
-                hip.bn_relu_pool_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c), nhwc(nxt), nidx)
-                pooled = (nxt, nidx)
-            else:
-                hip.bn_relu_siamese_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c))
-            diffs.append(_set_bound(d, bound))  # |a_t2 - a_t1| <= max(a_t1, a_t2) for ReLU outputs
-            bufs.append(buf if extra else None)
-            saved.append((idx, sv))
-            prev = (y1, st1)
-        meta.cat_buffers = bufs
+        _, sv, y1, st1, bound = _dc_forward(x, meta.dc, 2, meta.training, meta.save, materialize=False,
+                                            pool=meta.pool, x_bound=meta.x_bound)
+        meta.out_bound = bound
+        n2, h, w, c = y1.shape
+        buf = _empty((n2 // 2, h, w, c + meta.extra), y1)
+        d = buf[..., :c] if meta.extra else buf
+        sc, sh = _two_seg(st1)
+        idx = nxt = None
+        if not meta.last:
+            nxt = _empty((n2, h // 2, w // 2, c), y1)
+            idx = _empty((n2, h // 2, w // 2, c), y1, dtype=torch.uint8)
+        if nxt is not None and h % 2 == 0 and w % 2 == 0 and _OPTS['pool_diff']:
+            hip.bn_relu_pool_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c), nhwc(nxt), idx)  # one read of y1
+        else:
+            hip.bn_relu_siamese_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c))
+            if nxt is not None:
+                hip.bn_relu_maxpool2_fwd(nhwc(y1), st1.nseg, st1.scale, st1.shift, nhwc(nxt), idx)
+        _set_bound(d, bound)  # |a_t2 - a_t1| <= max(a_t1, a_t2) for ReLU outputs
+        meta.buf = buf if meta.extra else None
         if meta.save:
-            ctx.meta = meta
-            ctx.saved = saved
-        return tuple(diffs)
+            ctx.meta, ctx.saved = meta, (sv, idx)
+        return (d,) if nxt is None else (d, nxt)
 
     @staticmethod
-    def backward(ctx, *g_diffs):
-        with hip.conv_scope(*ctx.meta.scope):
-            return SiameseEncoderFn._backward(ctx, *g_diffs)
-
-    @staticmethod
-    def _backward(ctx, *g_diffs):
-        meta, saved = ctx.meta, ctx.saved
-        blocks = meta.blocks
-        L = len(blocks) - 1
-        grads = [None] * (8 * len(blocks))
-        g_pool = None
-        pool = _bounds(saved[0][1][1])
-        for level in range(L, -1, -1):
-            idx_next = saved[level + 1][0] if level < L else None
-            sv = saved[level][1]
-            y1 = sv[4]
-            gd = g_diffs[level]
-            if _OPTS['pooled_bn_bwd'] and (g_pool is not None or gd is not None):
-                ga = _PooledGrad(g_pool, idx_next if g_pool is not None else None, gd, 1)
-            else:
-                ga = torch.empty_like(y1)
-                hip.feature_grad(nhwc(g_pool) if g_pool is not None else hip._NULL,
-                                 idx_next if g_pool is not None else None, nhwc(gd) if gd is not None else hip._NULL,
-                                 1, nhwc(ga))
-            gx, pg = _dc_backward(ga, sv, blocks[level], need_dx=level > 0, pool=pool)
-            grads[8 * level:8 * level + 8] = pg
-            g_pool = gx
+    def backward(ctx, g_d, g_next=None):
+        meta = ctx.meta
+        with hip.conv_scope(*meta.scope):
+            sv, idx = ctx.saved
+            ga = _level_grad(g_next, idx, g_d, 1, sv[4])
+            gx, pg = _dc_backward(ga, sv, meta.dc, need_dx=ctx.needs_input_grad[0], pool=_bounds(sv[4]))
         ctx.saved = None
-        return (None, None, *grads)
+        return (gx, None, *pg)
 
 
 def run_siamese_encoder(inc, encoder, x: torch.Tensor, training: bool, extra: dict | None = None):
     """Feature differences per level (level 0 first) and the concat buffers they live in (None where plain)."""
     blocks = encoder_blocks(inc, encoder)
-    params = [p for dc in blocks for p in dc_params(dc)]
-    save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
-    meta = _Meta(blocks=blocks, nseg=2, training=training, save=save, extra=extra or {})
+    extra = extra or {}
+    pool, bound = _bounds(x), None
+    diffs, bufs, cur = [], [], x
     try:
-        diffs = list(SiameseEncoderFn.apply(x, meta, *params))
+        for level, dc in enumerate(blocks):
+            params = dc_params(dc)
+            save = torch.is_grad_enabled() and (cur.requires_grad or any(p.requires_grad for p in params))
+            meta = _Meta(dc=dc, training=training, save=save, last=level == len(blocks) - 1, pool=pool,
+                         x_bound=bound, extra=extra.get(level, 0))
+            outs = SiameseLevelFn.apply(cur, meta, *params)
+            diffs.append(outs[0])
+            bufs.append(meta.buf)
+            bound = meta.out_bound
+            if not meta.last:
+                cur = outs[1]
     finally:
         flush_bn_counters()
-    return diffs, meta.cat_buffers
+    return diffs, bufs
 
 
 # ------------------------------------------------------------------------------------------------
@@ -859,6 +857,8 @@ class DecoderFn(torch.autograd.Function):
         g = g_out
         if g is None:
             return (None, None, *g_skips, *grads, *head_grads)
+        if meta.head is None:
+            g = g.contiguous()  # e.g. the gradient of a permuted (NCHW) view of the output, from a standalone Up
         pool = _bounds(g)
         if meta.head is not None:
             y1, st1, w2, n_out, wshape, has_bias = ctx.head
@@ -991,7 +991,7 @@ def run_head(outc, x: torch.Tensor) -> torch.Tensor:
 # ------------------------------------------------------------------------------------------------
 # Standalone building blocks (DoubleConv / InConv / Down, networks.py:386-426) for callers that use a block on its
 # own (e.g. assessment_semantics.py:34 calls net.outc_sem_change directly).  The model forwards do not come here:
-# they run whole stages (EncoderFn, SiameseEncoderFn, DecoderFn).
+# they run whole stages (EncoderLevelFn, SiameseLevelFn, DecoderFn).
 # ------------------------------------------------------------------------------------------------
 def to_nhwc(x: torch.Tensor, c_pad: int | None = None) -> torch.Tensor:
     """NCHW -> contiguous NHWC fp32 (zero channels up to c_pad), differentiable."""
@@ -1088,6 +1088,19 @@ def cat_channels(*xs) -> torch.Tensor:
 # ------------------------------------------------------------------------------------------------
 # power_jaccard_loss
 # ------------------------------------------------------------------------------------------------
+# Exact-DataParallel loss (parallel.wrap_ddp(exact_dataparallel=True)): a callable that SUM-all-reduces a device
+# tensor in place across the ranks, applied to the loss kernels' partial sums, so every rank forms ONE loss over the
+# batch of all ranks, as nn.DataParallel's gathered-batch loss does (utils/networks.py:27, train_supervised.py:75).
+_LOSS_ALLREDUCE = None
+
+
+def set_loss_allreduce(fn):
+    """Install (fn) or remove (None) the cross-rank reduction of the loss sums; returns the previous one."""
+    global _LOSS_ALLREDUCE
+    prev, _LOSS_ALLREDUCE = _LOSS_ALLREDUCE, fn
+    return prev
+
+
 class PJaccardFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target):
@@ -1099,6 +1112,9 @@ class PJaccardFn(torch.autograd.Function):
         loss = _empty((), logits)
         ws = _ws(hip.pjaccard_workspace_bytes(logits.numel()), logits)
         hip.pjaccard_fwd(logits, target, sums, loss, ws)
+        if _LOSS_ALLREDUCE is not None:  # global {I, sum(p^2 + t^2)}, then D and the loss re-formed from them
+            _LOSS_ALLREDUCE(sums)
+            hip.pjaccard_loss_from_sums(sums, loss)
         ctx.save_for_backward(logits, target, sums)
         return loss
 
@@ -1138,6 +1154,9 @@ class MultiJaccardFn(torch.autograd.Function):
         sums = _empty((len(spec), 4), ts[0])
         loss = _empty((), ts[0])
         hip.jaccard_multi_fwd(terms, lab, n_samples, pixels, sums, loss)
+        if _LOSS_ALLREDUCE is not None:  # exact-DataParallel: every term over the samples of all ranks
+            _LOSS_ALLREDUCE(sums)
+            hip.jaccard_multi_loss_from_sums(terms, sums, loss)
         ctx.spec, ctx.dims = spec, (n_samples, pixels)
         ctx.save_for_backward(lab, sums, *ts)
         return loss

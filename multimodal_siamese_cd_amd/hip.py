@@ -173,6 +173,8 @@ _SIGS = {
     "scd_pjaccard_workspace_bytes": ([c_int64], c_size_t),
     "scd_pjaccard_fwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
     "scd_pjaccard_bwd": ([c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "scd_pjaccard_loss_from_sums": ([c_void_p, c_void_p, c_void_p], c_int),
+    "scd_jaccard_multi_loss_from_sums": ([c_void_p, c_int32, c_void_p, c_void_p, c_void_p], c_int),
     "scd_window_copy": ([NHWC, NHWC, c_int32, c_int32, c_void_p], c_int),
     "scd_window_label_sums": ([c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_augment_apply": ([c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -388,6 +390,7 @@ TUNE_NO_WGRAD_C16 = 1 << 23
 TUNE_NO_WGRAD_H2 = 1 << 24
 TUNE_NO_HALO16_C16 = 1 << 25
 TUNE_NO_HALO = 1 << 26
+TUNE_HALO16_LATE_LOAD = 1 << 27
 
 
 def tune_halo16_cfg(tile_id: int) -> int:
@@ -780,6 +783,11 @@ def pjaccard_bwd(logits, target, sums, gloss, glogits, gtarget=None):
                                   _ptr(gloss), glogits.data_ptr(), _ptr(gtarget), _stream()), "scd_pjaccard_bwd")
 
 
+def pjaccard_loss_from_sums(sums, loss):
+    """Re-form D and the loss from (all-reduced) sums {I, sum(p^2 + t^2), D} in place (exact-DataParallel loss)."""
+    _check(lib().scd_pjaccard_loss_from_sums(sums.data_ptr(), loss.data_ptr(), _stream()), "scd_pjaccard_loss_from_sums")
+
+
 def window_copy(src: NHWC, dst: NHWC, oy: int, ox: int):
     """dst[n, y, x] = src[n, y + oy, x + ox] where it exists, else 0 (Up's F.pad and its backward crop)."""
     _check(lib().scd_window_copy(src, dst, oy, ox, _stream()), "scd_window_copy")
@@ -865,3 +873,10 @@ def augment_apply(tiles: list, crop: int, params: torch.Tensor, scale=None, gamm
     _check(lib().scd_augment_apply(ptrs.data_ptr(), hw.data_ptr(), B, C, crop, params.data_ptr(), _ptr(sc), _ptr(gm),
                                    out.data_ptr(), _stream()), "scd_augment_apply")
     return out
+
+
+def jaccard_multi_loss_from_sums(terms, sums, loss):
+    """The multi-term loss re-formed from (all-reduced) per-term sums [n_terms][4] (exact-DataParallel loss)."""
+    arr = _jterms(terms)
+    _check(lib().scd_jaccard_multi_loss_from_sums(ctypes.cast(arr, c_void_p), len(terms), sums.data_ptr(),
+                                                  loss.data_ptr(), _stream()), "scd_jaccard_multi_loss_from_sums")

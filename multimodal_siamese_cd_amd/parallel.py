@@ -3,7 +3,7 @@
 Replaces the reference's single-process `nn.DataParallel(model)` (utils/networks.py:27).  Each rank owns a
 full replica and its own shard of image pairs (independent synthetic generator seeded per rank); the only
 data-path collective is the gradient all-reduce that DistributedDataParallel buckets and launches as the
-Siamese stage Functions return their gradients.  BatchNorm statistics stay per rank (like DataParallel's
+stage Functions (one per encoder level, then the decoder) return their gradients.  BatchNorm statistics stay per rank (like DataParallel's
 per-replica statistics) and running statistics are broadcast from rank 0 each forward
 (`broadcast_buffers=True`, DataParallel's replica-0 semantics, torch/nn/parallel/data_parallel.py:88-90).
 """
@@ -60,13 +60,55 @@ def params_outside_forward(module) -> tuple:
     return tuple(getattr(module, 'PARAMS_OUTSIDE_FORWARD', ()))
 
 
-def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 64, find_unused_parameters: bool | None = None):
+def allreduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place SUM over the ranks (the exact-DataParallel loss sums)."""
+    if is_distributed():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+def sum_allreduce_hook(process_group, bucket):
+    """DDP communication hook: gradient buckets SUMMED over the ranks (DDP's default divides by the world size).
+    With one global loss per step (exact-DataParallel mode) each rank's gradient is its shard's part of the global
+    gradient, and nn.DataParallel reduce-adds the replicas' gradients (torch/nn/parallel/data_parallel.py)."""
+    group = process_group if process_group is not None else dist.group.WORLD
+    fut = dist.all_reduce(bucket.buffer(), group=group, async_op=True).get_future()
+    return fut.then(lambda f: f.value()[0])
+
+
+def global_sums(local: torch.Tensor) -> torch.Tensor:
+    """The SUM over ranks of `local`, differentiable with the identity gradient to `local` (d global / d local = 1
+    per rank): the torch form of the exact-DataParallel loss sums, for losses written in torch (tests, oracle)."""
+    if not is_distributed():
+        return local
+    tot = local.detach().clone()
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    return local + (tot - local.detach())
+
+
+def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 16, find_unused_parameters: bool | None = None,
+             exact_dataparallel: bool = False):
     """Replace the DataParallel-style wrapper's pass-through by DDP when running under torchrun.
 
     Keeps the `.module` attribute and `module.` state_dict prefix of the reference's wrapper.
+
+    Overlap.  The encoder runs one autograd Function per level (engine.EncoderLevelFn / SiameseLevelFn), so a level's
+    gradients reach DDP when that level's backward returns, deepest level first.  16 MB buckets (SiameseUNet: 59 MB
+    of fp32 gradients, the decoder's 21 MB ready together, then down4 19 MB, down3 14 MB, ...) let the all-reduce of
+    each bucket run on RCCL's stream while the shallower, costlier levels' backward continues; only the last bucket
+    (the shallow levels, < 4 MB) is exposed.
     `find_unused_parameters=None` turns DDP's unused-parameter search on only for a model that declares
     parameters outside its forward graph (`params_outside_forward`).  Without it, the bucket holding such a
     parameter is never reduced, the replicas drift apart and the next step raises.
+
+    Loss semantics.  Default (the throughput mode): every rank takes power_jaccard_loss over its own shard and DDP
+    averages the gradients, i.e. the gradient of the MEAN of the per-shard losses.  The reference's nn.DataParallel
+    takes ONE loss over the gathered batch (utils/networks.py:27, train_supervised.py:75), a different function of
+    the logits (Jaccard is a ratio of batch sums: 7e-6 apart at bs=2).  exact_dataparallel=True reproduces
+    it: the loss kernels' partial sums (I, sum p^2 + t^2 per term) are SUM-all-reduced before the loss is formed
+    (engine.set_loss_allreduce, three floats per term), and the gradient buckets are SUMMED (sum_allreduce_hook).
+    BatchNorm statistics stay per rank and running statistics come from rank 0 (broadcast_buffers) in both modes,
+    as DataParallel's per-replica statistics with replica 0's buffers.
     """
     if not is_distributed():
         return wrapper
@@ -74,9 +116,14 @@ def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 64, find_unused_paramete
     if find_unused_parameters is None:
         find_unused_parameters = bool(params_outside_forward(module))
     ids = [device.index] if (device is not None and device.type == 'cuda') else None
-    return torch.nn.parallel.DistributedDataParallel(module, device_ids=ids, broadcast_buffers=True,
-                                                     bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
-                                                     find_unused_parameters=find_unused_parameters)
+    ddp = torch.nn.parallel.DistributedDataParallel(module, device_ids=ids, broadcast_buffers=True,
+                                                    bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
+                                                    find_unused_parameters=find_unused_parameters)
+    if exact_dataparallel:
+        from . import engine
+        ddp.register_comm_hook(None, sum_allreduce_hook)
+        engine.set_loss_allreduce(allreduce_sum_)
+    return ddp
 
 
 def allreduce_max(value: float, device) -> float:

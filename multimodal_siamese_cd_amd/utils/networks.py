@@ -111,7 +111,7 @@ class _HipNet(nn.Module):
 def _stream(inc, encoder, decoder, x, nseg, training, siamese, head=None):
     """inc + encoder (+ Siamese diff) + decoder of one stream; returns (decoder output, features).  With `head` (the
     OutConv that is the decoder output's only reader) the first item is the head's logits (engine.run_decoder)."""
-    if siamese and engine.option('fuse_siamese_encoder'):  # networks.py:141-150, fused (engine.SiameseEncoderFn)
+    if siamese and engine.option('fuse_siamese_encoder'):  # networks.py:141-150, fused (engine.SiameseLevelFn)
         n_levels = len(encoder.down_seq) + 1
         diffs, bufs = engine.run_siamese_encoder(inc, encoder, x, training,
                                                  engine.decoder_cat_channels(decoder, n_levels))

@@ -58,6 +58,36 @@ def decoder_layers(topology):
 # blocks
 # --------------------------------------------------------------------------------------------------
 RECORD = None  # set to a list to capture (bn key, pre-activation) pairs (used to find ReLU-kink pixels)
+# Branch matching (test infrastructure, tests/_parity.py BranchMatch): BRANCH(bn key, pre-activation) -> (mask, a)
+# gives the ReLU decisions (bool, the pre-activation's shape) and the fp32 activation an implementation under test
+# took at that BatchNorm output.  _relu then follows those decisions (y where mask, else 0; the gradient through
+# the mask) and the MaxPool2d after it takes that activation's argmax (first maximum of each 2x2 window, as
+# torch's CPU max_pool2d), so the oracle computes the gradient of the same piecewise-linear branch.
+BRANCH = None
+_LAST_A = None
+
+
+def _relu(y, key):
+    global _LAST_A
+    if BRANCH is None:
+        return F.relu(y)
+    m, _LAST_A = BRANCH(key, y)
+    return torch.where(m, y, torch.zeros_like(y))
+
+
+def _windows(t):
+    """(n, c, h, w) -> (n, c, h // 2, w // 2, 4): the 2x2 windows of MaxPool2d(2) (floor), (dy, dx) row-major."""
+    n, c, h, w = t.shape
+    h2, w2 = h // 2, w // 2
+    return t[:, :, :2 * h2, :2 * w2].reshape(n, c, h2, 2, w2, 2).permute(0, 1, 2, 4, 3, 5).reshape(n, c, h2, w2, 4)
+
+
+def _maxpool2(x):
+    """MaxPool2d(2) (networks.py:421); under BRANCH the window argmaxes of the matched activation."""
+    if BRANCH is None:
+        return F.max_pool2d(x, 2)
+    idx = _windows(_LAST_A).argmax(-1, keepdim=True)
+    return _windows(x).gather(-1, idx).squeeze(-1)
 
 
 def _bn(x, P, B, key, training):
@@ -73,9 +103,9 @@ def _bn(x, P, B, key, training):
 def double_conv(x, P, B, pre, training):
     """utils/networks.py:386-402."""
     x = F.conv2d(x, P[pre + 'conv.0.weight'], P[pre + 'conv.0.bias'], padding=1)
-    x = F.relu(_bn(x, P, B, pre + 'conv.1', training))
+    x = _relu(_bn(x, P, B, pre + 'conv.1', training), pre + 'conv.1')
     x = F.conv2d(x, P[pre + 'conv.3.weight'], P[pre + 'conv.3.bias'], padding=1)
-    x = F.relu(_bn(x, P, B, pre + 'conv.4', training))
+    x = _relu(_bn(x, P, B, pre + 'conv.4', training), pre + 'conv.4')
     return x
 
 
@@ -83,7 +113,7 @@ def encoder(x, P, B, inc, enc, topology, training):
     """InConv (405-412) + Encoder (313-343); returns the reversed feature list like Encoder.forward."""
     feats = [double_conv(x, P, B, inc + 'conv.', training)]
     for i in range(len(topology)):
-        pooled = F.max_pool2d(feats[-1], 2)
+        pooled = _maxpool2(feats[-1])  # the activation of the last _relu
         feats.append(double_conv(pooled, P, B, f'{enc}down_seq.down{i + 1}.mpconv.1.', training))
     return feats[::-1]
 

@@ -1,14 +1,21 @@
 """Shared parity machinery of the -m gpu model tests (test infrastructure, imports the oracle).
 
-Gradient bar with ReLU-kink handling.  Where the fp64 forward has a pre-activation within rounding of the ReLU kink
-(|z| < 1e-5 max|z| at some BatchNorm output), any fp32-class implementation routes the gradient of that pixel by
-the last bits of z.  check_gradients then still holds every tensor DOWNSTREAM of the latest kink layer (later in
-forward order, i.e. later in named_parameters order) to the strict bar, and accepts a tensor at or upstream of it
-only if at most 1% of its elements exceed the bar and its worst error stays below 3e-2.
+Gradients: branch matching.  A training step's gradient is a piecewise-linear function's: every ReLU decision
+(BatchNorm output > 0) and every MaxPool2d argmax picks a branch, and a pre-activation within rounding of the kink
+(or a near-tie in a pooling window) is decided by the last bits of the forward -- any two fp32-class implementations
+(the reference on CPU, the oracle, x3, h2) may take different branches there, and one such pixel moves upstream
+weight gradients by up to a few percent.  BranchMatch reads the decisions the GPU forward actually took
+(engine.trace_bn: every BatchNorm's conv output and coefficients) and the oracle follows them (siamese_oracle.BRANCH),
+so branch_matched_reference() returns the fp64 gradient of the SAME branch: the difference to the GPU's gradient is
+pure arithmetic error and every tensor is held to the strict bar, with no exemptions.
+
+The reference's own fp32 gradients (the fixtures) took their own branches; they pin the oracle in
+tests/test_oracle_golden.py, and the GPU tests check them loosely (norm-wise) beside the strict branch-matched bar.
 """
 from __future__ import annotations
 
 import contextlib
+from collections import namedtuple
 
 import numpy as np
 import torch
@@ -16,8 +23,9 @@ import torch.nn.functional as F
 
 KINK_REL = 1e-5
 KINK_MAX_ERR = 3e-2
-KINK_MAX_FRAC = 1e-2
 _CONV2D = F.conv2d
+
+Kink = namedtuple('Kink', 'key rel occ mask')
 
 
 def rel(a, b) -> float:
@@ -27,7 +35,8 @@ def rel(a, b) -> float:
 
 
 def record_kinks(model, P, B, batch, ocfg, dtype=torch.float64, kink_rel=KINK_REL):
-    """[(BatchNorm key, min|z| / max|z|)] of the oracle forward's kink-ambiguous pre-activations."""
+    """[Kink(BatchNorm key, min|z| / max|z|, occurrence, element mask)] of the oracle forward's kink-ambiguous
+    pre-activations."""
     from oracle import siamese_oracle as O
     Pd = {k: v.detach().to(dtype) for k, v in P.items()}
     Bd = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in B.items()}
@@ -38,8 +47,13 @@ def record_kinks(model, P, B, batch, ocfg, dtype=torch.float64, kink_rel=KINK_RE
         rec = O.RECORD
     finally:
         O.RECORD = None
-    return [(k, float(z.abs().min() / z.abs().max())) for k, z in rec
-            if float(z.abs().min()) < kink_rel * float(z.abs().max())]
+    out, occ = [], {}
+    for k, z in rec:
+        o = occ[k] = occ.get(k, -1) + 1
+        thr = kink_rel * float(z.abs().max())
+        if float(z.abs().min()) < thr:
+            out.append(Kink(k, float(z.abs().min() / z.abs().max()), o, z.abs() < thr))
+    return out
 
 
 def _is_pre_bn_bias(k: str) -> bool:
@@ -48,27 +62,118 @@ def _is_pre_bn_bias(k: str) -> bool:
 
 def check_gradients(got: dict, ref: dict, order: list, bars: dict, kinks: list) -> list:
     """got / ref: name -> tensor; order: parameter names in forward (named_parameters) order; bars: name -> the
-    relative max-norm bar.  Returns the list of failures (empty = pass) and prints the accepted kink cases."""
+    relative max-norm bar.  Without branch matching (the multi-rank test): a tensor over its bar is accepted only
+    upstream of the latest kink-ambiguous BatchNorm output (`kinks`, record_kinks) and within KINK_MAX_ERR.
+    Returns the list of failures (empty = pass)."""
     pos = {k: i for i, k in enumerate(order)}
-    last_kink = max((pos.get(k + '.weight', -1) for k, _ in kinks), default=-1)
+    last_kink = max((pos.get(kk[0] + '.weight', -1) for kk in kinks), default=-1)
     bad = []
     for k in order:
         if k not in ref or _is_pre_bn_bias(k):
             continue
         g, r = got[k].detach().double().cpu(), ref[k].detach().double().cpu()
-        den = r.abs().max().clamp_min(1e-30)
-        err = ((g - r).abs().max() / den).item()
+        err = ((g - r).abs().max() / r.abs().max().clamp_min(1e-30)).item()
         if err <= bars[k]:
             continue
-        frac = float(((g - r).abs() > bars[k] * den).double().mean())
-        ok = bool(kinks) and pos[k] <= last_kink and frac <= KINK_MAX_FRAC and err < KINK_MAX_ERR
-        print(f'{k:60s} err {err:.2e} > bar {bars[k]:.2e}; {100 * frac:.3f}% of elements over the bar; '
-              f'{"accepted (upstream of a ReLU-kink pre-activation)" if ok else "FAIL"}')
+        ok = bool(kinks) and pos[k] <= last_kink and err < KINK_MAX_ERR
+        why = 'upstream of the latest kink' if pos[k] <= last_kink else 'DOWNSTREAM of every kink'
+        print(f'{k:60s} err {err:.2e} > bar {bars[k]:.2e}; {why}; {"accepted" if ok else "FAIL"}')
         if not ok:
-            bad.append((k, err, frac))
+            bad.append((k, err))
     if kinks:
-        print('kink-ambiguous pre-activations (|z| < 1e-5 max|z|) in the fp64 forward:', kinks)
+        print('kink-ambiguous pre-activations:', [(kk[0], kk[1]) for kk in kinks])
     return bad
+
+
+class BranchMatch:
+    """siamese_oracle.BRANCH from a GPU forward's engine.trace_bn() record.
+
+    Per BatchNorm module and segment the GPU's pre-activation z = fma(y, scale, shift) is formed in fp64 (the product
+    of two fp32 values is exact there, so z > 0 is exactly the GPU's fmaf(...) > 0 decision); an oracle call is
+    matched to the batch chunk of that module's records closest to its own pre-activation (model-agnostic: the GPU
+    batches the Siamese branches and the decoder_sem runs of the dual-task model, the oracle calls them one by one).
+    The activation returned for the pooling argmax is relu(z) rounded to fp32, the values the GPU pooled."""
+
+    def __init__(self, trace, module, max_rel: float = 1e-3):
+        """module: the model (its named_modules name the traced BatchNorms), or a dict {id(bn): name}."""
+        names = module if isinstance(module, dict) else {id(m): n for n, m in module.named_modules()}
+        self.segs: dict = {}  # key -> [(y fp32 NHWC of one segment, scale, shift)], z formed per call (memory)
+        for bn, y, scale, shift, nseg in trace:
+            n, c = y.shape[0], y.shape[3]
+            per = n // nseg
+            y32 = y.detach().cpu()
+            sc = scale.detach().double().cpu().view(nseg, c)
+            sh = shift.detach().double().cpu().view(nseg, c)
+            for s in range(nseg):
+                self.segs.setdefault(names[id(bn)], []).append((y32[s * per:(s + 1) * per], sc[s], sh[s]))
+        self.max_rel = max_rel
+        self.worst = 0.0
+        self.calls = 0
+
+    def __call__(self, key, y):
+        nb = y.shape[0]
+        yd = y.detach().double()
+        den = yd.abs().max().clamp_min(1e-30)
+        best, best_d = None, float('inf')
+        for y32, sc, sh in self.segs[key]:
+            if tuple(y32.shape[1:]) != (y.shape[2], y.shape[3], y.shape[1]) or y32.shape[0] % nb:
+                continue
+            for i in range(0, y32.shape[0], nb):
+                z = (y32[i:i + nb].double() * sc + sh).permute(0, 3, 1, 2)
+                d = ((z - yd).abs().max() / den).item()
+                if d < best_d:
+                    best, best_d = z.contiguous(), d
+        if best is None or best_d > self.max_rel:
+            raise AssertionError(f'{key}: no GPU pre-activation within {self.max_rel} of the oracle\'s ({best_d:.2e})')
+        self.worst = max(self.worst, best_d)
+        self.calls += 1
+        return best > 0, torch.relu(best.float()).to(y.dtype)
+
+
+def branch_matched_reference(model_type, P, batch, ocfg, trace, module, loss_fn, training=True, buffers=None):
+    """(outputs, loss, {name: grad}) of the fp64 oracle following the branches of the GPU forward recorded in
+    `trace` (engine.trace_bn()).  loss_fn(outputs, batch) -> scalar (e.g. siamese_oracle.step_loss).  `buffers`
+    (fresh ones by default) are converted to fp64, updated by the forward, and copied back."""
+    from oracle import siamese_oracle as O
+    Pd = {k: v.detach().double().clone().requires_grad_(True) for k, v in P.items()}
+    if buffers is None:
+        buffers = O.fresh_buffers(O.param_shapes(model_type, ocfg))
+    Bd = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in buffers.items()}
+    bt = {k: (v.detach().cpu().double() if v.is_floating_point() else v.detach().cpu()) for k, v in batch.items()}
+    bm = BranchMatch(trace, module)
+    O.BRANCH = bm
+    try:
+        out = O.forward(model_type, Pd, Bd, bt['x_t1'], bt['x_t2'], ocfg, training)
+    finally:
+        O.BRANCH = None
+    with torch.no_grad():
+        for k, v in Bd.items():
+            buffers[k].copy_(v)
+    loss = loss_fn(out, bt)
+    loss.backward()
+    print(f'branch matching: {bm.calls} BatchNorm outputs matched, worst pre-activation distance {bm.worst:.2e}')
+    return out, loss, {k: v.grad for k, v in Pd.items() if v.grad is not None}
+
+
+def check_branch_matched(got: dict, ref: dict, order: list, bar: float) -> list:
+    """Every tensor (pre-BatchNorm conv biases aside: true gradient 0) within `bar` max-relative of the
+    branch-matched fp64 gradient.  Returns the failures; prints the worst tensor."""
+    bad, worst = [], (None, 0.0)
+    for k in order:
+        if k not in ref or _is_pre_bn_bias(k):
+            continue
+        e = rel(got[k], ref[k])
+        worst = max(worst, (k, e), key=lambda t: t[1])
+        if not e <= bar:
+            bad.append((k, e))
+    print(f'gradients vs the branch-matched fp64 oracle: worst {worst[1]:.2e} ({worst[0]}), bar {bar:.0e}')
+    return bad
+
+
+def rel_l2(a, b) -> float:
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
 def mask_mismatch(out, ref, tol=1e-4) -> int:

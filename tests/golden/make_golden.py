@@ -93,6 +93,10 @@ def main():
             return
     pj = loss_functions.get_criterion('PowerJaccardLoss')
     torch.set_num_threads(min(8, os.cpu_count() or 1))
+    if args.only in (None, DP_NAME):
+        make_dataparallel_fixture(networks, pj)
+        if args.only == DP_NAME:
+            return
 
     for name, mtype, topo, cin, s1, s2, b, hw, labeled in CONFIGS:
         if args.only and args.only != name:
@@ -161,6 +165,59 @@ def main():
         path = os.path.join(HERE, f'{name}.npz')
         np.savez_compressed(path, **rec)
         print(f'{name}: loss0={losses[0]:.6f} losses={losses} -> {os.path.getsize(path) / 1024:.0f} KiB')
+
+
+DP_NAME = 'siamese_t8-16_dp2'
+
+
+def make_dataparallel_fixture(networks, pj, shards=2, per_shard=2, hw=32):
+    """nn.DataParallel's computation on `shards` devices (utils/networks.py:27, train_supervised.py:71-76), run with
+    the reference modules on the CPU: the batch is scattered along dim 0, every replica runs its shard with its own
+    BatchNorm batch statistics, the logits are gathered and ONE power_jaccard_loss is taken over the gathered batch;
+    the replicas' parameter gradients are reduce-added (here: one module called per shard, so autograd sums them);
+    running statistics persist from replica 0 only (torch/nn/parallel/data_parallel.py: the device-0 replica shares
+    the module's buffers), so the other shards' buffer updates are undone."""
+    name = DP_NAME
+    cfgd = dict(TYPE='siameseunet', IN_CHANNELS=5, OUT_CHANNELS=1, TOPOLOGY=[8, 16], S1_BANDS=[0, 1], S2_BANDS=[2, 1, 0])
+    net = networks.create_network(ns_cfg(cfgd))
+    module = net.module
+    P0 = O.deterministic_params(O.param_shapes('siameseunet', cfgd), SEED)
+    with torch.no_grad():
+        for k, p in module.named_parameters():
+            p.copy_(P0[k])
+    batch = O.synthetic_batch(cfgd, shards * per_shard, hw, SEED + 3)
+    rec = {k: batch[k].numpy() for k in ('x_t1', 'x_t2', 'y_change', 'y_sem_t1', 'y_sem_t2')}
+    rec['is_labeled'] = batch['is_labeled'].numpy()
+    for k, v in P0.items():
+        rec['p0/' + k] = v.numpy()
+    module.train()
+    outs = []
+    params = dict(module.named_parameters())
+    for sh in range(shards):
+        sl = slice(sh * per_shard, (sh + 1) * per_shard)
+        if sh == 0:  # replica 0: the module itself (its buffers take the running-statistics update)
+            outs.append(module(batch['x_t1'][sl], batch['x_t2'][sl]))
+        else:  # another replica: the same parameters, private copies of the buffers (discarded)
+            bufs = {k: v.clone() for k, v in module.named_buffers()}
+            outs.append(torch.func.functional_call(module, {**params, **bufs}, (batch['x_t1'][sl], batch['x_t2'][sl])))
+    logits = torch.cat(outs, 0)
+    loss = pj(logits, batch['y_change'])
+    loss.backward()
+    rec['out/0'] = logits.detach().numpy()
+    rec['loss0'] = np.float32(loss.item())
+    for k, p in module.named_parameters():
+        rec['g/' + k] = p.grad.detach().numpy().copy()
+    for k, v in module.state_dict().items():
+        if 'running' in k or 'num_batches' in k:
+            rec['r1/' + k] = v.detach().numpy().copy()
+    meta = dict(name=name, cfg=cfgd, batch=shards * per_shard, shards=shards, hw=hw, seed=SEED, lr=LR, wd=WD,
+                alpha=ALPHA, labeled=None,
+                generator='reference utils/networks.py + utils/loss_functions.py run per shard as nn.DataParallel '
+                          '(CPU fp32, torch ' + torch.__version__ + ')')
+    rec['meta'] = np.array(json.dumps(meta))
+    path = os.path.join(HERE, f'{name}.npz')
+    np.savez_compressed(path, **rec)
+    print(f'{name}: loss0={loss.item():.6f} -> {os.path.getsize(path) / 1024:.0f} KiB')
 
 
 def make_metrics_fixture():

@@ -236,3 +236,68 @@ def test_eval_loader_sees_whole_split_under_ddp(tmp_path):
         assert res[r]['model_evaluation'] == len(aois)
         assert len(res[r]['train']) == 2             # the training loader shards (3 AOIs padded to 2 per rank)
     assert set(res[0]['train']) | set(res[1]['train']) == set(aois)
+
+
+# ---- exact-DataParallel mode against the reference's DataParallel computation (per-shard fixture) -----------------
+def _exact_pj(logits, target):
+    """power_jaccard_loss (utils/loss_functions.py:141-150) over the batch of ALL ranks: the local sums are
+    SUM-all-reduced (parallel.global_sums) before the ratio, as the HIP path's loss kernels do in this mode."""
+    p = torch.sigmoid(logits).flatten()
+    t = target.flatten()
+    s = parallel.global_sums(torch.stack([(p * t).sum(), (p ** 2 + t ** 2).sum()]))
+    return 1 - s[0] / (s[1] - s[0] + 1e-6)
+
+
+def _worker_exact(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from oracle.golden import Fixture
+    parallel.init_distributed('gloo')
+    fx = Fixture('siamese_t8-16_dp2')
+    shapes = orc.param_shapes('siameseunet', fx.cfg)
+    P = {k: torch.from_numpy(v.copy()) for k, v in fx.params0.items()}
+    net = parallel.wrap_ddp(OracleReplica(P, orc.fresh_buffers(shapes)), device=None, exact_dataparallel=True)
+    per = fx.meta['batch'] // world
+    b = {k: v[rank * per:(rank + 1) * per] for k, v in fx.batch().items()}
+    logits = net(b['x_t1'], b['x_t2'])
+    loss = _exact_pj(logits, b['y_change'])
+    loss.backward()
+    torch.save({'loss': loss.item(), 'logits': logits.detach().clone(),
+                'grads': {n.replace('__', '.'): p.grad.detach().clone() for n, p in net.module.named_parameters()},
+                'buffers': {n.replace('__', '.'): v.detach().clone() for n, v in net.module.named_buffers()}},
+               os.path.join(out_dir, f'rank{rank}.pt'))
+    from multimodal_siamese_cd_amd import engine
+    assert engine.set_loss_allreduce(None) is parallel.allreduce_sum_  # wrap_ddp installed the loss reduction
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_exact_dataparallel_matches_reference_dataparallel_world2():
+    """wrap_ddp(exact_dataparallel=True) on 2 ranks reproduces the reference's nn.DataParallel step on 2 devices
+    (tests/golden/siamese_t8-16_dp2.npz: the reference modules run per shard, one loss over the gathered logits,
+    replica gradients reduce-added, replica-0 running statistics): logits, loss, every gradient, rank 0's buffers."""
+    import numpy as np
+    from oracle.golden import Fixture, rel_err
+    fx = Fixture('siamese_t8-16_dp2')
+    world = fx.meta['shards']
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_exact, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+    ref_logits = fx.outputs[0]
+    got_logits = np.concatenate([r['logits'].numpy() for r in res])
+    assert rel_err(got_logits, ref_logits) < 1e-5
+    for r in res:
+        assert abs(r['loss'] - float(fx.z['loss0'])) < 1e-6
+    for n, g in fx.grads.items():
+        for r in res:  # every rank holds the summed (DataParallel reduce-add) gradient
+            got = r['grads'][n].numpy()
+            assert np.abs(got - g).max() <= 1e-5 * np.abs(g).max() + 1e-7, n
+    for n, v in fx.prefixed('r1/').items():
+        assert np.abs(res[0]['buffers'][n].numpy() - v).max() <= 1e-6 * max(np.abs(v).max(), 1.0), n
+    # the default mode (mean of per-shard losses) is a different function of the logits: documented, measurable
+    per = fx.meta['batch'] // world
+    z = torch.from_numpy(ref_logits)
+    y = fx.batch()['y_change']
+    mean_loss = sum(orc.power_jaccard_loss(z[i * per:(i + 1) * per], y[i * per:(i + 1) * per]) for i in range(world))
+    assert abs(float(mean_loss) / world - float(fx.z['loss0'])) > 1e-7
