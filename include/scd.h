@@ -58,10 +58,12 @@ int scd_device_check(int device);
  * ------------------------------------------------------------------------------------------- */
 /* dst[n, y, x, 0:c_count] = src[n, c_begin:c_begin+c_count, y, x]  (NCHW -> NHWC slice);
  * dst[n, y, x, c_count:dst.c] = 0 (channel padding to the MFMA K granule).
+ * `bound` (nullable, a device float): raised to max |value| written -- the SCD_MATH_H2 operand bound of the packed
+ * input (scd_igemm_t.src_bound of the input layer), at no extra pass.
  * replaces: the .to(device) input hand-off + implicit NCHW layout (train_supervised.py:68-69) and
  * the channel slicing/concats of DualStreamUNet/WhateverNet (networks.py:105-106,113-114,236,247). */
 int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, int32_t w, int32_t c_begin,
-                  int32_t c_count, scd_nhwc_t dst, scd_stream_t stream);
+                  int32_t c_count, scd_nhwc_t dst, float *bound, scd_stream_t stream);
 
 /* Conv2d 3x3 weight OIHW [co][ci][3][3] ->
  *   mode 0 (forward):   [co][9][ci_pad]           (zero for ci >= ci)
@@ -121,8 +123,9 @@ enum scd_conv_math {
 };
 /* ABI revision of this header (struct layouts and signatures); a binding checks it at load time.
  *   3: scd_igemm_t / scd_wgrad_t / scd_pack_job_t carry `math` (and `tune`); the process-wide mode setters
- *      (scd_set_conv_math, scd_set_halo16, scd_set_wgrad16) and every launch-time environment switch are gone. */
-#define SCD_ABI_VERSION 3
+ *      (scd_set_conv_math, scd_set_halo16, scd_set_wgrad16) and every launch-time environment switch are gone.
+ *   4: scd_pack_nchw takes a nullable `bound` (the input layer's h2 operand bound). */
+#define SCD_ABI_VERSION 4
 int scd_abi_version(void);
 /* The arithmetic scd_conv_igemm / scd_conv_wgrad will use for a descriptor (its `math`, or SCD_MATH_X3 / F32 where
  * the shape or the missing operand bounds keep the conv off the requested kernels); negative = invalid descriptor.

@@ -152,10 +152,11 @@ inline int math_split(int m) { return m != SCD_MATH_F32; }  // split-weight (x3,
 inline int math_planes(int m) { return m == SCD_MATH_BF16 ? 1 : m == SCD_MATH_X5 ? 5 : m == SCD_MATH_H2 ? 2 : 3; }
 inline int h2_prescale(uint32_t tune) { return (tune & SCD_TUNE_H2_NO_PRESCALE) ? 0 : 1; }
 // SCD_MATH_H2 weight splits exist for 3x3 convs (the halo16 kernels) and 1- / 4-tap convs (the ConvTranspose forward
-// and data grad, the gather16 kernel) whose source channels are a multiple of 32; every other conv keeps the x3
-// split.  wsplit of such a conv is in the h2 format.
+// and data grad, the gather16 kernel) whose source channels are a multiple of 32, and for the 16-channel input layer
+// (3x3, the igemm_halo16_c16 kernel); every other conv keeps the x3 split.  wsplit of such a conv is in the h2
+// format.
 inline bool h2_weight_format(int math, int ntaps, int c) {
-    return math == SCD_MATH_H2 && (ntaps == 9 || ntaps == 1 || ntaps == 4) && c % 32 == 0;
+    return math == SCD_MATH_H2 && (((ntaps == 9 || ntaps == 1 || ntaps == 4) && c % 32 == 0) || (ntaps == 9 && c == 16));
 }
 // h2 gather igemm (conv_gather16.hip): 0 when `a` does not take it, else 1 + tile id; launcher.
 int gather16_pick(const IgemmArgs &a);

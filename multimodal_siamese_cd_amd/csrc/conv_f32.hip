@@ -749,7 +749,7 @@ extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
     if (!math_split(a.math)) return SCD_MATH_F32;
     if (igemm_takes_halo16(a)) return a.math;  // under SCD_MATH_H2 only bounded h2-split convs take it
     if (igemm_takes_gather16(a)) return SCD_MATH_H2;
-    if (igemm_takes_c16(a)) return a.math == SCD_MATH_H2 ? SCD_MATH_X3 : a.math;
+    if (igemm_takes_c16(a)) return a.math;  // under SCD_MATH_H2 only bounded h2-split input layers take it
     return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
 }
 
@@ -803,8 +803,9 @@ static int conv_igemm_run(const scd_igemm_t *d, hipStream_t s, int bb_ntiles_tot
                   "(check scd_igemm_input_bn_supported)");
         return SCD_ERR_ARG;
     }
-    if (a.dst_bound && a.store_mode != 1 && !igemm_takes_halo16(a) && !igemm_takes_gather16(a)) {
-        set_error("igemm: dst_bound of a store_mode 0 conv needs the halo16 or gather16 kernel "
+    if (a.dst_bound && a.store_mode != 1 && !igemm_takes_halo16(a) && !igemm_takes_gather16(a) &&
+        !igemm_takes_c16(a)) {
+        set_error("igemm: dst_bound of a store_mode 0 conv needs the halo16, c16 or gather16 kernel "
                   "(ConvTranspose store_mode 1 convs take it on every split-bf16 kernel)");
         return SCD_ERR_ARG;
     }

@@ -615,9 +615,12 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
     constexpr int A_CH = HR * 4;  // 16-byte (4-channel) pieces
     constexpr int A_PER = (A_CH + NT - 1) / NT;
     constexpr int PA = HR * 32;
-    static_assert(NP == 1 || NP == 3 || NP == 5, "x3, x5 or bf16");
-    constexpr int XP = NP == 1 ? 1 : 3;
-    constexpr int WP = NP == 1 ? 1 : NP == 5 ? 2 : 3;
+    static_assert(NP == 1 || NP == 3 || NP == 4 || NP == 5, "x3, x5, bf16 or h2");
+    // NP 4: h2 as in igemm_halo16_x3 (fp16 h and pre-scaled m' planes of the halo scaled by the power of two of
+    // *src_bound, the weights' h2 split with its per-channel inverse scales, three f16 products per term pair)
+    constexpr bool H2 = NP == 4;
+    constexpr int XP = NP == 1 ? 1 : H2 ? 2 : 3;
+    constexpr int WP = NP == 1 ? 1 : (NP == 5 || H2) ? 2 : 3;
     // halo planes, then the statistics reduction ([2][WAVES_M][BN] floats) in a region of its own, so the next
     // tile's halo can be written while no wave is still reducing
     __shared__ __attribute__((aligned(16))) unsigned char smem[XP * PA + 2 * WAVES_M * BN * 4];
@@ -627,6 +630,8 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
     const int g = lane >> 4, l16 = lane & 15;
     const int tiles_x = a.wo / TW, tiles_y = a.ho / TR;
     const int ntile = a.grid_m * a.grid_n;
+    float xs = 1.f, xs_inv = 1.f;  // h2: power-of-two scale of the staged halo and its inverse
+    if constexpr (H2) h2_scale(*a.src_bound, xs, xs_inv);
 
     auto soff = [](int row, int col) { return row * 32 + ((((col >> 1) ^ (row >> 3)) & 1) << 4) + ((col & 1) << 3); };
     // tile -> (m-tile, n-tile): n slowest, so a block's consecutive tiles (stride gridDim.x) keep one weight tile
@@ -660,7 +665,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
     // 2s + (g >> 1) of step s
     const int KS16 = a.K / 16, NB32 = (a.n_out + 31) / 32;
     const uint32_t wplane_b = uint32_t(a.wplane) * 2u;
-    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, 3u * wplane_b);
+    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, uint32_t(WP) * wplane_b);
     uint32_t w_base[TN];
     auto load_W = [&](int st, u32x4 (&wq)[WP][TN]) {
         const bool pad = st == 4 && g >= 2;  // tap 9 does not exist
@@ -684,6 +689,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
     // registers during this tile's last MFMA step and epilogue.  Every wave of a block runs the same trip count.
     int tile = blockIdx.x;
     if (tile >= ntile) return;
+    float omax = 0.f;  // max |stored value| of this lane over its tiles (dst_bound)
     load_halo(tile);
     for (; tile < ntile; tile += gridDim.x) {
         int mt, img, y0, x0, n0;
@@ -711,7 +717,10 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
             if ((A_CH % NT == 0) || e < A_CH) {
                 const int o = soff(e >> 2, e & 3);
                 u32x2 h, m, l;
-                if constexpr (XP == 3) {
+                if constexpr (H2) {
+                    split2h_pre(ra[i] * xs, h, m);
+                    *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
+                } else if constexpr (XP == 3) {
                     split3(ra[i], h, m, l);
                     *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
                     *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
@@ -750,21 +759,48 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
             for (int p = 0; p < WP; ++p)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) wv[p][j] = __builtin_bit_cast(bf16x8, wq[p][j]);
-            constexpr int QW[6] = {1, 0, 2, 0, 1, 0};
-            constexpr int QX[6] = {1, 2, 0, 1, 0, 0};
+            if constexpr (H2) {
+                // (w_h 2^-11) x_m', w_m x_h, w_h x_h on the fp16 planes (igemm_halo16_x3's NP 4)
 #pragma unroll
-            for (int q = NP == 1 ? 5 : 0; q < 6; ++q)
-                if (NP != 5 || QW[q] != 2)
+                for (int j = 0; j < TN; ++j) {
+                    const u32x4 wh = __builtin_bit_cast(u32x4, wv[0][j]), wmv = __builtin_bit_cast(u32x4, wv[1][j]);
+                    const u32x4 wh_lo = f16_down11(wh);
 #pragma unroll
-                    for (int j = 0; j < TN; ++j)
+                    for (int i = 0; i < TM; ++i) {
+                        const u32x4 xh = __builtin_bit_cast(u32x4, xv[0][i]), xm = __builtin_bit_cast(u32x4, xv[1][i]);
+                        acc[j][i] = mfma16_f16(wh_lo, xm, acc[j][i]);
+                        acc[j][i] = mfma16_f16(wmv, xh, acc[j][i]);
+                        acc[j][i] = mfma16_f16(wh, xh, acc[j][i]);
+                    }
+                }
+            } else {
+                constexpr int QW[6] = {1, 0, 2, 0, 1, 0};
+                constexpr int QX[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
-                        for (int i = 0; i < TM; ++i)
-                            acc[j][i] =
-                                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[QW[q]][j], xv[QX[q]][i], acc[j][i], 0, 0, 0);
+                for (int q = NP == 1 ? 5 : 0; q < 6; ++q)
+                    if (NP != 5 || QW[q] != 2)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+#pragma unroll
+                            for (int i = 0; i < TM; ++i)
+                                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[QW[q]][j], xv[QX[q]][i],
+                                                                                    acc[j][i], 0, 0, 0);
+            }
             if (st < 4) load_W(st + 1, wq);
             if (st == 3 && more) load_halo(tile + gridDim.x);  // issued after the last weight step's loads
         }
 
+        if constexpr (H2) {  // undo the operand scales: per-channel weight inverse scales after the planes
+            const float *winv =
+                reinterpret_cast<const float *>(reinterpret_cast<const unsigned char *>(a.wsplit) + 2u * wplane_b);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wn * WCH + j * 16 + 4 * g;
+                const f32x4 sc = (n < NB32 * 32 ? gload4(winv + n) : f32x4{0.f, 0.f, 0.f, 0.f}) * xs_inv;
+#pragma unroll
+                for (int i = 0; i < TM; ++i) acc[j][i] *= sc;
+            }
+        }
         // acc[j][i][r]: channel n0 + wn*WCH + 16j + 4g + r, pixel wm*WPX + 16i + l16
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -773,7 +809,11 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int n = n0 + wn * WCH + j * 16 + 4 * g;
-                if (n < a.n_out) gstore4(a.dst + pix * a.ldc_d + n, acc[j][i] + bias4[j]);
+                if (n < a.n_out) {
+                    const f32x4 v = acc[j][i] + bias4[j];
+                    gstore4(a.dst + pix * a.ldc_d + n, v);
+                    omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+                }
             }
         }
         if (a.stat_rec) {  // as igemm_halo16_x3: tile mean, then M2 about it
@@ -823,6 +863,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
             // the next tile's first barrier orders these red1/red2 reads before the next writes
         }
     }
+    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the block ran every tile
 }
 
 // 0 when `a` does not take igemm_halo16_c16, else 1; *bm = 128 pixels per tile, *tw = tile width.
@@ -842,26 +883,36 @@ int halo16_c16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     return 0;
 }
 
-// Arithmetic of the kernels that keep the split-bf16 planes under every mode (the 16-channel input layer): the
-// mode's own, except h2 (whose fp16 weight split exists only for 32-channel multiples), which runs x3 here.
+// Planes of the kernels that keep the split-bf16 operands under every mode (the 16-channel input layer's weight
+// grad): the mode's own, except h2, which runs x3 there.
 static int bf16_planes(int math) { return math_planes(math) == 2 ? 3 : math_planes(math); }
+
+// Arithmetic of the input-layer kernel: the mode's own; h2 with its weight split and a bound of the input (the
+// descriptors the x3 view keeps the split for), else x3.
+static int c16_planes(const IgemmArgs &b) {
+    if (math_planes(b.math) == 2) return b.src_bound && h2_weight_format(b.math, 9, 16) ? 4 : 3;
+    return math_planes(b.math);
+}
 
 template <int TW>
 static void launch_c16_tw(const IgemmArgs &b, dim3 grid, hipStream_t s) {
-    switch (bf16_planes(b.math)) {
+    switch (c16_planes(b)) {
         case 1: hipLaunchKernelGGL((igemm_halo16_c16<TW, 1>), grid, dim3(256), 0, s, b); break;
+        case 4: hipLaunchKernelGGL((igemm_halo16_c16<TW, 4>), grid, dim3(256), 0, s, b); break;
         case 5: hipLaunchKernelGGL((igemm_halo16_c16<TW, 5>), grid, dim3(256), 0, s, b); break;
         default: hipLaunchKernelGGL((igemm_halo16_c16<TW, 3>), grid, dim3(256), 0, s, b);
     }
 }
 
 template <int TW>
-static int c16_resident(int math) {
-    static int cache[3] = {0, 0, 0};  // per arithmetic: bf16, x5, x3
-    const int k = bf16_planes(math) == 1 ? 0 : bf16_planes(math) == 5 ? 1 : 2;
+static int c16_resident(const IgemmArgs &b) {
+    static int cache[4] = {0, 0, 0, 0};  // per arithmetic: bf16, x5, x3, h2
+    const int pl = c16_planes(b);
+    const int k = pl == 1 ? 0 : pl == 5 ? 1 : pl == 4 ? 3 : 2;
     if (cache[k] > 0) return cache[k];
     const void *fn = k == 0   ? reinterpret_cast<const void *>(&igemm_halo16_c16<TW, 1>)
                      : k == 1 ? reinterpret_cast<const void *>(&igemm_halo16_c16<TW, 5>)
+                     : k == 3 ? reinterpret_cast<const void *>(&igemm_halo16_c16<TW, 4>)
                               : reinterpret_cast<const void *>(&igemm_halo16_c16<TW, 3>);
     int per_cu = 0, cus = 0, dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -884,7 +935,7 @@ void launch_halo16_c16(const IgemmArgs &a, int tw, hipStream_t s) {
     b.grid_n = (a.n_out + 63) / 64;
     b.remap = 0;
     const int64_t ntile = int64_t(b.grid_m) * b.grid_n;
-    const int cap = tw == 64 ? c16_resident<64>(a.math) : tw == 32 ? c16_resident<32>(a.math) : c16_resident<16>(a.math);
+    const int cap = tw == 64 ? c16_resident<64>(a) : tw == 32 ? c16_resident<32>(a) : c16_resident<16>(a);
     const int kt = int((a.tune & SCD_TUNE_C16_TILES_MASK) >> 16);
     const int k = kt == 0 ? 4 : kt == 15 ? 0 : kt;
     const int64_t blocks = k >= 1 ? (ntile + k - 1) / k : (ntile < cap ? ntile : cap);

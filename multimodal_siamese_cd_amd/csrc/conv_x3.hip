@@ -577,9 +577,10 @@ static int halo_pick(const IgemmArgs &a, int *bm, int *tw) {
 static IgemmArgs x3_view(const IgemmArgs &a) {
     IgemmArgs b = a;
     int bm = 0, tw = 0;
-    if (h2_weight_format(a.math, a.ntaps, a.c) &&
-        (!a.src_bound || (a.ntaps == 9 ? !halo16_pick(a, halo_eligible(a), &bm, &tw) : !gather16_pick(a))))
-        b.wsplit = nullptr;
+    const bool h2_kernel = a.ntaps != 9 ? gather16_pick(a) != 0
+                           : a.c == 16 ? halo16_c16_pick(a, halo_eligible(a), &bm, &tw) != 0
+                                       : halo16_pick(a, halo_eligible(a), &bm, &tw) != 0;
+    if (h2_weight_format(a.math, a.ntaps, a.c) && (!a.src_bound || !h2_kernel)) b.wsplit = nullptr;
     return b;
 }
 

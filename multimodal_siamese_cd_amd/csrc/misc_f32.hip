@@ -47,12 +47,14 @@ static int grid_for(int64_t total, int cap = 4096) {
 // one thread per float4 of the destination, so a wave's stores cover consecutive 16-byte groups of whole pixels;
 // the source planes are read 16 pixels x 4 channels per load.  Otherwise one thread per pixel with scalar stores,
 // so any channel offset works (the early-fusion t2 bands).
+// `bound`: raised to max |value| (one atomic per wave, after the loop every lane reaches).
 template <bool VEC>
 __global__ void pack_nchw_kernel(const float *__restrict__ src, int c, int hw, int c_begin, int c_count,
-                                 float *__restrict__ dst, int dc, int ldc) {
+                                 float *__restrict__ dst, int dc, int ldc, float *bound) {
     const int img = blockIdx.y;
     const float *s = src + (size_t(img) * c + c_begin) * hw;
     float *d = dst + size_t(img) * hw * ldc;
+    float vmax = 0.f;
     if (VEC) {
         const int q4 = dc >> 2;  // float4 groups per pixel
         const int total = hw * q4;
@@ -64,11 +66,17 @@ __global__ void pack_nchw_kernel(const float *__restrict__ src, int c, int hw, i
             v.z = c0 + 2 < c_count ? s[size_t(c0 + 2) * hw + pix] : 0.f;
             v.w = c0 + 3 < c_count ? s[size_t(c0 + 3) * hw + pix] : 0.f;
             *reinterpret_cast<float4 *>(d + size_t(pix) * ldc + c0) = v;
+            vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         }
     } else {
         for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < hw; pix += gridDim.x * blockDim.x)
-            for (int cc = 0; cc < dc; ++cc) d[size_t(pix) * ldc + cc] = cc < c_count ? s[size_t(cc) * hw + pix] : 0.f;
+            for (int cc = 0; cc < dc; ++cc) {
+                const float v = cc < c_count ? s[size_t(cc) * hw + pix] : 0.f;
+                d[size_t(pix) * ldc + cc] = v;
+                vmax = fmaxf(vmax, fabsf(v));
+            }
     }
+    if (bound) wave_max_bound(bound, vmax);
 }
 
 __global__ void pack_conv3x3_kernel(const float *__restrict__ w, int co, int ci, int ci_pad, int mode,
@@ -510,7 +518,7 @@ __global__ void pjaccard_bwd_kernel(const float *__restrict__ logits, const floa
 using namespace scd;
 
 // ------------------------------------------------------------------------------------------------
-extern "C" const char *scd_version(void) { return "libscd 0.3.0 (gfx950, ABI 3: per-descriptor conv arithmetic)"; }
+extern "C" const char *scd_version(void) { return "libscd 0.4.0 (gfx950, ABI 4: per-descriptor conv arithmetic, bounded input pack)"; }
 extern "C" const char *scd_last_error(void) { return g_err.c_str(); }
 
 extern "C" int scd_device_check(int device) {
@@ -529,7 +537,7 @@ extern "C" int scd_device_check(int device) {
 }
 
 extern "C" int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, int32_t w, int32_t c_begin,
-                             int32_t c_count, scd_nhwc_t dst, scd_stream_t stream) {
+                             int32_t c_count, scd_nhwc_t dst, float *bound, scd_stream_t stream) {
     clear_error();
     // dst may start at any channel offset (scalar stores): only shape checks here.
     if (!src || !dst.data || n != dst.n || h != dst.h || w != dst.w || dst.c < 1 || dst.ldc < dst.c || c_begin < 0 ||
@@ -553,10 +561,10 @@ extern "C" int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, 
     const dim3 grid(unsigned(std::min<int64_t>((per_img + 255) / 256, 4096)), unsigned(n));
     if (vec)
         hipLaunchKernelGGL(pack_nchw_kernel<true>, grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
-                           c_count, d, dst.c, dst.ldc);
+                           c_count, d, dst.c, dst.ldc, bound);
     else
         hipLaunchKernelGGL(pack_nchw_kernel<false>, grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
-                           c_count, d, dst.c, dst.ldc);
+                           c_count, d, dst.c, dst.ldc, bound);
     return launch_status("scd_pack_nchw");
 }
 

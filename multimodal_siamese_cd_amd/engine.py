@@ -371,8 +371,8 @@ def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool, mate
     cin = x.shape[3]
     if conv0.in_channels > cin:
         raise ValueError(f"DoubleConv expects {conv0.in_channels} input channels, got {cin}")
-    if pool is not None and x_bound is None and cin % 32 == 0:
-        x_bound = _bound_of(x, pool)
+    if pool is not None and x_bound is None and (cin % 32 == 0 or cin == 16):
+        x_bound = _bound_of(x, pool)  # the 16-channel input layer: the packing's bound (igemm_halo16_c16 h2)
     y0, t0 = _conv3x3_stats(x, packed_conv3x3(conv0.weight, 0, ci_pad=cin), conv0.bias,
                             conv0.out_channels, _bn_uses_batch_stats(bn0, training), src_bound=x_bound)
     b0 = _take(pool)
@@ -515,6 +515,11 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None):
         gw0 = _wgrad3x3(ga0, x, conv0.weight, None, None, None, rows_bn)
         return None, [gw0, dbias0, dg0, db0, gw1, dbias1, dg1, db1]
     dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0, d0)
+    if pool is not None and x_bound is None and \
+            hip.wgrad_arith(hip.wgrad_desc(nhwc(dy0), nhwc(x), 1, TAPS_3X3, None, d0, d0)) == 'h2':
+        # a source the forward left unbounded (the channel-padded input layer, whose forward kernel is x3): bounded
+        # here, where that puts its weight grad (the generic kernel) on h2
+        x_bound = _bound_of(x, pool)
     gw0 = _wgrad3x3(dy0, x, conv0.weight, None, d0, x_bound)
     gx = None
     if need_dx:
@@ -548,6 +553,12 @@ def _check_input_pair(x_t1: torch.Tensor, x_t2: torch.Tensor) -> None:
         raise ValueError(f"x_t1 is on {x_t1.device} but x_t2 is on {x_t2.device}")
 
 
+def _input_bound(like: torch.Tensor):
+    """Under h2, a zeroed device float the input packing raises to max |input| (the input layer's operand bound,
+    registered for the packed tensor: no extra pass), else None."""
+    return torch.zeros(1, device=like.device, dtype=_F32) if hip.conv_math() == 'h2' else None
+
+
 def pack_pair(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:
     """Siamese input: [2B, H, W, pad_in(C)] NHWC with t1 images first (one shared-encoder batch)."""
     _check_input_pair(x_t1, x_t2)
@@ -556,9 +567,10 @@ def pack_pair(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count:
     b, c, h, w = x_t1.shape
     c_count = c - c_begin if c_count is None else c_count
     out = torch.empty((2 * b, h, w, pad_in(c_count)), device=x_t1.device, dtype=_F32)
-    hip.pack_nchw(x_t1.float(), c_begin, c_count, out[:b])
-    hip.pack_nchw(x_t2.float(), c_begin, c_count, out[b:])
-    return out
+    bound = _input_bound(out)
+    hip.pack_nchw(x_t1.float(), c_begin, c_count, out[:b], bound=bound)
+    hip.pack_nchw(x_t2.float(), c_begin, c_count, out[b:], bound=bound)
+    return _set_bound(out, bound)
 
 
 def pack_stream(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:
@@ -571,9 +583,10 @@ def pack_stream(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_coun
     cp = pad_in(2 * c_count)
     out = torch.empty((b, h, w, cp), device=x_t1.device, dtype=_F32)
     # t1 bands -> channels [0, nb) (zero-padding the rest), then t2 bands -> [nb, 2nb)
-    hip.pack_nchw(x_t1.float(), c_begin, c_count, out, 0, cp)  # t1 bands -> [0, nb), zero-pad to cp
-    hip.pack_nchw(x_t2.float(), c_begin, c_count, out, c_count, c_count)  # t2 bands -> [nb, 2nb)
-    return out
+    bound = _input_bound(out)
+    hip.pack_nchw(x_t1.float(), c_begin, c_count, out, 0, cp, bound=bound)  # t1 bands -> [0, nb), zero-pad to cp
+    hip.pack_nchw(x_t2.float(), c_begin, c_count, out, c_count, c_count, bound=bound)  # t2 bands -> [nb, 2nb)
+    return _set_bound(out, bound)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -98,7 +98,7 @@ _SIGS = {
     "scd_abi_version": ([], c_int),
     "scd_last_error": ([], c_char_p),
     "scd_device_check": ([c_int], c_int),
-    "scd_pack_nchw": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, NHWC, c_void_p], c_int),
+    "scd_pack_nchw": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, NHWC, c_void_p, c_void_p], c_int),
     "scd_pack_conv3x3": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_pack_conv3x3_multi": ([c_void_p, c_int32, c_void_p], c_int),
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
@@ -189,7 +189,7 @@ _SIGS = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
-ABI_VERSION = 3  # SCD_ABI_VERSION of include/scd.h
+ABI_VERSION = 4  # SCD_ABI_VERSION of include/scd.h
 
 
 def load_library(path: str = LIB_PATH):
@@ -278,12 +278,15 @@ def _taps(taps):
 # ------------------------------------------------------------------------------------------------
 # thin wrappers
 # ------------------------------------------------------------------------------------------------
-def pack_nchw(src: torch.Tensor, c_begin: int, c_count: int, dst: torch.Tensor, dst_c_off: int = 0, dst_c=None):
+def pack_nchw(src: torch.Tensor, c_begin: int, c_count: int, dst: torch.Tensor, dst_c_off: int = 0, dst_c=None,
+              bound=None):
+    """`bound` (a device float): raised to max |value| packed (the input layer's h2 operand bound)."""
     n, c, h, w = src.shape
     src = src.contiguous()
     cc = dst.shape[3] - dst_c_off if dst_c is None else dst_c
     v = NHWC(dst.data_ptr() + 4 * dst_c_off, dst.shape[0], dst.shape[1], dst.shape[2], cc, dst.stride(2))
-    _check(lib().scd_pack_nchw(src.data_ptr(), n, c, h, w, c_begin, c_count, v, _stream()), "scd_pack_nchw")
+    _check(lib().scd_pack_nchw(src.data_ptr(), n, c, h, w, c_begin, c_count, v, _ptr(bound), _stream()),
+           "scd_pack_nchw")
 
 
 def pack_conv3x3(w: torch.Tensor, mode: int, ci_pad: int | None = None) -> torch.Tensor:
@@ -359,8 +362,12 @@ def split_bf16x3_frag(wpk: torch.Tensor, n_out: int, K: int) -> torch.Tensor:
 
 def h2_weight_format(K: int, ntaps: int) -> bool:
     """Whether the library expects the h2 split for a conv of this contraction (mirrors h2_weight_format in
-    conv_common.h: 3x3, 1-tap and 4-tap convs whose source channels are a multiple of 32, under SCD_MATH_H2)."""
-    return ntaps in (9, 1, 4) and K % ntaps == 0 and (K // ntaps) % 32 == 0 and conv_math() == 'h2'
+    conv_common.h: 3x3, 1-tap and 4-tap convs whose source channels are a multiple of 32, and the 16-channel 3x3
+    input layer, under SCD_MATH_H2)."""
+    if conv_math() != 'h2' or ntaps not in (9, 1, 4) or K % ntaps:
+        return False
+    c = K // ntaps
+    return c % 32 == 0 or (ntaps == 9 and c == 16)
 
 
 def _attach_split(wpk: torch.Tensor, n_out: int, K: int, ntaps: int) -> torch.Tensor:

@@ -29,11 +29,57 @@ import torch.nn as nn
 from .. import engine, hip
 
 
-def _check_topology(cfg):
-    topo = list(cfg.MODEL.TOPOLOGY)
-    bad = [t for t in topo if t % 8]
-    if bad:
-        raise ValueError(f"MODEL.TOPOLOGY entries must be multiples of 8 for the MFMA kernels, got {topo}")
+def _pad8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def _padded_topology(cfg):
+    """The channel counts the kernels run a TOPOLOGY at (multiples of 8, the MFMA K granule), or None when it needs
+    no padding."""
+    topo = [int(t) for t in cfg.MODEL.TOPOLOGY]
+    if any(t < 1 for t in topo):
+        raise ValueError(f"MODEL.TOPOLOGY entries must be positive, got {topo}")
+    return [_pad8(t) for t in topo] if any(t % 8 for t in topo) else None
+
+
+def _dim_map(real: int, padded: int, device, halves: bool = False):
+    """Positions of a parameter dimension's real channels in the padded twin's: a prefix, or (`halves`: the concat
+    inputs -- Up's DoubleConv after cat([skip, up]), the fusion heads after the cat of two decoders) two halves, each
+    padded on its own."""
+    if padded == real:
+        return None
+    if halves:
+        h = real // 2
+        if real % 2 or padded != 2 * _pad8(h):
+            raise ValueError(f"no two-half channel layout maps {real} onto {padded}")
+        return torch.cat([torch.arange(h, device=device), torch.arange(h, device=device) + padded // 2])
+    if padded != _pad8(real):
+        raise ValueError(f"no channel layout maps {real} onto {padded}")
+    return torch.arange(real, device=device)
+
+
+def _concat_input(model_type: str, name: str) -> bool:
+    """Parameters whose input dimension is a concat of two equally wide feature maps (networks.py:449, 119, 258)."""
+    if '.up_seq.' in name and name.endswith('.conv.conv.0.weight'):
+        return True
+    return (model_type == 'dualstreamunet' and name == 'outc.conv.weight') or name == 'outc_fusion.conv.weight'
+
+
+def _scatter(t: torch.Tensor, shape, maps) -> torch.Tensor:
+    """t placed into zeros of `shape` at the per-dimension positions `maps` (differentiable in t)."""
+    for d, m in enumerate(maps):
+        if m is not None:
+            sz = list(t.shape)
+            sz[d] = shape[d]
+            t = t.new_zeros(sz).index_copy(d, m, t)
+    return t
+
+
+def _gather(t: torch.Tensor, maps) -> torch.Tensor:
+    for d, m in enumerate(maps):
+        if m is not None:
+            t = t.index_select(d, m)
+    return t
 
 
 class ModelWrapper(nn.Module):
@@ -99,13 +145,83 @@ class _HipNet(nn.Module):
 
     def __init__(self, cfg):
         super().__init__()
-        _check_topology(cfg)
         self.cfg = cfg
         self.conv_math = engine.conv_math_for(cfg)
+        object.__setattr__(self, '_twin_topo', _padded_topology(cfg))
+        object.__setattr__(self, '_twin', None)
 
     def forward(self, x_t1, x_t2):
         with hip.conv_scope(self.conv_math):
+            if self._twin_topo is not None:
+                return self._twin_forward(x_t1, x_t2)
             return self._forward(x_t1, x_t2)
+
+    # Channel counts off the kernels' granule (any reference TOPOLOGY, e.g. [12, 20]).  The model keeps the reference's
+    # parameter shapes (state_dict, checkpoints, optimizer), and its forward runs a twin of the same family at the
+    # padded counts (outside the module tree: it owns no state).  Each forward hands the twin its parameters as
+    # differentiable zero-padded functions of the real ones (so autograd returns the real parameters' gradients) and
+    # its running statistics; padded channels have zero weights, bias and BatchNorm affine, so their activations are 0
+    # and they add exact zeros to every real channel.  Running statistics are copied back after a training forward.
+    def _twin_forward(self, x_t1, x_t2):
+        tw, (maps, bufs) = self._twin_ready(x_t1.device)
+        tw.train(self.training)
+        for k, p in self.named_parameters():
+            shape, m = maps[k]
+            mod_name, _, attr = k.rpartition('.')
+            object.__setattr__(tw.get_submodule(mod_name), attr, _scatter(p, shape, m))
+        with torch.no_grad():
+            for k, b in self.named_buffers():
+                tb, m = bufs[k]
+                if m and m[0] is not None:
+                    tb.index_copy_(0, m[0], b)
+                else:
+                    tb.copy_(b)
+        out = tw._forward(x_t1, x_t2)
+        if self.training:
+            with torch.no_grad():
+                for k, b in self.named_buffers():
+                    tb, m = bufs[k]
+                    b.copy_(_gather(tb, m) if m else tb)
+        return out
+
+    def _twin_ready(self, dev):
+        """(twin on `dev`, (parameter maps {name: (twin shape, per-dim positions)}, buffer maps {name: (twin buffer,
+        positions)})), built on first use."""
+        tw = self._twin
+        if tw is None:
+            import copy
+            cfg = copy.deepcopy(self.cfg)
+            if hasattr(cfg, 'defrost'):
+                cfg.defrost()
+            cfg.MODEL.TOPOLOGY = list(self._twin_topo)
+            tw = type(self)(cfg)
+            tw.conv_math = self.conv_math
+            object.__setattr__(self, '_twin', tw)
+            object.__setattr__(self, '_twin_maps', None)
+        if next(tw.buffers()).device != torch.device(dev):
+            tw.to(dev)
+            object.__setattr__(self, '_twin_maps', None)
+        if self._twin_maps is None:
+            tp = dict(tw.named_parameters())
+            tw_params = {k: tuple(v.shape) for k, v in tp.items()}
+            for mod in tw.modules():  # from now on the twin's parameters are plain tensor attributes set per forward
+                for k in list(mod._parameters):
+                    v = mod._parameters.pop(k)
+                    object.__setattr__(mod, k, v.detach())
+            maps = {}
+            mtype = str(self.cfg.MODEL.TYPE)
+            for k, p in self.named_parameters():
+                maps[k] = (tw_params[k], [_dim_map(r, q, dev, d == 1 and _concat_input(mtype, k))
+                                          for d, (r, q) in enumerate(zip(p.shape, tw_params[k]))])
+            bufs = {}
+            tb = dict(tw.named_buffers())
+            for k, b in self.named_buffers():
+                if b.dim() == 1:
+                    bufs[k] = (tb[k], [_dim_map(b.shape[0], tb[k].shape[0], dev)])
+                else:
+                    bufs[k] = (tb[k], [])
+            object.__setattr__(self, '_twin_maps', (maps, bufs))
+        return tw, self._twin_maps
 
 
 def _stream(inc, encoder, decoder, x, nseg, training, siamese, head=None):

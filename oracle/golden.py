@@ -13,7 +13,7 @@ import numpy as np
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tests', 'golden')
 NAMES = ('siamese_t8-16', 'siamese_t8-16-32', 'unet_t8-16', 'dualstream_t8-16', 'dtsiamese_t8-16',
          'whatevernet_t8-16', 'siamese_t8-16-32_odd', 'dualstream_t8-16_odd', 'whatevernet2_t8-16',
-         'siamese_t32-64', 'dtsiamese_t32-64', 'dualstream_t32-64')
+         'siamese_t32-64', 'dtsiamese_t32-64', 'dualstream_t32-64', 'siamese_t12-20', 'dualstream_t6-12')
 
 
 class Fixture:

@@ -96,7 +96,13 @@ class BranchMatch:
 
     def __init__(self, trace, module, max_rel: float = 1e-3):
         """module: the model (its named_modules name the traced BatchNorms), or a dict {id(bn): name}."""
-        names = module if isinstance(module, dict) else {id(m): n for n, m in module.named_modules()}
+        if isinstance(module, dict):
+            names = module
+        else:  # a model off the granule of 8 runs a padded twin (utils/networks.py): its BatchNorms, same names
+            names = {id(m): n for n, m in module.named_modules()}
+            twin = getattr(module, '_twin', None)
+            if twin is not None:
+                names.update({id(m): n for n, m in twin.named_modules()})
         self.segs: dict = {}  # key -> [(y fp32 NHWC of one segment, scale, shift)], z formed per call (memory)
         for bn, y, scale, shift, nseg in trace:
             n, c = y.shape[0], y.shape[3]
@@ -115,11 +121,12 @@ class BranchMatch:
         yd = y.detach().double()
         den = yd.abs().max().clamp_min(1e-30)
         best, best_d = None, float('inf')
-        for y32, sc, sh in self.segs[key]:
-            if tuple(y32.shape[1:]) != (y.shape[2], y.shape[3], y.shape[1]) or y32.shape[0] % nb:
+        c = y.shape[1]
+        for y32, sc, sh in self.segs[key]:  # a padded twin's channels: the real ones are the prefix
+            if tuple(y32.shape[1:3]) != (y.shape[2], y.shape[3]) or y32.shape[3] < c or y32.shape[0] % nb:
                 continue
             for i in range(0, y32.shape[0], nb):
-                z = (y32[i:i + nb].double() * sc + sh).permute(0, 3, 1, 2)
+                z = (y32[i:i + nb, :, :, :c].double() * sc[:c] + sh[:c]).permute(0, 3, 1, 2)
                 d = ((z - yd).abs().max() / den).item()
                 if d < best_d:
                     best, best_d = z.contiguous(), d

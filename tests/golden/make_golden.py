@@ -46,6 +46,10 @@ CONFIGS = [
     ('siamese_t32-64', 'siameseunet', [32, 64], 5, [0, 1], [2, 1, 0], 2, 64, None),
     ('dtsiamese_t32-64', 'dtsiameseunet', [32, 64], 5, [0, 1], [2, 1, 0], 2, 64, None),
     ('dualstream_t32-64', 'dualstreamunet', [32, 64], 5, [0, 1], [2, 1, 0], 2, 64, None),
+    # channel counts off the kernels' granule of 8 (the twin padding of utils/networks.py); [6, 12] puts two 6-wide
+    # halves into the Up and head concats (12 -> 2 x 8, not a 16-wide prefix)
+    ('siamese_t12-20', 'siameseunet', [12, 20], 5, [0, 1], [2, 1, 0], 2, 32, None),
+    ('dualstream_t6-12', 'dualstreamunet', [6, 12], 5, [0, 1], [2, 1, 0], 2, 32, None),
 ]
 LR = 1e-3
 WD = 0.01

@@ -426,7 +426,8 @@ def test_wgrad_halo(dev, n, h, w, ci, co):
 @pytest.mark.parametrize('n,h,w,co', [(2, 8, 64, 64), (1, 4, 64, 128), (3, 2, 64, 72), (2, 24, 48, 64)])
 def test_conv_16_channel_source_forward(dev, n, h, w, co):
     """The input layer's forward conv (16-channel source, two taps per 32-deep MFMA step) against fp64 under
-    x3 / x5 / bf16, with bias and fused BatchNorm tile statistics (against the host on the kernel's output)."""
+    x3 / x5 / bf16 / h2 (with the input's bound; without one h2 keeps x3), with bias and fused BatchNorm tile
+    statistics (against the host on the kernel's output)."""
     from multimodal_siamese_cd_amd import hip
     ci = 16
     g = torch.Generator().manual_seed(n * w + co)
@@ -437,20 +438,27 @@ def test_conv_16_channel_source_forward(dev, n, h, w, co):
     b = torch.randn(co, generator=g)
     ref = nhwc_t(F.conv2d(nchw(x).double(), wt.double(), b.double(), padding=1))
     errs = {}
-    for m in ('f32', 'x3', 'x5', 'bf16'):
+    for m in ('f32', 'x3', 'x5', 'bf16', 'h2'):
         prev = hip.set_conv_math(m)
         try:
             xd, wd, bd = x.to(dev), wt.to(dev), b.to(dev)
             wpk = hip.pack_conv3x3(wd, 0)
             y = torch.empty(n, h, w, co, device=dev)
+            xb = None
+            if m == 'h2':
+                xb = torch.zeros(1, device=dev)
+                hip.absmax_bound(hip.nhwc(xd), xb)
+                assert hip.igemm_arith(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y)) == 'x3'
             if m == 'f32':
                 hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, bd, hip.nhwc(y))
             else:
-                assert hip.igemm_arith(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y)) == m
-                ntiles, tpx = hip.igemm_stat_tiles(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y))
+                assert hip.igemm_arith(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y), src_bound=xb) == m
+                ntiles, tpx = hip.igemm_stat_tiles(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, hip.nhwc(y),
+                                                   src_bound=xb)
                 assert tpx == 128 and ntiles * tpx == n * h * w
                 rec = torch.empty(ntiles * co * 2, device=dev)
-                hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, bd, hip.nhwc(y), stat_rec=rec)
+                hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_3X3, wpk, co, bd, hip.nhwc(y), stat_rec=rec,
+                               src_bound=xb)
                 tw = next(c for c in (16, 32, 64) if w % c == 0 and h % (128 // c) == 0)
                 tr = 128 // tw
                 yy = y.double().cpu().reshape(n, h // tr, tr, w // tw, tw, co).permute(0, 1, 3, 2, 4, 5)
@@ -462,6 +470,16 @@ def test_conv_16_channel_source_forward(dev, n, h, w, co):
             hip.set_conv_math(prev)
         errs[m] = rel(y, ref)
     assert errs['x3'] <= 2 * errs['f32'] + 1e-7 and errs['x5'] < 1e-5 and errs['bf16'] < 2e-2, errs
+    assert errs['h2'] <= 2 * errs['f32'] + 1e-7, errs
+    # without a bound the h2-split weights are ignored and the per-tap x3 kernel runs: the same accuracy
+    prev = hip.set_conv_math('h2')
+    try:
+        y2 = torch.empty(n, h, w, co, device=dev)
+        hip.conv_igemm(hip.nhwc(x.to(dev)), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wt.to(dev), 0), co, b.to(dev),
+                       hip.nhwc(y2))
+    finally:
+        hip.set_conv_math(prev)
+    assert rel(y2, ref) <= 2 * errs['f32'] + 1e-7
 
 
 @pytest.mark.parametrize('n,h,w,co', [(2, 4, 32, 64), (3, 32, 48, 128), (1, 2, 16, 64)])
@@ -940,16 +958,22 @@ def test_halo_math_accuracy_vs_fp64(dev, ci, co):
 ])
 def test_pack_nchw(dev, n, c, h, w, c_begin, c_count, dst_c, off, ldc):
     """scd_pack_nchw vs torch: NCHW band slice -> NHWC channel slice, zero-filled above c_count, and the
-    channels outside the slice untouched."""
+    channels outside the slice untouched; the bound output is exactly the max |value| packed (raised, never
+    lowered: a larger starting value stays)."""
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(11)
-    x = torch.rand(n, c, h, w, generator=g)
+    x = torch.randn(n, c, h, w, generator=g) * 3
     buf = torch.full((n, h, w, ldc), -7.0, device=dev)
-    hip.pack_nchw(x.to(dev), c_begin, c_count, buf, off, dst_c)
+    bound = torch.zeros(1, device=dev)
+    hip.pack_nchw(x.to(dev), c_begin, c_count, buf, off, dst_c, bound=bound)
     exp = torch.full((n, h, w, ldc), -7.0)
     exp[..., off:off + dst_c] = 0.0
     exp[..., off:off + c_count] = x[:, c_begin:c_begin + c_count].permute(0, 2, 3, 1)
     assert torch.equal(buf.cpu(), exp)
+    assert bound.item() == x[:, c_begin:c_begin + c_count].abs().max().item()
+    big = torch.full((1,), 1e6, device=dev)
+    hip.pack_nchw(x.to(dev), c_begin, c_count, buf, off, dst_c, bound=big)
+    assert big.item() == 1e6
 
 
 WGRAD_PLANS = [  # n, h, w, ci, co: 64 / 128-row blocks, the 16-channel input-layer kernel, split-K ranges
