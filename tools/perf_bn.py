@@ -65,6 +65,31 @@ def main():
         print(f'{name:8s} {n:3d} {s:4d} {co:5d} | ' + ' | '.join(cells), flush=True)
     for k in tot:
         print(f'{k:6s} total {tot[k]:8.2f} ms  {byt[k] / tot[k] / 1e9:5.2f} TB/s')
+    # the encoder levels' backward: da = maxpool_bwd(gy, idx) -/+ the Siamese difference gradient, formed on the fly
+    # (scd_bn_relu_backward_pooled, the pair kernels); algorithmic bytes per y element: 2 x (y 4 + difference 2 (one
+    # t1/t2 pair reads it once) + pooled gradient 1 + argmax 0.25) + dy 4 = 18.5
+    print(f'{"level":8s} {"n":>3s} {"hw":>4s} {"c":>5s} | {"pooled bwd ms":>13s} {"TB/s":>5s}')
+    tp, bp = 0.0, 0.0
+    for name, n, s, _, co in layers(args.batch):
+        if not (name.startswith('enc') and name.endswith('b')):
+            continue
+        y = torch.randn(n, s, s, co, device=dev)
+        gy = torch.randn(n, s // 2, s // 2, co, device=dev)
+        idx = torch.randint(0, 4, (n, s // 2, s // 2, co), device=dev, dtype=torch.uint8)
+        cat = torch.randn(n // 2, s, s, 2 * co, device=dev)
+        dy = torch.empty_like(y)
+        gamma = torch.rand(co, device=dev) + 0.5
+        sm, si = torch.randn(2 * co, device=dev), torch.rand(2 * co, device=dev) + 0.5
+        sc, sh = torch.rand(2 * co, device=dev), torch.randn(2 * co, device=dev)
+        dg, db, dbias = torch.empty(co, device=dev), torch.empty(co, device=dev), torch.empty(co, device=dev)
+        ws = torch.empty(hip.bn_workspace_bytes(n, s, s, co, 2), dtype=torch.uint8, device=dev)
+        t = timeit(lambda: hip.bn_relu_backward_pooled(hip.nhwc(y), hip.nhwc(gy), idx, hip.nhwc(cat, 0, co), 1, 2, sm,
+                                                       si, gamma, sc, sh, dg, db, dbias, hip.nhwc(dy), ws), args.reps)
+        b = 18.5 * y.numel()
+        tp += t
+        bp += b
+        print(f'{name:8s} {n:3d} {s:4d} {co:5d} | {t:13.3f} {b / t / 1e9:5.2f}', flush=True)
+    print(f'pooled total {tp:8.2f} ms  {bp / tp / 1e9:5.2f} TB/s')
 
 
 if __name__ == '__main__':
