@@ -76,7 +76,19 @@ __global__ void pack_nchw_kernel(const float *__restrict__ src, int c, int hw, i
                 vmax = fmaxf(vmax, fabsf(v));
             }
     }
-    if (bound) wave_max_bound(bound, vmax);
+    if (bound) {  // one atomic per block (the launch caps the blocks under a bound: one hot address)
+        __shared__ float wmax[8];
+        vmax = fabsf(vmax);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = vmax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float m = wmax[0];
+            for (int k = 1; k < int(blockDim.x >> 6); ++k) m = fmaxf(m, wmax[k]);
+            atomic_max_bound(bound, m);
+        }
+    }
 }
 
 __global__ void pack_conv3x3_kernel(const float *__restrict__ w, int co, int ci, int ci_pad, int mode,
@@ -558,7 +570,8 @@ extern "C" int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, 
         set_error("pack_nchw: image too large");
         return SCD_ERR_ARG;
     }
-    const dim3 grid(unsigned(std::min<int64_t>((per_img + 255) / 256, 4096)), unsigned(n));
+    // under a bound at most 64 blocks per image (each block's maximum goes to one address by atomic)
+    const dim3 grid(unsigned(std::min<int64_t>((per_img + 255) / 256, bound ? 64 : 4096)), unsigned(n));
     if (vec)
         hipLaunchKernelGGL(pack_nchw_kernel<true>, grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
                            c_count, d, dst.c, dst.ldc, bound);

@@ -256,7 +256,7 @@ def test_fused_input_bn_model_step(dev):
     assert not check_branch_matched(g1, gref, list(P), GRAD_TOL)
 
 
-@pytest.mark.parametrize('name', ['siamese_t8-16', 'whatevernet_t8-16'])
+@pytest.mark.parametrize('name', ['siamese_t8-16', 'whatevernet_t8-16', 'siamese_t32-64'])
 def test_fused_siamese_encoder_matches_unfused(dev, name):
     """SiameseLevelFn (BN + ReLU fused into pool / difference, zero-copy concat) vs the plain encoder +
     SiameseDiffFn path: logits bit-identical, gradients equal up to summation order."""
@@ -283,7 +283,8 @@ def test_fused_siamese_encoder_matches_unfused(dev, name):
             assert rel_err(res[0][1][k].numpy(), res[1][1][k].numpy()) < 1e-5, k
 
 
-@pytest.mark.parametrize('name', ['siamese_t8-16', 'siamese_t8-16-32_odd', 'unet_t8-16', 'dtsiamese_t8-16'])
+@pytest.mark.parametrize('name', ['siamese_t8-16', 'siamese_t8-16-32_odd', 'unet_t8-16', 'dtsiamese_t8-16',
+                                  'siamese_t32-64', 'dtsiamese_t32-64'])  # the last two under h2 (32/64 channels)
 def test_fused_head_bit_identical(dev, name):
     """The 1x1 head fused into the decoder stage (engine fuse_head: forward through the last BatchNorm's
     coefficients, backward through scd_bn_relu_backward_head) vs the materialised decoder output + HeadFn:

@@ -33,6 +33,16 @@ def main():
     print(f'torch copy {t_c:.3f} ms {8 * big.numel() / t_c / 1e9:.2f} TB/s | add {t_add:.3f} ms '
           f'{12 * big.numel() / t_add / 1e9:.2f} TB/s  ({big.numel() / 1e6:.0f} M floats)', flush=True)
     del big, big2, out
+    # the input packing (NCHW 5 bands -> NHWC 16 channels), without and with the h2 input bound
+    xin = torch.rand(args.batch, 5, 256, 256, device=dev)
+    xpk = torch.empty(args.batch, 256, 256, 16, device=dev)
+    bnd = torch.zeros(1, device=dev)
+    t_p = timeit(lambda: hip.pack_nchw(xin, 0, 5, xpk), args.reps)
+    t_pb = timeit(lambda: hip.pack_nchw(xin, 0, 5, xpk, bound=bnd), args.reps)
+    pb = 4 * (xin.numel() + xpk.numel())
+    print(f'pack_nchw {t_p:.3f} ms {pb / t_p / 1e9:.2f} TB/s | with bound {t_pb:.3f} ms {pb / t_pb / 1e9:.2f} TB/s '
+          f'(bound {bnd.item():.6f} vs max {xin.max().item():.6f})', flush=True)
+    del xin, xpk
     tot = {'stats': 0.0, 'apply': 0.0, 'bwd': 0.0}
     byt = {'stats': 0.0, 'apply': 0.0, 'bwd': 0.0}
     print(f'{"layer":8s} {"n":>3s} {"hw":>4s} {"c":>5s} | {"stats ms":>8s} {"TB/s":>5s} | {"apply ms":>8s} {"TB/s":>5s} | '
