@@ -124,8 +124,10 @@ enum scd_conv_math {
 /* ABI revision of this header (struct layouts and signatures); a binding checks it at load time.
  *   3: scd_igemm_t / scd_wgrad_t / scd_pack_job_t carry `math` (and `tune`); the process-wide mode setters
  *      (scd_set_conv_math, scd_set_halo16, scd_set_wgrad16) and every launch-time environment switch are gone.
- *   4: scd_pack_nchw takes a nullable `bound` (the input layer's h2 operand bound). */
-#define SCD_ABI_VERSION 4
+ *   4: scd_pack_nchw takes a nullable `bound` (the input layer's h2 operand bound).
+ *   5: scd_bn_relu_backward_coef takes `da_bound` / `dy_bound` (the h2 bound of the dy a weight grad forms itself);
+ *      the 16-channel-source weight grad runs h2 when both scd_wgrad_t bounds are set. */
+#define SCD_ABI_VERSION 5
 int scd_abi_version(void);
 /* The arithmetic scd_conv_igemm / scd_conv_wgrad will use for a descriptor (its `math`, or SCD_MATH_X3 / F32 where
  * the shape or the missing operand bounds keep the conv off the requested kernels); negative = invalid descriptor.
@@ -156,6 +158,7 @@ int scd_abi_version(void);
 #define SCD_TUNE_NO_HALO16_C16    (1u << 25)  /* input-layer forward on the per-tap x3 kernel                     */
 #define SCD_TUNE_NO_HALO          (1u << 26)  /* no halo kernels at all (per-tap kernels)                         */
 #define SCD_TUNE_HALO16_LATE_LOAD (1u << 27)  /* single-buffered halo16: next chunk's halo loaded at the last tap  */
+#define SCD_TUNE_BF16_1XN         (1u << 28)  /* bf16 halo16 fwd / data grad on the 1xN wave tiles of h2             */
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);
@@ -277,7 +280,9 @@ typedef struct scd_wgrad {
     const float *src_shift;
     int32_t src_nseg;
     /* math == SCD_MATH_H2 only: device floats bounding |rows| and |src| (as read, after the src transform), as
-     * scd_igemm_t.src_bound.  With both set the 16x16x32 halo weight grad runs the fp16 two-term split; else x3. */
+     * scd_igemm_t.src_bound; with rows_y set (below), rows_bound bounds the dY formed from the rows
+     * (scd_bn_relu_backward_coef's dy_bound).  With both set the 16x16x32 halo weight grads (64-channel multiples
+     * and the 16-channel source) run the fp16 two-term split; else x3. */
     const float *rows_bound;
     const float *src_bound;
     /* Optional fused BatchNorm + ReLU backward of the rows (the input layer's: its dy is read by this weight grad
@@ -393,11 +398,15 @@ int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const 
 /* The statistics half of scd_bn_relu_backward(_tiles), for a consumer that forms dy itself (scd_wgrad_t.rows_y):
  * coef[nseg][c][2] = {mean(dz), mean(dz*xhat)} per segment, dgamma, dbeta, and dbias_prev = sum(dy) formed from the
  * sums (zero up to rounding: the BatchNorm removes the mean).  tile_rec = conv-epilogue records as in
- * scd_bn_relu_backward_tiles (da may then be null), or NULL for a partial pass over (y, da). */
+ * scd_bn_relu_backward_tiles (da may then be null), or NULL for a partial pass over (y, da).
+ * dy_bound (optional, needs da_bound = a device bound of |da|): raised to an upper bound of |dy| over every segment from
+ * the statistics alone, |gamma*invstd| (da_bound + |k1| + sqrt(n - 1) |k2|) plus rounding slack -- the SCD_MATH_H2
+ * rows bound (scd_wgrad_t.rows_bound) of the weight grad that forms this dy. */
 int scd_bn_relu_backward_coef(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
                               const float *save_invstd, const float *gamma, const float *scale, const float *shift,
                               const float *tile_rec, int32_t ntiles, float *coef, float *dgamma, float *dbeta,
-                              float *dbias_prev, void *ws, size_t ws_bytes, scd_stream_t stream);
+                              float *dbias_prev, const float *da_bound, float *dy_bound, void *ws, size_t ws_bytes,
+                              scd_stream_t stream);
 
 /* out[c] = sum over all pixels of x[., c] (ConvTranspose2d bias grad, networks.py:433); workspace as
  * scd_bn_workspace_bytes(n, h, w, c, 1).  replaces: the bias-grad reduction of convolution_backward. */

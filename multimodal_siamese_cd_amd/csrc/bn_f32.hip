@@ -791,13 +791,26 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__rest
     }
 }
 
+// Upper bound of |dy| = |gamma*invstd*(dz - k1 - xhat*k2)| over one segment and channel of n values from the statistics
+// alone (the SCD_MATH_H2 operand bound of a weight grad that forms dy itself, scd_wgrad_t.rows_y): |dz| <= the bound
+// of the incoming gradient, |xhat| <= sqrt(n - 1) (as bn_act_bound) plus the rounding of (y - mean) * invstd in fp32;
+// a relative 2^-10 covers the rounding of the expression.
+__device__ __forceinline__ float bn_dy_bound(double da_bound, double n, double gamma, double mean, double inv, double k1,
+                                             double k2) {
+    const double xhat = sqrt(n > 1 ? n - 1 : 0.0) * (1.0 + 0x1p-10) + fabs(mean) * inv * 0x1p-20 + 1.0;
+    return float(fabs(gamma * inv) * (da_bound + fabs(k1) + xhat * fabs(k2)) * (1.0 + 0x1p-10));
+}
+
 // one workgroup per channel: coef[seg][C][2] = {mean(dz), mean(dz*xhat)}; dgamma/dbeta summed over segments.
 // dbias (optional; the deferred form, whose dy is formed by its consumer and never summed): sum(dy) from the sums,
 // sum_seg gamma*invstd * (S1 - pseg * k1) -- zero but for the rounding of k1, as BatchNorm removes the mean.
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__restrict__ rec, int C, int nseg,
                                                               int ncps, int nrec, int64_t pseg, float *coef,
                                                               float *dgamma, float *dbeta, const float *gamma = nullptr,
-                                                              const float *sinv = nullptr, float *dbias = nullptr) {
+                                                              const float *sinv = nullptr, float *dbias = nullptr,
+                                                              const float *smean = nullptr,
+                                                              const float *da_bound = nullptr,
+                                                              float *dy_bound = nullptr) {
     __shared__ double a1[BN_THREADS], a2[BN_THREADS];
     const int c = blockIdx.x;
     const int t = threadIdx.x;
@@ -841,8 +854,11 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__res
                 a2[0] += a2[k];
             }
             const float k1 = float(a1[0] / double(pseg));
+            const float k2 = float(a2[0] / double(pseg));
             coef[(s * C + c) * 2 + 0] = k1;
-            coef[(s * C + c) * 2 + 1] = float(a2[0] / double(pseg));
+            coef[(s * C + c) * 2 + 1] = k2;
+            if (dy_bound) atomic_max_bound(dy_bound, bn_dy_bound(double(*da_bound), double(pseg), gamma ? gamma[c] : 1.0,
+                                                                 smean[s * C + c], sinv[s * C + c], k1, k2));
             tb += a1[0];
             tg += a2[0];
             if (dbias) {
@@ -1364,15 +1380,16 @@ extern "C" int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t n
 extern "C" int scd_bn_relu_backward_coef(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,
                                          const float *save_invstd, const float *gamma, const float *scale,
                                          const float *shift, const float *tile_rec, int32_t ntiles, float *coef,
-                                         float *dgamma, float *dbeta, float *dbias_prev, void *ws, size_t ws_bytes,
-                                         scd_stream_t stream) {
+                                         float *dgamma, float *dbeta, float *dbias_prev, const float *da_bound,
+                                         float *dy_bound, void *ws, size_t ws_bytes, scd_stream_t stream) {
     clear_error();
     SCD_TRY(bn_check(y, nseg));
     SCD_TRY(check_view(da, "bn_bwd_coef.da", tile_rec != nullptr));
     if ((!tile_rec && (da.n != y.n || da.h != y.h || da.w != y.w || da.c != y.c)) || !save_mean || !save_invstd ||
-        !scale || !shift || !coef || (tile_rec && (ntiles < nseg || ntiles % nseg || pixels(y) % ntiles))) {
-        set_error("bn_relu_backward_coef: shape mismatch / null / %d tiles not divisible into %d segments", ntiles,
-                  nseg);
+        !scale || !shift || !coef || (tile_rec && (ntiles < nseg || ntiles % nseg || pixels(y) % ntiles)) ||
+        (dy_bound && !da_bound)) {
+        set_error("bn_relu_backward_coef: shape mismatch / null / %d tiles not divisible into %d segments / dy_bound "
+                  "without da_bound", ntiles, nseg);
         return SCD_ERR_ARG;
     }
     if (!ws || ws_bytes < scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg)) {
@@ -1383,7 +1400,8 @@ extern "C" int scd_bn_relu_backward_coef(scd_nhwc_t y, scd_nhwc_t da, int32_t ns
     hipStream_t s = as_stream(stream);
     if (tile_rec) {
         hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, tile_rec, y.c, nseg, ntiles / nseg,
-                           ntiles, g.pseg, coef, dgamma, dbeta, gamma, save_invstd, dbias_prev);
+                           ntiles, g.pseg, coef, dgamma, dbeta, gamma, save_invstd, dbias_prev, save_mean, da_bound,
+                           dy_bound);
     } else {
         float *rec = static_cast<float *>(ws);
         hipLaunchKernelGGL(bn_bwd_partial<DaPlain>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
@@ -1391,7 +1409,7 @@ extern "C" int scd_bn_relu_backward_coef(scd_nhwc_t y, scd_nhwc_t da, int32_t ns
                            DaPlain{static_cast<const float *>(da.data), da.ldc}, y.c, g.pseg, g.ncps, g.chunk, g.nrec,
                            g.qpb, save_mean, save_invstd, scale, shift, rec);
         hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
-                           coef, dgamma, dbeta, gamma, save_invstd, dbias_prev);
+                           coef, dgamma, dbeta, gamma, save_invstd, dbias_prev, save_mean, da_bound, dy_bound);
     }
     return launch_status("scd_bn_relu_backward_coef");
 }

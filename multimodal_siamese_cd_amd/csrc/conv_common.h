@@ -130,7 +130,8 @@ void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
 // dY rows per block of the halo weight grad (64 or 128; threads = 4 * rows): plan and launch use the same value.
 int wgrad16_rblock(int math, uint32_t tune, int R, bool bounded);
 // 16-channel-source variant (the input layer), same eligibility otherwise (conv_halo16.hip).
-const void *wgrad_halo16_c16_fn(int math);
+const void *wgrad_halo16_c16_fn(int math, uint32_t tune, bool bounded);
+int wgrad_c16_planes(int math, uint32_t tune, bool bounded);  // 4 = h2 (both operands bounded), else as the x3 kernels
 void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s);
 // Halo weight grad (3x3 / stride 1 / same size, R and C multiples of 64, maps in 2x16 patches).
 inline const void *wgrad_halo_fn(int math, uint32_t tune, bool bounded, int rblock) {

@@ -963,7 +963,9 @@ static int wgrad_halo_resident(const scd_wgrad_t *d, bool c16, bool bounded, int
     // bf16 / h2 blocks
     static int caches[2][12] = {{0}};
     const int m = math_planes(d->math);
-    const int planes = m == 1 ? 0 : m == 5 ? 1 : (m == 2 && bounded && !c16) ? 3 : 2;
+    const int planes = m == 1 ? 0 : m == 5 ? 1
+                       : (m == 2 && bounded && (!c16 || wgrad_c16_planes(d->math, d->tune, bounded) == 4)) ? 3
+                                                                                                      : 2;
     const bool r128 = !c16 && rblock == 128;
     const int lay = (d->tune & SCD_TUNE_W16_LAYOUT_2X2) ? 1 : 0;
     int &cache = caches[lay][r128 ? 9 + (planes == 3) : c16 ? 5 + planes : 1 + planes];
@@ -972,7 +974,7 @@ static int wgrad_halo_resident(const scd_wgrad_t *d, bool c16, bool bounded, int
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu,
-                                                     c16 ? wgrad_halo16_c16_fn(d->math)
+                                                     c16 ? wgrad_halo16_c16_fn(d->math, d->tune, bounded)
                                                          : wgrad_halo_fn(d->math, d->tune, bounded, rblock),
                                                      r128 ? 512 : 256, 0) !=
             hipSuccess ||
@@ -1023,7 +1025,10 @@ extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
     SCD_TRY(wgrad_validate(d));
     if (!math_split(d->math)) return SCD_MATH_F32;
     if (wgrad_halo_ok(d)) return d->math == SCD_MATH_H2 && !wgrad_bounded(d) ? SCD_MATH_X3 : d->math;
-    if (wgrad_c16_ok(d)) return d->math == SCD_MATH_H2 ? SCD_MATH_X3 : d->math;
+    if (wgrad_c16_ok(d))
+        return d->math != SCD_MATH_H2 ? d->math
+               : wgrad_c16_planes(d->math, d->tune, wgrad_bounded(d)) == 4 ? SCD_MATH_H2
+                                                                          : SCD_MATH_X3;
     return wgrad_generic_h2(d) ? SCD_MATH_H2 : SCD_MATH_X3;
 }
 

@@ -531,20 +531,35 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
 //   0: 2x2 waves of 64 px x 64 ch  (128 x 128), 2 waves/SIMD
 //   1: 2x2 waves of 64 px x 32 ch  (128 x 64),  3 waves/SIMD
 //   2: 2x2 waves of 32 px x 64 ch  (64 x 128),  3 waves/SIMD
-//   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 only (no duplicated weight loads)
-//   4: 1x2 waves of 128 px x 32 ch (128 x 64),  2 waves/SIMD, h2 only (the same wave tile on 64-channel outputs)
+//   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 (and bf16, wide_1xn_ok): no duplicated weight loads
+//   4: 1x2 waves of 128 px x 32 ch (128 x 64),  2 waves/SIMD, the same wave tile on 64-channel outputs
 constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}, {4, 128, 64}};
 
-// The h2 arithmetics only (tile experiments that instantiate no x3 / x5 / bf16 variants).
+// The 1 x N wave tiles: the h2 arithmetic, and bf16 (one plane: double buffering always fits) where
+// wide_1xn_ok selects them.
 template <int WM, int WN, int TM, int TN, int OCC>
-void launch16_h2only(const IgemmArgs &a, int tw, hipStream_t s) {
+void launch16_1xn(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
+    if (math_planes(a.math) == 1) {
+        if (halo16_db(a.tune, false))
+            launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
+        else
+            launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
+        return;
+    }
     const bool db2 = tw != 64 && halo16_db(a.tune, true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
     if (db2)
         launch16c<WM, WN, TM, TN, OCC, true, 4>(a, tw, s);
     else
         launch16c<WM, WN, TM, TN, OCC, false, 4>(a, tw, s);
+}
+
+// Whether the 1 x N wave tiles (ids 3, 4) may run: h2 with its weight split, a bound and the pre-scaled low term;
+// bf16 under SCD_TUNE_BF16_1XN.
+bool wide_1xn_ok(const IgemmArgs &a) {
+    if (math_planes(a.math) == 1) return (a.tune & SCD_TUNE_BF16_1XN) != 0;
+    return a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune);
 }
 
 }  // namespace
@@ -561,18 +576,13 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     else if (a.n_out >= 128)
         // 128 x 128 at 2 waves/SIMD: +4..17% over the 32x32x16 halo kernel on the 128..512-channel layers; under h2
         // as 1 x 4 waves of 128 px x 32 ch (no weight fragment loaded by two waves; SCD_H2_TILE=0: 2 x 2)
-        id = (a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune) && h2_wide_tile(a.tune))
-                 ? 3
-                 : 0;
+        id = (wide_1xn_ok(a) && h2_wide_tile(a.tune)) ? 3 : 0;
     else if (a.n_out >= 64)
         // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
-        id = (a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune) && h2_tile64(a.tune)) ? 4
-                                                                                                              : 1;
+        id = (wide_1xn_ok(a) && h2_tile64(a.tune)) ? 4 : 1;
     else
         return 0;
-    if (id < 0 || id > 4 ||
-        (id > 2 && !(a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune))))
-        return 0;
+    if (id < 0 || id > 4 || (id > 2 && !wide_1xn_ok(a))) return 0;
     *bm = kCfg[id].bm;
     const int pref = 16;  // preferred tile width, the smallest halo per pixel (180 rows for 128 px)
     for (int cand : {pref, 64, 32, 16})
@@ -587,8 +597,8 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
     switch (cfg - 1) {
         case 0: launch16<2, 2, 4, 4, 2>(a, tw, s); break;
         case 1: launch16<2, 2, 4, 2, 3>(a, tw, s); break;
-        case 3: launch16_h2only<1, 4, 8, 2, 2>(a, tw, s); break;
-        case 4: launch16_h2only<1, 2, 8, 2, 2>(a, tw, s); break;
+        case 3: launch16_1xn<1, 4, 8, 2, 2>(a, tw, s); break;
+        case 4: launch16_1xn<1, 2, 8, 2, 2>(a, tw, s); break;
         default: launch16<2, 2, 2, 4, 3>(a, tw, s); break;
     }
 }
@@ -882,10 +892,6 @@ int halo16_c16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
         }
     return 0;
 }
-
-// Planes of the kernels that keep the split-bf16 operands under every mode (the 16-channel input layer's weight
-// grad): the mode's own, except h2, which runs x3 there.
-static int bf16_planes(int math) { return math_planes(math) == 2 ? 3 : math_planes(math); }
 
 // Arithmetic of the input-layer kernel: the mode's own; h2 with its weight split and a bound of the input (the
 // descriptors the x3 view keeps the split for), else x3.
@@ -1291,6 +1297,16 @@ __device__ __forceinline__ void c16_read_x(s16x4 (&f)[6], uint32_t xbase) {
 template <int T, int WAIT, int NP>
 __device__ __forceinline__ void c16_tap(f32x4 (&acc)[9], bf16x8 (&dv)[3], s16x4 (&f)[6]) {
     bf16x8 x0 = cat8(f[0], f[1]), x1 = cat8(f[2], f[3]), x2 = cat8(f[4], f[5]);
+    if constexpr (NP == 4) {  // h2 (as w16_half): x_m dy_h, (x_h 2^-11) dy_m', x_h dy_h on the fp16 planes
+        lds_wait<WAIT>(x0, x1);
+        if (T == 0) lds_wait<WAIT>(dv[0], dv[1]);
+        const u32x4 xh = __builtin_bit_cast(u32x4, x0), xm = __builtin_bit_cast(u32x4, x1);
+        const u32x4 dh = __builtin_bit_cast(u32x4, dv[0]), dm = __builtin_bit_cast(u32x4, dv[1]);
+        acc[T] = mfma16_f16(xm, dh, acc[T]);
+        acc[T] = mfma16_f16(f16_down11(xh), dm, acc[T]);
+        acc[T] = mfma16_f16(xh, dh, acc[T]);
+        return;
+    }
     if constexpr (NP != 1) {
         if constexpr (NP == 3)
             lds_wait<WAIT>(x0, x1, x2);
@@ -1325,6 +1341,8 @@ __device__ __forceinline__ void c16_chain(f32x4 (&acc)[9], bf16x8 (&dv)[3], s16x
 
 // RBN: the rows are dL/da of a = relu(BN(y)) and each staged dY piece is formed as the BatchNorm backward's apply
 // would write it (bn_bwd_dy4, the same bits), so that gradient is never written or re-read (the input layer's).
+// NP 4: h2 (as wgrad_halo16_x3<4, ...>): dY scaled by the power of two of *rows_bound (with RBN a bound of the formed
+// dY, scd_bn_relu_backward_coef's dy_bound) and split with its low term pre-scaled, X by that of *src_bound.
 template <int NP, bool RBN>
 __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
     constexpr int PH = 2, PW = 16, P = PH * PW;
@@ -1333,10 +1351,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
     constexpr int PA = P * RS, PB = HP * RSX;           // plane bytes
     constexpr int A_CH = P * 16, B_CH = HP * 4;         // 4-channel pieces: dY 32 px x 64 r, X 72 px x 16 c
     constexpr int A_PER = A_CH / 256, B_PER = (B_CH + 255) / 256;
-    static_assert(NP == 1 || NP == 3 || NP == 5, "x3, x5 or bf16");
-    constexpr int DP = NP == 1 ? 1 : 3;
+    static_assert(NP == 1 || NP == 3 || NP == 4 || NP == 5, "x3, x5, bf16 or h2");
+    constexpr bool H2 = NP == 4;
+    constexpr int DP = w16_dp<NP>();
     constexpr int XP = w16_xp<NP>();
     __shared__ __attribute__((aligned(16))) unsigned char smem[DP * PA + XP * PB];
+    float ds = 1.f, ds_inv = 1.f, xs = 1.f, xs_inv = 1.f;  // h2: power-of-two operand scales
+    if constexpr (H2) {
+        h2_scale(*a.rows_bound, ds, ds_inv);
+        h2_scale(*a.src_bound, xs, xs_inv);
+    }
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -1358,8 +1382,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
         const int img = pi / pimg, pr = pi - img * pimg;
         if (a.src_scale) {
             const int ch = (img / a.src_seg_imgs) * a.C + (tid & 3) * 4;
-            x_sc = gload4(a.src_scale + ch);
-            x_sh = gload4(a.src_shift + ch);
+            x_sc = gload4(a.src_scale + ch) * xs;  // h2: the scale folds into the transform exactly
+            x_sh = gload4(a.src_shift + ch) * xs;
         }
         if constexpr (RBN) {
             const int c = r0 + (tid & 15) * 4, o = (img / a.rows_seg_imgs) * a.R + c;
@@ -1399,7 +1423,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
             const int o = (e >> 4) * RS + (e & 15) * 8;
             u32x2 h, m, l;
             if constexpr (RBN) ra[i] = bn_bwd_dy4(ya[i], ra[i], r_mu, r_iv, r_sc, r_sf, r_k1, r_k2, r_mul);
-            if constexpr (DP == 3) {
+            if constexpr (H2) {
+                split2h_pre(ra[i] * ds, h, m);
+                *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
+            } else if constexpr (DP == 3) {
                 split3(ra[i], h, m, l);
                 *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
                 *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
@@ -1417,10 +1444,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
                     const bool v = (x_valid >> i) & 1u;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                } else if constexpr (H2) {
+                    rb[i] *= xs;
                 }
                 const int e = tid + i * 256;
                 const int o = DP * PA + (e >> 2) * RSX + (e & 3) * 8;
-                if constexpr (XP >= 2) {
+                if constexpr (H2) {
+                    split2h(rb[i], h, m);
+                    *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
+                } else if constexpr (XP >= 2) {
                     split3(rb[i], h, m, l);
                     *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
                     if constexpr (XP == 3) *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
@@ -1453,9 +1485,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
             s16x4 fa[6];
             tr_read<0 * PA + 0>(fa[0], dbase);
             tr_read<0 * PA + 8 * RS>(fa[1], dbase);
-            if constexpr (DP == 3) {
+            if constexpr (DP >= 2) {
                 tr_read<1 * PA + 0>(fa[2], dbase);
                 tr_read<1 * PA + 8 * RS>(fa[3], dbase);
+            }
+            if constexpr (DP == 3) {
                 tr_read<2 * PA + 0>(fa[4], dbase);
                 tr_read<2 * PA + 8 * RS>(fa[5], dbase);
             }
@@ -1474,6 +1508,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
         }
     }
 
+    if constexpr (H2) {
+        const float k = ds_inv * xs_inv;  // exact: a power of two
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t] *= k;
+    }
     // acc[t][q]: r = r0 + 16 wid + (lane & 15), c = 4g + q
     float *slab = a.slabs + size_t(split) * a.R * a.Ng;
     const int row = r0 + 16 * wid + w16;
@@ -1481,17 +1520,28 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
     for (int t = 0; t < 9; ++t) gstore4(slab + size_t(row) * a.Ng + t * 16 + 4 * g, acc[t]);
 }
 
-const void *wgrad_halo16_c16_fn(int math) {
-    switch (bf16_planes(math)) {
+// h2 runs where both operands are bounded, x3 otherwise.
+static int wgrad16_planes(int math, uint32_t tune, bool bounded) {
+    return math_planes(math) == 2 ? (bounded ? (h2_prescale(tune) ? 4 : 2) : 3) : math_planes(math);
+}
+// The 16-channel kernel's arithmetic: h2 with the pre-scaled low term only (SCD_TUNE_H2_NO_PRESCALE keeps it on x3).
+int wgrad_c16_planes(int math, uint32_t tune, bool bounded) {
+    const int np = wgrad16_planes(math, tune, bounded);
+    return np == 2 ? 3 : np;
+}
+const void *wgrad_halo16_c16_fn(int math, uint32_t tune, bool bounded) {
+    switch (wgrad_c16_planes(math, tune, bounded)) {
         case 1: return reinterpret_cast<const void *>(&wgrad_halo16_c16<1, false>);
+        case 4: return reinterpret_cast<const void *>(&wgrad_halo16_c16<4, false>);
         case 5: return reinterpret_cast<const void *>(&wgrad_halo16_c16<5, false>);
         default: return reinterpret_cast<const void *>(&wgrad_halo16_c16<3, false>);
     }
 }
 template <bool RBN>
 static void launch_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
-    switch (bf16_planes(a.math)) {
+    switch (wgrad_c16_planes(a.math, a.tune, a.rows_bound && a.src_bound)) {
         case 1: hipLaunchKernelGGL((wgrad_halo16_c16<1, RBN>), grid, dim3(256), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((wgrad_halo16_c16<4, RBN>), grid, dim3(256), 0, s, a); break;
         case 5: hipLaunchKernelGGL((wgrad_halo16_c16<5, RBN>), grid, dim3(256), 0, s, a); break;
         default: hipLaunchKernelGGL((wgrad_halo16_c16<3, RBN>), grid, dim3(256), 0, s, a);
     }
@@ -1501,11 +1551,6 @@ void launch_wgrad_halo16_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
         launch_c16<true>(a, grid, s);
     else
         launch_c16<false>(a, grid, s);
-}
-
-// h2 runs where both operands are bounded, x3 otherwise.
-static int wgrad16_planes(int math, uint32_t tune, bool bounded) {
-    return math_planes(math) == 2 ? (bounded ? (h2_prescale(tune) ? 4 : 2) : 3) : math_planes(math);
 }
 // Wave layout of the h2 and bf16 variants (W16L): SCD_TUNE_W16_LAYOUT_2X2 keeps the 2x2 layout, default along c.
 // x3 / x5 keep 2x2: their third dY plane does not fit four r blocks in registers.

@@ -530,7 +530,7 @@ __global__ void pjaccard_bwd_kernel(const float *__restrict__ logits, const floa
 using namespace scd;
 
 // ------------------------------------------------------------------------------------------------
-extern "C" const char *scd_version(void) { return "libscd 0.4.0 (gfx950, ABI 4: per-descriptor conv arithmetic, bounded input pack)"; }
+extern "C" const char *scd_version(void) { return "libscd 0.5.0 (gfx950, ABI 5: per-descriptor conv arithmetic, bounded input pack, h2 input-layer weight grad)"; }
 extern "C" const char *scd_last_error(void) { return g_err.c_str(); }
 
 extern "C" int scd_device_check(int device) {

@@ -460,8 +460,9 @@ def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, dy_bo
     return dy, dgamma, dbeta, dbias
 
 
-def _bn_backward_coef(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None):
-    """The statistics half of _bn_backward (hip.bn_relu_backward_coef): (dgamma, dbeta, dbias, coef)."""
+def _bn_backward_coef(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, da_bound=None, dy_bound=None):
+    """The statistics half of _bn_backward (hip.bn_relu_backward_coef): (dgamma, dbeta, dbias, coef).  `dy_bound`
+    (h2, with `da_bound` bounding g): a zeroed device float raised to a bound of the dy the consumer forms."""
     c = y.shape[3]
     dgamma, dbeta = _empty((c,), y), _empty((c,), y)
     dbias = _empty((c,), y) if conv_bias_grad else None
@@ -470,25 +471,31 @@ def _bn_backward_coef(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None):
     ws = _ws(hip.bn_workspace_bytes(n, h, w, c, st.nseg), y)
     hip.bn_relu_backward_coef(nhwc(y), nhwc(g), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift,
                               tiles[0] if tiles is not None else None, tiles[1] if tiles is not None else 0, coef,
-                              dgamma, dbeta, dbias, ws)
+                              dgamma, dbeta, dbias, ws, da_bound, dy_bound)
     return dgamma, dbeta, dbias, coef
 
 
 def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Tensor, st0: _BNSaved,
-                  src_bound=None):
+                  src_bound=None, pool=None):
     """Data-grad conv producing dL/da0, with BN0's backward partial sums fused into its epilogue when the kernel
-    offers them.  Returns (ga0, tiles or None)."""
+    offers them.  Returns (ga0, tiles or None, bound of ga0 or None).  `pool` (h2): the epilogue also raises a bound
+    of ga0 where the kernel runs h2 (for a consumer that forms BN0's dy itself, _bn_backward_coef)."""
     n, h, w, _ = dy1.shape
     ga0 = _empty((n, h, w, n_out), dy1)
+    gb = None
+    if pool is not None and hip.igemm_arith(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(ga0),
+                                            src_bound=src_bound) == 'h2':
+        gb = pool.take()
     if _OPTS['fuse_bn_bwd'] and st0.smean is not None:
         ntiles, _ = hip.igemm_bn_bwd_tiles(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(ga0), src_bound)
         if ntiles and ntiles % st0.nseg == 0:
             rec = _empty((n_out * ntiles * 2,), dy1)
             hip.conv_igemm(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, None, nhwc(ga0),
-                           bn_bwd=(y0, st0.nseg, st0.smean, st0.sinv, st0.scale, st0.shift, rec), src_bound=src_bound)
-            return ga0, (rec, ntiles)
-    hip.conv_igemm(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, None, nhwc(ga0), src_bound=src_bound)
-    return ga0, None
+                           bn_bwd=(y0, st0.nseg, st0.smean, st0.sinv, st0.scale, st0.shift, rec), src_bound=src_bound,
+                           dst_bound=gb)
+            return ga0, (rec, ntiles), gb
+    hip.conv_igemm(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, None, nhwc(ga0), src_bound=src_bound, dst_bound=gb)
+    return ga0, None, gb
 
 
 def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None):
@@ -506,13 +513,17 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None):
         gw1 = _wgrad3x3(dy1, y0, conv1.weight, (st0.scale, st0.shift, st0.nseg), d1, b0)
     else:
         gw1 = _wgrad3x3(dy1, a0, conv1.weight, None, d1, b0)
-    ga0, tiles0 = _dgrad_bn_bwd(dy1, packed_conv3x3(conv1.weight, 1), conv1.in_channels, y0, st0, d1)
+    ga0, tiles0, gb0 = _dgrad_bn_bwd(dy1, packed_conv3x3(conv1.weight, 1), conv1.in_channels, y0, st0, d1,
+                                     pool if not need_dx else None)
     d0 = _take(pool)
     if not need_dx and _OPTS['defer_bn_bwd'] and hip.wgrad_rows_bn_supported(nhwc(ga0), nhwc(x), 1, TAPS_3X3):
-        # the input layer: dy0 has one reader, the weight grad, which forms it while staging
-        dg0, db0, dbias0, coef = _bn_backward_coef(y0, ga0, st0, bn0, conv0.bias is not None, tiles0)
+        # the input layer: dy0 has one reader, the weight grad, which forms it while staging; under h2 its bound
+        # comes from the statistics and the bound of ga0 (the h2 input-layer weight grad)
+        rb0 = d0 if gb0 is not None and x_bound is not None else None
+        dg0, db0, dbias0, coef = _bn_backward_coef(y0, ga0, st0, bn0, conv0.bias is not None, tiles0,
+                                                   gb0 if rb0 is not None else None, rb0)
         rows_bn = (nhwc(y0), st0.nseg, st0.smean, st0.sinv, bn0.weight, st0.scale, st0.shift, coef)
-        gw0 = _wgrad3x3(ga0, x, conv0.weight, None, None, None, rows_bn)
+        gw0 = _wgrad3x3(ga0, x, conv0.weight, None, rb0, x_bound, rows_bn)
         return None, [gw0, dbias0, dg0, db0, gw1, dbias1, dg1, db1]
     dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0, d0)
     if pool is not None and x_bound is None and \

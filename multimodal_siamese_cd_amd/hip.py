@@ -151,7 +151,7 @@ _SIGS = {
     ),
     "scd_bn_relu_backward_coef": (
         [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
-         c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
         c_int,
     ),
     "scd_channel_sum": ([NHWC, c_void_p, c_void_p, c_size_t, c_void_p], c_int),
@@ -189,7 +189,7 @@ _SIGS = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
-ABI_VERSION = 4  # SCD_ABI_VERSION of include/scd.h
+ABI_VERSION = 5  # SCD_ABI_VERSION of include/scd.h
 
 
 def load_library(path: str = LIB_PATH):
@@ -398,6 +398,7 @@ TUNE_NO_WGRAD_H2 = 1 << 24
 TUNE_NO_HALO16_C16 = 1 << 25
 TUNE_NO_HALO = 1 << 26
 TUNE_HALO16_LATE_LOAD = 1 << 27
+TUNE_BF16_1XN = 1 << 28
 
 
 def tune_halo16_cfg(tile_id: int) -> int:
@@ -707,13 +708,16 @@ def bn_relu_backward_tiles(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, s
 
 
 def bn_relu_backward_coef(y: NHWC, da: NHWC, nseg, smean, sinv, gamma, scale, shift, tile_rec, ntiles, coef, dgamma,
-                          dbeta, dbias, ws):
+                          dbeta, dbias, ws, da_bound=None, dy_bound=None):
     """The statistics half of bn_relu_backward(_tiles): coef [nseg][C][2], dgamma, dbeta, dbias (sum dy, from the
-    sums) for a consumer that forms dy itself (wgrad_plan(..., rows_bn=...)).  tile_rec None: a pass over (y, da)."""
+    sums) for a consumer that forms dy itself (wgrad_plan(..., rows_bn=...)).  tile_rec None: a pass over (y, da).
+    `dy_bound` (with `da_bound`, a bound of |da|): raised to a bound of |dy| from the statistics (the h2 rows bound of
+    that consumer)."""
     _check(
         lib().scd_bn_relu_backward_coef(y, da, nseg, smean.data_ptr(), sinv.data_ptr(), _ptr(gamma), scale.data_ptr(),
                                         shift.data_ptr(), _ptr(tile_rec), ntiles, coef.data_ptr(), _ptr(dgamma),
-                                        _ptr(dbeta), _ptr(dbias), ws.data_ptr(), ws.numel(), _stream()),
+                                        _ptr(dbeta), _ptr(dbias), _ptr(da_bound), _ptr(dy_bound), ws.data_ptr(),
+                                        ws.numel(), _stream()),
         "scd_bn_relu_backward_coef")
 
 

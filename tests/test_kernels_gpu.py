@@ -565,13 +565,15 @@ def test_batchnorm_relu_train_forward_backward(dev, n, h, w, c, nseg):
     assert (dbias.cpu() - y.grad.sum((0, 1, 2))).abs().max() < 1e-3 * y.grad.abs().max()
 
 
-@pytest.mark.parametrize('math', ['x3', 'bf16'])
+@pytest.mark.parametrize('math', ['x3', 'bf16', 'h2'])
 @pytest.mark.parametrize('n,h,w,co,nseg,tiles', [(4, 8, 32, 64, 2, False), (2, 4, 16, 128, 1, False),
                                                  (4, 16, 16, 64, 2, True)])
 def test_wgrad_c16_deferred_bn_backward(dev, math, n, h, w, co, nseg, tiles):
     """The input layer's weight grad forming dy = BN-backward(y, da) while staging (scd_wgrad_t.rows_y, coefficients
     from scd_bn_relu_backward_coef) equals the BatchNorm backward's materialised dy fed to the same kernel, bit for
-    bit; dgamma / dbeta are the full backward's; the conv-bias grad (sum dy, 0 in exact arithmetic) stays ~0."""
+    bit; dgamma / dbeta are the full backward's; the conv-bias grad (sum dy, 0 in exact arithmetic) stays ~0.
+    h2: the coefficient pass's dy bound (from the statistics and a bound of da) bounds the materialised dy, both
+    weight grads run h2 under that bound, and the result is within 2e-6 of the fp64 weight grad."""
     from multimodal_siamese_cd_amd import hip
     ci = 16
     g = torch.Generator().manual_seed(n * co + nseg + h)
@@ -607,8 +609,18 @@ def test_wgrad_c16_deferred_bn_backward(dev, math, n, h, w, co, nseg, tiles):
             hip.bn_relu_backward(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, *o, hip.nhwc(dy), ws)
         assert hip.wgrad_rows_bn_supported(hip.nhwc(da), hip.nhwc(x), 1, hip.TAPS_3X3)
 
+        coef = torch.empty(nseg * co * 2, device=dev)
+        q = [torch.empty(co, device=dev) for _ in range(3)]
+        da_bound = da.abs().max().reshape(1) if math == 'h2' else None
+        dy_bound = torch.zeros(1, device=dev) if math == 'h2' else None
+        x_bound = x.abs().max().reshape(1) if math == 'h2' else None
+        hip.bn_relu_backward_coef(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, rec, ntiles, coef,
+                                  *q, ws, da_bound, dy_bound)
+
         def wgrad(rows, rows_bn=None):
-            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(rows), hip.nhwc(x), 1, hip.TAPS_3X3, rows_bn=rows_bn)
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(rows), hip.nhwc(x), 1, hip.TAPS_3X3, None, dy_bound, x_bound,
+                                               rows_bn=rows_bn)
+            assert hip.wgrad_arith(d) == math
             slabs = torch.empty(nbytes // 4, device=dev)
             hip.conv_wgrad(d, slabs)
             dw = torch.empty(co, ci, 3, 3, device=dev)
@@ -616,14 +628,16 @@ def test_wgrad_c16_deferred_bn_backward(dev, math, n, h, w, co, nseg, tiles):
             return dw
 
         ref = wgrad(dy)
-        coef = torch.empty(nseg * co * 2, device=dev)
-        q = [torch.empty(co, device=dev) for _ in range(3)]
-        hip.bn_relu_backward_coef(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, rec, ntiles, coef,
-                                  *q, ws)
         out = wgrad(da, (hip.nhwc(y), nseg, smean, sinv, gamma, scale, shift, coef))
     finally:
         hip.set_conv_math(prev)
     assert torch.equal(out, ref)
+    if math == 'h2':
+        amax = dy.abs().max().item()
+        assert amax <= dy_bound.item() < 4096 * amax * (n * h * w) ** 0.5
+        exact = torch.nn.grad.conv2d_weight(x.double().cpu().permute(0, 3, 1, 2), (co, ci, 3, 3),
+                                            dy.double().cpu().permute(0, 3, 1, 2), padding=1)
+        assert rel(out.double().cpu(), exact) < 2e-6
     assert torch.equal(q[0], o[0]) and torch.equal(q[1], o[1])
     scale_dy = dy.abs().max().item()
     assert q[2].abs().max().item() < 1e-3 * scale_dy and o[2].abs().max().item() < 1e-3 * scale_dy
