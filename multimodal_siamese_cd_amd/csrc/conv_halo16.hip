@@ -531,23 +531,16 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
 //   0: 2x2 waves of 64 px x 64 ch  (128 x 128), 2 waves/SIMD
 //   1: 2x2 waves of 64 px x 32 ch  (128 x 64),  3 waves/SIMD
 //   2: 2x2 waves of 32 px x 64 ch  (64 x 128),  3 waves/SIMD
-//   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 (and bf16, wide_1xn_ok): no duplicated weight loads
-//   4: 1x2 waves of 128 px x 32 ch (128 x 64),  2 waves/SIMD, the same wave tile on 64-channel outputs
+//   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 only (no duplicated weight loads)
+//   4: 1x2 waves of 128 px x 32 ch (128 x 64),  2 waves/SIMD, h2 only (the same wave tile on 64-channel outputs)
 constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}, {4, 128, 64}};
 
-// The 1 x N wave tiles: the h2 arithmetic, and bf16 (one plane: double buffering always fits) where
-// wide_1xn_ok selects them.
+// The 1 x N wave tiles: the h2 arithmetic only (bf16 on them measured slower: 21.38 vs 21.05 ms per bf16 step,
+// the 64-channel layers -5..-15%, same-box A/B, round 3; not kept).
 template <int WM, int WN, int TM, int TN, int OCC>
 void launch16_1xn(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16;
     const int hr = (BM / tw + 2) * (tw + 2);
-    if (math_planes(a.math) == 1) {
-        if (halo16_db(a.tune, false))
-            launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
-        else
-            launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
-        return;
-    }
     const bool db2 = tw != 64 && halo16_db(a.tune, true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
     if (db2)
         launch16c<WM, WN, TM, TN, OCC, true, 4>(a, tw, s);
@@ -555,10 +548,8 @@ void launch16_1xn(const IgemmArgs &a, int tw, hipStream_t s) {
         launch16c<WM, WN, TM, TN, OCC, false, 4>(a, tw, s);
 }
 
-// Whether the 1 x N wave tiles (ids 3, 4) may run: h2 with its weight split, a bound and the pre-scaled low term;
-// bf16 under SCD_TUNE_BF16_1XN.
+// Whether the 1 x N wave tiles (ids 3, 4) may run: h2 with its weight split, a bound and the pre-scaled low term.
 bool wide_1xn_ok(const IgemmArgs &a) {
-    if (math_planes(a.math) == 1) return (a.tune & SCD_TUNE_BF16_1XN) != 0;
     return a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune);
 }
 

@@ -996,11 +996,13 @@ __global__ void split_bf16x3_kernel(const float *__restrict__ src, int64_t n4, u
 // from the OIHW parameter (one launch per training step instead of two per conv).
 // ------------------------------------------------------------------------------------------------
 constexpr int kPackJobs = 48;
+constexpr int kPackCW = 64;  // inner columns (mode 0: input channels, mode 1: output channels) per tile
+constexpr int kPackLD = kPackCW + 1;  // LDS row stride: the strided fills hit distinct banks
 struct PackJobs {
     scd_pack_job_t j[kPackJobs];
-    int first_block[kPackJobs + 1];
-    int first_row[kPackJobs + 1];  // h2 jobs: padded split rows (NB * 32) of the row-scale pass, prefix sums
-    int h2[kPackJobs];             // split in the SCD_MATH_H2 format (fp16 h, m planes + per-row inverse scales)
+    int first_block[kPackJobs + 1];  // tiles (32 rows x kPackCW inner columns x 9 taps), prefix sums
+    int first_rs[kPackJobs + 1];     // h2 jobs: 32-row groups of the row-scale pass, prefix sums
+    int h2[kPackJobs];               // split in the SCD_MATH_H2 format (fp16 h, m planes + per-row inverse scales)
     int n;
 };
 
@@ -1009,84 +1011,107 @@ __device__ __forceinline__ float *h2_row_inv(uint16_t *split, int64_t plane) {
     return reinterpret_cast<float *>(split + 2 * plane);
 }
 
-// One wave per padded split row of every h2 job: the row's max |w| -> its power-of-two inverse scale (the split
-// pass below scales the row by the reciprocal).  Rows of the packed layout are output channels (mode 0) or input
-// channels (mode 1, the data-grad layout); the max is read from the OIHW parameter directly.
+// Rows, inner width and K of a job's packed layout: mode 0 [co][9][ci_pad], mode 1 [ci][9][co] (taps flipped).
+__device__ __forceinline__ void pack_dims(const scd_pack_job_t &J, int &rows, int &kin, int &K) {
+    rows = J.mode == 0 ? J.co : J.ci;
+    kin = J.mode == 0 ? J.ci_pad : J.co;
+    K = 9 * kin;
+}
+
+// One block per 32-row group of every h2 job: the rows' max |w| -> their power-of-two inverse scales (the tile pass
+// below scales each row by the reciprocal).  The OIHW parameter is read in whole contiguous runs: mode 0 rows are
+// output channels (w[r][*][*], one wave per row), mode 1 rows are input channels, whose 32-row group is the run
+// w[o][r0 .. r0+31][*] of every output channel o (each thread keeps the max of its two fixed positions in the run).
 __global__ __launch_bounds__(256) void pack_rowscale_kernel(PackJobs jobs) {
-    const int wave = int(blockIdx.x) * 4 + int(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wave >= jobs.first_row[jobs.n]) return;
+    __shared__ unsigned smax[32];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     int q = 0;
-    while (q + 1 < jobs.n && wave >= jobs.first_row[q + 1]) ++q;
+    while (q + 1 < jobs.n && b >= jobs.first_rs[q + 1]) ++q;
     const scd_pack_job_t J = jobs.j[q];
-    const int r = wave - jobs.first_row[q];
-    const int rows = J.mode == 0 ? J.co : J.ci;
-    const int K = 9 * (J.mode == 0 ? J.ci_pad : J.co);
-    float mx = 0.f;
-    if (r < rows) {
-        if (J.mode == 0) {
-            const int n = J.ci * 9;
-            for (int e = lane; e < n; e += 64) mx = fmaxf(mx, fabsf(J.w[size_t(r) * n + e]));
-        } else {
-            const int n = J.co * 9;
-            for (int e = lane; e < n; e += 64) {
-                const int o = e / 9, t = e - o * 9;
-                mx = fmaxf(mx, fabsf(J.w[(size_t(o) * J.ci + r) * 9 + t]));
-            }
-        }
-    }
+    int rows, kin, K;
+    pack_dims(J, rows, kin, K);
+    const int r0 = (b - jobs.first_rs[q]) * 32;
+    if (tid < 32) smax[tid] = 0u;
+    __syncthreads();
+    if (J.mode == 0) {
+        const int n = J.ci * 9;
+        for (int rr = wid; rr < 32; rr += 4) {
+            float mx = 0.f;
+            if (r0 + rr < rows)
+                for (int e = lane; e < n; e += 64) mx = fmaxf(mx, fabsf(J.w[size_t(r0 + rr) * n + e]));
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-    if (lane == 0) {
+            for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+            if (lane == 0) smax[rr] = __float_as_uint(mx);
+        }
+    } else {
+        const int nr = min(32, rows - r0), run = nr * 9;
+        float ma = 0.f, mb = 0.f;
+        for (int o = 0; o < J.co; ++o) {
+            const float *src = J.w + (size_t(o) * J.ci + r0) * 9;
+            if (tid < run) ma = fmaxf(ma, fabsf(src[tid]));
+            if (tid + 256 < run) mb = fmaxf(mb, fabsf(src[tid + 256]));
+        }
+        if (tid < run) atomicMax(&smax[tid / 9], __float_as_uint(ma));  // non-negative floats order as integers
+        if (tid + 256 < run) atomicMax(&smax[(tid + 256) / 9], __float_as_uint(mb));
+    }
+    __syncthreads();
+    if (tid < 32) {
         float sc, inv;
-        h2_scale(mx, sc, inv);
-        h2_row_inv(J.split, int64_t((rows + 31) / 32) * 32 * K)[r] = inv;
+        h2_scale(__uint_as_float(smax[tid]), sc, inv);
+        h2_row_inv(J.split, int64_t((rows + 31) / 32) * 32 * K)[r0 + tid] = inv;
     }
 }
 
-// Element (row r, column k) of the packed layout of job J.
-__device__ __forceinline__ float packed_at(const scd_pack_job_t &J, int r, int k) {
-    if (J.mode == 0) {  // [co][9][ci_pad]
-        const int t = k / J.ci_pad, c = k - t * J.ci_pad;
-        return c < J.ci ? J.w[(size_t(r) * J.ci + c) * 9 + t] : 0.f;
-    }
-    const int t = k / J.co, o = k - t * J.co;  // [ci][9][co], taps flipped
-    return J.w[(size_t(o) * J.ci + r) * 9 + (8 - t)];
-}
-
+// One block per tile of 32 rows x kPackCW inner columns x 9 taps of a job's packed layout.  The tile's OIHW values
+// are read in contiguous runs into LDS (mode 0: w[r][c0 ..][*] per row; mode 1: w[o][r0 .. r0+31][*] per output
+// channel), then written as coalesced packed rows and, with a split, as whole 1 KB fragment slots (fragment order of
+// scd_split_bf16x3_frag / scd_split_h2_frag).  The same values and split arithmetic as the element-wise pack.
 __global__ __launch_bounds__(256) void pack_multi_kernel(PackJobs jobs) {
+    __shared__ float T[32 * 9 * kPackLD];  // [row][tap][inner column]
+    const int b = blockIdx.x, tid = threadIdx.x;
     int q = 0;
-    while (q + 1 < jobs.n && int(blockIdx.x) >= jobs.first_block[q + 1]) ++q;
+    while (q + 1 < jobs.n && b >= jobs.first_block[q + 1]) ++q;
     const scd_pack_job_t J = jobs.j[q];
-    const int rows = J.mode == 0 ? J.co : J.ci;
-    const int K = 9 * (J.mode == 0 ? J.ci_pad : J.co);
-    const int64_t P = int64_t(rows) * K;
+    int rows, kin, K;
+    pack_dims(J, rows, kin, K);
+    const int nchunk = (kin + kPackCW - 1) / kPackCW;
+    const int tile = b - jobs.first_block[q];
+    const int nb = tile / nchunk, c0 = (tile - nb * nchunk) * kPackCW;
+    const int cw = min(kPackCW, kin - c0);
+    const int r0 = nb * 32;
+    if (J.mode == 0) {  // T[rr][t][j] = w[r0 + rr][c0 + j][t] (zero for padded channels and rows)
+        const int run = cw * 9;
+        for (int e = tid; e < 32 * run; e += 256) {
+            const int rr = e / run, f = e - rr * run, j = f / 9, t = f - j * 9;
+            const int r = r0 + rr, c = c0 + j;
+            T[(rr * 9 + t) * kPackLD + j] = (r < rows && c < J.ci) ? J.w[(size_t(r) * J.ci + c) * 9 + t] : 0.f;
+        }
+    } else {  // T[rr][t][j] = w[c0 + j][r0 + rr][8 - t]
+        for (int e = tid; e < cw * 288; e += 256) {
+            const int j = e / 288, f = e - j * 288, rr = f / 9, t = f - rr * 9;
+            const int r = r0 + rr;
+            T[(rr * 9 + (8 - t)) * kPackLD + j] = r < rows ? J.w[(size_t(c0 + j) * J.ci + r) * 9 + t] : 0.f;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < 32 * 9 * cw; e += 256) {  // packed rows: out[r][t * kin + c0 + j]
+        const int rr = e / (9 * cw), f = e - rr * 9 * cw, t = f / cw, j = f - t * cw;
+        if (r0 + rr < rows) J.out[size_t(r0 + rr) * K + t * kin + c0 + j] = T[(rr * 9 + t) * kPackLD + j];
+    }
+    if (!J.split) return;
     const int KS = K / 16, NB = (rows + 31) / 32;
-    const int64_t S = J.split ? int64_t(NB) * KS * 64 : 0;
-    const int64_t plane = S * 8;
-    const int64_t stride = int64_t(jobs.first_block[q + 1] - jobs.first_block[q]) * blockDim.x;
-    for (int64_t e = int64_t(blockIdx.x - jobs.first_block[q]) * blockDim.x + threadIdx.x; e < P + S; e += stride) {
-        if (e < P) {
-            const int r = int(e / K);
-            J.out[e] = packed_at(J, r, int(e - int64_t(r) * K));
-            continue;
-        }
-        const int64_t f = e - P;  // split slot: 8 consecutive k of one row, fragment order
-        const int lane = int(f & 63);
-        const int64_t fk = f >> 6;
-        const int nb = int(fk / KS), ks = int(fk - int64_t(nb) * KS);
-        const int r = nb * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
-        f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
-        if (r < rows) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                v0[i] = packed_at(J, r, k0 + i);
-                v1[i] = packed_at(J, r, k0 + 4 + i);
-            }
-        }
-        uint16_t *o = J.split + f * 8;
+    const int64_t plane = int64_t(NB) * KS * 64 * 8;
+    const int nkb = cw / 16;  // 16-column fragment blocks per tap in this tile (kin % 16 == 0 with a split)
+    for (int e = tid; e < 9 * nkb * 64; e += 256) {
+        const int lane = e & 63, tk = e >> 6, t = tk / nkb, kb = tk - t * nkb;
+        const int rr = lane & 31, j0 = kb * 16 + 8 * (lane >> 5);
+        const int ks = (t * kin + c0) / 16 + kb;
+        const float *src = T + (rr * 9 + t) * kPackLD + j0;
+        f32x4 v0 = {src[0], src[1], src[2], src[3]}, v1 = {src[4], src[5], src[6], src[7]};
+        uint16_t *o = J.split + ((int64_t(nb) * KS + ks) * 64 + lane) * 8;
         u32x2 h0, m0, l0, h1, m1, l1;
         if (jobs.h2[q]) {
-            const float sc = 1.f / h2_row_inv(J.split, plane)[r];  // exact: a power of two
+            const float sc = 1.f / h2_row_inv(J.split, plane)[r0 + rr];  // exact: a power of two
             split2h(v0 * sc, h0, m0);
             split2h(v1 * sc, h1, m1);
             *reinterpret_cast<u32x4 *>(o) = u32x4{h0[0], h0[1], h1[0], h1[1]};
@@ -1115,27 +1140,25 @@ extern "C" int scd_pack_conv3x3_multi(const scd_pack_job_t *jobs, int32_t n, scd
         PackJobs pj;
         pj.n = std::min(kPackJobs, n - base);
         pj.first_block[0] = 0;
-        pj.first_row[0] = 0;
+        pj.first_rs[0] = 0;
         for (int i = 0; i < pj.n; ++i) {
             const scd_pack_job_t &J = jobs[base + i];
-            const int rows = J.mode == 0 ? J.co : J.ci, K = 9 * (J.mode == 0 ? J.ci_pad : J.co);
-            pj.h2[i] = J.split && h2_weight_format(J.math, 9, K / 9);
-            pj.first_row[i + 1] = pj.first_row[i] + (pj.h2[i] ? (rows + 31) / 32 * 32 : 0);
+            const int rows = J.mode == 0 ? J.co : J.ci, kin = J.mode == 0 ? J.ci_pad : J.co, K = 9 * kin;
             if (!J.w || !J.out || J.co < 1 || J.ci < 1 || J.ci_pad < J.ci || (J.mode != 0 && J.mode != 1) ||
                 (J.split && (K % 16 || !aligned16(J.split)))) {
                 set_error("pack_conv3x3_multi: job %d: bad arguments (split needs K %% 16 == 0, 16-byte alignment)",
                           base + i);
                 return SCD_ERR_ARG;
             }
-            const int64_t work = int64_t(rows) * K + (J.split ? int64_t((rows + 31) / 32) * (K / 16) * 64 * 8 : 0);
-            const int blocks = int(std::min<int64_t>(std::max<int64_t>((work + 2047) / 2048, 1), 1024));
+            pj.h2[i] = J.split && h2_weight_format(J.math, 9, kin);
+            const int groups = (rows + 31) / 32;
+            pj.first_rs[i + 1] = pj.first_rs[i] + (pj.h2[i] ? groups : 0);
             pj.j[i] = J;
-            pj.first_block[i + 1] = pj.first_block[i] + blocks;
+            pj.first_block[i + 1] = pj.first_block[i] + groups * ((kin + kPackCW - 1) / kPackCW);
         }
         if (pj.n == 0) break;
-        if (pj.first_row[pj.n] > 0)
-            hipLaunchKernelGGL(pack_rowscale_kernel, dim3((pj.first_row[pj.n] + 3) / 4), dim3(256), 0,
-                               as_stream(stream), pj);
+        if (pj.first_rs[pj.n] > 0)
+            hipLaunchKernelGGL(pack_rowscale_kernel, dim3(pj.first_rs[pj.n]), dim3(256), 0, as_stream(stream), pj);
         hipLaunchKernelGGL(pack_multi_kernel, dim3(pj.first_block[pj.n]), dim3(256), 0, as_stream(stream), pj);
         SCD_TRY(launch_status("scd_pack_conv3x3_multi"));
     }

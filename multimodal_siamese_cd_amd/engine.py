@@ -182,18 +182,28 @@ def _ws(nbytes: int, like: torch.Tensor):
 # to max |dy| as it writes dy (dy_bound); scd_absmax_bound covers the rest (eval mode, the ConvT half of a concat).
 # A bound is a one-float device tensor; bounds are only allocated under h2.
 # ------------------------------------------------------------------------------------------------
-class _Bounds:
-    """Zero-initialised device floats handed out one at a time (one fill launch per 64)."""
+_ARENA_FLOATS = 4096
+_ZERO_ARENA: dict = {}  # device -> [zeroed float buffer, floats handed out]
 
-    def __init__(self, like: torch.Tensor, chunk: int = 64):
-        self.device, self.chunk = like.device, chunk
-        self.buf, self.i = None, 0
+
+def _zero_float(device) -> torch.Tensor:
+    """A fresh zero-initialised device float, carved from a per-device arena: one fill launch per 4096 bounds
+    instead of one per stage and input (~30 fills per training step before).  A float is never handed out twice."""
+    ent = _ZERO_ARENA.get(device)
+    if ent is None or ent[1] == _ARENA_FLOATS:
+        ent = _ZERO_ARENA[device] = [torch.zeros(_ARENA_FLOATS, device=device, dtype=_F32), 0]
+    ent[1] += 1
+    return ent[0][ent[1] - 1:ent[1]]
+
+
+class _Bounds:
+    """Zero-initialised device floats handed out one at a time (from the per-device arena)."""
+
+    def __init__(self, like: torch.Tensor):
+        self.device = like.device
 
     def take(self) -> torch.Tensor:
-        if self.buf is None or self.i == self.chunk:
-            self.buf, self.i = torch.zeros(self.chunk, device=self.device, dtype=_F32), 0
-        self.i += 1
-        return self.buf[self.i - 1:self.i]
+        return _zero_float(self.device)
 
 
 def _bounds(like: torch.Tensor):
@@ -567,7 +577,7 @@ def _check_input_pair(x_t1: torch.Tensor, x_t2: torch.Tensor) -> None:
 def _input_bound(like: torch.Tensor):
     """Under h2, a zeroed device float the input packing raises to max |input| (the input layer's operand bound,
     registered for the packed tensor: no extra pass), else None."""
-    return torch.zeros(1, device=like.device, dtype=_F32) if hip.conv_math() == 'h2' else None
+    return _zero_float(like.device) if hip.conv_math() == 'h2' else None
 
 
 def pack_pair(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count: int | None = None) -> torch.Tensor:

@@ -398,7 +398,6 @@ TUNE_NO_WGRAD_H2 = 1 << 24
 TUNE_NO_HALO16_C16 = 1 << 25
 TUNE_NO_HALO = 1 << 26
 TUNE_HALO16_LATE_LOAD = 1 << 27
-TUNE_BF16_1XN = 1 << 28
 
 
 def tune_halo16_cfg(tile_id: int) -> int:

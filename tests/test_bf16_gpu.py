@@ -55,17 +55,8 @@ def nhwc_t(t):
 SHAPES = [(2, 16, 32, 64, 128), (2, 16, 16, 128, 64), (1, 16, 16, 512, 512), (4, 8, 16, 64, 64), (2, 32, 32, 256, 256)]
 
 
-@pytest.fixture(params=['default', '1xn'])
-def bf16_tile(request, bf16):
-    """The bf16 halo tiles: the library default and the 1 x N wave tiles of h2 (SCD_TUNE_BF16_1XN)."""
-    from multimodal_siamese_cd_amd import hip
-    prev = hip.set_tune(hip.TUNE_BF16_1XN if request.param == '1xn' else 0)
-    yield request.param
-    hip.set_tune(prev)
-
-
 @pytest.mark.parametrize('n,h,w,ci,co', SHAPES)
-def test_bf16_conv_forward_and_data_grad(dev, bf16_tile, n, h, w, ci, co):
+def test_bf16_conv_forward_and_data_grad(dev, bf16, n, h, w, ci, co):
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(n + h + ci + co)
     x = torch.randn(n, h, w, ci, generator=g)

@@ -1024,3 +1024,36 @@ def test_wgrad_slabs_fully_written(dev, math, tune, n, h, w, ci, co):
     hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
     e = rel(dw, ref)
     assert e < (2e-2 if arith == 'bf16' else 2e-5), (arith, e)
+
+
+@pytest.mark.parametrize('arith', ['f32', 'x3', 'bf16', 'h2'])
+def test_batched_weight_pack_equals_standalone(dev, arith):
+    """scd_pack_conv3x3_multi (LDS-staged 32-row x 64-column tiles, one launch for every job) writes the packed fp32
+    layout and the split bytes the standalone pack + split would, for both layouts, on shapes with padded channels,
+    row counts off the 32-row group and inner widths off the 64-column tile."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(7)
+    shapes = [(64, 5, 16), (96, 64, 64), (48, 80, 80), (512, 512, 512), (64, 128, 128), (16, 32, 32)]
+    ws = [(torch.randn(co, ci, 3, 3, generator=g) * 10 ** (2 * torch.rand(co, 1, 1, 1, generator=g) - 1)).to(dev)
+          for co, ci, _ in shapes]
+    jobs = []
+    for (co, ci, cp), w in zip(shapes, ws):
+        jobs.append((w, 0, cp))
+        if ci == cp and co % 16 == 0:
+            jobs.append((w, 1, ci))
+    prev = hip.set_conv_math(arith)
+    try:
+        multi = hip.pack_conv3x3_multi(jobs)
+        for (w, mode, cp), got in zip(jobs, multi):
+            ref = hip.pack_conv3x3(w, mode, cp if mode == 0 else None)
+            assert torch.equal(got, ref), (tuple(w.shape), mode)
+            a, b = getattr(got, '_x3', None), getattr(ref, '_x3', None)
+            assert (a is None) == (b is None), (tuple(w.shape), mode)
+            if a is not None:
+                rows, K = (w.shape[0], 9 * cp) if mode == 0 else (w.shape[1], 9 * w.shape[0])
+                if arith == 'h2':  # two fp16 planes and the row scales; the rest of the buffer is not written
+                    n = 2 * ((rows + 31) // 32 * 32) * K + 2 * ((rows + 31) // 32 * 32)
+                    a, b = a[:n], b[:n]
+                assert torch.equal(a, b), (tuple(w.shape), mode)
+    finally:
+        hip.set_conv_math(prev)
