@@ -135,7 +135,7 @@ int scd_abi_version(void);
 /* Kernel-variant selection, scd_igemm_t.tune / scd_wgrad_t.tune.  0 = the library's measured defaults; the other
  * values select variants kept for bit-identity tests and A/B measurements.  Every variant computes the same
  * outputs (bit-identical where the tests say so, else equal up to fp32 summation order). */
-#define SCD_TUNE_HALO16_CFG(id)   ((uint32_t)((id) + 1))  /* force 16x16x32 halo tile id 0..4 (id 3, 4: h2 only) */
+#define SCD_TUNE_HALO16_CFG(id)   ((uint32_t)((id) + 1))  /* force 16x16x32 halo tile id 0..5 (3-5: h2 only) */
 #define SCD_TUNE_HALO16_OFF       0xFu                    /* the 32x32x16 halo kernel instead                     */
 #define SCD_TUNE_HALO16_MASK      0xFu
 #define SCD_TUNE_H2_TILE_2X2      (1u << 4)   /* h2, >= 128 outputs: 2x2 waves instead of 1x4                     */
@@ -158,6 +158,7 @@ int scd_abi_version(void);
 #define SCD_TUNE_NO_HALO16_C16    (1u << 25)  /* input-layer forward on the per-tap x3 kernel                     */
 #define SCD_TUNE_NO_HALO          (1u << 26)  /* no halo kernels at all (per-tap kernels)                         */
 #define SCD_TUNE_HALO16_LATE_LOAD (1u << 27)  /* single-buffered halo16: next chunk's halo loaded at the last tap  */
+#define SCD_TUNE_H2_TILE64_256    (1u << 28)  /* h2, 64..127 outputs: 256 x 64 tiles (2x2 waves of 128 px x 32 ch)  */
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);

@@ -533,7 +533,9 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
 //   2: 2x2 waves of 32 px x 64 ch  (64 x 128),  3 waves/SIMD
 //   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 only (no duplicated weight loads)
 //   4: 1x2 waves of 128 px x 32 ch (128 x 64),  2 waves/SIMD, h2 only (the same wave tile on 64-channel outputs)
-constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}, {4, 128, 64}};
+//   5: 2x2 waves of 128 px x 32 ch (256 x 64),  2 waves/SIMD, h2 only (SCD_TUNE_H2_TILE64_256: the 64-channel wave
+//      tile of config 4 on a 16 x 16 pixel patch, whose halo is 1.27 rows per pixel instead of 1.41)
+constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}, {4, 128, 64}, {5, 256, 64}};
 
 // The 1 x N wave tiles: the h2 arithmetic only (bf16 on them measured slower: 21.38 vs 21.05 ms per bf16 step,
 // the 64-channel layers -5..-15%, same-box A/B, round 3; not kept).
@@ -570,18 +572,21 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
         id = (wide_1xn_ok(a) && h2_wide_tile(a.tune)) ? 3 : 0;
     else if (a.n_out >= 64)
         // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
-        id = (wide_1xn_ok(a) && h2_tile64(a.tune)) ? 4 : 1;
+        id = (wide_1xn_ok(a) && h2_tile64(a.tune)) ? ((a.tune & SCD_TUNE_H2_TILE64_256) ? 5 : 4) : 1;
     else
         return 0;
-    if (id < 0 || id > 4 || (id > 2 && !wide_1xn_ok(a))) return 0;
-    *bm = kCfg[id].bm;
-    const int pref = 16;  // preferred tile width, the smallest halo per pixel (180 rows for 128 px)
-    for (int cand : {pref, 64, 32, 16})
-        if (a.wo % cand == 0 && a.ho % (*bm / cand) == 0 && *bm / cand >= 1 && *bm % cand == 0) {
-            *tw = cand;
-            return 1 + id;
-        }
-    return 0;
+    if (id < 0 || id > 5 || (id > 2 && !wide_1xn_ok(a))) return 0;
+    for (;;) {
+        *bm = kCfg[id].bm;
+        const int pref = 16;  // preferred tile width, the smallest halo per pixel (180 rows for 128 px)
+        for (int cand : {pref, 64, 32, 16})
+            if (a.wo % cand == 0 && a.ho % (*bm / cand) == 0 && *bm / cand >= 1 && *bm % cand == 0) {
+                *tw = cand;
+                return 1 + id;
+            }
+        if (id != 5) return 0;
+        id = 4;  // the 256-pixel patch does not tile this map: the 128-pixel one
+    }
 }
 
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
@@ -590,6 +595,7 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
         case 1: launch16<2, 2, 4, 2, 3>(a, tw, s); break;
         case 3: launch16_1xn<1, 4, 8, 2, 2>(a, tw, s); break;
         case 4: launch16_1xn<1, 2, 8, 2, 2>(a, tw, s); break;
+        case 5: launch16_1xn<2, 2, 8, 2, 2>(a, tw, s); break;
         default: launch16<2, 2, 2, 4, 3>(a, tw, s); break;
     }
 }

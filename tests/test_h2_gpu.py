@@ -539,3 +539,49 @@ def test_h2_tile_layouts_bit_identical(dev, h2, env, ci, co, mode):
     assert torch.equal(outs[0][0], outs[1][0])
     if outs[0][1] is not None:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize('ci,mode', [(64, 'stats'), (128, 'bn_bwd'), (64, 'in_bn'), (256, 'plain')])
+def test_h2_tile64_256_matches_128(dev, h2, ci, mode):
+    """The 256 x 64 tile of the 64-channel outputs (SCD_TUNE_H2_TILE64_256: 2 x 2 waves of 128 px x 32 ch on a 16 x 16
+    patch) accumulates every output in the order of the 128 x 64 tile: outputs are bit-identical; its epilogue records
+    cover 256-pixel tiles, so their per-channel totals agree with the 128-pixel tiles' to fp32 summation order."""
+    from multimodal_siamese_cd_amd import hip
+    from multimodal_siamese_cd_amd.hip import TAPS_3X3, nhwc
+    n, h, w, nseg, co = 4, 32, 32, 2, 64
+    g = torch.Generator(device=dev).manual_seed(ci + 5)
+    x = torch.randn(n, h, w, ci, device=dev, generator=g)
+    wpk = hip.pack_conv3x3(torch.randn(co, ci, 3, 3, device=dev, generator=g) / (3 * ci ** 0.5), 0)
+    sc = torch.rand(nseg * ci, device=dev, generator=g) + 0.5
+    sh = torch.randn(nseg * ci, device=dev, generator=g) * 0.1
+    bound = x.abs().max().reshape(1) * (2.0 if mode == 'in_bn' else 1.0)
+    yb = torch.randn(n, h, w, co, device=dev, generator=g)
+    mu, iv = torch.randn(nseg * co, device=dev, generator=g) * 0.1, torch.rand(nseg * co, device=dev, generator=g) + .5
+    bsc, bsh = torch.rand(nseg * co, device=dev, generator=g) + 0.5, torch.randn(nseg * co, device=dev, generator=g)
+    outs = []
+    for tune in (0, hip.TUNE_H2_TILE64_256):
+        with hip.conv_scope(tune=tune):
+            y = torch.full((n, h, w, co), 7.0, device=dev)
+            extra, tot = {}, None
+            if mode == 'in_bn':
+                extra['in_bn'] = (sc, sh, nseg)
+            elif mode == 'stats':
+                nt, tp = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), src_bound=bound)
+                assert tp == (256 if tune else 128)
+                rec = extra['stat_rec'] = torch.full((nt * co * 2,), 9.0, device=dev)
+            elif mode == 'bn_bwd':
+                nt, tp = hip.igemm_bn_bwd_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), bound)
+                assert tp == (256 if tune else 128)
+                rec = torch.full((co * nt * 2,), 9.0, device=dev)
+                extra['bn_bwd'] = (yb, nseg, mu, iv, bsc, bsh, rec)
+            assert hip.igemm_arith(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), src_bound=bound) == 'h2'
+            hip.conv_igemm(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, None, nhwc(y), src_bound=bound, **extra)
+            if mode == 'stats':  # per-channel sum of the tile means times the tile pixels = the channel total
+                tot = rec.view(nt, co, 2)[..., 0].double().sum(0) * tp
+            elif mode == 'bn_bwd':
+                tot = rec.view(co, nt, 2).double().sum(1)
+            outs.append((y.cpu(), None if tot is None else tot.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        a, b = outs[0][1], outs[1][1]
+        assert ((a - b).abs().max() / b.abs().max()).item() < 1e-5
