@@ -402,23 +402,32 @@ struct PooledCells {
 
 // dL/da of the four pixels of `cell` (flat cell index over images) at channel quad c; ok[k]: pixel k exists.
 __device__ __forceinline__ void cell_grads(const PooledCells &P, uint32_t cell, int c, f4 (&g)[4], int64_t (&pix)[4],
-                                           bool (&ok)[4]) {
+                                           bool (&ok)[4], const float *fallback) {
     const DaPooled &d = P.da;
     const uint32_t img = fdiv(cell, P.div_cimg);
     const uint32_t r = cell - img * uint32_t(P.ch * P.cw);
     const int cy = int(fdiv(r, P.div_cw)), cx = int(r) - cy * P.cw;
-    f4 gp = {0.f, 0.f, 0.f, 0.f};
-    uint32_t pk = 0xffffffffu;  // no pooled gradient: no byte matches a sub-pixel
-    if (d.gy && cy < d.hy && cx < d.wy) {
-        const int64_t q = (int64_t(img) * d.hy + cy) * d.wy + cx;
-        pk = *reinterpret_cast<const uint32_t *>(d.idx + q * d.C + c);
-        gp = ld4(d.gy + q * d.ldgy + c);
+    // Every load is unconditional (addresses clamped into the maps, the values selected afterwards), so a cell's
+    // loads issue together: guarded loads had each waited for the previous one (one memory latency per pixel).
+    // No branches around the loads either: a missing operand (no pooled gradient, no skip) reads `fallback` (valid
+    // memory: the BatchNorm input) and is discarded, so the loads need no wait before the block joins.
+    const bool has_gy = d.gy && d.hy > 0 && d.wy > 0;  // uniform
+    const bool in = has_gy && cy < d.hy && cx < d.wy;
+    const int64_t q = has_gy ? (int64_t(img) * d.hy + min(cy, d.hy - 1)) * d.wy + min(cx, d.wy - 1) : 0;
+    uint32_t pk = *reinterpret_cast<const uint32_t *>(
+        (has_gy ? d.idx : reinterpret_cast<const uint8_t *>(fallback)) + q * d.C + c);
+    f4 gp = ld4((has_gy ? d.gy : fallback) + q * d.ldgy + c);
+    const int simg = d.gs ? int(img - fdiv(img, d.div_gsn) * uint32_t(d.gsn)) : 0;
+    const float sg = (d.gs && d.skip_mode == 1 && int(img) < d.gsn) ? -1.f : 1.f;
+    f4 sv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int yy = min(2 * cy + (k >> 1), d.hx - 1), xx = min(2 * cx + (k & 1), d.wx - 1);
+        sv[k] = ld4((d.gs ? d.gs : fallback) + (d.gs ? ((int64_t(simg) * d.hx + yy) * d.wx + xx) * d.ldgs : 0) + c);
     }
-    int simg = 0;
-    float sg = 1.f;
-    if (d.gs) {
-        simg = int(img - fdiv(img, d.div_gsn) * uint32_t(d.gsn));
-        sg = (d.skip_mode == 1 && int(img) < d.gsn) ? -1.f : 1.f;
+    if (!in) {  // no pooled gradient: no byte matches a sub-pixel
+        pk = 0xffffffffu;
+        gp = f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -428,15 +437,17 @@ __device__ __forceinline__ void cell_grads(const PooledCells &P, uint32_t cell, 
         const uint32_t want = uint32_t(k);
         f4 v = {((pk >> 0) & 0xff) == want ? gp.x : 0.f, ((pk >> 8) & 0xff) == want ? gp.y : 0.f,
                 ((pk >> 16) & 0xff) == want ? gp.z : 0.f, ((pk >> 24) & 0xff) == want ? gp.w : 0.f};
-        if (d.gs && ok[k]) {
-            const f4 sv = ld4(d.gs + ((int64_t(simg) * d.hx + yy) * d.wx + xx) * d.ldgs + c);
-            v.x += sg * sv.x;
-            v.y += sg * sv.y;
-            v.z += sg * sv.z;
-            v.w += sg * sv.w;
-        }
-        g[k] = v;
+        // the skip term of a missing pixel (ok[k] false) reads a clamped neighbour: its g is never used; a select,
+        // not a branch, so the caller's loads can be scheduled above
+        const f4 t = {v.x + sg * sv[k].x, v.y + sg * sv[k].y, v.z + sg * sv[k].z, v.w + sg * sv[k].w};
+        g[k] = d.gs ? t : v;
     }
+}
+
+// The address a cell's pixel k is loaded from: itself, or (a pixel past the map edge, whose value is discarded) the
+// cell's first pixel, which always exists.
+__device__ __forceinline__ int64_t cell_load_pix(const int64_t (&pix)[4], const bool (&ok)[4], int k) {
+    return ok[k] ? pix[k] : pix[0];
 }
 
 // cell_grads for a Siamese pair (skip_mode 1, two segments of gsn images): `cell` lies in a t1 image, its partner
@@ -448,15 +459,26 @@ __device__ __forceinline__ void cell_grads_pair(const PooledCells &P, uint32_t c
     const uint32_t img = fdiv(cell, P.div_cimg);
     const uint32_t r = cell - img * uint32_t(P.ch * P.cw);
     const int cy = int(fdiv(r, P.div_cw)), cx = int(r) - cy * P.cw;
-    f4 gp0 = {0.f, 0.f, 0.f, 0.f}, gp1 = gp0;
-    uint32_t pk0 = 0xffffffffu, pk1 = 0xffffffffu;
-    if (d.gy && cy < d.hy && cx < d.wy) {
-        const int64_t q0 = (int64_t(img) * d.hy + cy) * d.wy + cx;
-        const int64_t q1 = q0 + int64_t(d.gsn) * d.hy * d.wy;
-        pk0 = *reinterpret_cast<const uint32_t *>(d.idx + q0 * d.C + c);
-        pk1 = *reinterpret_cast<const uint32_t *>(d.idx + q1 * d.C + c);
-        gp0 = ld4(d.gy + q0 * d.ldgy + c);
-        gp1 = ld4(d.gy + q1 * d.ldgy + c);
+    // unconditional loads (clamped addresses, values selected afterwards): see cell_grads
+    // a missing pooled gradient reads the skip gradient's memory (valid; discarded): no branch around the loads
+    const bool has_gy = d.gy && d.hy > 0 && d.wy > 0;  // uniform
+    const bool in = has_gy && cy < d.hy && cx < d.wy;
+    const int64_t q0 = has_gy ? (int64_t(img) * d.hy + min(cy, d.hy - 1)) * d.wy + min(cx, d.wy - 1) : 0;
+    const int64_t q1 = has_gy ? q0 + int64_t(d.gsn) * d.hy * d.wy : 0;
+    const uint8_t *ib = has_gy ? d.idx : reinterpret_cast<const uint8_t *>(d.gs);
+    const float *gb = has_gy ? d.gy : d.gs;
+    uint32_t pk0 = *reinterpret_cast<const uint32_t *>(ib + q0 * d.C + c);
+    uint32_t pk1 = *reinterpret_cast<const uint32_t *>(ib + q1 * d.C + c);
+    f4 gp0 = ld4(gb + q0 * d.ldgy + c), gp1 = ld4(gb + q1 * d.ldgy + c);
+    f4 svs[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int yy = min(2 * cy + (k >> 1), d.hx - 1), xx = min(2 * cx + (k & 1), d.wx - 1);
+        svs[k] = ld4(d.gs + ((int64_t(img) * d.hx + yy) * d.wx + xx) * d.ldgs + c);
+    }
+    if (!in) {
+        pk0 = pk1 = 0xffffffffu;
+        gp0 = gp1 = f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -468,8 +490,8 @@ __device__ __forceinline__ void cell_grads_pair(const PooledCells &P, uint32_t c
                  ((pk0 >> 16) & 0xff) == want ? gp0.z : 0.f, ((pk0 >> 24) & 0xff) == want ? gp0.w : 0.f};
         f4 v1 = {((pk1 >> 0) & 0xff) == want ? gp1.x : 0.f, ((pk1 >> 8) & 0xff) == want ? gp1.y : 0.f,
                  ((pk1 >> 16) & 0xff) == want ? gp1.z : 0.f, ((pk1 >> 24) & 0xff) == want ? gp1.w : 0.f};
-        if (ok[k]) {
-            const f4 sv = ld4(d.gs + pix[k] * d.ldgs + c);
+        {  // unconditional: a missing pixel's (ok[k] false) gradient is never used (see cell_grads)
+            const f4 sv = svs[k];
             const float m = -1.f, p1 = 1.f;
             v0.x += m * sv.x;
             v0.y += m * sv.y;
@@ -537,9 +559,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial_pair(const f
             cell_grads_pair(P, uint32_t(cell), c, g0, g1, pix, ok);
             f4 y0[4], y1[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                y0[k] = ok[k] ? ld4(y + pix[k] * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
-                y1[k] = ok[k] ? ld4(y + (pix[k] + poff) * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < 4; ++k) {  // unconditional (a missing pixel reads the cell's first; not used)
+                y0[k] = ld4(y + cell_load_pix(pix, ok, k) * ldy + c);
+                y1[k] = ld4(y + (cell_load_pix(pix, ok, k) + poff) * ldy + c);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -576,10 +598,10 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const float 
             f4 g[4];
             int64_t pix[4];
             bool ok[4];
-            cell_grads(P, uint32_t(cell), c, g, pix, ok);
+            cell_grads(P, uint32_t(cell), c, g, pix, ok, y);
             f4 yv[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) yv[k] = ok[k] ? ld4(y + pix[k] * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < 4; ++k) yv[k] = ld4(y + cell_load_pix(pix, ok, k) * ldy + c);  // see above
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (ok[k]) {
@@ -638,10 +660,10 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const float *_
             f4 g[4];
             int64_t pix[4];
             bool ok[4];
-            cell_grads(P, uint32_t(cell), c, g, pix, ok);
+            cell_grads(P, uint32_t(cell), c, g, pix, ok, y);
             f4 yv[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) yv[k] = ok[k] ? ld4(y + pix[k] * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < 4; ++k) yv[k] = ld4(y + cell_load_pix(pix, ok, k) * ldy + c);  // see above
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (ok[k]) {
@@ -697,9 +719,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply_pair(
             cell_grads_pair(P, uint32_t(cell), c, g0, g1, pix, ok);
             f4 y0[4], y1[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                y0[k] = ok[k] ? ld4(y + pix[k] * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
-                y1[k] = ok[k] ? ld4(y + (pix[k] + poff) * ldy + c) : f4{0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < 4; ++k) {  // unconditional (a missing pixel reads the cell's first; not used)
+                y0[k] = ld4(y + cell_load_pix(pix, ok, k) * ldy + c);
+                y1[k] = ld4(y + (cell_load_pix(pix, ok, k) + poff) * ldy + c);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k)
