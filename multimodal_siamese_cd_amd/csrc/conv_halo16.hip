@@ -533,8 +533,8 @@ void launch16(const IgemmArgs &a, int tw, hipStream_t s) {
 //   2: 2x2 waves of 32 px x 64 ch  (64 x 128),  3 waves/SIMD
 //   3: 1x4 waves of 128 px x 32 ch (128 x 128), 2 waves/SIMD, h2 only (no duplicated weight loads)
 //   4: 1x2 waves of 128 px x 32 ch (128 x 64),  2 waves/SIMD, h2 only (the same wave tile on 64-channel outputs)
-//   5: 2x2 waves of 128 px x 32 ch (256 x 64),  2 waves/SIMD, h2 only (SCD_TUNE_H2_TILE64_256: the 64-channel wave
-//      tile of config 4 on a 16 x 16 pixel patch, whose halo is 1.27 rows per pixel instead of 1.41)
+//   5: 2x2 waves of 128 px x 32 ch (256 x 64),  2 waves/SIMD, h2 only (the wave tile of config 4 on a 16 x 16 pixel
+//      patch, whose halo is 1.27 rows per pixel instead of 1.41: 64-channel sources; SCD_TUNE_H2_TILE64_128 keeps 4)
 constexpr H16Cfg kCfg[] = {{0, 128, 128}, {1, 128, 64}, {2, 64, 128}, {3, 128, 128}, {4, 128, 64}, {5, 256, 64}};
 
 // The 1 x N wave tiles: the h2 arithmetic only (bf16 on them measured slower: 21.38 vs 21.05 ms per bf16 step,
@@ -572,7 +572,9 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
         id = (wide_1xn_ok(a) && h2_wide_tile(a.tune)) ? 3 : 0;
     else if (a.n_out >= 64)
         // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
-        id = (wide_1xn_ok(a) && h2_tile64(a.tune)) ? ((a.tune & SCD_TUNE_H2_TILE64_256) ? 5 : 4) : 1;
+        // h2 on 1 x 2 waves; 64-channel sources (K = 576, two 32-channel chunks) on the 256 x 64 tile of 2 x 2 such
+        // waves (enc0b fwd / dgrad -4..-5%, up2b -2%; 128- and 256-channel sources measured neutral or slower)
+        id = (wide_1xn_ok(a) && h2_tile64(a.tune)) ? ((a.c == 64 && !(a.tune & SCD_TUNE_H2_TILE64_128)) ? 5 : 4) : 1;
     else
         return 0;
     if (id < 0 || id > 5 || (id > 2 && !wide_1xn_ok(a))) return 0;

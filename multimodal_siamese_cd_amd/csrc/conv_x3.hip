@@ -1001,7 +1001,7 @@ constexpr int kPackLD = kPackCW + 1;  // LDS row stride: the strided fills hit d
 struct PackJobs {
     scd_pack_job_t j[kPackJobs];
     int first_block[kPackJobs + 1];  // tiles (32 rows x kPackCW inner columns x 9 taps), prefix sums
-    int first_rs[kPackJobs + 1];     // h2 jobs: 32-row groups of the row-scale pass, prefix sums
+    int first_rs[kPackJobs + 1];     // h2 jobs: padded split rows (NB * 32) of the row-scale pass, prefix sums
     int h2[kPackJobs];               // split in the SCD_MATH_H2 format (fp16 h, m planes + per-row inverse scales)
     int n;
 };
@@ -1018,47 +1018,38 @@ __device__ __forceinline__ void pack_dims(const scd_pack_job_t &J, int &rows, in
     K = 9 * kin;
 }
 
-// One block per 32-row group of every h2 job: the rows' max |w| -> their power-of-two inverse scales (the tile pass
-// below scales each row by the reciprocal).  The OIHW parameter is read in whole contiguous runs: mode 0 rows are
-// output channels (w[r][*][*], one wave per row), mode 1 rows are input channels, whose 32-row group is the run
-// w[o][r0 .. r0+31][*] of every output channel o (each thread keeps the max of its two fixed positions in the run).
+// One wave per padded split row of every h2 job: the row's max |w| -> its power-of-two inverse scale (the tile pass
+// below scales the row by the reciprocal).  Rows of the packed layout are output channels (mode 0) or input channels
+// (mode 1, the data-grad layout); the max is read from the OIHW parameter directly.  (A block per 32-row group reading
+// the mode-1 rows as contiguous runs w[o][r0 .. r0+31][*] walked the output channels serially: 9x slower.)
 __global__ __launch_bounds__(256) void pack_rowscale_kernel(PackJobs jobs) {
-    __shared__ unsigned smax[32];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wave = int(blockIdx.x) * 4 + int(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (wave >= jobs.first_rs[jobs.n]) return;
     int q = 0;
-    while (q + 1 < jobs.n && b >= jobs.first_rs[q + 1]) ++q;
+    while (q + 1 < jobs.n && wave >= jobs.first_rs[q + 1]) ++q;
     const scd_pack_job_t J = jobs.j[q];
     int rows, kin, K;
     pack_dims(J, rows, kin, K);
-    const int r0 = (b - jobs.first_rs[q]) * 32;
-    if (tid < 32) smax[tid] = 0u;
-    __syncthreads();
-    if (J.mode == 0) {
-        const int n = J.ci * 9;
-        for (int rr = wid; rr < 32; rr += 4) {
-            float mx = 0.f;
-            if (r0 + rr < rows)
-                for (int e = lane; e < n; e += 64) mx = fmaxf(mx, fabsf(J.w[size_t(r0 + rr) * n + e]));
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-            if (lane == 0) smax[rr] = __float_as_uint(mx);
+    const int r = wave - jobs.first_rs[q];
+    float mx = 0.f;
+    if (r < rows) {
+        if (J.mode == 0) {
+            const int n = J.ci * 9;
+            for (int e = lane; e < n; e += 64) mx = fmaxf(mx, fabsf(J.w[size_t(r) * n + e]));
+        } else {
+            const int n = J.co * 9;
+            for (int e = lane; e < n; e += 64) {
+                const int o = e / 9, t = e - o * 9;
+                mx = fmaxf(mx, fabsf(J.w[(size_t(o) * J.ci + r) * 9 + t]));
+            }
         }
-    } else {
-        const int nr = min(32, rows - r0), run = nr * 9;
-        float ma = 0.f, mb = 0.f;
-        for (int o = 0; o < J.co; ++o) {
-            const float *src = J.w + (size_t(o) * J.ci + r0) * 9;
-            if (tid < run) ma = fmaxf(ma, fabsf(src[tid]));
-            if (tid + 256 < run) mb = fmaxf(mb, fabsf(src[tid + 256]));
-        }
-        if (tid < run) atomicMax(&smax[tid / 9], __float_as_uint(ma));  // non-negative floats order as integers
-        if (tid + 256 < run) atomicMax(&smax[(tid + 256) / 9], __float_as_uint(mb));
     }
-    __syncthreads();
-    if (tid < 32) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    if (lane == 0) {
         float sc, inv;
-        h2_scale(__uint_as_float(smax[tid]), sc, inv);
-        h2_row_inv(J.split, int64_t((rows + 31) / 32) * 32 * K)[r0 + tid] = inv;
+        h2_scale(mx, sc, inv);
+        h2_row_inv(J.split, int64_t((rows + 31) / 32) * 32 * K)[r] = inv;
     }
 }
 
@@ -1079,19 +1070,44 @@ __global__ __launch_bounds__(256) void pack_multi_kernel(PackJobs jobs) {
     const int nb = tile / nchunk, c0 = (tile - nb * nchunk) * kPackCW;
     const int cw = min(kPackCW, kin - c0);
     const int r0 = nb * 32;
+    // 8 loads in flight per thread: unconditional (an element outside the weight reads w[0]), selected afterwards
+    constexpr int U = 8;
+    auto fill = [&](auto at) {  // at(e, ok, src, dst): element e of the tile's OIHW run
+        const int total = J.mode == 0 ? 32 * cw * 9 : cw * 288;
+        for (int e0 = tid; e0 < total; e0 += 256 * U) {
+            float v[U];
+            int dst[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = e0 + u * 256;
+                bool ok;
+                size_t src;
+                at(e, ok, src, dst[u]);
+                ok = ok && e < total;
+                v[u] = J.w[ok ? src : 0];
+                v[u] = ok ? v[u] : 0.f;
+                dst[u] = e < total ? dst[u] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (dst[u] >= 0) T[dst[u]] = v[u];
+        }
+    };
     if (J.mode == 0) {  // T[rr][t][j] = w[r0 + rr][c0 + j][t] (zero for padded channels and rows)
         const int run = cw * 9;
-        for (int e = tid; e < 32 * run; e += 256) {
+        fill([&](int e, bool &ok, size_t &src, int &dst) {
             const int rr = e / run, f = e - rr * run, j = f / 9, t = f - j * 9;
-            const int r = r0 + rr, c = c0 + j;
-            T[(rr * 9 + t) * kPackLD + j] = (r < rows && c < J.ci) ? J.w[(size_t(r) * J.ci + c) * 9 + t] : 0.f;
-        }
+            ok = r0 + rr < rows && c0 + j < J.ci;
+            src = (size_t(r0 + rr) * J.ci + c0 + j) * 9 + t;
+            dst = (rr * 9 + t) * kPackLD + j;
+        });
     } else {  // T[rr][t][j] = w[c0 + j][r0 + rr][8 - t]
-        for (int e = tid; e < cw * 288; e += 256) {
+        fill([&](int e, bool &ok, size_t &src, int &dst) {
             const int j = e / 288, f = e - j * 288, rr = f / 9, t = f - rr * 9;
-            const int r = r0 + rr;
-            T[(rr * 9 + (8 - t)) * kPackLD + j] = r < rows ? J.w[(size_t(c0 + j) * J.ci + r) * 9 + t] : 0.f;
-        }
+            ok = r0 + rr < rows;
+            src = (size_t(c0 + j) * J.ci + r0 + rr) * 9 + t;
+            dst = (rr * 9 + (8 - t)) * kPackLD + j;
+        });
     }
     __syncthreads();
     for (int e = tid; e < 32 * 9 * cw; e += 256) {  // packed rows: out[r][t * kin + c0 + j]
@@ -1152,13 +1168,14 @@ extern "C" int scd_pack_conv3x3_multi(const scd_pack_job_t *jobs, int32_t n, scd
             }
             pj.h2[i] = J.split && h2_weight_format(J.math, 9, kin);
             const int groups = (rows + 31) / 32;
-            pj.first_rs[i + 1] = pj.first_rs[i] + (pj.h2[i] ? groups : 0);
+            pj.first_rs[i + 1] = pj.first_rs[i] + (pj.h2[i] ? groups * 32 : 0);
             pj.j[i] = J;
             pj.first_block[i + 1] = pj.first_block[i] + groups * ((kin + kPackCW - 1) / kPackCW);
         }
         if (pj.n == 0) break;
         if (pj.first_rs[pj.n] > 0)
-            hipLaunchKernelGGL(pack_rowscale_kernel, dim3(pj.first_rs[pj.n]), dim3(256), 0, as_stream(stream), pj);
+            hipLaunchKernelGGL(pack_rowscale_kernel, dim3((pj.first_rs[pj.n] + 3) / 4), dim3(256), 0, as_stream(stream),
+                               pj);
         hipLaunchKernelGGL(pack_multi_kernel, dim3(pj.first_block[pj.n]), dim3(256), 0, as_stream(stream), pj);
         SCD_TRY(launch_status("scd_pack_conv3x3_multi"));
     }

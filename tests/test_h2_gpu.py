@@ -520,7 +520,8 @@ def test_h2_tile_layouts_bit_identical(dev, h2, env, ci, co, mode):
     mu, iv = torch.randn(nseg * co, device=dev, generator=g) * 0.1, torch.rand(nseg * co, device=dev, generator=g) + .5
     bsc, bsh = torch.rand(nseg * co, device=dev, generator=g) + 0.5, torch.randn(nseg * co, device=dev, generator=g)
     outs = []
-    for tune in (0, getattr(hip, env)):
+    # both layouts on 128-pixel tiles (64-channel sources otherwise take the 256 x 64 tile: test_h2_tile64_256_...)
+    for tune in (hip.TUNE_H2_TILE64_128, hip.TUNE_H2_TILE64_128 | getattr(hip, env)):
         with hip.conv_scope(tune=tune):
             y = torch.full((n, h, w, co), 7.0, device=dev)
             extra, rec = {}, None
@@ -541,11 +542,12 @@ def test_h2_tile_layouts_bit_identical(dev, h2, env, ci, co, mode):
         assert torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize('ci,mode', [(64, 'stats'), (128, 'bn_bwd'), (64, 'in_bn'), (256, 'plain')])
+@pytest.mark.parametrize('ci,mode', [(64, 'stats'), (64, 'bn_bwd'), (64, 'in_bn'), (64, 'plain')])
 def test_h2_tile64_256_matches_128(dev, h2, ci, mode):
-    """The 256 x 64 tile of the 64-channel outputs (SCD_TUNE_H2_TILE64_256: 2 x 2 waves of 128 px x 32 ch on a 16 x 16
-    patch) accumulates every output in the order of the 128 x 64 tile: outputs are bit-identical; its epilogue records
-    cover 256-pixel tiles, so their per-channel totals agree with the 128-pixel tiles' to fp32 summation order."""
+    """The 256 x 64 tile of the 64-channel outputs of 64-channel sources (the default; 2 x 2 waves of 128 px x 32 ch on a
+    16 x 16 patch) accumulates every output in the order of the 128 x 64 tile (SCD_TUNE_H2_TILE64_128): outputs are
+    bit-identical; its epilogue records cover 256-pixel tiles, so their per-channel totals agree with the 128-pixel
+    tiles' to fp32 summation order."""
     from multimodal_siamese_cd_amd import hip
     from multimodal_siamese_cd_amd.hip import TAPS_3X3, nhwc
     n, h, w, nseg, co = 4, 32, 32, 2, 64
@@ -559,7 +561,7 @@ def test_h2_tile64_256_matches_128(dev, h2, ci, mode):
     mu, iv = torch.randn(nseg * co, device=dev, generator=g) * 0.1, torch.rand(nseg * co, device=dev, generator=g) + .5
     bsc, bsh = torch.rand(nseg * co, device=dev, generator=g) + 0.5, torch.randn(nseg * co, device=dev, generator=g)
     outs = []
-    for tune in (0, hip.TUNE_H2_TILE64_256):
+    for tune in (hip.TUNE_H2_TILE64_128, 0):
         with hip.conv_scope(tune=tune):
             y = torch.full((n, h, w, co), 7.0, device=dev)
             extra, tot = {}, None
@@ -567,11 +569,11 @@ def test_h2_tile64_256_matches_128(dev, h2, ci, mode):
                 extra['in_bn'] = (sc, sh, nseg)
             elif mode == 'stats':
                 nt, tp = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), src_bound=bound)
-                assert tp == (256 if tune else 128)
+                assert tp == (128 if tune else 256)
                 rec = extra['stat_rec'] = torch.full((nt * co * 2,), 9.0, device=dev)
             elif mode == 'bn_bwd':
                 nt, tp = hip.igemm_bn_bwd_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), bound)
-                assert tp == (256 if tune else 128)
+                assert tp == (128 if tune else 256)
                 rec = torch.full((co * nt * 2,), 9.0, device=dev)
                 extra['bn_bwd'] = (yb, nseg, mu, iv, bsc, bsh, rec)
             assert hip.igemm_arith(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), src_bound=bound) == 'h2'
