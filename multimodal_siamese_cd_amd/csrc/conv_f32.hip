@@ -411,6 +411,25 @@ __global__ void wgrad_group_sum(float *__restrict__ slabs, int nsplit, int per, 
     slabs[e + size_t(k0) * total] = (s0 + s1) + (s2 + s3);
 }
 
+// wgrad_group_sum on 16-byte pieces (total % 4 == 0, 16-byte aligned slabs): per element the same sums in the same
+// order (bit-identical), four slabs' 16-byte loads in flight per thread instead of 4-byte ones.
+__global__ void wgrad_group_sum4(float *__restrict__ slabs, int nsplit, int per, size_t total) {
+    const size_t e = (blockIdx.x * size_t(blockDim.x) + threadIdx.x) * 4;
+    if (e >= total) return;
+    const int k0 = blockIdx.y * per;
+    const int k1 = min(k0 + per, nsplit);
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+    int k = k0;
+    for (; k + 3 < k1; k += 4) {
+        s0 += gload4(slabs + e + size_t(k) * total);
+        s1 += gload4(slabs + e + size_t(k + 1) * total);
+        s2 += gload4(slabs + e + size_t(k + 2) * total);
+        s3 += gload4(slabs + e + size_t(k + 3) * total);
+    }
+    for (; k < k1; ++k) s0 += gload4(slabs + e + size_t(k) * total);
+    *reinterpret_cast<f32x4 *>(slabs + e + size_t(k0) * total) = (s0 + s1) + (s2 + s3);
+}
+
 // Level 2, one workgroup per (row r, block of kFinCB channels): sum the (group) slabs of the block's 9 column runs
 // [t][c0, c0 + kFinCB) into LDS (coalesced reads; the slab loads of one element issued together, summed in slab
 // order), then write the parameter-order run [c0, c0 + kFinCB)[t] (coalesced writes; LDS rows padded by one float
@@ -1271,7 +1290,11 @@ extern "C" int scd_wgrad_finalize(float *slabs, int32_t nsplit, int32_t R, int32
     if (G > 1) {
         const int per = (nsplit + G - 1) / G;
         G = (nsplit + per - 1) / per;
-        hipLaunchKernelGGL(wgrad_group_sum, dim3(base_blocks, G), dim3(256), 0, s, slabs, nsplit, per, total);
+        if (total % 4 == 0 && aligned16(slabs))
+            hipLaunchKernelGGL(wgrad_group_sum4, dim3(unsigned((total / 4 + 255) / 256), G), dim3(256), 0, s, slabs,
+                               nsplit, per, total);
+        else
+            hipLaunchKernelGGL(wgrad_group_sum, dim3(base_blocks, G), dim3(256), 0, s, slabs, nsplit, per, total);
         nsum = G;
         gstride = per;
     }
