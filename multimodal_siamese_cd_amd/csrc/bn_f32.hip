@@ -997,15 +997,21 @@ __global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const float *__re
     const int64_t pbeg = int64_t(blockIdx.x) * chunk;
     const int64_t pend = min(pbeg + chunk, npix);
     f4 acc = {0.f, 0.f, 0.f, 0.f};
-    auto value = [&](int64_t p, f4 v) {
+    // The weighted path's per-pixel operands (the head gradient, the segment's coefficients) are loaded together
+    // with the pixels, before any use; 32-bit index math where the map allows (npix < 2^31: the head's 256^2 maps)
+    const bool small = npix < (int64_t(1) << 31);
+    auto img_of = [&](int64_t p) { return small ? int64_t(uint32_t(p) / uint32_t(hw)) : p / hw; };
+    auto seg_of = [&](int64_t p) { return small ? int64_t(uint32_t(p) / uint32_t(pseg)) : p / pseg; };
+    auto wgt_at = [&](int64_t p) {
+        const int64_t img = img_of(p), pix = p - img * hw;
+        return wgt[(img * n_out + o) * hw + pix];
+    };
+    auto value = [&](int64_t p, f4 v, float wv) {
         if (scale) {
-            const int64_t sc_off = (p / pseg) * C + c;
+            const int64_t sc_off = seg_of(p) * C + c;
             v = bn_relu4(v, ld4(scale + sc_off), ld4(shift + sc_off));
         }
-        if (wgt) {
-            const int64_t img = p / hw, pix = p - img * hw;
-            v *= wgt[(img * n_out + o) * hw + pix];
-        }
+        if (wgt) v *= wv;
         return v;
     };
     if (c < C) {
@@ -1013,16 +1019,23 @@ __global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const float *__re
         for (; p + 3 * npl < pend; p += 4 * npl) {
             f4 v0 = ld4(x + p * ldx + c), v1 = ld4(x + (p + npl) * ldx + c);
             f4 v2 = ld4(x + (p + 2 * npl) * ldx + c), v3 = ld4(x + (p + 3 * npl) * ldx + c);
+            float w0 = 1.f, w1 = 1.f, w2 = 1.f, w3 = 1.f;
+            if (wgt) {  // uniform
+                w0 = wgt_at(p);
+                w1 = wgt_at(p + npl);
+                w2 = wgt_at(p + 2 * npl);
+                w3 = wgt_at(p + 3 * npl);
+            }
             PIN4(v0, v1, v2, v3);
             if (wgt || scale) {
-                v0 = value(p, v0);
-                v1 = value(p + npl, v1);
-                v2 = value(p + 2 * npl, v2);
-                v3 = value(p + 3 * npl, v3);
+                v0 = value(p, v0, w0);
+                v1 = value(p + npl, v1, w1);
+                v2 = value(p + 2 * npl, v2, w2);
+                v3 = value(p + 3 * npl, v3, w3);
             }
             acc += (v0 + v1) + (v2 + v3);
         }
-        for (; p < pend; p += npl) acc += value(p, ld4(x + p * ldx + c));
+        for (; p < pend; p += npl) acc += value(p, ld4(x + p * ldx + c), wgt ? wgt_at(p) : 1.f);
     }
     sh[tid] = acc;
     __syncthreads();

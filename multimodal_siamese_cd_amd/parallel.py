@@ -87,7 +87,7 @@ def global_sums(local: torch.Tensor) -> torch.Tensor:
 
 
 def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 16, find_unused_parameters: bool | None = None,
-             exact_dataparallel: bool = False):
+             exact_dataparallel: bool = False, single_rank: bool = False):
     """Replace the DataParallel-style wrapper's pass-through by DDP when running under torchrun.
 
     Keeps the `.module` attribute and `module.` state_dict prefix of the reference's wrapper.
@@ -109,8 +109,10 @@ def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 16, find_unused_paramete
     (engine.set_loss_allreduce, three floats per term), and the gradient buckets are SUMMED (sum_allreduce_hook).
     BatchNorm statistics stay per rank and running statistics come from rank 0 (broadcast_buffers) in both modes,
     as DataParallel's per-replica statistics with replica 0's buffers.
+    `single_rank`: wrap even in a one-rank process group (the RCCL / DDP bucket path on one GPU,
+    tests/test_rccl_gpu.py); without it a single process keeps the reference's pass-through wrapper.
     """
-    if not is_distributed():
+    if not is_distributed() and not (single_rank and dist.is_available() and dist.is_initialized()):
         return wrapper
     module = wrapper.module if hasattr(wrapper, 'module') else wrapper
     if find_unused_parameters is None:
