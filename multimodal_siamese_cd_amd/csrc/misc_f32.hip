@@ -343,13 +343,10 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restric
         for (int qq = q; qq < cq; qq += G) {
             float4 v[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {  // unconditional loads (a pixel past the end reads the last one): no waits
+            for (int u = 0; u < U; ++u) {
                 const int64_t p = p0 + u * ppw + pp;
-                v[u] = *reinterpret_cast<const float4 *>(x + (p < npix ? p : npix - 1) * ldx + 4 * qq);
+                v[u] = p < npix ? *reinterpret_cast<const float4 *>(x + p * ldx + 4 * qq) : make_float4(0, 0, 0, 0);
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (p0 + u * ppw + pp >= npix) v[u] = make_float4(0, 0, 0, 0);
             if (scale) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
