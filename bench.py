@@ -70,6 +70,14 @@ def conv_flops(cfg, batch: int, size: int):
     return f3, fT
 
 
+def kernel_class(kind: str, ntaps: int, src_c: int) -> str:
+    """The kernel family a conv launch runs on: 3x3 forward / data grad (igemm_halo16_x3), 3x3 weight grad
+    (wgrad_halo16_x3), the 16-channel input layer (igemm / wgrad_halo16_c16), ConvTranspose (gather16 / generic)."""
+    if ntaps == 9:
+        return f"{kind}_3x3_input_layer" if src_c == 16 else f"{kind}_3x3"
+    return f"{kind}_convT"
+
+
 class KernelTimer:
     """HIP-event brackets around every MFMA conv launch (on torch's current stream, where libscd launches)."""
 
@@ -92,7 +100,7 @@ class KernelTimer:
             r = timer._igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k)
             e.record()
             flops = 2.0 * src.n * out_h * out_w * n_out * len(taps[0]) * src.c
-            timer.events.append(('igemm', s, e, flops, arith))
+            timer.events.append(('igemm', s, e, flops, arith, kernel_class('igemm', len(taps[0]), src.c)))
             return r
 
         def wgrad(d, slabs):
@@ -104,7 +112,7 @@ class KernelTimer:
             r = timer._wgrad(d, slabs)
             e.record()
             flops = 2.0 * d.rows.n * d.rows.h * d.rows.w * d.rows.c * d.ntaps * d.src.c
-            timer.events.append(('wgrad', s, e, flops, arith))
+            timer.events.append(('wgrad', s, e, flops, arith, kernel_class('wgrad', d.ntaps, d.src.c)))
             return r
 
         hip.conv_igemm = igemm
@@ -113,10 +121,29 @@ class KernelTimer:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, s, e, _, _ in self.events:
+        for name, s, e, *_ in self.events:
             n, t = out.get(name, (0, 0.0))
             out[name] = (n + 1, t + s.elapsed_time(e))
         return out
+
+    def by_class(self, reps):
+        """Per kernel class (kernel_class): launches, ms, FLOPs per step, TFLOP/s and the fraction of that class's
+        flop-weighted arithmetic peak; the class with the most time is the step's dominant kernel."""
+        out = {}
+        for _, s, e, fl, arith, cls in self.events:
+            c = out.setdefault(cls, {'n': 0, 'ms': 0.0, 'flop': 0.0, 'tpeak': 0.0})
+            c['n'] += 1
+            c['ms'] += s.elapsed_time(e)
+            c['flop'] += fl
+            c['tpeak'] += fl / (PEAKS[arith] * 1e12)
+        res = {}
+        for cls, c in out.items():
+            ach = c['flop'] / (c['ms'] * 1e-3) / 1e12
+            peak = c['flop'] / c['tpeak'] / 1e12
+            res[cls] = {"launches_per_step": c['n'] // reps, "ms_per_step": round(c['ms'] / reps, 3),
+                        "tflop_per_step": round(c['flop'] / reps / 1e12, 4), "achieved": round(ach, 2),
+                        "peak": round(peak, 1), "frac": round(ach / peak, 4)}
+        return res
 
     def peak(self):
         """Harmonic flop-weighted matrix-core peak of the timed launches (TFLOP/s) and each arithmetic's share."""
@@ -303,6 +330,11 @@ def main():
             "launches_per_step": {k: v[0] // reps for k, v in summ.items()},
             "ms_per_family": {k: round(v[1] / reps, 3) for k, v in summ.items()},
         }
+        # the same HIP events per kernel class; the class with the most time is the step's dominant kernel
+        classes = timer.by_class(reps)
+        dom = max(classes, key=lambda k: classes[k]["ms_per_step"])
+        result["roofline"]["by_class"] = classes
+        result["roofline"]["dominant_kernel"] = dict(classes[dom], **{"class": dom})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, size=size)
     if rank == 0:
