@@ -332,9 +332,10 @@ def main():
         }
         # the same HIP events per kernel class; the class with the most time is the step's dominant kernel
         classes = timer.by_class(reps)
-        dom = max(classes, key=lambda k: classes[k]["ms_per_step"])
         result["roofline"]["by_class"] = classes
-        result["roofline"]["dominant_kernel"] = dict(classes[dom], **{"class": dom})
+        if classes:
+            dom = max(classes, key=lambda k: classes[k]["ms_per_step"])
+            result["roofline"]["dominant_kernel"] = dict(classes[dom], **{"class": dom})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, size=size)
     if rank == 0:
