@@ -122,7 +122,7 @@ void launch_halo16_c16(const IgemmArgs &a, int tw, hipStream_t s);
 // Whether launch_igemm_x3 would run the halo16 kernel for `a` (the only one with the input transform).
 bool igemm_takes_halo16(const IgemmArgs &a);
 bool igemm_takes_c16(const IgemmArgs &a);  // igemm_halo16_c16 (16-channel source)
-bool igemm_takes_gather16(const IgemmArgs &a);  // igemm_gather16_h2 (ConvTranspose forward / data grad)
+bool igemm_takes_gather16(const IgemmArgs &a);  // igemm_gather16, h2 or bf16 (ConvTranspose forward / data grad)
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
 // 16x16x32-MFMA halo weight grad (conv_halo16.hip).
 const void *wgrad_halo16_fn(int math, uint32_t tune, bool bounded, int rblock);  // bounded: h2 under SCD_MATH_H2
@@ -159,7 +159,7 @@ inline int h2_prescale(uint32_t tune) { return (tune & SCD_TUNE_H2_NO_PRESCALE) 
 inline bool h2_weight_format(int math, int ntaps, int c) {
     return math == SCD_MATH_H2 && (((ntaps == 9 || ntaps == 1 || ntaps == 4) && c % 32 == 0) || (ntaps == 9 && c == 16));
 }
-// h2 gather igemm (conv_gather16.hip): 0 when `a` does not take it, else 1 + tile id; launcher.
+// gather igemm (conv_gather16.hip; h2 or bf16): 0 when `a` does not take it, else 1 + tile id; launcher.
 int gather16_pick(const IgemmArgs &a);
 void launch_gather16(const IgemmArgs &a, int cfg, hipStream_t s);
 

@@ -767,7 +767,7 @@ extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
     SCD_TRY(igemm_query_prepare(d, a));
     if (!math_split(a.math)) return SCD_MATH_F32;
     if (igemm_takes_halo16(a)) return a.math;  // under SCD_MATH_H2 only bounded h2-split convs take it
-    if (igemm_takes_gather16(a)) return SCD_MATH_H2;
+    if (igemm_takes_gather16(a)) return a.math;  // h2 (bounded, h2 split) or bf16
     if (igemm_takes_c16(a)) return a.math;  // under SCD_MATH_H2 only bounded h2-split input layers take it
     return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
 }

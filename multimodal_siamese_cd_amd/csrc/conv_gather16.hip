@@ -1,5 +1,6 @@
-// Gather igemm on v_mfma_f32_16x16x32_f16 in the h2 arithmetic (x3_common.h): the ConvTranspose2d(k=2, s=2)
-// forward (one tap, pixel-shuffle store, networks.py:433) and its data grad (four taps gathered with stride 2).
+// Gather igemm in the h2 arithmetic (x3_common.h; v_mfma_f32_16x16x32_f16) or in bf16 (v_mfma_f32_16x16x32_bf16):
+// the ConvTranspose2d(k=2, s=2) forward (one tap, pixel-shuffle store, networks.py:433) and its data grad (four taps
+// gathered with stride 2).
 //
 // These convs have no tap reuse (every source pixel feeds one k-step of one output pixel), so the halo16 kernel's
 // shape does not apply; they ran on the generic per-tap x3 kernel (igemm_x3: six 32x32x16 bf16 products per
@@ -14,23 +15,27 @@
 //   - roles as in the halo16 kernel: A = weights (rows = output channels), B = pixels, so a lane's accumulator
 //     holds 4 consecutive channels of one pixel and leaves as one 16-byte store (store_mode 1: to the pixel
 //     (2y + di, 2x + dj) of the upsampled map, with dst_bound raised to the max |stored value|).
-// The products (w_h 2^-11) x_m', w_m x_h, w_h x_h are the halo16 kernel's NP = 4 expressions.
+// The products (w_h 2^-11) x_m', w_m x_h, w_h x_h are the halo16 kernel's NP = 4 expressions; NP = 1 (bf16) stages
+// one bf16 plane (RNE) and runs w_h x_h on plane 0 of the bf16 weight split, the bf16 halo16 kernel's product.
 #include "x3_common.h"
 
 namespace scd {
 
-template <int WM, int WN, int TM, int TN, int SK, int OCC>
-__global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16_h2(IgemmArgs a) {
+template <int WM, int WN, int TM, int TN, int SK, int OCC, int NP>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a) {
+    static_assert(NP == 1 || NP == 4, "bf16 or h2");
+    constexpr bool H2 = NP == 4;
+    constexpr int XP = H2 ? 2 : 1;  // activation planes (LDS) = weight planes (registers)
     constexpr int NT = 64 * WM * WN;
     constexpr int WPX = TM * 16, WCH = TN * 16;
     constexpr int BM = WM * WPX, BN = WN * WCH;
     constexpr int PL = BM * 64;          // one fp16 plane of one 32-channel k-step
-    constexpr int STG = SK * 2 * PL;     // one stage: SK k-steps x (h, m)
+    constexpr int STG = SK * XP * PL;    // one stage: SK k-steps x (h, m) / (h)
     constexpr int A_PER = BM * 8 / NT;   // 16-byte (4-channel) pieces per thread and k-step
     static_assert((BM * 8) % NT == 0 && NT % 8 == 0, "pieces tile the block");
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STG];
-    float xs, xs_inv;
-    h2_scale(*a.src_bound, xs, xs_inv);
+    float xs = 1.f, xs_inv = 1.f;
+    if constexpr (H2) h2_scale(*a.src_bound, xs, xs_inv);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid % WM, wn = wid / WM;
@@ -77,7 +82,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16_h2(IgemmArgs
         w_base[j] = nb < NB32 ? uint32_t(nb * KS16 + (g >> 1)) * 1024u + uint32_t(16 * (cb & 1) + l16 + 32 * (g & 1)) * 16u
                               : kOOB;
     }
-    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, 2u * wplane_b);
+    const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, uint32_t(XP) * wplane_b);
 
     const int cpk = a.c / 32;
     const int nk = a.ntaps * cpk;  // k-steps (a multiple of SK: gather16_pick)
@@ -103,16 +108,21 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16_h2(IgemmArgs
 #pragma unroll
             for (int i = 0; i < A_PER; ++i) {
                 u32x2 h, m;
-                split2h_pre(ra[s][i] * xs, h, m);
-                *reinterpret_cast<u32x2 *>(sb + s * 2 * PL + a_off[i]) = h;
-                *reinterpret_cast<u32x2 *>(sb + s * 2 * PL + PL + a_off[i]) = m;
+                if constexpr (H2) {
+                    split2h_pre(ra[s][i] * xs, h, m);
+                    *reinterpret_cast<u32x2 *>(sb + s * XP * PL + PL + a_off[i]) = m;
+                } else {
+                    h[0] = cvt_pk_bf16(ra[s][i][0], ra[s][i][1]);
+                    h[1] = cvt_pk_bf16(ra[s][i][2], ra[s][i][3]);
+                }
+                *reinterpret_cast<u32x2 *>(sb + s * XP * PL + a_off[i]) = h;
             }
     };
-    u32x4 wq[2][TN];
+    u32x4 wq[XP][TN];
     auto load_W = [&](int q) {
         const uint32_t ko = uint32_t(q) * 2048u;  // 32-deep step = two 16-deep fragments
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < XP; ++p)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
                 wq[p][j] = bload4u(rs_w, w_base[j] == kOOB ? kOOB : w_base[j] + ko + uint32_t(p) * wplane_b);
@@ -144,17 +154,25 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16_h2(IgemmArgs
             u32x4 xh[TM], xm[TM];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                xh[i] = *reinterpret_cast<const u32x4 *>(sb + s * 2 * PL + x_rd[i]);
-                xm[i] = *reinterpret_cast<const u32x4 *>(sb + s * 2 * PL + PL + x_rd[i]);
+                xh[i] = *reinterpret_cast<const u32x4 *>(sb + s * XP * PL + x_rd[i]);
+                if constexpr (H2) xm[i] = *reinterpret_cast<const u32x4 *>(sb + s * XP * PL + PL + x_rd[i]);
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const u32x4 wl = f16_down11(wq[0][j]);
+                if constexpr (H2) {
+                    const u32x4 wl = f16_down11(wq[0][j]);
 #pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    acc[j][i] = mfma16_f16(wl, xm[i], acc[j][i]);
-                    acc[j][i] = mfma16_f16(wq[1][j], xh[i], acc[j][i]);
-                    acc[j][i] = mfma16_f16(wq[0][j], xh[i], acc[j][i]);
+                    for (int i = 0; i < TM; ++i) {
+                        acc[j][i] = mfma16_f16(wl, xm[i], acc[j][i]);
+                        acc[j][i] = mfma16_f16(wq[XP - 1][j], xh[i], acc[j][i]);
+                        acc[j][i] = mfma16_f16(wq[0][j], xh[i], acc[j][i]);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+                        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wq[0][j]),
+                                                                            __builtin_bit_cast(bf16x8, xh[i]),
+                                                                            acc[j][i], 0, 0, 0);
                 }
             }
             if (st * SK + s + 1 < nk) load_W(st * SK + s + 1);  // next k-step's fragments (L2), one step ahead
@@ -164,14 +182,14 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16_h2(IgemmArgs
         __syncthreads();
     }
 
-    // undo the operand scales (powers of two: exact), add the bias, store 4 channels per lane
+    // h2: undo the operand scales (powers of two: exact); add the bias, store 4 channels per lane
     const float *winv = reinterpret_cast<const float *>(reinterpret_cast<const unsigned char *>(a.wsplit) + 2u * wplane_b);
     float omax = 0.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * WCH + j * 16 + 4 * g;
         if (n >= a.n_out) continue;  // n_out % 4 == 0: a lane's 4 channels are all in or all out
-        const f32x4 sc = gload4(winv + n) * xs_inv;
+        const f32x4 sc = H2 ? gload4(winv + n) * xs_inv : f32x4{1.f, 1.f, 1.f, 1.f};
         int oc = n, di = 0, dj = 0;
         if (a.store_mode == 1) {
             const int ij = n / a.cout;
@@ -206,23 +224,33 @@ constexpr int kSK = 2;  // 32-channel k-steps per stage
 
 int gather16_enabled(uint32_t tune) { return (tune & SCD_TUNE_NO_GATHER16) ? 0 : 1; }
 
-template <int WM, int WN, int TM, int TN, int OCC>
+template <int WM, int WN, int TM, int TN, int OCC, int NP>
 void launch_g16(const IgemmArgs &a, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     IgemmArgs b = a;
     b.grid_m = (a.M + BM - 1) / BM;
     b.grid_n = (a.n_out + BN - 1) / BN;
     b.remap = xcd_remap_enabled(a.tune);
-    hipLaunchKernelGGL((igemm_gather16_h2<WM, WN, TM, TN, kSK, OCC>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN), 0,
+    hipLaunchKernelGGL((igemm_gather16<WM, WN, TM, TN, kSK, OCC, NP>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN), 0,
                        s, b);
+}
+
+// h2 with the h2 weight split and a source bound; bf16 on plane 0 of the bf16 weight split (no bound needed)
+bool gather16_h2(const IgemmArgs &a) { return a.src_bound && h2_weight_format(a.math, a.ntaps, a.c); }
+
+template <int WM, int WN, int TM, int TN, int OCC>
+void launch_g16_math(const IgemmArgs &a, hipStream_t s) {
+    if (gather16_h2(a))
+        launch_g16<WM, WN, TM, TN, OCC, 4>(a, s);
+    else
+        launch_g16<WM, WN, TM, TN, OCC, 1>(a, s);
 }
 }  // namespace
 
-// 1 + tile id when `a` takes the gather kernel (h2-split weights, a bound of the source, the shape constraints
-// below), else 0.  Convs with 9 taps go to the halo kernels instead.
+// 1 + tile id when `a` takes the gather kernel (h2-split weights and a bound of the source, or the bf16 arithmetic;
+// the shape constraints below), else 0.  Convs with 9 taps go to the halo kernels instead.
 int gather16_pick(const IgemmArgs &a) {
-    if (!a.wsplit || !a.src_bound || a.ntaps == 9 || !h2_weight_format(a.math, a.ntaps, a.c) ||
-        !gather16_enabled(a.tune))
+    if (!a.wsplit || a.ntaps == 9 || !(gather16_h2(a) || a.math == SCD_MATH_BF16) || !gather16_enabled(a.tune))
         return 0;
     if (a.c % 32 || (a.ntaps * (a.c / 32)) % kSK || a.n_out % 64 || a.ldc_s % 4 || a.ldc_d % 4 || a.K != a.ntaps * a.c ||
         (reinterpret_cast<uintptr_t>(a.src) & 15) || (reinterpret_cast<uintptr_t>(a.dst) & 15) ||
@@ -236,9 +264,9 @@ int gather16_pick(const IgemmArgs &a) {
 
 void launch_gather16(const IgemmArgs &a, int cfg, hipStream_t s) {
     switch (cfg - 1) {
-        case 0: launch_g16<2, 2, 4, 4, 2>(a, s); break;
-        case 1: launch_g16<2, 2, 4, 2, 2>(a, s); break;
-        default: launch_g16<2, 2, 2, 4, 2>(a, s); break;
+        case 0: launch_g16_math<2, 2, 4, 4, 2>(a, s); break;
+        case 1: launch_g16_math<2, 2, 4, 2, 2>(a, s); break;
+        default: launch_g16_math<2, 2, 2, 4, 2>(a, s); break;
     }
 }
 

@@ -213,10 +213,48 @@ class _Conv16(torch.autograd.Function):
         return gx, gw, gy.sum((0, 2, 3))
 
 
+_CONVT2D = F.conv_transpose2d
+
+
+class _ConvT16(torch.autograd.Function):
+    """A ConvTranspose2d(k=2, s=2) with the bf16 configs' arithmetic (libscd's gather kernel, bf16 instance): the
+    forward (fwd16) and the data grad (bwd16) on bf16-rounded operands, exact products, fp32 (here double)
+    accumulation; the weight grad at fp32 accuracy (the generic weight-grad kernel keeps the x3 arithmetic)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, fwd16, bwd16):
+        ctx.save_for_backward(x, w)
+        ctx.bwd16 = bwd16
+        xx, ww = (r16(x), r16(w)) if fwd16 else (x, w)
+        return _CONVT2D(xx.double(), ww.double(), None, stride=2).float() + b[None, :, None, None]
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gg, ww = (r16(gy), r16(w)) if ctx.bwd16 else (gy, w)
+        gx = _CONV2D(gg.double(), ww.double(), None, stride=2).float()  # the transpose of the ConvT
+        with torch.enable_grad():
+            wr = w.detach().double().requires_grad_(True)
+            gw, = torch.autograd.grad(_CONVT2D(x.detach().double(), wr, None, stride=2), wr, gy.double())
+        return gx, gw.float(), gy.sum((0, 2, 3)), None, None
+
+
+def convT_bf16(x, w, b=None, stride=1, padding=0, *a, **k):
+    """F.conv_transpose2d with the bf16 configs' arithmetic where libscd's gather kernel takes the launch (forward:
+    in-channels % 32, 4 x out-channels % 64; data grad: out-channels % 32, in-channels % 64); fp32 otherwise."""
+    if tuple(w.shape[2:]) == (2, 2) and stride == 2 and padding == 0 and not a and not k:
+        fwd16 = w.shape[0] % 32 == 0 and w.shape[1] % 16 == 0
+        bwd16 = w.shape[1] % 32 == 0 and w.shape[0] % 64 == 0
+        if fwd16 or bwd16:
+            return _ConvT16.apply(x, w, b if b is not None else w.new_zeros(w.shape[1]), fwd16, bwd16)
+    return _CONVT2D(x, w, b, stride, padding, *a, **k)
+
+
 @contextlib.contextmanager
 def bf16_conv_oracle():
     """Inside: every 3x3 conv the bf16 kernels take (source channels a multiple of 32, or an input layer of at most
-    16 bands, zero-padded to the 16-channel kernels) runs through _Conv16; the rest stays fp32."""
+    16 bands, zero-padded to the 16-channel kernels) runs through _Conv16, every ConvTranspose through convT_bf16;
+    the rest stays fp32."""
     def conv(x, w, b=None, stride=1, padding=0, *a, **k):
         if (w.shape[2:] == (3, 3) and (w.shape[1] % 32 == 0 or w.shape[1] <= 16) and stride == 1
                 and padding == 1):
@@ -224,10 +262,12 @@ def bf16_conv_oracle():
         return _CONV2D(x, w, b, stride, padding, *a, **k)
 
     F.conv2d = conv
+    F.conv_transpose2d = convT_bf16
     try:
         yield
     finally:
         F.conv2d = _CONV2D
+        F.conv_transpose2d = _CONVT2D
 
 
 def record_arith(monkeypatch, dev):

@@ -13,6 +13,8 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+from _parity import _CONVT2D, convT_bf16
+
 TOL = 1e-5
 _CONV2D = F.conv2d  # unpatched (the model test swaps F.conv2d inside the oracle run)
 
@@ -74,6 +76,43 @@ def test_bf16_conv_forward_and_data_grad(dev, bf16, n, h, w, ci, co):
     hip.conv_igemm(hip.nhwc(dy.to(dev)), h, w, 1, hip.TAPS_3X3, hip.pack_conv3x3(wd, 1), ci, None, hip.nhwc(dx))
     ref_dx = nhwc_t(torch.nn.grad.conv2d_input((n, ci, h, w), r16(wt).double(), nchw(r16(dy)).double(), padding=1))
     assert rel(dx, ref_dx) < TOL
+
+
+@pytest.mark.parametrize('n,h,w,ci,co', [(2, 8, 8, 64, 64), (3, 5, 7, 128, 64), (8, 64, 64, 64, 64),
+                                         (2, 16, 16, 256, 128), (1, 4, 4, 512, 512)])
+def test_bf16_convT_gather16(dev, bf16, n, h, w, ci, co):
+    """The ConvTranspose forward (1 tap, pixel-shuffle store into a concat slice) and data grad (4 taps, stride-2
+    gather from a channel slice) take the gather kernel's bf16 instance (no bound needed): fp32-accurate against
+    the ConvT of the bf16-rounded operands, a bf16-sized distance from the exact result."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * h * w + ci + 1)
+    x = torch.randn(n, h, w, ci, generator=g)
+    wt = torch.randn(ci, co, 2, 2, generator=g) / 8
+    b = torch.randn(co, generator=g)
+    wf, wb = hip.pack_convT2x2(wt.to(dev), 0), hip.pack_convT2x2(wt.to(dev), 1)
+    xd = x.to(dev)
+    cat = torch.zeros(n, 2 * h, 2 * w, co + 32, device=dev)
+    assert hip.igemm_arith(hip.nhwc(xd), h, w, 1, hip.TAPS_1, wf, 4 * co, hip.nhwc(cat, 32, co), store_mode=1) == 'bf16'
+    hip.conv_igemm(hip.nhwc(xd), h, w, 1, hip.TAPS_1, wf, 4 * co, b.to(dev), hip.nhwc(cat, 32, co), store_mode=1)
+    up = nchw(cat[..., 32:])
+    ref16 = _CONVT2D(nchw(r16(x)).double(), r16(wt).double(), b.double(), stride=2)
+    ref32 = _CONVT2D(nchw(x).double(), wt.double(), b.double(), stride=2)
+    assert rel(up, ref16) < TOL
+    assert rel(up, ref32) > 1e-4  # bf16 operands really used
+    assert torch.equal(cat[..., :32], torch.zeros_like(cat[..., :32]))
+    gcat = torch.randn(n, 2 * h, 2 * w, co + 32, generator=g)
+    gcd = gcat.to(dev)
+    assert hip.igemm_arith(hip.nhwc(gcd, 32, co), h, w, 2, hip.TAPS_2X2, wb, ci, hip.nhwc(xd)) == 'bf16'
+    gx = torch.empty(n, h, w, ci, device=dev)
+    hip.conv_igemm(hip.nhwc(gcd, 32, co), h, w, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx))
+    ref_gx = _CONV2D(nchw(r16(gcat[..., 32:])).double(), r16(wt).double(), None, stride=2)
+    assert rel(nchw(gx), ref_gx) < TOL
+    # the emulation the model-level oracles use agrees with the kernels
+    xr = nchw(x).requires_grad_(True)
+    y = convT_bf16(xr, wt, b, stride=2)
+    assert rel(up, y.detach()) < TOL
+    y.backward(nchw(gcat[..., 32:]))
+    assert rel(nchw(gx), xr.grad) < TOL
 
 
 @pytest.mark.parametrize('n,h,w,ci,co', SHAPES)
@@ -142,12 +181,15 @@ def _oracle_step(P, B, batch, ocfg, bf16_convs: bool):
     P = {k: v.detach().clone().requires_grad_(True) for k, v in P.items()}
     B = {k: v.clone() for k, v in B.items()}
     F.conv2d = conv
+    if bf16_convs:
+        F.conv_transpose2d = convT_bf16  # the ConvTranspose forward / data grad on the bf16 gather kernel
     try:
         out = O.forward('siameseunet', P, B, batch['x_t1'], batch['x_t2'], ocfg, True)
         loss = O.power_jaccard_loss(out, batch['y_change'])
         loss.backward()
     finally:
         F.conv2d = _CONV2D
+        F.conv_transpose2d = _CONVT2D
     return out.detach(), loss.detach(), {k: v.grad for k, v in P.items()}
 
 
