@@ -146,6 +146,8 @@ void launch_wgrad_x3(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hip
 // h2 variants of the generic weight grad (both operand bounds; tiles wgrad_x3_h2_tile accepts), conv_x3.hip.
 bool wgrad_x3_h2_tile(int tile_id);
 void launch_wgrad_x3_h2(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
+// bf16 variants of the generic weight grad (the ConvTranspose weight grad under SCD_MATH_BF16), conv_x3.hip.
+void launch_wgrad_x3_bf16(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
 // Conv arithmetic of a launch (scd_igemm_t.math / scd_wgrad_t.math; enum scd_conv_math in scd.h).
 inline bool math_valid(int m) { return m >= SCD_MATH_F32 && m <= SCD_MATH_H2; }
 inline int math_split(int m) { return m != SCD_MATH_F32; }  // split-weight (x3, x5, bf16 or h2) pipeline

@@ -977,6 +977,10 @@ static bool wgrad_generic_h2(const scd_wgrad_t *d) {
            wgrad_x3_h2_tile(wgrad_tile(d->rows.c, d->ntaps * d->src.c).id);
 }
 
+// The generic weight grad in bf16: the ConvTranspose weight grad (4 taps) under SCD_MATH_BF16; the 3x3 weight grads
+// the halo kernels do not take keep x3.
+static bool wgrad_generic_bf16(const scd_wgrad_t *d) { return d->math == SCD_MATH_BF16 && d->ntaps == 4; }
+
 static int wgrad_halo_resident(const scd_wgrad_t *d, bool c16, bool bounded, int rblock) {
     // per halo weight-grad kernel: 16x16x32 x3 / x5 / bf16 / h2 (x layout); 16-channel x3 / x5 / bf16; the 128-row
     // bf16 / h2 blocks
@@ -1048,7 +1052,7 @@ extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
         return d->math != SCD_MATH_H2 ? d->math
                : wgrad_c16_planes(d->math, d->tune, wgrad_bounded(d)) == 4 ? SCD_MATH_H2
                                                                           : SCD_MATH_X3;
-    return wgrad_generic_h2(d) ? SCD_MATH_H2 : SCD_MATH_X3;
+    return wgrad_generic_h2(d) ? SCD_MATH_H2 : wgrad_generic_bf16(d) ? SCD_MATH_BF16 : SCD_MATH_X3;
 }
 
 extern "C" int scd_wgrad_rows_per_block(const scd_wgrad_t *d) {
@@ -1256,6 +1260,8 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     if (math_split(a.math)) {
         if (wgrad_generic_h2(d))
             launch_wgrad_x3_h2(a, t.id, grid, block, s);
+        else if (wgrad_generic_bf16(d))
+            launch_wgrad_x3_bf16(a, t.id, grid, block, s);
         else
             launch_wgrad_x3(a, t.id, grid, block, s);
         return launch_status("scd_conv_wgrad");

@@ -675,12 +675,13 @@ struct TrPlane {
 // NP = 4: the h2 arithmetic (x3_common.h) for convs outside the halo kernels (the ConvTranspose weight grad): both
 // operands scaled by the powers of two of *rows_bound / *src_bound and split into fp16 h and pre-scaled m' planes,
 // three v_mfma_f32_32x32x16_f16 products (a_h 2^-11) b_m' + a_m' (b_h 2^-11) + a_h b_h, scales undone in the
-// epilogue.
+// epilogue.  NP = 1: bf16 (the ConvTranspose weight grad of the bf16 configs), both operands rounded to bf16 (RNE),
+// one v_mfma_f32_32x32x16_bf16 product.
 template <int WAVES_M, int WAVES_N, int TM, int TN, int NP = 3>
 __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
-    static_assert(NP == 3 || NP == 4, "x3 or h2");
+    static_assert(NP == 1 || NP == 3 || NP == 4, "bf16, x3 or h2");
     constexpr bool H2 = NP == 4;
-    constexpr int NPL = H2 ? 2 : 3;  // planes per operand
+    constexpr int NPL = H2 ? 2 : NP == 1 ? 1 : 3;  // planes per operand
     constexpr int BK = 16;
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int BM = WAVES_M * TM * 32;
@@ -798,12 +799,15 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
                 u32x2 h, m, l;
                 if constexpr (H2) {
                     split2h_pre(ra[i] * rsc, h, m);
+                } else if constexpr (NP == 1) {
+                    h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
+                    h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
                 } else {
                     split3(ra[i], h, m, l);
                     *reinterpret_cast<u32x2 *>(S + 2 * PA + a_off[i]) = l;
                 }
                 *reinterpret_cast<u32x2 *>(S + a_off[i]) = h;
-                *reinterpret_cast<u32x2 *>(S + PA + a_off[i]) = m;
+                if constexpr (NPL > 1) *reinterpret_cast<u32x2 *>(S + PA + a_off[i]) = m;
             }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
@@ -811,12 +815,15 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
                 u32x2 h, m, l;
                 if constexpr (H2) {
                     split2h_pre(rb[i] * ssc, h, m);
+                } else if constexpr (NP == 1) {
+                    h[0] = cvt_pk_bf16(rb[i][0], rb[i][1]);
+                    h[1] = cvt_pk_bf16(rb[i][2], rb[i][3]);
                 } else {
                     split3(rb[i], h, m, l);
                     *reinterpret_cast<u32x2 *>(S + 2 * PB + b_off[i]) = l;
                 }
                 *reinterpret_cast<u32x2 *>(S + b_off[i]) = h;
-                *reinterpret_cast<u32x2 *>(S + PB + b_off[i]) = m;
+                if constexpr (NPL > 1) *reinterpret_cast<u32x2 *>(S + PB + b_off[i]) = m;
             }
     };
 
@@ -890,7 +897,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
                 constexpr int QA[6] = {1, 0, 2, 0, 1, 0};
                 constexpr int QB[6] = {1, 2, 0, 1, 0, 0};
 #pragma unroll
-                for (int q = 0; q < 6; ++q)
+                for (int q = NP == 1 ? 5 : 0; q < 6; ++q)  // bf16: the hh product only
 #pragma unroll
                     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -950,6 +957,17 @@ void launch_wgrad_x3_h2(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, 
         case 2: hipLaunchKernelGGL((wgrad_x3<2, 2, 1, 3, 4>), grid, block, 0, s, a); break;
         case 3: hipLaunchKernelGGL((wgrad_x3<2, 1, 1, 3, 4>), grid, block, 0, s, a); break;
         default: hipLaunchKernelGGL((wgrad_x3<1, 4, 1, 1, 4>), grid, block, 0, s, a); break;
+    }
+}
+
+// bf16 (SCD_MATH_BF16): the ConvTranspose weight grad (4 taps), every tile.
+void launch_wgrad_x3_bf16(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s) {
+    switch (tile_id) {
+        case 0: hipLaunchKernelGGL((wgrad_x3<2, 2, 2, 2, 1>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((wgrad_x3<1, 4, 2, 2, 1>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((wgrad_x3<2, 2, 1, 3, 1>), grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((wgrad_x3<2, 1, 1, 3, 1>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((wgrad_x3<1, 4, 1, 1, 1>), grid, block, 0, s, a); break;
     }
 }
 

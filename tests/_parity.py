@@ -217,9 +217,9 @@ _CONVT2D = F.conv_transpose2d
 
 
 class _ConvT16(torch.autograd.Function):
-    """A ConvTranspose2d(k=2, s=2) with the bf16 configs' arithmetic (libscd's gather kernel, bf16 instance): the
-    forward (fwd16) and the data grad (bwd16) on bf16-rounded operands, exact products, fp32 (here double)
-    accumulation; the weight grad at fp32 accuracy (the generic weight-grad kernel keeps the x3 arithmetic)."""
+    """A ConvTranspose2d(k=2, s=2) with the bf16 configs' arithmetic (libscd: the gather kernel's and the generic
+    weight grad's bf16 instances): the forward (fwd16) and the data grad (bwd16, where the gather kernel takes them)
+    and the weight grad (always) on bf16-rounded operands, exact products, fp32 (here double) accumulation."""
 
     @staticmethod
     def forward(ctx, x, w, b, fwd16, bwd16):
@@ -235,18 +235,18 @@ class _ConvT16(torch.autograd.Function):
         gx = _CONV2D(gg.double(), ww.double(), None, stride=2).float()  # the transpose of the ConvT
         with torch.enable_grad():
             wr = w.detach().double().requires_grad_(True)
-            gw, = torch.autograd.grad(_CONVT2D(x.detach().double(), wr, None, stride=2), wr, gy.double())
+            gw, = torch.autograd.grad(_CONVT2D(r16(x.detach()).double(), wr, None, stride=2), wr, r16(gy).double())
         return gx, gw.float(), gy.sum((0, 2, 3)), None, None
 
 
 def convT_bf16(x, w, b=None, stride=1, padding=0, *a, **k):
-    """F.conv_transpose2d with the bf16 configs' arithmetic where libscd's gather kernel takes the launch (forward:
-    in-channels % 32, 4 x out-channels % 64; data grad: out-channels % 32, in-channels % 64); fp32 otherwise."""
+    """F.conv_transpose2d(k=2, s=2) with the bf16 configs' arithmetic: forward and data grad in bf16 where libscd's
+    gather kernel takes the launch (forward: in-channels % 32, 4 x out-channels % 64; data grad: out-channels % 32,
+    in-channels % 64), fp32 otherwise; the weight grad in bf16."""
     if tuple(w.shape[2:]) == (2, 2) and stride == 2 and padding == 0 and not a and not k:
         fwd16 = w.shape[0] % 32 == 0 and w.shape[1] % 16 == 0
         bwd16 = w.shape[1] % 32 == 0 and w.shape[0] % 64 == 0
-        if fwd16 or bwd16:
-            return _ConvT16.apply(x, w, b if b is not None else w.new_zeros(w.shape[1]), fwd16, bwd16)
+        return _ConvT16.apply(x, w, b if b is not None else w.new_zeros(w.shape[1]), fwd16, bwd16)
     return _CONVT2D(x, w, b, stride, padding, *a, **k)
 
 

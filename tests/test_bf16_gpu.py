@@ -83,7 +83,8 @@ def test_bf16_conv_forward_and_data_grad(dev, bf16, n, h, w, ci, co):
 def test_bf16_convT_gather16(dev, bf16, n, h, w, ci, co):
     """The ConvTranspose forward (1 tap, pixel-shuffle store into a concat slice) and data grad (4 taps, stride-2
     gather from a channel slice) take the gather kernel's bf16 instance (no bound needed): fp32-accurate against
-    the ConvT of the bf16-rounded operands, a bf16-sized distance from the exact result."""
+    the ConvT of the bf16-rounded operands, a bf16-sized distance from the exact result; the weight grad likewise on
+    the generic weight grad's bf16 instance."""
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(n * h * w + ci + 1)
     x = torch.randn(n, h, w, ci, generator=g)
@@ -107,12 +108,25 @@ def test_bf16_convT_gather16(dev, bf16, n, h, w, ci, co):
     hip.conv_igemm(hip.nhwc(gcd, 32, co), h, w, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx))
     ref_gx = _CONV2D(nchw(r16(gcat[..., 32:])).double(), r16(wt).double(), None, stride=2)
     assert rel(nchw(gx), ref_gx) < TOL
+    # weight grad: rows = the ConvT input, src = g_up gathered with stride 2 -> the generic weight grad's bf16 instance
+    d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(xd), hip.nhwc(gcd, 32, co), 2, hip.TAPS_2X2)
+    assert hip.wgrad_arith(d) == 'bf16'
+    slabs = torch.empty(nbytes // 4, device=dev)
+    hip.conv_wgrad(d, slabs)
+    gw = torch.empty(ci, co, 2, 2, device=dev)
+    hip.wgrad_finalize(slabs, nsplit, ci, 4, co, 1, co, gw)
+    xr = nchw(r16(x)).double()
+    wr = wt.double().requires_grad_(True)
+    _CONVT2D(xr, wr, None, stride=2).backward(nchw(r16(gcat[..., 32:])).double())
+    assert rel(gw, wr.grad) < TOL
     # the emulation the model-level oracles use agrees with the kernels
     xr = nchw(x).requires_grad_(True)
-    y = convT_bf16(xr, wt, b, stride=2)
+    wr = wt.clone().requires_grad_(True)
+    y = convT_bf16(xr, wr, b, stride=2)
     assert rel(up, y.detach()) < TOL
     y.backward(nchw(gcat[..., 32:]))
     assert rel(nchw(gx), xr.grad) < TOL
+    assert rel(gw, wr.grad) < TOL
 
 
 @pytest.mark.parametrize('n,h,w,ci,co', SHAPES)
