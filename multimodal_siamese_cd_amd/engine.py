@@ -19,6 +19,7 @@ exactly: per-branch batch statistics, two running-stat updates (t1 first), summe
 from __future__ import annotations
 
 import contextlib
+import contextvars
 import weakref
 from dataclasses import dataclass
 
@@ -1125,14 +1126,24 @@ def cat_channels(*xs) -> torch.Tensor:
 # Exact-DataParallel loss (parallel.wrap_ddp(exact_dataparallel=True)): a callable that SUM-all-reduces a device
 # tensor in place across the ranks, applied to the loss kernels' partial sums, so every rank forms ONE loss over the
 # batch of all ranks, as nn.DataParallel's gathered-batch loss does (utils/networks.py:27, train_supervised.py:75).
-_LOSS_ALLREDUCE = None
+# It is scoped, not process-wide: only a loss formed inside `loss_reduction(fn)` (trainers.step_loss enters it for a
+# model wrapped in that mode, parallel.loss_scope) runs the collective; any other loss in the process (a rank-0
+# validation loss, a second model) stays local and issues no collective.
+_LOSS_ALLREDUCE = contextvars.ContextVar('scd_loss_allreduce', default=None)
 
 
-def set_loss_allreduce(fn):
-    """Install (fn) or remove (None) the cross-rank reduction of the loss sums; returns the previous one."""
-    global _LOSS_ALLREDUCE
-    prev, _LOSS_ALLREDUCE = _LOSS_ALLREDUCE, fn
-    return prev
+@contextlib.contextmanager
+def loss_reduction(fn):
+    """Inside: the loss kernels' partial sums are reduced by fn (None: local)."""
+    tok = _LOSS_ALLREDUCE.set(fn)
+    try:
+        yield
+    finally:
+        _LOSS_ALLREDUCE.reset(tok)
+
+
+def current_loss_reduction():
+    return _LOSS_ALLREDUCE.get()
 
 
 class PJaccardFn(torch.autograd.Function):
@@ -1146,8 +1157,9 @@ class PJaccardFn(torch.autograd.Function):
         loss = _empty((), logits)
         ws = _ws(hip.pjaccard_workspace_bytes(logits.numel()), logits)
         hip.pjaccard_fwd(logits, target, sums, loss, ws)
-        if _LOSS_ALLREDUCE is not None:  # global {I, sum(p^2 + t^2)}, then D and the loss re-formed from them
-            _LOSS_ALLREDUCE(sums)
+        red = _LOSS_ALLREDUCE.get()
+        if red is not None:  # global {I, sum(p^2 + t^2)}, then D and the loss re-formed from them
+            red(sums)
             hip.pjaccard_loss_from_sums(sums, loss)
         ctx.save_for_backward(logits, target, sums)
         return loss
@@ -1188,8 +1200,9 @@ class MultiJaccardFn(torch.autograd.Function):
         sums = _empty((len(spec), 4), ts[0])
         loss = _empty((), ts[0])
         hip.jaccard_multi_fwd(terms, lab, n_samples, pixels, sums, loss)
-        if _LOSS_ALLREDUCE is not None:  # exact-DataParallel: every term over the samples of all ranks
-            _LOSS_ALLREDUCE(sums)
+        red = _LOSS_ALLREDUCE.get()
+        if red is not None:  # exact-DataParallel: every term over the samples of all ranks
+            red(sums)
             hip.jaccard_multi_loss_from_sums(terms, sums, loss)
         ctx.spec, ctx.dims = spec, (n_samples, pixels)
         ctx.save_for_backward(lab, sums, *ts)

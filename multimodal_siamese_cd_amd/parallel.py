@@ -9,6 +9,7 @@ per-replica statistics) and running statistics are broadcast from rank 0 each fo
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -106,7 +107,9 @@ def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 16, find_unused_paramete
     takes ONE loss over the gathered batch (utils/networks.py:27, train_supervised.py:75), a different function of
     the logits (Jaccard is a ratio of batch sums: 7e-6 apart at bs=2).  exact_dataparallel=True reproduces
     it: the loss kernels' partial sums (I, sum p^2 + t^2 per term) are SUM-all-reduced before the loss is formed
-    (engine.set_loss_allreduce, three floats per term), and the gradient buckets are SUMMED (sum_allreduce_hook).
+    (three floats per term), and the gradient buckets are SUMMED (sum_allreduce_hook).  The loss reduction belongs
+    to the wrapped model, not to the process: the wrapper is marked (`exact_dataparallel`), and only a loss formed
+    under `loss_scope(net)` (trainers.step_loss(cfg, out, batch, net)) runs the collective.
     BatchNorm statistics stay per rank and running statistics come from rank 0 (broadcast_buffers) in both modes,
     as DataParallel's per-replica statistics with replica 0's buffers.
     `single_rank`: wrap even in a one-rank process group (the RCCL / DDP bucket path on one GPU,
@@ -121,11 +124,19 @@ def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 16, find_unused_paramete
     ddp = torch.nn.parallel.DistributedDataParallel(module, device_ids=ids, broadcast_buffers=True,
                                                     bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
                                                     find_unused_parameters=find_unused_parameters)
+    ddp.exact_dataparallel = bool(exact_dataparallel)
     if exact_dataparallel:
-        from . import engine
         ddp.register_comm_hook(None, sum_allreduce_hook)
-        engine.set_loss_allreduce(allreduce_sum_)
     return ddp
+
+
+def loss_scope(net):
+    """The context a training step's loss is formed in: for a model wrapped with exact_dataparallel=True the loss
+    kernels' partial sums are SUM-all-reduced over the ranks (engine.loss_reduction); otherwise nothing changes."""
+    from . import engine
+    if getattr(net, 'exact_dataparallel', False):
+        return engine.loss_reduction(allreduce_sum_)
+    return contextlib.nullcontext()
 
 
 def allreduce_max(value: float, device) -> float:

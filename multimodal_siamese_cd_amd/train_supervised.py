@@ -47,7 +47,9 @@ def run_training(cfg, device, max_steps: int | None = None):
     rank, _, world = parallel.env_rank()
     net = networks.create_network(cfg)
     net.to(device)
-    net = parallel.wrap_ddp(net, device)
+    # TRAINER.EXACT_DATAPARALLEL: the reference's gathered-batch loss of nn.DataParallel (one loss over all ranks'
+    # pairs, summed gradients) instead of DDP's mean of per-rank losses (parallel.wrap_ddp)
+    net = parallel.wrap_ddp(net, device, exact_dataparallel=bool(cfg.TRAINER.get('EXACT_DATAPARALLEL', False)))
     optimizer = torch.optim.AdamW(net.parameters(), lr=float(cfg.TRAINER.LR), weight_decay=0.01)
     gen = torch.Generator(device=device).manual_seed(parallel.rank_seed(cfg.SEED, rank))
     steps_per_epoch = int(cfg.TRAINER.get('STEPS_PER_EPOCH', 100))
@@ -74,7 +76,7 @@ def run_training(cfg, device, max_steps: int | None = None):
             net.train()
             optimizer.zero_grad(set_to_none=True)
             out = net(batch['x_t1'], batch['x_t2'])
-            loss = trainers.step_loss(cfg, out, batch)
+            loss = trainers.step_loss(cfg, out, batch, net)
             loss.backward()
             optimizer.step()
             losses.append(loss.detach())

@@ -59,8 +59,16 @@ def mmcr_loss(sup_criterion, cons_criterion, outputs, batch, alpha: float, cons_
     return loss
 
 
-def step_loss(cfg, outputs, batch):
-    """Dispatch on the model family the way the reference's three trainers do."""
+def step_loss(cfg, outputs, batch, net=None):
+    """Dispatch on the model family the way the reference's three trainers do.  `net`: the (wrapped) model the
+    outputs come from; a model wrapped with exact_dataparallel=True forms ONE loss over the batch of all ranks
+    (parallel.loss_scope), any other loss stays local."""
+    from . import parallel
+    with parallel.loss_scope(net):
+        return _step_loss(cfg, outputs, batch)
+
+
+def _step_loss(cfg, outputs, batch):
     t = cfg.MODEL.TYPE
     crit = loss_functions.get_criterion(cfg.MODEL.LOSS_TYPE)
     if t == 'dtsiameseunet':

@@ -23,6 +23,10 @@ import torch.nn.functional as F
 
 KINK_REL = 1e-5
 KINK_MAX_ERR = 3e-2
+# Largest distance (max-relative) a GPU pre-activation may have from the branch-matched oracle's and still be adopted.
+# h2 / x3 forwards sit at 1e-6-class distances (fp32 arithmetic); the guard leaves one decade of margin over the
+# kink band, and every adopted decision is bounded by the band itself (BranchMatch.__call__).
+MATCH_MAX_REL = 1e-4
 _CONV2D = F.conv2d
 
 Kink = namedtuple('Kink', 'key rel occ mask')
@@ -94,8 +98,14 @@ class BranchMatch:
     batches the Siamese branches and the decoder_sem runs of the dual-task model, the oracle calls them one by one).
     The activation returned for the pooling argmax is relu(z) rounded to fp32, the values the GPU pooled."""
 
-    def __init__(self, trace, module, max_rel: float = 1e-3):
-        """module: the model (its named_modules name the traced BatchNorms), or a dict {id(bn): name}."""
+    def __init__(self, trace, module, max_rel: float = MATCH_MAX_REL, kink_rel: float = KINK_REL):
+        """module: the model (its named_modules name the traced BatchNorms), or a dict {id(bn): name}.
+
+        Every adopted decision is bounded: a ReLU decision of the GPU that differs from the sign of the oracle's own
+        pre-activation must lie in the kink band |z_oracle| <= kink_rel * max|z_oracle|, and a 2x2 window whose GPU
+        argmax differs from the argmax of the oracle's own activation must be a near-tie (the two candidates' oracle
+        activations within kink_rel * max|z_oracle|).  Anything else is a wrong branch, not a rounding choice, and
+        raises.  The counts are kept (flips, pool_flips) and printed."""
         if isinstance(module, dict):
             names = module
         else:  # a model off the granule of 8 runs a padded twin (utils/networks.py): its BatchNorms, same names
@@ -113,8 +123,13 @@ class BranchMatch:
             for s in range(nseg):
                 self.segs.setdefault(names[id(bn)], []).append((y32[s * per:(s + 1) * per], sc[s], sh[s]))
         self.max_rel = max_rel
+        self.kink_rel = kink_rel
         self.worst = 0.0
         self.calls = 0
+        self.flips = 0  # ReLU decisions adopted from the GPU against the oracle's own sign (all inside the kink band)
+        self.pool_flips = 0  # 2x2 windows whose adopted argmax differs from the oracle's own (all near-ties)
+        self.elements = 0
+        self.windows = 0
 
     def __call__(self, key, y):
         nb = y.shape[0]
@@ -134,7 +149,41 @@ class BranchMatch:
             raise AssertionError(f'{key}: no GPU pre-activation within {self.max_rel} of the oracle\'s ({best_d:.2e})')
         self.worst = max(self.worst, best_d)
         self.calls += 1
-        return best > 0, torch.relu(best.float()).to(y.dtype)
+        band = self.kink_rel * float(den)
+        mask = best > 0
+        flip = mask != (yd > 0)
+        nflip = int(flip.sum())
+        if nflip:
+            far = flip & (yd.abs() > band)
+            if bool(far.any()):
+                raise AssertionError(
+                    f'{key}: {int(far.sum())} GPU ReLU decisions differ from the oracle\'s outside the kink band '
+                    f'(|z| up to {float(yd.abs()[far].max() / den):.2e} of max, band {self.kink_rel:.0e})')
+        self.flips += nflip
+        self.elements += flip.numel()
+        a = torch.relu(best.float())
+        if y.shape[2] >= 2 and y.shape[3] >= 2:  # a MaxPool2d(2) may follow: its window argmaxes are adopted too
+            from oracle.siamese_oracle import _windows
+            wg = _windows(a.double())
+            wo = _windows(torch.relu(yd))
+            ig, io = wg.argmax(-1, keepdim=True), wo.argmax(-1, keepdim=True)
+            diff = (ig != io).squeeze(-1)
+            npf = int(diff.sum())
+            if npf:
+                gap = (wo.gather(-1, io) - wo.gather(-1, ig)).squeeze(-1)[diff]
+                if float(gap.max()) > band:
+                    raise AssertionError(
+                        f'{key}: {int((gap > band).sum())} pooling windows whose GPU argmax is not a near-tie of the '
+                        f'oracle\'s (gap up to {float(gap.max() / den):.2e} of max, band {self.kink_rel:.0e})')
+            self.pool_flips += npf
+            self.windows += diff.numel()
+        return mask, a.to(y.dtype)
+
+    def summary(self) -> str:
+        return (f'{self.calls} BatchNorm outputs matched, worst pre-activation distance {self.worst:.2e} '
+                f'(guard {self.max_rel:.0e}); ReLU decisions adopted against the oracle\'s sign: {self.flips} of '
+                f'{self.elements} (all within {self.kink_rel:.0e} of max); pooling argmaxes adopted: {self.pool_flips} '
+                f'of {self.windows} windows (all near-ties)')
 
 
 def branch_matched_reference(model_type, P, batch, ocfg, trace, module, loss_fn, training=True, buffers=None):
@@ -158,7 +207,7 @@ def branch_matched_reference(model_type, P, batch, ocfg, trace, module, loss_fn,
             buffers[k].copy_(v)
     loss = loss_fn(out, bt)
     loss.backward()
-    print(f'branch matching: {bm.calls} BatchNorm outputs matched, worst pre-activation distance {bm.worst:.2e}')
+    print(f'branch matching: {bm.summary()}')
     return out, loss, {k: v.grad for k, v in Pd.items() if v.grad is not None}
 
 

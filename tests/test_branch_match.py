@@ -62,3 +62,51 @@ def test_branch_match_rejects_a_foreign_trace():
         assert 'no GPU pre-activation' in str(e)
     else:
         raise AssertionError('a foreign trace was accepted')
+
+
+def _bm_one(z_gpu):
+    """A BranchMatch over one traced BatchNorm output whose GPU pre-activation is z_gpu (NCHW, scale 1, shift 0)."""
+    from _parity import BranchMatch
+    tag = object()
+    c = z_gpu.shape[1]
+    return BranchMatch([(tag, z_gpu.permute(0, 2, 3, 1).contiguous(), torch.ones(c), torch.zeros(c), 1)],
+                       {id(tag): 'k'})
+
+
+def test_branch_match_bounds_relu_flips():
+    """A GPU ReLU decision against the oracle's own sign is adopted only inside the 1e-5 kink band: a flip at
+    3e-6 of max is counted, one at 3e-5 of max (still within the 1e-4 distance guard) raises."""
+    torch.manual_seed(0)
+    z = torch.rand(1, 4, 6, 6) + 0.5
+    z[0, 1, 2, 3] = 3e-6 * float(z.max())
+    bm = _bm_one(torch.where(z.abs() < 1e-5 * z.max(), -z, z))
+    m, _ = bm('k', z.double())
+    assert bm.flips == 1 and not bool(m[0, 1, 2, 3])
+    z[0, 1, 2, 3] = 3e-5 * float(z.max())
+    bm = _bm_one(torch.where(z.abs() < 1e-4 * z.max(), -z, z))
+    try:
+        bm('k', z.double())
+    except AssertionError as e:
+        assert 'outside the kink band' in str(e)
+    else:
+        raise AssertionError('a ReLU flip outside the kink band was adopted')
+
+
+def test_branch_match_bounds_pool_argmax():
+    """A GPU pooling argmax that differs from the oracle's is adopted only at a near-tie."""
+    z = torch.full((1, 1, 2, 2), 0.5)
+    z[0, 0, 0, 0] = 1.0
+    z[0, 0, 1, 1] = 1.0 - 4e-6
+    g = z.clone()
+    g[0, 0, 1, 1] = 1.0 + 4e-6  # within 1e-5 of max of the oracle's winner: a near-tie
+    bm = _bm_one(g)
+    bm('k', z.double())
+    assert bm.pool_flips == 1 and bm.flips == 0
+    z[0, 0, 1, 1] = 1.0 - 4e-5
+    g[0, 0, 1, 1] = 1.0 + 4e-5  # distance 8e-5 < the 1e-4 guard, but a real argmax change
+    try:
+        _bm_one(g)('k', z.double())
+    except AssertionError as e:
+        assert 'near-tie' in str(e)
+    else:
+        raise AssertionError('a pooling argmax change outside the near-tie band was adopted')

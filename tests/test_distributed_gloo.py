@@ -268,7 +268,14 @@ def _worker_exact(rank, world, port, out_dir):
                 'buffers': {n.replace('__', '.'): v.detach().clone() for n, v in net.module.named_buffers()}},
                os.path.join(out_dir, f'rank{rank}.pt'))
     from multimodal_siamese_cd_amd import engine
-    assert engine.set_loss_allreduce(None) is parallel.allreduce_sum_  # wrap_ddp installed the loss reduction
+    # the loss reduction belongs to the wrapped model: on inside its loss scope, off everywhere else in the process
+    assert net.exact_dataparallel and engine.current_loss_reduction() is None
+    with parallel.loss_scope(net):
+        assert engine.current_loss_reduction() is parallel.allreduce_sum_
+    assert engine.current_loss_reduction() is None
+    plain = parallel.wrap_ddp(OracleReplica(P, orc.fresh_buffers(shapes)), device=None)
+    with parallel.loss_scope(plain):
+        assert engine.current_loss_reduction() is None
     torch.distributed.destroy_process_group()
 
 

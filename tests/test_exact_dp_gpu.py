@@ -45,7 +45,7 @@ def _worker(rank, world, port, out_dir):
     per = fx.meta['batch'] // world
     b = {k: v[rank * per:(rank + 1) * per].to(dev) for k, v in fx.batch().items()}
     out = net(b['x_t1'], b['x_t2'])
-    loss = trainers.step_loss(cfg, out, b)
+    loss = trainers.step_loss(cfg, out, b, net)
     loss.backward()
     torch.cuda.synchronize()
     torch.save({'loss': loss.item(), 'logits': out.detach().cpu(),

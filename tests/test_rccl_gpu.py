@@ -53,7 +53,7 @@ def _worker(rank, port, out_dir):
             net = parallel.wrap_ddp(net, dev, exact_dataparallel=True, single_rank=True)
             out['wrapped'] = type(net).__name__
         y = net(b['x_t1'], b['x_t2'])
-        loss = trainers.step_loss(cfg, y, b)
+        loss = trainers.step_loss(cfg, y, b, net)
         loss.backward()
         torch.cuda.synchronize()
         mod = net.module

@@ -251,3 +251,59 @@ def test_models_of_different_arithmetic_coexist(dev):
     for p, g in zip(nb.parameters(), alone_b[1]):
         assert torch.equal(p.grad, g)
     assert rel(out_a.detach(), out_b.detach()) > 1e-4  # really two arithmetics
+
+
+def test_baseline_siamese_bs64_north_star_batch(dev, monkeypatch):
+    """The north-star batch (bs=64 per GPU, 256x256, SiameseUNet [64,128,256,512], h2): the Siamese level-0 maps are
+    128 x 256^2 x 64 fp32 = 2.15 GB, so the level-0 convs and weight grads run as image chunks below 2 GiB
+    (DESIGN 3.1c), and the BatchNorm-derived h2 operand bounds (|gamma| sqrt(n-1) + |beta|, n = 4.2 M) are at their
+    loosest.  A full training step on the GPU against the reference's own fp32 arithmetic (the oracle, its own
+    branches, forward under no_grad to keep host memory bounded): logits within 1e-4 (north_star), change masks
+    bit-exact outside the |logit| < 1e-4 max band, loss within 1e-5, BatchNorm running statistics within 1e-5 and
+    num_batches_tracked exact; the backward (chunked data and weight grads) must produce finite gradients."""
+    from oracle import siamese_oracle as O
+    from multimodal_siamese_cd_amd import trainers
+    from multimodal_siamese_cd_amd.utils import networks
+    cfg = _cfg('baseline_siamese', 'siameseunet', FULL, PRECISION='fp32')
+    bs, size = 64, 256
+    assert 2 * bs * size * size * FULL[0] * 4 > 2 ** 31  # the chunked launch path is the one under test
+    P, batch = _setup(cfg, bs, size)
+    net = networks.create_network(cfg)
+    with torch.no_grad():
+        for k, p in net.module.named_parameters():
+            p.copy_(P[k])
+    net.to(dev).train()
+    seen = record_arith(monkeypatch, dev)
+    b = {k: v.to(dev) for k, v in batch.items()}
+    out = net(b['x_t1'], b['x_t2'])
+    loss = trainers.step_loss(cfg, out, b)
+    loss.backward()
+    monkeypatch.undo()
+    torch.cuda.synchronize()
+    assert net.module.conv_math == 'h2'
+    _check_routing(seen, 'h2')
+    logits, loss = out.detach().cpu(), loss.item()
+    sd = {k: v.detach().cpu() for k, v in net.module.state_dict().items()}
+    for k, p in net.module.named_parameters():
+        assert p.grad is not None and bool(torch.isfinite(p.grad).all()), k
+    del out, b, net
+    torch.cuda.empty_cache()
+    ocfg = _ocfg(cfg)
+    B = O.fresh_buffers(O.param_shapes('siameseunet', ocfg))
+    with torch.no_grad():
+        ref = O.forward('siameseunet', P, B, batch['x_t1'], batch['x_t2'], ocfg, True)
+        ref_loss = O.step_loss('siameseunet', ref, batch, 0.5).item()
+    e = rel(logits, ref)
+    mm = mask_mismatch(logits.numpy(), ref.numpy())
+    print(f'bs=64: logits rel err {e:.2e}, mask mismatches outside the band {mm}, loss {loss:.7f} vs {ref_loss:.7f}')
+    assert e < 1e-4
+    assert mm == 0
+    assert abs(loss - ref_loss) < 1e-5
+    worst = 0.0
+    for k, v in B.items():
+        if k.endswith('running_mean') or k.endswith('running_var'):
+            worst = max(worst, rel(sd[k], v))
+            assert rel(sd[k], v) < 1e-5, k
+        elif k.endswith('num_batches_tracked'):
+            assert int(sd[k]) == int(v), k
+    print(f'bs=64: BatchNorm running statistics worst rel err {worst:.2e}')
