@@ -1,23 +1,36 @@
 """Throughput benchmark of the Siamese U-Net training step on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config baseline_siamese] [--batch B] [--math x3|bf16|f32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config baseline_siamese] [--batch B]
+                    [--math h2|x3|x5|bf16|f32]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 One step = zero_grad -> SiameseUNet forward (HIP) -> power_jaccard_loss -> backward (HIP) -> AdamW step,
 on synthetic 256x256 SAR(2)+optical(3) pairs generated on the device (weak scaling: every rank draws its
 own batch).  Rank 0 prints ONE JSON line; `value` is pairs/s of the whole job (all ranks' pairs / max rank time).
 
+Conv arithmetic.  A model carries it per launch descriptor (no library mode, no environment switch): a config with
+MODEL.PRECISION fp32 runs h2 (the default: each fp32 operand as a two-term fp16 split after power-of-two scaling,
+three fp16 MFMA products, fp32 accumulation; fp32-class results), MODEL.PRECISION bf16 runs bf16; `--math` overrides
+it (x3: exact three-term bf16 split, six products; x5: x3 less one product; f32: fp32 MFMA).  `dtype` names the
+arithmetic: "f32 (h2 split-fp16)" for the default.
+
 Measurement extras (rank 0, after the timed region):
   roofline      the MFMA conv kernels (every conv launch of one step) bracketed by HIP events on the launch
                 stream: algorithmic conv FLOPs per step / summed kernel time.  The peak is each launch's own
-                matrix-core ceiling, combined as flops / sum(flops_i / peak_i):
-                  - fp32 MFMA: 157.3 TFLOP/s;
-                  - split-bf16 x3: bf16 dense 2516.6 / 6 products = 419.4 fp32-equivalent TFLOP/s
-                    (MI355X_MICROARCH.md);
-                  - bf16 (--math bf16, or a config with MODEL.PRECISION: bf16): bf16 dense 2516.6 TFLOP/s.
-                The arithmetic of every launch comes from the library (scd_igemm_arith / scd_wgrad_arith).
-  cpu_baseline  the CPU oracle (oracle/siamese_oracle.py, torch fp32 on host cores) running the same training
-                step on a bounded sample (bs=2, 256x256).
+                matrix-core ceiling (the library reports every launch's arithmetic: scd_igemm_arith /
+                scd_wgrad_arith), combined flop-weighted harmonically:
+                  - h2: fp16 dense 2516.8 / 3 products = 838.9 fp32-equivalent TFLOP/s;
+                  - x3: bf16 dense 2516.8 / 6 products = 419.5; x5: / 5 = 503.4;
+                  - bf16: bf16 dense 2516.8; fp32 MFMA: 157.3 (MI355X_MICROARCH.md).
+                by_class / dominant_kernel split the same events per kernel family.
+  step_roofline the survey's whole-step formula: 3x3-stack train FLOP/pair x pairs/s/GPU over the
+                peak of the arithmetic the step runs (h2 838.9 for the default), with the nominal fp32-MFMA ratio
+                beside it, labelled as such.
+  cpu_baseline  the CPU oracle (oracle/siamese_oracle.py, torch fp32 on every host core this process may use)
+                running the same training step on bounded samples at bs=2 and bs=8, 256x256.
+  distributed   under torchrun: process-group backend, world size, per-rank ms per step (min / max) and the exposed
+                gradient all-reduce on rank 0 (HIP events: from the last parameter gradient the backward produces to
+                the end of backward, where DDP's reducer makes the compute stream wait for the last bucket).
 """
 from __future__ import annotations
 
@@ -156,40 +169,69 @@ class KernelTimer:
         return sum(ev[3] for ev in self.events) / reps
 
 
-def cpu_baseline(cfg, min_seconds: float = 10.0, max_steps: int = 64, batch: int = 2, size: int = 256):
-    """The CPU oracle (torch fp32 on host cores) running the same training step on a bounded sample:
-    whole steps until `min_seconds` of CPU work have been timed (at least 2, at most `max_steps`)."""
+def host_cores() -> tuple:
+    """(cores this process may run on: the CPU affinity set, capped by a cgroup CPU quota; os.cpu_count(); model)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    model = 'unknown'
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return n, os.cpu_count(), model
+
+
+def cpu_baseline(cfg, batches=(2, 8), min_seconds=(8.0, 6.0), size: int = 256):
+    """The CPU oracle (torch fp32 on every host core this process may use) running the same training step on bounded
+    samples, one per batch size (bs=2 and bs=8 at 256x256): whole steps after one warm-up until
+    `min_seconds` of CPU work have been timed (at least 2 steps).  `value` is the larger batch's rate."""
     from oracle import siamese_oracle as O
 
-    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(os.cpu_count() or 1, 16)
+    threads, ncpu, model = host_cores()
     torch.set_num_threads(threads)
     ocfg = dict(TOPOLOGY=list(cfg.MODEL.TOPOLOGY), IN_CHANNELS=cfg.MODEL.IN_CHANNELS, OUT_CHANNELS=1,
                 S1_BANDS=list(cfg.DATALOADER.S1_BANDS), S2_BANDS=list(cfg.DATALOADER.S2_BANDS))
     mtype = cfg.MODEL.TYPE
     shapes = O.param_shapes(mtype, ocfg)
-    P = {k: v.requires_grad_(True) for k, v in O.deterministic_params(shapes, 7).items()}
-    B = O.fresh_buffers(shapes)
-    b = O.synthetic_batch(ocfg, batch, size, 8)
-    opt = torch.optim.AdamW(list(P.values()), lr=1e-4, weight_decay=0.01)
+    by_batch, notes = {}, []
+    for batch, tmin in zip(batches, min_seconds):
+        P = {k: v.requires_grad_(True) for k, v in O.deterministic_params(shapes, 7).items()}
+        B = O.fresh_buffers(shapes)
+        b = O.synthetic_batch(ocfg, batch, size, 8)
+        opt = torch.optim.AdamW(list(P.values()), lr=1e-4, weight_decay=0.01)
 
-    def step():
-        opt.zero_grad()
-        out = O.forward(mtype, P, B, b['x_t1'], b['x_t2'], ocfg, True)
-        loss = O.step_loss(mtype, out, b, 0.5)
-        loss.backward()
-        opt.step()
+        def step():
+            opt.zero_grad()
+            out = O.forward(mtype, P, B, b['x_t1'], b['x_t2'], ocfg, True)
+            loss = O.step_loss(mtype, out, b, 0.5)
+            loss.backward()
+            opt.step()
 
-    step()  # warm-up
-    t0 = time.perf_counter()
-    steps = 0
-    while steps < 2 or (time.perf_counter() - t0 < min_seconds and steps < max_steps):
-        step()
-        steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt, 4), "unit": "image-pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} timed training steps (after 1 warm-up) of the CPU oracle ({mtype}), bs={batch}, "
-                      f"{size}x{size}, {cfg.MODEL.IN_CHANNELS}-ch, TOPOLOGY {list(cfg.MODEL.TOPOLOGY)}, fp32, "
-                      f"torch {torch.__version__} with {threads} threads ({dt:.1f} s)"}
+        step()  # warm-up
+        t0 = time.perf_counter()
+        steps = 0
+        while steps < 2 or time.perf_counter() - t0 < tmin:
+            step()
+            steps += 1
+        dt = time.perf_counter() - t0
+        by_batch[str(batch)] = round(batch * steps / dt, 4)
+        notes.append(f"bs={batch}: {steps} steps in {dt:.1f} s")
+    return {"value": by_batch[str(batches[-1])], "unit": "image-pairs/s", "cores": threads, "kind": "port",
+            "by_batch": by_batch, "cpu_model": model, "os_cpu_count": ncpu,
+            "sample": f"timed training steps (after 1 warm-up each) of the CPU oracle ({mtype}), {size}x{size}, "
+                      f"{cfg.MODEL.IN_CHANNELS}-ch, TOPOLOGY {list(cfg.MODEL.TOPOLOGY)}, fp32, torch "
+                      f"{torch.__version__}, {threads} threads (the cores this process may use; os.cpu_count() "
+                      f"{ncpu}); " + '; '.join(notes)}
 
 
 def main():
@@ -215,7 +257,8 @@ def main():
     if args.math:
         cfg.MODEL.CONV_MATH = args.math
     math = engine.conv_math_for(cfg)  # create_network gives the model this arithmetic (hip.conv_scope per forward)
-    dtype = 'bf16' if math == 'bf16' else 'f32'
+    dtype = {'bf16': 'bf16', 'h2': 'f32 (h2 split-fp16)', 'x3': 'f32 (x3 split-bf16)',
+             'x5': 'f32 (x5 split-bf16, 5 products)', 'f32': 'f32'}[math]
     batch = args.batch or int(cfg.TRAINER.BATCH_SIZE)
     size = args.size or int(cfg.AUGMENTATION.CROP_SIZE)
     torch.manual_seed(cfg.SEED)
@@ -232,7 +275,7 @@ def main():
 
     def step():
         opt.zero_grad(set_to_none=True)
-        loss = trainers.step_loss(cfg, net(b['x_t1'], b['x_t2']), b)  # the config's trainer recipe
+        loss = trainers.step_loss(cfg, net(b['x_t1'], b['x_t2']), b, net)  # the config's trainer recipe
         loss.backward()
         opt.step()
         return loss
@@ -249,8 +292,8 @@ def main():
         loss = step()
     torch.cuda.synchronize()
     parallel.barrier(dev)
-    dt = time.perf_counter() - t0
-    dt = parallel.allreduce_max(dt, dev)
+    dt_local = time.perf_counter() - t0
+    dt = parallel.allreduce_max(dt_local, dev)
     last_loss = float(loss.item())
 
     value = batch * world * args.steps / dt
@@ -277,11 +320,14 @@ def main():
         "loss_first_last": [round(first_loss, 6), round(last_loss, 6)],
     }
     if cfg.MODEL.TYPE == 'siameseunet':  # SURVEY 8(d) formula (273.3 GF/pair at 256^2, 5-ch)
-        dpeak = BF16_MFMA_PEAK_TFLOPS if dtype == 'bf16' else FP32_MFMA_PEAK_TFLOPS
+        dpeak = PEAKS[math]
+        per_gpu = f3 / batch * (value / world)
         result["step_roofline"] = {
-            "formula": f"3x3-stack train FLOP/pair x pairs/s/GPU / {dtype} MFMA peak ({dpeak})",
+            "formula": f"3x3-stack train FLOP/pair x pairs/s/GPU / the {math} arithmetic's matrix-core peak "
+                       f"({dpeak:.1f} TFLOP/s)",
             "gflop_per_pair_3x3": round(f3 / batch / 1e9, 2),
-            "frac": round(f3 / batch * (value / world) / (dpeak * 1e12), 4)}
+            "frac": round(per_gpu / (dpeak * 1e12), 4),
+            "nominal_frac_of_fp32_mfma_peak": round(per_gpu / (FP32_MFMA_PEAK_TFLOPS * 1e12), 4)}
 
     if not args.no_kernel_timing:
         # every rank runs the instrumented steps (DDP's collectives must match); rank 0 records the HIP events
@@ -336,6 +382,20 @@ def main():
         if classes:
             dom = max(classes, key=lambda k: classes[k]["ms_per_step"])
             result["roofline"]["dominant_kernel"] = dict(classes[dom], **{"class": dom})
+    if parallel.is_distributed():  # every rank: the probe steps and the report run collectives
+        probe = parallel.ExposedAllreduceProbe(net.module, dev)
+        exposed = []
+        for _ in range(3):
+            opt.zero_grad(set_to_none=True)
+            loss = trainers.step_loss(cfg, net(b['x_t1'], b['x_t2']), b, net)
+            probe.begin()
+            loss.backward()
+            exposed.append(probe.end())
+            opt.step()
+        probe.remove()
+        rep = parallel.distributed_report(1000.0 * dt_local / args.steps, exposed, dev)
+        rep['bucket_cap_mb'] = 16
+        result["distributed"] = rep
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, size=size)
     if rank == 0:

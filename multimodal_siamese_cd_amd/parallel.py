@@ -154,3 +154,80 @@ def barrier(device=None):
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+def gather_floats(value: float, device=None) -> list:
+    """Every rank's `value`, in rank order (one SUM all-reduce of a one-hot vector)."""
+    if not is_distributed():
+        return [float(value)]
+    on_dev = device is not None and getattr(device, 'type', 'cpu') == 'cuda' and dist.get_backend() == 'nccl'
+    t = torch.zeros(dist.get_world_size(), dtype=torch.float64, device=device if on_dev else 'cpu')
+    t[dist.get_rank()] = float(value)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+class ExposedAllreduceProbe:
+    """The gradient all-reduce time a DDP backward leaves exposed, measured on this rank.
+
+    Every parameter gets a tensor hook that stamps the moment its gradient is produced (a HIP event on the stream
+    the backward runs on, or the host clock on CPU); `end()` stamps the return of backward(), by which point DDP's
+    reducer has made the compute stream wait for every bucket's all-reduce.  Exposed = end - the last gradient
+    stamp: the all-reduce time that overlapped no backward kernel."""
+
+    def __init__(self, module, device=None):
+        self.cuda = device is not None and getattr(device, 'type', 'cpu') == 'cuda'
+        self.active = False
+        self.marks, self.t0, self.t1 = [], None, None
+        self.handles = [p.register_hook(self._hook) for p in module.parameters() if p.requires_grad]
+
+    def _stamp(self):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        import time
+        return time.perf_counter()
+
+    def _hook(self, grad):
+        if self.active:
+            self.marks.append(self._stamp())
+
+    def begin(self):
+        self.marks = []
+        self.active = True
+        self.t0 = self._stamp()
+
+    def end(self) -> dict:
+        """{backward_ms, last_grad_ms, exposed_ms} of the backward between begin() and now."""
+        self.t1 = self._stamp()
+        self.active = False
+        if self.cuda:
+            torch.cuda.synchronize()
+            last = max((self.t0.elapsed_time(m) for m in self.marks), default=0.0)
+            total = self.t0.elapsed_time(self.t1)
+        else:
+            last = max(((m - self.t0) * 1e3 for m in self.marks), default=0.0)
+            total = (self.t1 - self.t0) * 1e3
+        return {'backward_ms': total, 'last_grad_ms': last, 'exposed_ms': max(total - last, 0.0)}
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+        self.handles = []
+
+
+def distributed_report(ms_per_step: float, exposed: list, device=None) -> dict:
+    """The bench line's `distributed` fields (every rank calls it; collectives inside): backend, world size as the
+    process group reports it, per-rank ms per step (min / max over ranks), and rank 0's exposed all-reduce
+    (median of the probe's steps)."""
+    per_rank = gather_floats(ms_per_step, device)
+    med = sorted(e['exposed_ms'] for e in exposed)[len(exposed) // 2] if exposed else None
+    bwd = sorted(e['backward_ms'] for e in exposed)[len(exposed) // 2] if exposed else None
+    return {'backend': dist.get_backend() if is_distributed() else None,
+            'world_size': dist.get_world_size() if is_distributed() else 1,
+            'ms_per_step_by_rank': {'min': round(min(per_rank), 3), 'max': round(max(per_rank), 3),
+                                    'all': [round(v, 3) for v in per_rank]},
+            'exposed_allreduce_ms_rank0': None if med is None else round(med, 3),
+            'backward_ms_rank0': None if bwd is None else round(bwd, 3),
+            'probe_steps': len(exposed)}

@@ -308,3 +308,47 @@ def test_exact_dataparallel_matches_reference_dataparallel_world2():
     y = fx.batch()['y_change']
     mean_loss = sum(orc.power_jaccard_loss(z[i * per:(i + 1) * per], y[i * per:(i + 1) * per]) for i in range(world))
     assert abs(float(mean_loss) / world - float(fx.z['loss0'])) > 1e-7
+
+
+# ---- the bench line's multi-rank fields (bench.py `distributed`) ---------------------------------------------------
+def _worker_report(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    parallel.init_distributed('gloo')
+    net = parallel.wrap_ddp(_model(), device=None, bucket_cap_mb=1)
+    probe = parallel.ExposedAllreduceProbe(net.module, torch.device('cpu'))
+    b = _shard(rank)
+    exposed = []
+    for _ in range(3):
+        net.zero_grad(set_to_none=True)
+        loss = orc.power_jaccard_loss(net(b['x_t1'], b['x_t2']), b['y_change'])
+        probe.begin()
+        loss.backward()
+        exposed.append(probe.end())
+    n_marks = len(probe.marks)
+    probe.remove()
+    rep = parallel.distributed_report(10.0 + rank, exposed, None)
+    torch.save({'rep': rep, 'exposed': exposed, 'marks': n_marks,
+                'n_params': sum(1 for _ in net.module.parameters())}, os.path.join(out_dir, f'rank{rank}.pt'))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_bench_distributed_fields_world2():
+    """parallel.distributed_report / ExposedAllreduceProbe, as bench.py uses them under torchrun: the backend and
+    world size from the process group, every rank's ms per step gathered in rank order (min / max), and an exposed
+    all-reduce time between 0 and the backward's span, from one gradient stamp per parameter."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_report, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+    for r in res:
+        rep = r['rep']
+        assert rep['backend'] == 'gloo' and rep['world_size'] == world
+        assert rep['ms_per_step_by_rank'] == {'min': 10.0, 'max': 11.0, 'all': [10.0, 11.0]}
+        assert rep['probe_steps'] == 3
+        assert 0.0 <= rep['exposed_allreduce_ms_rank0'] <= rep['backward_ms_rank0']
+        assert r['marks'] == r['n_params']  # every parameter's gradient stamped once per backward
+        for e in r['exposed']:
+            assert 0.0 < e['last_grad_ms'] <= e['backward_ms']
