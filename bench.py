@@ -246,6 +246,8 @@ def main():
     ap.add_argument('--no-kernel-timing', action='store_true')
     ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16', 'h2'],
                     help='conv arithmetic (default: from the config, engine.conv_math_for: MODEL.PRECISION fp32 -> h2)')
+    ap.add_argument('--storage', default=None, choices=['fp32', 'bf16'],
+                    help='activation / gradient storage (default: engine.act_storage_for: bf16 for the bf16 arithmetic)')
     args = ap.parse_args()
 
     rank, local_rank, world = parallel.init_distributed()
@@ -256,7 +258,10 @@ def main():
     cfg = experiment_manager.load_cfg(args.config)
     if args.math:
         cfg.MODEL.CONV_MATH = args.math
+    if args.storage:
+        cfg.MODEL.ACT_STORAGE = args.storage
     math = engine.conv_math_for(cfg)  # create_network gives the model this arithmetic (hip.conv_scope per forward)
+    storage = 'bf16' if engine.act_storage_for(cfg, math) == torch.bfloat16 else 'fp32'  # activations in HBM
     dtype = {'bf16': 'bf16', 'h2': 'f32 (h2 split-fp16)', 'x3': 'f32 (x3 split-bf16)',
              'x5': 'f32 (x5 split-bf16, 5 products)', 'f32': 'f32'}[math]
     batch = args.batch or int(cfg.TRAINER.BATCH_SIZE)
@@ -314,7 +319,7 @@ def main():
         "data": "synthetic (on-device U[0,1) pairs, Bernoulli(0.05) change masks; random-init weights)",
         "config": {"workload": f"{args.config}: {cfg.MODEL.TYPE} TOPOLOGY {list(cfg.MODEL.TOPOLOGY)}, "
                                f"{cfg.MODEL.IN_CHANNELS}-ch SAR+optical, {size}x{size}, bs={batch}/GPU, "
-                               f"conv math {math}, train step incl. AdamW",
+                               f"conv math {math}, {storage} activation storage, train step incl. AdamW",
                    "global_batch": batch * world, "tile": size, "parallelism": f"dp{world}",
                    "topology": list(cfg.MODEL.TOPOLOGY)},
         "loss_first_last": [round(first_loss, 6), round(last_loss, 6)],

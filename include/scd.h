@@ -10,8 +10,15 @@
  *
  * Conventions
  *  - Every function returns int: 0 = ok, negative = error; scd_last_error() (thread-local) has text.
- *  - Activations are NHWC fp32.  An scd_nhwc_t is a *channel slice* view: element (n,y,x,c) lives at
- *    data[((n*h + y)*w + x)*ldc + c].  data must be 16-byte aligned, c and ldc multiples of 4.
+ *  - Activations are NHWC.  An scd_nhwc_t is a *channel slice* view: element (n,y,x,c) lives at
+ *    data[((n*h + y)*w + x)*ldc + c].  c and ldc are multiples of 4; data is 16-byte aligned (fp32) or 8-byte
+ *    aligned (bf16).
+ *  - Element type (ABI 6): a view is fp32 (dtype 0, the value of a zero-initialised view) or bf16 (the activation
+ *    and gradient storage of the bf16 configs).  A bf16 element is loaded exactly, every kernel computes in fp32,
+ *    and a bf16 result is rounded to nearest-even once, when it is stored.  The NHWC views of one call share one
+ *    type (scd_pack_nchw's NCHW fp32 source and the fp32 heads/losses aside); a bf16 conv view needs
+ *    SCD_MATH_BF16 and a shape the bf16 kernels take (the query functions report 0 / negative otherwise).
+ *    Statistics (BatchNorm records, weight-grad slabs, bounds) stay fp32.
  *  - The library never allocates, frees or synchronises.  Workspaces are caller-owned (torch caching
  *    allocator); size them with the *_workspace_bytes() queries.  All launches are asynchronous on the
  *    caller's stream (a hipStream_t passed as void*; NULL = legacy default stream).
@@ -39,10 +46,17 @@ enum scd_status {
     SCD_ERR_WORKSPACE = -5,   /* workspace too small                                    */
 };
 
+/* Element type of a view (scd_nhwc_t.dtype). */
+enum scd_dtype {
+    SCD_DT_F32 = 0,
+    SCD_DT_BF16 = 1
+};
+
 /* NHWC channel-slice view. */
 typedef struct scd_nhwc {
     void *data;
     int32_t n, h, w, c, ldc;
+    int32_t dtype; /* enum scd_dtype (ABI 6; fills the struct's former tail padding: size and offsets unchanged) */
 } scd_nhwc_t;
 
 /* ---------------------------------------------------------------------------------------------
@@ -126,8 +140,9 @@ enum scd_conv_math {
  *      (scd_set_conv_math, scd_set_halo16, scd_set_wgrad16) and every launch-time environment switch are gone.
  *   4: scd_pack_nchw takes a nullable `bound` (the input layer's h2 operand bound).
  *   5: scd_bn_relu_backward_coef takes `da_bound` / `dy_bound` (the h2 bound of the dy a weight grad forms itself);
- *      the 16-channel-source weight grad runs h2 when both scd_wgrad_t bounds are set. */
-#define SCD_ABI_VERSION 5
+ *      the 16-channel-source weight grad runs h2 when both scd_wgrad_t bounds are set.
+ *   6: scd_nhwc_t.dtype: bf16 activation / gradient storage (the bf16 configs), every NHWC kernel. */
+#define SCD_ABI_VERSION 6
 int scd_abi_version(void);
 /* The arithmetic scd_conv_igemm / scd_conv_wgrad will use for a descriptor (its `math`, or SCD_MATH_X3 / F32 where
  * the shape or the missing operand bounds keep the conv off the requested kernels); negative = invalid descriptor.

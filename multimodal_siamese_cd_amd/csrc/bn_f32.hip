@@ -49,12 +49,10 @@ static BnGeom bn_geom(const scd_nhwc_t &y, int nseg) {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ f4 ld4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
 __device__ __forceinline__ f4 fabs4(f4 v) { return f4{fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)}; }
 __device__ __forceinline__ f4 fmax4(f4 a, f4 b) {
     return f4{fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w)};
 }
-__device__ __forceinline__ void st4(float *p, f4 v) { *reinterpret_cast<f4 *>(p) = v; }
 // Keep a batch of loads in flight: an opaque use of the loaded registers right after issuing them stops
 // hipcc from sinking each load next to its consumer (which serialised the loop at vmcnt(0) per load).
 #define PIN4(a, b, c, d) asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d))
@@ -96,7 +94,8 @@ __device__ __forceinline__ Chunk chunk_of(int64_t pseg, int ncps, int chunk) {
 // ------------------------------------------------------------------------------------------------
 // forward statistics
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const float *__restrict__ y, int ldc, int C,
+template <class T>
+__global__ __launch_bounds__(BN_THREADS) void bn_stats_partial(const T *__restrict__ y, int ldc, int C,
                                                                int64_t pseg, int ncps, int chunk, int nrec, int qpb,
                                                                float *__restrict__ rec) {
     __shared__ Welford4 sh[BN_THREADS];
@@ -299,7 +298,8 @@ __device__ __forceinline__ f4 bn_relu4(f4 y, f4 sc, f4 sh) {
 }
 
 // grid: (chunks, segments); each thread walks quads of its segment's pixels.
-__global__ __launch_bounds__(256) void bn_relu_apply_kernel(const float *__restrict__ y, int ldy, float *__restrict__ a,
+template <class T>
+__global__ __launch_bounds__(256) void bn_relu_apply_kernel(const T *__restrict__ y, int ldy, T *__restrict__ a,
                                                             int lda, int C, int64_t pseg, const float *__restrict__ scale,
                                                             const float *__restrict__ shift) {
     const int seg = blockIdx.y;
@@ -320,19 +320,21 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(const float *__restr
 // relu_mask / bn_bwd_dy4: common.h (shared with the weight grad's fused dY staging)
 
 // Incoming gradient dL/da of the BatchNorm + ReLU backward, read at (pixel p, channel quad c).
+template <class T>
 struct DaPlain {  // a materialised tensor
-    const float *da;
+    const T *da;
     int ldda;
     __device__ __forceinline__ f4 operator()(int64_t p, int c) const { return ld4(da + p * ldda + c); }
 };
 // The encoder level's gradient, formed on the fly with the expressions of feature_grad_kernel (misc_f32.hip):
 // MaxPool2d backward of the next level's input gradient gy through the argmax bytes, plus -/+ the gradient of
 // the Siamese feature difference (skip_mode 1: t1 images subtract) or a plain skip gradient (skip_mode 0).
+template <class T>
 struct DaPooled {
-    const float *gy;  // (n, h/2, w/2, C) or null
+    const T *gy;  // (n, h/2, w/2, C) or null
     const uint8_t *idx;
     int hy, wy, ldgy;
-    const float *gs;  // (gsn, h, w, C) or null
+    const T *gs;  // (gsn, h, w, C) or null
     int gsn, ldgs, skip_mode;
     int hx, wx, C;
     FastDiv div_hw, div_w, div_gsn;
@@ -394,16 +396,18 @@ struct DaHead {
 // The DaPooled gradient over 2x2 cells: cell (img, cy, cx) covers the full-resolution pixels (2cy + i, 2cx + j) that
 // exist (ceil(h/2) x ceil(w/2) cells per image), so the pooled gradient and its argmax bytes are read and decoded once
 // per cell instead of once per pixel, with the cell's four pixels' loads in flight together.
+template <class T>
 struct PooledCells {
-    DaPooled da;
+    DaPooled<T> da;
     int ch, cw;                 // cells per image column / row
     FastDiv div_cimg, div_cw;   // ch * cw, cw
 };
 
 // dL/da of the four pixels of `cell` (flat cell index over images) at channel quad c; ok[k]: pixel k exists.
-__device__ __forceinline__ void cell_grads(const PooledCells &P, uint32_t cell, int c, f4 (&g)[4], int64_t (&pix)[4],
-                                           bool (&ok)[4], const float *fallback) {
-    const DaPooled &d = P.da;
+template <class T>
+__device__ __forceinline__ void cell_grads(const PooledCells<T> &P, uint32_t cell, int c, f4 (&g)[4], int64_t (&pix)[4],
+                                           bool (&ok)[4], const T *fallback) {
+    const DaPooled<T> &d = P.da;
     const uint32_t img = fdiv(cell, P.div_cimg);
     const uint32_t r = cell - img * uint32_t(P.ch * P.cw);
     const int cy = int(fdiv(r, P.div_cw)), cx = int(r) - cy * P.cw;
@@ -453,9 +457,10 @@ __device__ __forceinline__ int64_t cell_load_pix(const int64_t (&pix)[4], const 
 // cell_grads for a Siamese pair (skip_mode 1, two segments of gsn images): `cell` lies in a t1 image, its partner
 // cell (same place) in image img + gsn.  The difference gradient is read once for both (t1 subtracts it, t2 adds
 // it, with cell_grads' expressions: bit-identical).  pix[k] is the t1 pixel; its t2 partner is pix[k] + gsn*hx*wx.
-__device__ __forceinline__ void cell_grads_pair(const PooledCells &P, uint32_t cell, int c, f4 (&g0)[4], f4 (&g1)[4],
+template <class T>
+__device__ __forceinline__ void cell_grads_pair(const PooledCells<T> &P, uint32_t cell, int c, f4 (&g0)[4], f4 (&g1)[4],
                                                 int64_t (&pix)[4], bool (&ok)[4]) {
-    const DaPooled &d = P.da;
+    const DaPooled<T> &d = P.da;
     const uint32_t img = fdiv(cell, P.div_cimg);
     const uint32_t r = cell - img * uint32_t(P.ch * P.cw);
     const int cy = int(fdiv(r, P.div_cw)), cx = int(r) - cy * P.cw;
@@ -466,7 +471,7 @@ __device__ __forceinline__ void cell_grads_pair(const PooledCells &P, uint32_t c
     const int64_t q0 = has_gy ? (int64_t(img) * d.hy + min(cy, d.hy - 1)) * d.wy + min(cx, d.wy - 1) : 0;
     const int64_t q1 = has_gy ? q0 + int64_t(d.gsn) * d.hy * d.wy : 0;
     const uint8_t *ib = has_gy ? d.idx : reinterpret_cast<const uint8_t *>(d.gs);
-    const float *gb = has_gy ? d.gy : d.gs;
+    const T *gb = has_gy ? d.gy : d.gs;
     uint32_t pk0 = *reinterpret_cast<const uint32_t *>(ib + q0 * d.C + c);
     uint32_t pk1 = *reinterpret_cast<const uint32_t *>(ib + q1 * d.C + c);
     f4 gp0 = ld4(gb + q0 * d.ldgy + c), gp1 = ld4(gb + q1 * d.ldgy + c);
@@ -536,8 +541,9 @@ __device__ __forceinline__ void pooled_rec2(f4 (&sh1)[BN_THREADS], f4 (&sh2)[BN_
 
 // bn_bwd_pooled_partial for a Siamese pair: block k covers chunk k of the t1 segment and chunk k of the t2 segment
 // (same cells), reading the shared difference gradient once; same per-chunk records, bit-identical.
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial_pair(const float *__restrict__ y, int ldy,
-                                                                         PooledCells P, int C, int64_t cseg, int ncps,
+template <class T>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial_pair(const T *__restrict__ y, int ldy,
+                                                                         PooledCells<T> P, int C, int64_t cseg, int ncps,
                                                                          int chunk, int nrec, int qpb,
                                                                          const float *smean, const float *sinv,
                                                                          const float *scale, const float *shift,
@@ -580,7 +586,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial_pair(const f
 }
 
 // bn_bwd_partial over cells: rec[c][chunk][2] = {sum dz, sum dz*xhat} of the chunk's cells' pixels.
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const float *__restrict__ y, int ldy, PooledCells P,
+template <class T>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const T *__restrict__ y, int ldy, PooledCells<T> P,
                                                                     int C, int64_t cseg, int ncps, int chunk, int nrec,
                                                                     int qpb, const float *smean, const float *sinv,
                                                                     const float *scale, const float *shift,
@@ -634,8 +641,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const float 
 }
 
 // bn_bwd_apply over cells (see bn_bwd_pooled_partial); brec[c][chunk] (conv bias grad) and dy_bound optional.
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const float *__restrict__ y, int ldy, PooledCells P,
-                                                                  float *__restrict__ dy, int lddy, int C, int64_t cseg,
+template <class T>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const T *__restrict__ y, int ldy, PooledCells<T> P,
+                                                                  T *__restrict__ dy, int lddy, int C, int64_t cseg,
                                                                   int ncps, int chunk, int nrec, int qpb,
                                                                   const float *smean, const float *sinv,
                                                                   const float *gamma, const float *scale,
@@ -667,7 +675,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const float *_
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (ok[k]) {
-                    const f4 ov = bn_bwd_dy4(yv[k], g[k], mu, iv, sc, sf, k1, k2, mul);
+                    const f4 ov = stored4(dy, bn_bwd_dy4(yv[k], g[k], mu, iv, sc, sf, k1, k2, mul));
                     st4(dy + pix[k] * lddy + c, ov);
                     acc += ov;
                     amax = fmax4(amax, fabs4(ov));
@@ -692,8 +700,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const float *_
 
 // bn_bwd_pooled_apply for a Siamese pair (see bn_bwd_pooled_partial_pair): both segments' dy per cell, the conv-bias
 // records of chunk k of each segment, bit-identical.
+template <class T>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply_pair(
-    const float *__restrict__ y, int ldy, PooledCells P, float *__restrict__ dy, int lddy, int C, int64_t cseg, int ncps,
+    const T *__restrict__ y, int ldy, PooledCells<T> P, T *__restrict__ dy, int lddy, int C, int64_t cseg, int ncps,
     int chunk, int nrec, int qpb, const float *smean, const float *sinv, const float *gamma, const float *scale,
     const float *shift, const float *coef, float *__restrict__ brec, float *dy_bound) {
     __shared__ f4 sh[BN_THREADS];
@@ -726,8 +735,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply_pair(
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (ok[k]) {
-                    const f4 o0 = bn_bwd_dy4(y0[k], g0[k], mu0, iv0, sc0, sf0, k10, k20, mul0);
-                    const f4 o1 = bn_bwd_dy4(y1[k], g1[k], mu1, iv1, sc1, sf1, k11, k21, mul1);
+                    const f4 o0 = stored4(dy, bn_bwd_dy4(y0[k], g0[k], mu0, iv0, sc0, sf0, k10, k20, mul0));
+                    const f4 o1 = stored4(dy, bn_bwd_dy4(y1[k], g1[k], mu1, iv1, sc1, sf1, k11, k21, mul1));
                     st4(dy + pix[k] * lddy + c, o0);
                     st4(dy + (pix[k] + poff) * lddy + c, o1);
                     acc0 += o0;
@@ -757,8 +766,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply_pair(
 }
 
 // per (chunk) record {sum dz, sum dz*xhat}, rec[c][chunk][2]
-template <class DA>
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const float *__restrict__ y, int ldy, DA da, int C,
+template <class T, class DA>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const T *__restrict__ y, int ldy, DA da, int C,
                                                              int64_t pseg, int ncps, int chunk, int nrec, int qpb,
                                                              const float *smean, const float *sinv, const float *scale,
                                                              const float *shift, float *__restrict__ rec) {
@@ -898,9 +907,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize(const float *__res
 }
 
 // dy = gamma*invstd*(dz - k1 - xhat*k2); optional per-chunk sums of dy (conv bias grad), brec[c][chunk]
-template <class DA>
-__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restrict__ y, int ldy, DA da,
-                                                           float *__restrict__ dy, int lddy, int C, int64_t pseg,
+template <class T, class DA>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const T *__restrict__ y, int ldy, DA da,
+                                                           T *__restrict__ dy, int lddy, int C, int64_t pseg,
                                                            int ncps, int chunk, int nrec, int qpb, const float *smean,
                                                            const float *sinv, const float *gamma, const float *scale,
                                                            const float *shift, const float *coef,
@@ -928,10 +937,10 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
             f4 g2 = da(p + 2 * npl, c), g3 = da(p + 3 * npl, c);
             PIN4(y0, y1, y2, y3);
             PIN4(g0, g1, g2, g3);
-            const f4 o0 = bn_bwd_dy4(y0, g0, mu, iv, sc, sf, k1, k2, mul);
-            const f4 o1 = bn_bwd_dy4(y1, g1, mu, iv, sc, sf, k1, k2, mul);
-            const f4 o2 = bn_bwd_dy4(y2, g2, mu, iv, sc, sf, k1, k2, mul);
-            const f4 o3 = bn_bwd_dy4(y3, g3, mu, iv, sc, sf, k1, k2, mul);
+            const f4 o0 = stored4(dy, bn_bwd_dy4(y0, g0, mu, iv, sc, sf, k1, k2, mul));
+            const f4 o1 = stored4(dy, bn_bwd_dy4(y1, g1, mu, iv, sc, sf, k1, k2, mul));
+            const f4 o2 = stored4(dy, bn_bwd_dy4(y2, g2, mu, iv, sc, sf, k1, k2, mul));
+            const f4 o3 = stored4(dy, bn_bwd_dy4(y3, g3, mu, iv, sc, sf, k1, k2, mul));
             st4(dy + p * lddy + c, o0);
             st4(dy + (p + npl) * lddy + c, o1);
             st4(dy + (p + 2 * npl) * lddy + c, o2);
@@ -941,7 +950,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const float *__restri
         }
         for (; p < ch.end; p += npl) {
             const f4 y0 = ld4(y + p * ldy + c);
-            const f4 o0 = bn_bwd_dy4(y0, da(p, c), mu, iv, sc, sf, k1, k2, mul);
+            const f4 o0 = stored4(dy, bn_bwd_dy4(y0, da(p, c), mu, iv, sc, sf, k1, k2, mul));
             st4(dy + p * lddy + c, o0);
             acc += o0;
             if (dy_bound) amax = fmax4(amax, fabs4(o0));
@@ -984,7 +993,8 @@ __global__ __launch_bounds__(BN_THREADS) void sum_records(const float *__restric
 //   v = x, or (scale given) relu(fma(x, scale[seg][c], shift[seg][c])) -- the head's input read through the last
 //   BatchNorm + ReLU with bn_relu_apply_kernel's expression (pseg pixels per segment).
 // Four pixels' loads in flight per thread on both paths.
-__global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const float *__restrict__ x, int ldx, int C,
+template <class T>
+__global__ __launch_bounds__(BN_THREADS) void chan_sum_partial(const T *__restrict__ x, int ldx, int C,
                                                                int64_t npix, int chunk, int nrec, int qpb,
                                                                const float *__restrict__ wgt, int hw, int n_out,
                                                                int o, const float *__restrict__ scale,
@@ -1083,9 +1093,10 @@ int weighted_channel_sum(const scd_nhwc_t &x, const float *wgt, int n_out, int o
         return SCD_ERR_ARG;
     }
     float *rec = static_cast<float *>(ws);
-    hipLaunchKernelGGL(chan_sum_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(x.data), x.ldc, x.c, pixels(x), g.chunk, g.nrec, g.qpb, wgt, x.h * x.w, n_out,
-                       o, scale, shift, pixels(x) / nseg, rec);
+    SCD_WITH_T(x.dtype, T,
+               hipLaunchKernelGGL(chan_sum_partial<T>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                                  view_ptr<const T>(x), x.ldc, x.c, pixels(x), g.chunk, g.nrec, g.qpb, wgt, x.h * x.w,
+                                  n_out, o, scale, shift, pixels(x) / nseg, rec));
     hipLaunchKernelGGL(sum_records, dim3(x.c), dim3(BN_THREADS), 0, s, rec, g.nrec, out);
     return SCD_OK;
 }
@@ -1121,8 +1132,9 @@ extern "C" int scd_bn_train_stats(scd_nhwc_t y, int32_t nseg, const float *gamma
     const BnGeom g = bn_geom(y, nseg);
     hipStream_t s = as_stream(stream);
     float *rec = static_cast<float *>(ws);
-    hipLaunchKernelGGL(bn_stats_partial, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, rec);
+    SCD_WITH_T(y.dtype, T,
+               hipLaunchKernelGGL(bn_stats_partial<T>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                                  view_ptr<const T>(y), y.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, rec));
     hipLaunchKernelGGL(bn_stats_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, gamma,
                        beta, eps, momentum, update_running, running_mean, running_var, save_mean, save_invstd, scale,
                        shift, act_bound);
@@ -1192,19 +1204,21 @@ extern "C" int scd_bn_relu_apply(scd_nhwc_t y, int32_t nseg, const float *scale,
         set_error("bn_relu_apply: shape mismatch");
         return SCD_ERR_ARG;
     }
+    const int dt = common_dtype("bn_relu_apply", {&y, &a});
+    if (dt < 0) return SCD_ERR_ARG;
     const int64_t pseg = pixels(y) / nseg;
     const int64_t total = pseg * (y.c / 4);
     int blocks = int((total + 255) / 256);
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(blocks, nseg), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(y.data), y.ldc, static_cast<float *>(a.data), a.ldc, y.c, pseg,
-                       scale, shift);
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL(bn_relu_apply_kernel<T>, dim3(blocks, nseg), dim3(256), 0, as_stream(stream),
+                                  view_ptr<const T>(y), y.ldc, view_ptr<T>(a), a.ldc, y.c, pseg, scale, shift));
     return launch_status("scd_bn_relu_apply");
 }
 
 namespace scd {
 // partial -> finalize -> apply (+ conv-bias sums) over a gradient source DA
-template <class DA>
+template <class T, class DA>
 static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *save_mean, const float *save_invstd,
                             const float *gamma, const float *scale, const float *shift, float *dgamma, float *dbeta,
                             float *dbias_prev, const scd_nhwc_t &dy, float *dy_bound, void *ws, hipStream_t s) {
@@ -1212,13 +1226,13 @@ static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *s
     float *rec = static_cast<float *>(ws);
     float *brec = rec + size_t(g.nrec) * y.c * 2;
     float *coef = brec + size_t(g.nrec) * y.c;
-    hipLaunchKernelGGL(bn_bwd_partial<DA>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, da, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb,
+    hipLaunchKernelGGL((bn_bwd_partial<T, DA>), dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       view_ptr<const T>(y), y.ldc, da, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb,
                        save_mean, save_invstd, scale, shift, rec);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
                        coef, dgamma, dbeta);
-    hipLaunchKernelGGL(bn_bwd_apply<DA>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, da, static_cast<float *>(dy.data), dy.ldc, y.c,
+    hipLaunchKernelGGL((bn_bwd_apply<T, DA>), dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       view_ptr<const T>(y), y.ldc, da, view_ptr<T>(dy), dy.ldc, y.c,
                        g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
                        dbias_prev ? brec : nullptr, dy_bound);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
@@ -1232,17 +1246,18 @@ static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *s
 #ifndef SCD_BN_POOLED_PAIR
 #define SCD_BN_POOLED_PAIR 1
 #endif
-static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled &da, int nseg, const float *save_mean,
+template <class T>
+static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled<T> &da, int nseg, const float *save_mean,
                                    const float *save_invstd, const float *gamma, const float *scale, const float *shift,
                                    float *dgamma, float *dbeta, float *dbias_prev, const scd_nhwc_t &dy,
                                    float *dy_bound, void *ws, hipStream_t s) {
     if (!SCD_BN_POOLED_CELLS) {
-        bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy,
-                        dy_bound, ws, s);
+        bn_backward_run<T>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy,
+                           dy_bound, ws, s);
         return;
     }
     const BnGeom g = bn_geom(y, nseg);
-    PooledCells P;
+    PooledCells<T> P;
     P.da = da;
     P.ch = (y.h + 1) / 2;
     P.cw = (y.w + 1) / 2;
@@ -1258,25 +1273,25 @@ static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled &da, int 
     // Siamese pairs (-DSCD_BN_POOLED_PAIR=0: one image per cell walk): the t1 and t2 cells at one place in one block,
     // the shared difference gradient read once instead of once per branch
     if (SCD_BN_POOLED_PAIR && nseg == 2 && da.gs && da.skip_mode == 1 && 2 * da.gsn == y.n) {
-        hipLaunchKernelGGL(bn_bwd_pooled_partial_pair, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
-                           static_cast<const float *>(y.data), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
+        hipLaunchKernelGGL(bn_bwd_pooled_partial_pair<T>, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
+                           view_ptr<const T>(y), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
                            save_invstd, scale, shift, rec);
         hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, ncps, nrec, g.pseg,
                            coef, dgamma, dbeta);
-        hipLaunchKernelGGL(bn_bwd_pooled_apply_pair, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
-                           static_cast<const float *>(y.data), y.ldc, P, static_cast<float *>(dy.data), dy.ldc, y.c,
+        hipLaunchKernelGGL(bn_bwd_pooled_apply_pair<T>, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
+                           view_ptr<const T>(y), y.ldc, P, view_ptr<T>(dy), dy.ldc, y.c,
                            cseg, ncps, chunk, nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
                            dbias_prev ? brec : nullptr, dy_bound);
         if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, nrec, dbias_prev);
         return;
     }
-    hipLaunchKernelGGL(bn_bwd_pooled_partial, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
+    hipLaunchKernelGGL(bn_bwd_pooled_partial<T>, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       view_ptr<const T>(y), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
                        save_invstd, scale, shift, rec);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, ncps, nrec, g.pseg, coef,
                        dgamma, dbeta);
-    hipLaunchKernelGGL(bn_bwd_pooled_apply, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, P, static_cast<float *>(dy.data), dy.ldc, y.c, cseg,
+    hipLaunchKernelGGL(bn_bwd_pooled_apply<T>, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       view_ptr<const T>(y), y.ldc, P, view_ptr<T>(dy), dy.ldc, y.c, cseg,
                        ncps, chunk, nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
                        dbias_prev ? brec : nullptr, dy_bound);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, nrec, dbias_prev);
@@ -1300,8 +1315,11 @@ extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, c
         set_error("bn_relu_backward: workspace too small");
         return SCD_ERR_WORKSPACE;
     }
-    bn_backward_run(y, DaPlain{static_cast<const float *>(da.data), da.ldc}, nseg, save_mean, save_invstd, gamma, scale,
-                    shift, dgamma, dbeta, dbias_prev, dy, dy_bound, ws, as_stream(stream));
+    const int dt = common_dtype("bn_relu_backward", {&y, &da, &dy});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               bn_backward_run<T>(y, DaPlain<T>{view_ptr<const T>(da), da.ldc}, nseg, save_mean, save_invstd, gamma,
+                                  scale, shift, dgamma, dbeta, dbias_prev, dy, dy_bound, ws, as_stream(stream)));
     return launch_status("scd_bn_relu_backward");
 }
 
@@ -1323,8 +1341,11 @@ extern "C" int scd_bn_relu_backward_head(scd_nhwc_t y, const float *gout, const 
         return SCD_ERR_WORKSPACE;
     }
     const DaHead da{gout, w_head, n_out, y.c, y.h * y.w, make_fastdiv(uint32_t(y.h * y.w))};
-    bn_backward_run(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy, dy_bound,
-                    ws, as_stream(stream));
+    const int dt = common_dtype("bn_relu_backward_head", {&y, &dy});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               bn_backward_run<T>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev,
+                                  dy, dy_bound, ws, as_stream(stream)));
     return launch_status("scd_bn_relu_backward_head");
 }
 
@@ -1357,24 +1378,28 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
         set_error("bn_relu_backward_pooled: workspace too small");
         return SCD_ERR_WORKSPACE;
     }
-    DaPooled da;
-    da.gy = static_cast<const float *>(gy.data);
-    da.idx = idx;
-    da.hy = gy.h;
-    da.wy = gy.w;
-    da.ldgy = gy.ldc;
-    da.gs = static_cast<const float *>(gskip.data);
-    da.gsn = gskip.n > 0 ? gskip.n : 1;
-    da.ldgs = gskip.ldc;
-    da.skip_mode = skip_mode;
-    da.hx = y.h;
-    da.wx = y.w;
-    da.C = y.c;
-    da.div_hw = make_fastdiv(uint32_t(y.h * y.w));
-    da.div_w = make_fastdiv(uint32_t(y.w));
-    da.div_gsn = make_fastdiv(uint32_t(da.gsn));
-    bn_backward_run_pooled(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev, dy,
-                           dy_bound, ws, as_stream(stream));
+    const int dt = common_dtype("bn_relu_backward_pooled", {&y, &gy, &gskip, &dy});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T, {
+        DaPooled<T> da;
+        da.gy = view_ptr<const T>(gy);
+        da.idx = idx;
+        da.hy = gy.h;
+        da.wy = gy.w;
+        da.ldgy = gy.ldc;
+        da.gs = view_ptr<const T>(gskip);
+        da.gsn = gskip.n > 0 ? gskip.n : 1;
+        da.ldgs = gskip.ldc;
+        da.skip_mode = skip_mode;
+        da.hx = y.h;
+        da.wx = y.w;
+        da.C = y.c;
+        da.div_hw = make_fastdiv(uint32_t(y.h * y.w));
+        da.div_w = make_fastdiv(uint32_t(y.w));
+        da.div_gsn = make_fastdiv(uint32_t(da.gsn));
+        bn_backward_run_pooled<T>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev,
+                                  dy, dy_bound, ws, as_stream(stream));
+    });
     return launch_status("scd_bn_relu_backward_pooled");
 }
 
@@ -1404,10 +1429,13 @@ extern "C" int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t n
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, tile_rec, y.c, nseg, ntiles / nseg, ntiles,
                        g.pseg, coef, dgamma, dbeta);
-    hipLaunchKernelGGL(bn_bwd_apply<DaPlain>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       static_cast<const float *>(y.data), y.ldc, DaPlain{static_cast<const float *>(da.data), da.ldc},
-                       static_cast<float *>(dy.data), dy.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean,
-                       save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr, dy_bound);
+    const int dt = common_dtype("bn_relu_backward_tiles", {&y, &da, &dy});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL((bn_bwd_apply<T, DaPlain<T>>), dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                                  view_ptr<const T>(y), y.ldc, DaPlain<T>{view_ptr<const T>(da), da.ldc},
+                                  view_ptr<T>(dy), dy.ldc, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean,
+                                  save_invstd, gamma, scale, shift, coef, dbias_prev ? brec : nullptr, dy_bound));
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
     return launch_status("scd_bn_relu_backward_tiles");
 }
@@ -1439,10 +1467,13 @@ extern "C" int scd_bn_relu_backward_coef(scd_nhwc_t y, scd_nhwc_t da, int32_t ns
                            dy_bound);
     } else {
         float *rec = static_cast<float *>(ws);
-        hipLaunchKernelGGL(bn_bwd_partial<DaPlain>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                           static_cast<const float *>(y.data), y.ldc,
-                           DaPlain{static_cast<const float *>(da.data), da.ldc}, y.c, g.pseg, g.ncps, g.chunk, g.nrec,
-                           g.qpb, save_mean, save_invstd, scale, shift, rec);
+        const int dt = common_dtype("bn_relu_backward_coef", {&y, &da});
+        if (dt < 0) return SCD_ERR_ARG;
+        SCD_WITH_T(dt, T,
+                   hipLaunchKernelGGL((bn_bwd_partial<T, DaPlain<T>>), dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                                      view_ptr<const T>(y), y.ldc, DaPlain<T>{view_ptr<const T>(da), da.ldc}, y.c,
+                                      g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean, save_invstd, scale, shift,
+                                      rec));
         hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
                            coef, dgamma, dbeta, gamma, save_invstd, dbias_prev, save_mean, da_bound, dy_bound);
     }
@@ -1484,8 +1515,8 @@ extern "C" int scd_absmax_bound(scd_nhwc_t x, int32_t nseg, const float *scale, 
                                 scd_stream_t stream) {
     clear_error();
     SCD_TRY(bn_check(x, nseg));
-    if (!bound || (!scale) != (!shift) || (scale && (!aligned16(scale) || !aligned16(shift)))) {
-        set_error("absmax_bound: null bound or unpaired / unaligned coefficients");
+    if (!bound || (!scale) != (!shift) || (scale && (!aligned16(scale) || !aligned16(shift))) || is_bf16(x)) {
+        set_error("absmax_bound: null bound, unpaired / unaligned coefficients or a bf16 view (h2 bounds are fp32-only)");
         return SCD_ERR_ARG;
     }
     const int64_t pseg = pixels(x) / nseg;

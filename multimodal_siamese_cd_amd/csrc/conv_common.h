@@ -80,6 +80,7 @@ struct IgemmArgs {
     float *dst_bound;  // optional: raised to max |stored output| (x3 / halo16 / gather16 kernels; scd_igemm_t.dst_bound)
     int math;          // SCD_MATH_* of this launch (scd_igemm_t.math)
     uint32_t tune;     // SCD_TUNE_* bits (scd_igemm_t.tune)
+    int sb;            // 1: src, dst and bb_y are bf16 views (ABI 6); the pointers above then address bf16 elements
 };
 
 struct WgradArgs {
@@ -107,6 +108,7 @@ struct WgradArgs {
     int rows_seg_imgs;
     int math;       // SCD_MATH_* of this launch (scd_wgrad_t.math)
     uint32_t tune;  // SCD_TUNE_* bits (scd_wgrad_t.tune)
+    int sb;         // 1: rows, src and rows_y are bf16 views (ABI 6)
 };
 
 // Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels
@@ -148,6 +150,9 @@ bool wgrad_x3_h2_tile(int tile_id);
 void launch_wgrad_x3_h2(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
 // bf16 variants of the generic weight grad (the ConvTranspose weight grad under SCD_MATH_BF16), conv_x3.hip.
 void launch_wgrad_x3_bf16(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s);
+// bf16 storage (a.sb): the kernels that take bf16 views are the bf16-arithmetic instances of the halo16, c16, gather16
+// and generic (ConvTranspose) weight-grad kernels.
+inline int elem_size(int sb) { return sb ? 2 : 4; }
 // Conv arithmetic of a launch (scd_igemm_t.math / scd_wgrad_t.math; enum scd_conv_math in scd.h).
 inline bool math_valid(int m) { return m >= SCD_MATH_F32 && m <= SCD_MATH_H2; }
 inline int math_split(int m) { return m != SCD_MATH_F32; }  // split-weight (x3, x5, bf16 or h2) pipeline

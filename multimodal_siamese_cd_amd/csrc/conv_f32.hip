@@ -546,6 +546,14 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     SCD_TRY(check_view(d->src, "igemm.src"));
     SCD_TRY(check_view(d->dst, "igemm.dst"));
     SCD_TRY(check_taps(d->ntaps, d->dy, d->dx));
+    const int dt = common_dtype("igemm", {&d->src, &d->dst, d->bn_bwd ? &d->bn_bwd->y : nullptr});
+    if (dt < 0) return SCD_ERR_ARG;
+    if (dt == SCD_DT_BF16 && d->math != SCD_MATH_BF16) {
+        set_error("igemm: bf16 views need math SCD_MATH_BF16 (got %d)", d->math);
+        return SCD_ERR_ARG;
+    }
+    a.sb = dt == SCD_DT_BF16 ? 1 : 0;
+    const int eb = elem_size(a.sb);
     if (d->src.c % 8) {
         set_error("igemm: src.c=%d must be a multiple of 8 (pad channels)", d->src.c);
         return SCD_ERR_ARG;
@@ -623,9 +631,9 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     if (const scd_bn_bwd_tiles_t *b = d->bn_bwd) {
         if (!b->y.data || !b->rec || !b->save_mean || !b->save_invstd || !b->scale || !b->shift || b->nseg < 1 ||
             b->y.n != d->dst.n || b->y.h != d->dst.h || b->y.w != d->dst.w || b->y.c != d->n_out ||
-            d->dst.n % b->nseg || b->y.ldc % 4 || (reinterpret_cast<uintptr_t>(b->y.data) & 15) ||
+            d->dst.n % b->nseg || b->y.ldc % 4 || (reinterpret_cast<uintptr_t>(b->y.data) & (a.sb ? 7 : 15)) ||
             !aligned16(b->save_mean) || !aligned16(b->save_invstd) || !aligned16(b->scale) || !aligned16(b->shift)) {
-            set_error("igemm: bn_bwd needs y shaped like dst (c = n_out, 16-byte aligned, ldc %% 4 == 0), all "
+            set_error("igemm: bn_bwd needs y shaped like dst (c = n_out, aligned, ldc %% 4 == 0), all "
                       "coefficient arrays 16-byte aligned and nseg | n");
             return SCD_ERR_ARG;
         }
@@ -639,7 +647,7 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
         a.bb_rec = b->rec;
     }
     {
-        const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * 4 + int64_t(d->src.c) * 4;
+        const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * eb + int64_t(d->src.c) * eb;
         a.src_bytes = sb < (int64_t(1) << 31) ? uint32_t(sb) : 0u;
     }
     a.src_bound = d->src_bound;
@@ -660,7 +668,7 @@ namespace scd {
 // launches over image ranges.  A chunk keeps whole BatchNorm coefficient segments or divides one, so the
 // per-segment coefficient pointers are offset instead of the kernels learning an image base; fused
 // statistics / BN-backward records are per image tile, so their pointers advance by whole images.
-static int64_t img_bytes(const scd_nhwc_t &v) { return int64_t(v.h) * v.w * v.ldc * 4; }
+static int64_t img_bytes(const scd_nhwc_t &v) { return int64_t(v.h) * v.w * v.ldc * elem_bytes(v); }
 static int image_chunk(int64_t bytes_per_img, int n, int seg) {
     const int64_t lim = ((int64_t(1) << 31) - 1) / std::max<int64_t>(bytes_per_img, 1);
     if (lim >= n) return n;
@@ -769,6 +777,10 @@ extern "C" int scd_igemm_arith(const scd_igemm_t *d) {
     if (igemm_takes_halo16(a)) return a.math;  // under SCD_MATH_H2 only bounded h2-split convs take it
     if (igemm_takes_gather16(a)) return a.math;  // h2 (bounded, h2 split) or bf16
     if (igemm_takes_c16(a)) return a.math;  // under SCD_MATH_H2 only bounded h2-split input layers take it
+    if (a.sb) {
+        set_error("igemm: no bf16-storage kernel takes this shape");
+        return SCD_ERR_ARG;
+    }
     return a.c % 16 == 0 ? SCD_MATH_X3 : SCD_MATH_F32;  // launch_igemm_x3's eligibility
 }
 
@@ -829,6 +841,11 @@ static int conv_igemm_run(const scd_igemm_t *d, hipStream_t s, int bb_ntiles_tot
         return SCD_ERR_ARG;
     }
     if (math_split(a.math) && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");
+    if (a.sb) {
+        set_error("igemm: bf16 views need the bf16 halo16 / c16 / gather16 kernels; this shape takes none "
+                  "(check scd_igemm_arith)");
+        return SCD_ERR_ARG;
+    }
     if (a.dst_bound) {
         set_error("igemm: dst_bound needs the split-bf16 kernels (math x3 / h2 and src.c %% 16 == 0)");
         return SCD_ERR_ARG;
@@ -888,8 +905,15 @@ static int wgrad_validate(const scd_wgrad_t *d) {
         set_error("wgrad: problem too large for 32-bit pixel indexing");
         return SCD_ERR_ARG;
     }
+    const int dt = common_dtype("wgrad", {&d->rows, &d->src, d->rows_y.data ? &d->rows_y : nullptr});
+    if (dt < 0) return SCD_ERR_ARG;
+    if (dt == SCD_DT_BF16 && d->math != SCD_MATH_BF16) {
+        set_error("wgrad: bf16 views need math SCD_MATH_BF16 (got %d)", d->math);
+        return SCD_ERR_ARG;
+    }
     return SCD_OK;
 }
+static bool wgrad_sb(const scd_wgrad_t *d) { return is_bf16(d->rows); }
 // Workgroups of one wgrad instantiation that the whole chip holds at once (occupancy API x CUs), cached.
 static int wgrad_resident_blocks(const WgradTile &t, int math) {
     const int x3 = math_split(math);
@@ -1047,6 +1071,10 @@ extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
     clear_error();
     SCD_TRY(wgrad_validate(d));
     if (!math_split(d->math)) return SCD_MATH_F32;
+    if (wgrad_sb(d) && !wgrad_halo_ok(d) && !wgrad_c16_ok(d) && !wgrad_generic_bf16(d)) {
+        set_error("wgrad: no bf16-storage kernel takes this shape");
+        return SCD_ERR_ARG;
+    }
     if (wgrad_halo_ok(d)) return d->math == SCD_MATH_H2 && !wgrad_bounded(d) ? SCD_MATH_X3 : d->math;
     if (wgrad_c16_ok(d))
         return d->math != SCD_MATH_H2 ? d->math
@@ -1160,6 +1188,13 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
         return SCD_ERR_WORKSPACE;
     }
     WgradArgs a;
+    a.sb = wgrad_sb(d) ? 1 : 0;
+    const int eb = elem_size(a.sb);
+    if (a.sb && !wgrad_halo_ok(d) && !wgrad_c16_ok(d) && !wgrad_generic_bf16(d)) {
+        set_error("wgrad: bf16 views need the bf16 halo16 / c16 / ConvTranspose weight-grad kernels; this shape takes "
+                  "none (check scd_wgrad_arith)");
+        return SCD_ERR_ARG;
+    }
     a.rows = static_cast<const float *>(d->rows.data);
     a.ho = d->rows.h;
     a.wo = d->rows.w;
@@ -1182,8 +1217,8 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     a.div_w = make_fastdiv(uint32_t(d->rows.w));
     a.div_c = make_fastdiv(uint32_t(d->src.c));
     // byte extents for the x3 kernel's buffer loads (32-bit offsets)
-    const int64_t rb = (pixels(d->rows) - 1) * d->rows.ldc * 4 + int64_t(d->rows.c) * 4;
-    const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * 4 + int64_t(d->src.c) * 4;
+    const int64_t rb = (pixels(d->rows) - 1) * d->rows.ldc * eb + int64_t(d->rows.c) * eb;
+    const int64_t sb = (pixels(d->src) - 1) * d->src.ldc * eb + int64_t(d->src.c) * eb;
     if (rb >= (int64_t(1) << 31) || sb >= (int64_t(1) << 31)) {
         set_error("wgrad: operands above 2 GiB are not supported (32-bit buffer offsets)");
         return SCD_ERR_ARG;
@@ -1204,7 +1239,7 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     a.rows_seg_imgs = d->rows.n;
     if (d->rows_y.data) {
         const scd_nhwc_t &y = d->rows_y;
-        const int64_t yb = (pixels(y) - 1) * y.ldc * 4 + int64_t(y.c) * 4;
+        const int64_t yb = (pixels(y) - 1) * y.ldc * eb + int64_t(y.c) * eb;
         if (check_view(y, "wgrad.rows_y") != SCD_OK || y.n != d->rows.n || y.h != d->rows.h || y.w != d->rows.w ||
             y.c != d->rows.c || y.ldc % 4 || d->rows_nseg < 1 || d->rows.n % d->rows_nseg || !d->rows_mean ||
             !d->rows_invstd || !d->rows_scale || !d->rows_shift || !d->rows_coef || !aligned16(d->rows_mean) ||

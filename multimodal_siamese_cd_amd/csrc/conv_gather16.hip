@@ -21,9 +21,12 @@
 
 namespace scd {
 
-template <int WM, int WN, int TM, int TN, int SK, int OCC, int NP>
+// SB: bf16 storage of src and dst (bf16 arithmetic only).
+template <int WM, int WN, int TM, int TN, int SK, int OCC, int NP, bool SB = false>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a) {
     static_assert(NP == 1 || NP == 4, "bf16 or h2");
+    static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
+    using ST = typename std::conditional<SB, bf16_t, float>::type;
     constexpr bool H2 = NP == 4;
     constexpr int XP = H2 ? 2 : 1;  // activation planes (LDS) = weight planes (registers)
     constexpr int NT = 64 * WM * WN;
@@ -55,7 +58,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
 
     // this thread's pieces: pixel rows (tid >> 3) + i * NT / 8, channel piece tid & 7 of every k-step
     const int col = tid & 7;
-    const float *a_base[A_PER];
+    const ST *a_base[A_PER];
     int a_sy[A_PER], a_sx[A_PER], a_off[A_PER];
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
@@ -69,7 +72,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
         const uint32_t ox = r - oy * uint32_t(a.wo);
         a_sy[i] = ok ? int(oy) * a.stride : -(1 << 20);
         a_sx[i] = int(ox) * a.stride;
-        a_base[i] = a.src + (size_t(int(img) * a.hs + (ok ? a_sy[i] : 0)) * a.ws + a_sx[i]) * a.ldc_s + col * 4;
+        a_base[i] = reinterpret_cast<const ST *>(a.src) + (size_t(int(img) * a.hs + (ok ? a_sy[i] : 0)) * a.ws + a_sx[i]) * a.ldc_s +
+                    col * 4;
         a_off[i] = soff(row, col);
     }
     const int KS16 = a.K / 16, NB32 = (a.n_out + 31) / 32;
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
 
     const int cpk = a.c / 32;
     const int nk = a.ntaps * cpk;  // k-steps (a multiple of SK: gather16_pick)
-    f32x4 ra[SK][A_PER];
+    StageT<SB> ra[SK][A_PER];
     auto load_stage = [&](int st) {
 #pragma unroll
         for (int s = 0; s < SK; ++s) {
@@ -97,7 +101,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
 #pragma unroll
             for (int i = 0; i < A_PER; ++i) {
                 const bool v = unsigned(a_sy[i] + dyt) < unsigned(a.hs) && unsigned(a_sx[i] + dxt) < unsigned(a.ws);
-                ra[s][i] = v ? gload4(a_base[i] + toff) : f32x4{0.f, 0.f, 0.f, 0.f};
+                if constexpr (SB)
+                    ra[s][i] = v ? *(const __attribute__((address_space(1))) u32x2 *)(a_base[i] + toff) : u32x2{0u, 0u};
+                else
+                    ra[s][i] = v ? gload4(a_base[i] + toff) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
         }
     };
@@ -112,8 +119,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
                     split2h_pre(ra[s][i] * xs, h, m);
                     *reinterpret_cast<u32x2 *>(sb + s * XP * PL + PL + a_off[i]) = m;
                 } else {
-                    h[0] = cvt_pk_bf16(ra[s][i][0], ra[s][i][1]);
-                    h[1] = cvt_pk_bf16(ra[s][i][2], ra[s][i][3]);
+                    h = stage_bits<SB>(ra[s][i]);
                 }
                 *reinterpret_cast<u32x2 *>(sb + s * XP * PL + a_off[i]) = h;
             }
@@ -211,7 +217,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
                 const uint32_t ox = r - oy * uint32_t(a.wo);
                 pix = size_t(int(img) * a.dst_h + 2 * int(oy) + di) * a.dst_w + 2 * int(ox) + dj;
             }
-            *(__attribute__((address_space(1))) f32x4 *)(a.dst + pix * a.ldc_d + oc) = v;
+            store_q<SB>(a.dst, pix * a.ldc_d + oc, v);
             omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
         }
     }
@@ -224,15 +230,15 @@ constexpr int kSK = 2;  // 32-channel k-steps per stage
 
 int gather16_enabled(uint32_t tune) { return (tune & SCD_TUNE_NO_GATHER16) ? 0 : 1; }
 
-template <int WM, int WN, int TM, int TN, int OCC, int NP>
+template <int WM, int WN, int TM, int TN, int OCC, int NP, bool SB = false>
 void launch_g16(const IgemmArgs &a, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     IgemmArgs b = a;
     b.grid_m = (a.M + BM - 1) / BM;
     b.grid_n = (a.n_out + BN - 1) / BN;
     b.remap = xcd_remap_enabled(a.tune);
-    hipLaunchKernelGGL((igemm_gather16<WM, WN, TM, TN, kSK, OCC, NP>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN), 0,
-                       s, b);
+    hipLaunchKernelGGL((igemm_gather16<WM, WN, TM, TN, kSK, OCC, NP, SB>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN),
+                       0, s, b);
 }
 
 // h2 with the h2 weight split and a source bound; bf16 on plane 0 of the bf16 weight split (no bound needed)
@@ -242,6 +248,8 @@ template <int WM, int WN, int TM, int TN, int OCC>
 void launch_g16_math(const IgemmArgs &a, hipStream_t s) {
     if (gather16_h2(a))
         launch_g16<WM, WN, TM, TN, OCC, 4>(a, s);
+    else if (a.sb)
+        launch_g16<WM, WN, TM, TN, OCC, 1, true>(a, s);
     else
         launch_g16<WM, WN, TM, TN, OCC, 1>(a, s);
 }
@@ -253,7 +261,8 @@ int gather16_pick(const IgemmArgs &a) {
     if (!a.wsplit || a.ntaps == 9 || !(gather16_h2(a) || a.math == SCD_MATH_BF16) || !gather16_enabled(a.tune))
         return 0;
     if (a.c % 32 || (a.ntaps * (a.c / 32)) % kSK || a.n_out % 64 || a.ldc_s % 4 || a.ldc_d % 4 || a.K != a.ntaps * a.c ||
-        (reinterpret_cast<uintptr_t>(a.src) & 15) || (reinterpret_cast<uintptr_t>(a.dst) & 15) ||
+        (reinterpret_cast<uintptr_t>(a.src) & (a.sb ? 7 : 15)) || (reinterpret_cast<uintptr_t>(a.dst) & (a.sb ? 7 : 15)) ||
+        (a.sb && a.math != SCD_MATH_BF16) ||
         (a.bias && (reinterpret_cast<uintptr_t>(a.bias) & 15)) || (a.store_mode != 0 && a.store_mode != 1) ||
         (a.store_mode == 1 && (a.cout % 4 || a.n_out != 4 * a.cout)) || 2 * a.wplane * 2 >= (int64_t(1) << 31))
         return 0;

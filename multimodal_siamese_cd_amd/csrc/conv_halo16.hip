@@ -49,8 +49,11 @@ __device__ __forceinline__ void gstore4(float *p, f32x4 v) { *(__attribute__((ad
 // 2 = the two-term fp16 split (SCD_MATH_H2, x3_common.h: three v_mfma_f32_16x16x32_f16 products; the halo is
 // scaled by the power of two of *src_bound while staged, the weights come pre-scaled per output channel, and the
 // epilogue multiplies both inverse scales back out -- exact, powers of two).
-template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP>
+// SB: bf16 storage of src / dst / the BatchNorm-backward y (bf16 arithmetic only, StageT in x3_common.h).
+template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP, bool SB = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
+    static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
+    constexpr uint32_t EB = SB ? 2u : 4u;  // bytes per element
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int WPX = TM * 16, WCH = TN * 16;
     constexpr int BM = WAVES_M * WPX, BN = WAVES_N * WCH;
@@ -113,7 +116,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
         const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
         const bool ok = in && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
-        a_boff[i] = ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * 4u : kOOB;
+        a_boff[i] = ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * EB : kOOB;
         a_off[i] = in ? soff(hp, col) : -1;
     }
     // Weight fragments from the 32-row fragment-major split (scd_split_bf16x3_frag): the 16 rows x 8 k of
@@ -129,13 +132,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                               : kOOB;
     }
 
-    f32x4 ra[A_PER];
+    StageT<SB> ra[A_PER];
     f32x4 in_sc, in_sh;  // IN_BN coefficients of this thread's 4 channels (col = tid & 7 for every piece)
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
     const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, uint32_t(WP) * wplane_b);
     auto load_A = [&](int cc) {
 #pragma unroll
-        for (int i = 0; i < A_PER; ++i) ra[i] = bload4(rs_src, a_boff[i] == kOOB ? kOOB : a_boff[i] + cc * 128u);
+        for (int i = 0; i < A_PER; ++i) ra[i] = bload_q<SB>(rs_src, a_boff[i] == kOOB ? kOOB : a_boff[i] + cc * 32u * EB);
         if constexpr (IN_BN) {
             const int ch = (img / a.in_seg_imgs) * a.c + cc * 32 + (tid & 7) * 4;
             in_sc = gload4(a.in_scale + ch);
@@ -152,29 +155,30 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         for (int i = 0; i < A_PER; ++i)
             if ((A_CH % NT == 0) || a_off[i] >= 0) {
                 u32x2 h, m, l;
+                f32x4 x = stage_f32<SB>(ra[i]);
                 if constexpr (IN_BN) {
-                    f32x4 v;
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        v[q] = a_boff[i] == kOOB ? 0.f : fmaxf(fmaf(ra[i][q], in_sc[q], in_sh[q]), 0.f);
-                    ra[i] = v;
+                        x[q] = a_boff[i] == kOOB ? 0.f : fmaxf(fmaf(x[q], in_sc[q], in_sh[q]), 0.f);
                 }
                 if constexpr (H2) {
-                    if constexpr (!IN_BN) ra[i] *= xs;
+                    if constexpr (!IN_BN) x *= xs;
                     if constexpr (NP == 4)
-                        split2h_pre(ra[i], h, m);
+                        split2h_pre(x, h, m);
                     else
-                        split2h(ra[i], h, m);
+                        split2h(x, h, m);
                     *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
                     *reinterpret_cast<u32x2 *>(sb + PA + a_off[i]) = m;
                 } else if constexpr (XP == 3) {
-                    split3(ra[i], h, m, l);
+                    split3(x, h, m, l);
                     *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
                     *reinterpret_cast<u32x2 *>(sb + PA + a_off[i]) = m;
                     *reinterpret_cast<u32x2 *>(sb + 2 * PA + a_off[i]) = l;
                 } else {
-                    h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
-                    h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
+                    if constexpr (SB && !IN_BN)
+                        h = ra[i];  // the stored bf16 is the operand
+                    else
+                        h = u32x2{cvt_pk_bf16(x[0], x[1]), cvt_pk_bf16(x[2], x[3])};
                     *reinterpret_cast<u32x2 *>(sb + a_off[i]) = h;
                 }
             }
@@ -313,11 +317,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         for (int j = 0; j < TN; ++j) {
             const int n = n0 + wn * WCH + j * 16 + 4 * g;
             if (n < a.n_out) {
-                const f32x4 v = acc[j][i] + bias4[j];
-                gstore4(a.dst + pix * a.ldc_d + n, v);
+                const f32x4 v = store_q<SB>(a.dst, pix * a.ldc_d + n, acc[j][i] + bias4[j]);
+                if constexpr (SB) acc[j][i] = v;  // the statistics / BN-backward sums see the stored values
                 omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
             }
         }
+    }
+    if constexpr (SB) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};  // already in acc
     }
     if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the wave takes part
 
@@ -395,7 +403,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                 for (int i = qg * TMG; i < (qg + 1) * TMG; ++i) {
                     const int p = wm * WPX + i * 16 + l16;
                     const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
-                    const f32x4 y4 = nok ? gload4(a.bb_y + pix * a.bb_ldy + n) : z4;
+                    const f32x4 y4 = nok ? load_q<SB>(a.bb_y, pix * a.bb_ldy + n) : z4;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float dz = fmaf(y4[r], sc[r], sf[r]) > 0.f ? acc[j][i][r] : 0.f;
@@ -442,7 +450,7 @@ int halo16_mode(uint32_t tune) {
     return v == SCD_TUNE_HALO16_OFF ? 0 : v == 0 ? 1 : int(v) + 1;
 }
 
-template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN, bool DB, int NP>
+template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN, bool DB, int NP, bool SB = false>
 void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     IgemmArgs b = a;
@@ -451,11 +459,11 @@ void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     b.remap = halo_remap(a.tune);
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
     if (tw == 64)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN, DB, NP>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN, DB, NP, SB>), grid, block, 0, s, b);
     else if (tw == 32)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN, DB, NP>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN, DB, NP, SB>), grid, block, 0, s, b);
     else
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN, DB, NP>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN, DB, NP, SB>), grid, block, 0, s, b);
 }
 
 // h2: the activation / gradient operand's low term pre-scaled by 2^11 (x3_common.h; floor 2^-36 instead of 2^-25
@@ -478,6 +486,15 @@ int halo16_db(uint32_t tune, bool h2) {
 
 template <int WM, int WN, int TM, int TN, int OCC, bool DB, int NP>
 void launch16c(const IgemmArgs &a, int tw, hipStream_t s) {
+    if constexpr (NP == 1) {  // the bf16 arithmetic: fp32 or bf16 storage
+        if (a.sb) {
+            if (a.in_scale)
+                launch16b<WM, WN, TM, TN, OCC, true, DB, NP, true>(a, tw, s);
+            else
+                launch16b<WM, WN, TM, TN, OCC, false, DB, NP, true>(a, tw, s);
+            return;
+        }
+    }
     if (a.in_scale)
         launch16b<WM, WN, TM, TN, OCC, true, DB, NP>(a, tw, s);
     else
@@ -560,8 +577,9 @@ bool wide_1xn_ok(const IgemmArgs &a) {
 // 0 when `a` does not take this kernel, else 1 + config id; *bm = pixels per tile, *tw = tile width.
 int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     const int mode = halo16_mode(a.tune);
-    if (!mode || !eligible || a.c % 32 || a.n_out % 4 || a.ldc_d % 4 || (reinterpret_cast<uintptr_t>(a.dst) & 15) ||
-        (a.bias && (reinterpret_cast<uintptr_t>(a.bias) & 15)))
+    if (!mode || !eligible || a.c % 32 || a.n_out % 4 || a.ldc_d % 4 ||
+        (reinterpret_cast<uintptr_t>(a.dst) & (a.sb ? 7 : 15)) || (a.bias && (reinterpret_cast<uintptr_t>(a.bias) & 15)) ||
+        (a.sb && a.math != SCD_MATH_BF16))
         return 0;
     int id;
     if (mode >= 2)
@@ -613,8 +631,10 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
 // same epilogue (bias, 16-byte stores, fused BatchNorm statistics) as igemm_halo16_x3.
 // 2 x 2 waves of 64 px x 32 ch: 128 px x 64 ch per block.
 // ------------------------------------------------------------------------------------------------
-template <int TW, int NP>
+template <int TW, int NP, bool SB = false>
 __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
+    static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
+    constexpr uint32_t EB = SB ? 2u : 4u;
     constexpr int WAVES_M = 2, TM = 4, TN = 2, NT = 256;
     constexpr int WPX = TM * 16, WCH = TN * 16;
     constexpr int BM = WAVES_M * WPX, BN = 2 * WCH;
@@ -656,7 +676,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
     };
 
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
-    f32x4 ra[A_PER];
+    StageT<SB> ra[A_PER];
     auto load_halo = [&](int tile) {
         int mt, img, y0, x0, n0;
         coords(tile, mt, img, y0, x0, n0);
@@ -667,7 +687,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
             const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
             const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
             const bool ok = e < A_CH && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
-            ra[i] = bload4(rs_src, ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * 4u : kOOB);
+            ra[i] = bload_q<SB>(rs_src, ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * EB : kOOB);
         }
     };
     // weights: the 16 rows x 8 k of lane group g are 256 contiguous bytes of a 1 KB 32x16 fragment; fragment
@@ -734,8 +754,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
                     *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
                     *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
                 } else {
-                    h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
-                    h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
+                    h = stage_bits<SB>(ra[i]);
                 }
                 *reinterpret_cast<u32x2 *>(smem + o) = h;
             }
@@ -819,11 +838,15 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
             for (int j = 0; j < TN; ++j) {
                 const int n = n0 + wn * WCH + j * 16 + 4 * g;
                 if (n < a.n_out) {
-                    const f32x4 v = acc[j][i] + bias4[j];
-                    gstore4(a.dst + pix * a.ldc_d + n, v);
+                    const f32x4 v = store_q<SB>(a.dst, pix * a.ldc_d + n, acc[j][i] + bias4[j]);
+                    if constexpr (SB) acc[j][i] = v;  // statistics of the stored values
                     omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
                 }
             }
+        }
+        if constexpr (SB) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};  // already in acc
         }
         if (a.stat_rec) {  // as igemm_halo16_x3: tile mean, then M2 about it
             float mean[TN][4];
@@ -880,8 +903,8 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
 int halo16_c16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     if (!halo16_mode(a.tune) || !eligible || (a.tune & SCD_TUNE_NO_HALO16_C16) || a.c != 16 || a.K != 144 ||
         a.in_scale || a.bb_rec ||
-        a.n_out % 4 || a.ldc_d % 4 || (reinterpret_cast<uintptr_t>(a.dst) & 15) ||
-        (a.bias && (reinterpret_cast<uintptr_t>(a.bias) & 15)))
+        a.n_out % 4 || a.ldc_d % 4 || (reinterpret_cast<uintptr_t>(a.dst) & (a.sb ? 7 : 15)) ||
+        (a.bias && (reinterpret_cast<uintptr_t>(a.bias) & 15)) || (a.sb && a.math != SCD_MATH_BF16))
         return 0;
     for (int cand : {16, 32, 64})
         if (a.wo % cand == 0 && a.ho % (128 / cand) == 0) {
@@ -902,7 +925,12 @@ static int c16_planes(const IgemmArgs &b) {
 template <int TW>
 static void launch_c16_tw(const IgemmArgs &b, dim3 grid, hipStream_t s) {
     switch (c16_planes(b)) {
-        case 1: hipLaunchKernelGGL((igemm_halo16_c16<TW, 1>), grid, dim3(256), 0, s, b); break;
+        case 1:
+            if (b.sb)
+                hipLaunchKernelGGL((igemm_halo16_c16<TW, 1, true>), grid, dim3(256), 0, s, b);
+            else
+                hipLaunchKernelGGL((igemm_halo16_c16<TW, 1>), grid, dim3(256), 0, s, b);
+            break;
         case 4: hipLaunchKernelGGL((igemm_halo16_c16<TW, 4>), grid, dim3(256), 0, s, b); break;
         case 5: hipLaunchKernelGGL((igemm_halo16_c16<TW, 5>), grid, dim3(256), 0, s, b); break;
         default: hipLaunchKernelGGL((igemm_halo16_c16<TW, 3>), grid, dim3(256), 0, s, b);
@@ -1089,8 +1117,10 @@ __device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][W16L<LC>::CB][W16L<LC>
 // RG = 2 (LC 1 only): a block of 8 waves owns 128 rows r x 64 channels c; the two 4-wave groups share the
 // staged X halo, which is then split and stored once per 128 rows instead of per 64 (the staging per MFMA,
 // a third of the kernel's time at RG 1, drops by ~35%).
-template <int NP, int LC, int RG>
+template <int NP, int LC, int RG, bool SB = false>
 __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a) {
+    static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
+    constexpr uint32_t EB = SB ? 2u : 4u;
     constexpr int NT = 256 * RG;
     constexpr int PH = 2, PW = 16, P = PH * PW;
     constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
@@ -1129,7 +1159,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
     const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
 
-    f32x4 ra[A_PER], rb[B_PER];
+    StageT<SB> ra[A_PER], rb[B_PER];
     f32x4 x_sc, x_sh;      // src transform coefficients of this thread's 4 channels (cq = tid & 15)
     uint32_t x_valid = 0;  // bit i: halo piece i is inside the image (the padding stays zero)
     auto load_patch = [&](int pi) {
@@ -1145,8 +1175,8 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * NT, q = e / CQ, cq = e % CQ;
             const int py = q >> 4, px = q & 15;
-            const uint32_t off = uint32_t(((img * a.ho + y0 + py) * a.wo + x0 + px) * a.ldc_r + r0 + cq * 4) * 4u;
-            ra[i] = bload4(rs_rows, off);
+            const uint32_t off = uint32_t(((img * a.ho + y0 + py) * a.wo + x0 + px) * a.ldc_r + r0 + cq * 4) * EB;
+            ra[i] = bload_q<SB>(rs_rows, off);
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
@@ -1155,7 +1185,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
             const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
             const bool v = e < B_CH && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
             x_valid |= uint32_t(v) << i;
-            rb[i] = bload4(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + cq * 4) * 4u : kOOB);
+            rb[i] = bload_q<SB>(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + cq * 4) * EB : kOOB);
         }
     };
     auto store_patch = [&]() {
@@ -1175,14 +1205,26 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
                 *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
                 *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
             } else {
-                h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
-                h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
+                h = stage_bits<SB>(ra[i]);
             }
             *reinterpret_cast<u32x2 *>(smem + o) = h;
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
-            if (tid + i * NT < B_CH) {
+            if constexpr (SB) {
+                if (tid + i * NT < B_CH) {
+                    u32x2 h = rb[i];
+                    if (a.src_scale) {  // bf16 -> the BatchNorm + ReLU transform in fp32 -> the bf16 operand
+                        const bool v = (x_valid >> i) & 1u;
+                        f32x4 x = unpk_bf16x4(rb[i]);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) x[q] = v ? fmaxf(fmaf(x[q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                        h = pk_bf16x4(x);
+                    }
+                    const int e = tid + i * NT;
+                    *reinterpret_cast<u32x2 *>(smem + DP * PA + (e >> 4) * RS + (e & 15) * 8) = h;
+                }
+            } else if (tid + i * NT < B_CH) {
                 u32x2 h, m, l;
                 if (a.src_scale) {
                     const bool v = (x_valid >> i) & 1u;
@@ -1342,8 +1384,10 @@ __device__ __forceinline__ void c16_chain(f32x4 (&acc)[9], bf16x8 (&dv)[3], s16x
 // would write it (bn_bwd_dy4, the same bits), so that gradient is never written or re-read (the input layer's).
 // NP 4: h2 (as wgrad_halo16_x3<4, ...>): dY scaled by the power of two of *rows_bound (with RBN a bound of the formed
 // dY, scd_bn_relu_backward_coef's dy_bound) and split with its low term pre-scaled, X by that of *src_bound.
-template <int NP, bool RBN>
+template <int NP, bool RBN, bool SB = false>
 __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
+    static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
+    constexpr uint32_t EB = SB ? 2u : 4u;
     constexpr int PH = 2, PW = 16, P = PH * PW;
     constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
     constexpr int RS = kW16RS, RSX = kC16RS;
@@ -1373,7 +1417,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
     const __amdgpu_buffer_rsrc_t rs_y = make_rsrc(RBN ? a.rows_y : a.rows, RBN ? a.y_bytes : 0u);
 
-    f32x4 ra[A_PER], rb[B_PER], ya[RBN ? A_PER : 1];
+    StageT<SB> ra[A_PER], rb[B_PER], ya[RBN ? A_PER : 1];
     f32x4 x_sc, x_sh;      // src transform coefficients of this thread's 4 channels (cq = tid & 3)
     f32x4 r_mu, r_iv, r_sc, r_sf, r_k1, r_k2, r_mul;  // RBN: this thread's 4 rows r0 + 4 (tid & 15) + 0..3
     uint32_t x_valid = 0;  // bit i: halo piece i is inside the image (the padding stays zero)
@@ -1402,8 +1446,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
             const int e = tid + i * 256, q = e >> 4, cq = e & 15;
             const int py = q >> 4, px = q & 15;
             const int pix = (img * a.ho + y0 + py) * a.wo + x0 + px;
-            ra[i] = bload4(rs_rows, uint32_t(pix * a.ldc_r + r0 + cq * 4) * 4u);
-            if constexpr (RBN) ya[i] = bload4(rs_y, uint32_t(pix * a.ldc_y + r0 + cq * 4) * 4u);
+            ra[i] = bload_q<SB>(rs_rows, uint32_t(pix * a.ldc_r + r0 + cq * 4) * EB);
+            if constexpr (RBN) ya[i] = bload_q<SB>(rs_y, uint32_t(pix * a.ldc_y + r0 + cq * 4) * EB);
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
@@ -1412,7 +1456,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
             const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
             const bool v = e < B_CH && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
             x_valid |= uint32_t(v) << i;
-            rb[i] = bload4(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + cq * 4) * 4u : kOOB);
+            rb[i] = bload_q<SB>(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + cq * 4) * EB : kOOB);
         }
     };
     auto store_patch = [&]() {
@@ -1421,7 +1465,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
             const int e = tid + i * 256;
             const int o = (e >> 4) * RS + (e & 15) * 8;
             u32x2 h, m, l;
-            if constexpr (RBN) ra[i] = bn_bwd_dy4(ya[i], ra[i], r_mu, r_iv, r_sc, r_sf, r_k1, r_k2, r_mul);
+            if constexpr (SB) {  // dY formed in fp32 from the bf16 da and y, rounded once (as bn_bwd_apply stores it)
+                if constexpr (RBN)
+                    h = pk_bf16x4(bn_bwd_dy4(unpk_bf16x4(ya[i]), unpk_bf16x4(ra[i]), r_mu, r_iv, r_sc, r_sf, r_k1,
+                                             r_k2, r_mul));
+                else
+                    h = ra[i];
+                *reinterpret_cast<u32x2 *>(smem + o) = h;
+                continue;
+            } else {
+                if constexpr (RBN) ra[i] = bn_bwd_dy4(ya[i], ra[i], r_mu, r_iv, r_sc, r_sf, r_k1, r_k2, r_mul);
+            }
             if constexpr (H2) {
                 split2h_pre(ra[i] * ds, h, m);
                 *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
@@ -1430,14 +1484,26 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
                 *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
                 *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
             } else {
-                h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
-                h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
+                h = stage_bits<SB>(ra[i]);
             }
             *reinterpret_cast<u32x2 *>(smem + o) = h;
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
-            if (tid + i * 256 < B_CH) {
+            if constexpr (SB) {
+                if (tid + i * 256 < B_CH) {
+                    u32x2 h = rb[i];
+                    if (a.src_scale) {
+                        const bool v = (x_valid >> i) & 1u;
+                        f32x4 x = unpk_bf16x4(rb[i]);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) x[q] = v ? fmaxf(fmaf(x[q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                        h = pk_bf16x4(x);
+                    }
+                    const int e = tid + i * 256;
+                    *reinterpret_cast<u32x2 *>(smem + DP * PA + (e >> 2) * RSX + (e & 3) * 8) = h;
+                }
+            } else if (tid + i * 256 < B_CH) {
                 u32x2 h, m, l;
                 if (a.src_scale) {
                     const bool v = (x_valid >> i) & 1u;
@@ -1539,7 +1605,12 @@ const void *wgrad_halo16_c16_fn(int math, uint32_t tune, bool bounded) {
 template <bool RBN>
 static void launch_c16(const WgradArgs &a, dim3 grid, hipStream_t s) {
     switch (wgrad_c16_planes(a.math, a.tune, a.rows_bound && a.src_bound)) {
-        case 1: hipLaunchKernelGGL((wgrad_halo16_c16<1, RBN>), grid, dim3(256), 0, s, a); break;
+        case 1:
+            if (a.sb)
+                hipLaunchKernelGGL((wgrad_halo16_c16<1, RBN, true>), grid, dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL((wgrad_halo16_c16<1, RBN>), grid, dim3(256), 0, s, a);
+            break;
         case 4: hipLaunchKernelGGL((wgrad_halo16_c16<4, RBN>), grid, dim3(256), 0, s, a); break;
         case 5: hipLaunchKernelGGL((wgrad_halo16_c16<5, RBN>), grid, dim3(256), 0, s, a); break;
         default: hipLaunchKernelGGL((wgrad_halo16_c16<3, RBN>), grid, dim3(256), 0, s, a);
@@ -1567,14 +1638,14 @@ static const void *w16_kernel(int lc, int rb) {
            : lc      ? reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 1, 1>)
                      : reinterpret_cast<const void *>(&wgrad_halo16_x3<NP, 0, 1>);
 }
-template <int NP>
+template <int NP, bool SB = false>
 static void w16_launch(int lc, int rb, const WgradArgs &a, dim3 grid, hipStream_t s) {
     if (rb == 128)
-        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 2>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 2, SB>), grid, dim3(512), 0, s, a);
     else if (lc)
-        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 1>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 1, SB>), grid, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 0, 1>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 0, 1, SB>), grid, dim3(256), 0, s, a);
 }
 const void *wgrad_halo16_fn(int math, uint32_t tune, bool bounded, int rblock) {
     switch (wgrad16_planes(math, tune, bounded)) {
@@ -1590,7 +1661,12 @@ void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
     const bool bounded = a.rows_bound && a.src_bound;
     const int lc = w16_layout(a.tune), rb = wgrad16_rblock(a.math, a.tune, a.R, bounded);
     switch (wgrad16_planes(a.math, a.tune, bounded)) {
-        case 1: w16_launch<1>(lc, rb, a, grid, s); break;
+        case 1:
+            if (a.sb)
+                w16_launch<1, true>(lc, rb, a, grid, s);
+            else
+                w16_launch<1>(lc, rb, a, grid, s);
+            break;
         case 2: w16_launch<2>(lc, rb, a, grid, s); break;
         case 4: w16_launch<4>(lc, rb, a, grid, s); break;
         case 5: hipLaunchKernelGGL((wgrad_halo16_x3<5, 0, 1>), grid, dim3(256), 0, s, a); break;

@@ -603,7 +603,7 @@ int halo_stat_tiles(const IgemmArgs &a0, int *tile_pixels) {
     const IgemmArgs a = x3_view(a0);
     if (!math_split(a.math)) return 0;
     if (!halo16_pick(a, halo_eligible(a), &bm, &tw) && !halo16_c16_pick(a, halo_eligible(a), &bm, &tw) &&
-        !halo_pick(a, &bm, &tw))
+        (a.sb || !halo_pick(a, &bm, &tw)))
         return 0;
     *tile_pixels = bm;
     return a.n_img * (a.ho * a.wo / bm);
@@ -625,6 +625,7 @@ bool launch_igemm_x3(const IgemmArgs &a0, hipStream_t s) {
         launch_halo16_c16(a, tw, s);
         return true;
     }
+    if (a.sb) return false;  // bf16 storage: only the bf16 kernels above (the caller reports the unsupported shape)
     switch (halo_pick(a, &bm, &tw)) {
         case 1: launch_halo<2, 2, 2, 2>(a, tw, s); return true;
         case 2: launch_halo<4, 1, 2, 2>(a, tw, s); return true;
@@ -677,9 +678,12 @@ struct TrPlane {
 // three v_mfma_f32_32x32x16_f16 products (a_h 2^-11) b_m' + a_m' (b_h 2^-11) + a_h b_h, scales undone in the
 // epilogue.  NP = 1: bf16 (the ConvTranspose weight grad of the bf16 configs), both operands rounded to bf16 (RNE),
 // one v_mfma_f32_32x32x16_bf16 product.
-template <int WAVES_M, int WAVES_N, int TM, int TN, int NP = 3>
+// SB: bf16 storage of rows and src (the bf16 configs' ConvTranspose weight grad; bf16 arithmetic only).
+template <int WAVES_M, int WAVES_N, int TM, int TN, int NP = 3, bool SB = false>
 __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
     static_assert(NP == 1 || NP == 3 || NP == 4, "bf16, x3 or h2");
+    static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
+    constexpr uint32_t EB = SB ? 2u : 4u;
     constexpr bool H2 = NP == 4;
     constexpr int NPL = H2 ? 2 : NP == 1 ? 1 : 3;  // planes per operand
     constexpr int BK = 16;
@@ -754,14 +758,14 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
         b_off[i] = NPL * PA + LB::off(b_k[i], q * 8);
     }
 
-    f32x4 ra[A_PER], rb[B_PER];
+    StageT<SB> ra[A_PER], rb[B_PER];
     const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
     auto load_stage = [&](int kb) {
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int m = kb + a_k[i];
-            ra[i] = bload4(rs_rows, (a_ok[i] && m < kend) ? uint32_t(m * a.ldc_r + a_r[i]) * 4u : kOOB);
+            ra[i] = bload_q<SB>(rs_rows, (a_ok[i] && m < kend) ? uint32_t(m * a.ldc_r + a_r[i]) * EB : kOOB);
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
@@ -769,7 +773,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
             const int sx = b_ox[i] * a.stride + b_dx[i];
             const bool v = b_ok[i] && (kb + b_k[i] < kend) && unsigned(sy) < unsigned(a.hs) &&
                            unsigned(sx) < unsigned(a.ws);
-            rb[i] = bload4(rs_src, v ? uint32_t(((b_img[i] * a.hs + sy) * a.ws + sx) * a.ldc_s + b_c[i]) * 4u : kOOB);
+            rb[i] = bload_q<SB>(rs_src, v ? uint32_t(((b_img[i] * a.hs + sy) * a.ws + sx) * a.ldc_s + b_c[i]) * EB : kOOB);
         }
     };
     auto advance = [&]() {
@@ -800,8 +804,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
                 if constexpr (H2) {
                     split2h_pre(ra[i] * rsc, h, m);
                 } else if constexpr (NP == 1) {
-                    h[0] = cvt_pk_bf16(ra[i][0], ra[i][1]);
-                    h[1] = cvt_pk_bf16(ra[i][2], ra[i][3]);
+                    h = stage_bits<SB>(ra[i]);
                 } else {
                     split3(ra[i], h, m, l);
                     *reinterpret_cast<u32x2 *>(S + 2 * PA + a_off[i]) = l;
@@ -816,8 +819,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
                 if constexpr (H2) {
                     split2h_pre(rb[i] * ssc, h, m);
                 } else if constexpr (NP == 1) {
-                    h[0] = cvt_pk_bf16(rb[i][0], rb[i][1]);
-                    h[1] = cvt_pk_bf16(rb[i][2], rb[i][3]);
+                    h = stage_bits<SB>(rb[i]);
                 } else {
                     split3(rb[i], h, m, l);
                     *reinterpret_cast<u32x2 *>(S + 2 * PB + b_off[i]) = l;
@@ -961,7 +963,21 @@ void launch_wgrad_x3_h2(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, 
 }
 
 // bf16 (SCD_MATH_BF16): the ConvTranspose weight grad (4 taps), every tile.
+template <bool SB>
+static void launch_wgrad_x3_bf16_sb(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s) {
+    switch (tile_id) {
+        case 0: hipLaunchKernelGGL((wgrad_x3<2, 2, 2, 2, 1, SB>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((wgrad_x3<1, 4, 2, 2, 1, SB>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((wgrad_x3<2, 2, 1, 3, 1, SB>), grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((wgrad_x3<2, 1, 1, 3, 1, SB>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((wgrad_x3<1, 4, 1, 1, 1, SB>), grid, block, 0, s, a); break;
+    }
+}
 void launch_wgrad_x3_bf16(const WgradArgs &a, int tile_id, dim3 grid, dim3 block, hipStream_t s) {
+    if (a.sb) {
+        launch_wgrad_x3_bf16_sb<true>(a, tile_id, grid, block, s);
+        return;
+    }
     switch (tile_id) {
         case 0: hipLaunchKernelGGL((wgrad_x3<2, 2, 2, 2, 1>), grid, block, 0, s, a); break;
         case 1: hipLaunchKernelGGL((wgrad_x3<1, 4, 2, 2, 1>), grid, block, 0, s, a); break;

@@ -7,7 +7,8 @@ namespace scd {
 
 // dst[n, y, x, :] = src[n, y + oy, x + ox, :] where that pixel exists, else 0.  One row of dst per grid.y
 // step, channel quads of the row across grid.x (the row-decomposed grid of misc_f32.hip).
-__global__ void window_copy_kernel(const float *__restrict__ src, int hs, int ws, int lds, float *__restrict__ dst,
+template <class T>
+__global__ void window_copy_kernel(const T *__restrict__ src, int hs, int ws, int lds, T *__restrict__ dst,
                                    int hd, int wd, int ldd, int C, int oy, int ox, int rows, FastDiv div_cq) {
     const int cq = C / 4;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -18,10 +19,9 @@ __global__ void window_copy_kernel(const float *__restrict__ src, int hs, int ws
     for (int row = blockIdx.y; row < rows; row += gridDim.y) {
         const int img = row / hd, y = row - img * hd;
         const int sy = y + oy;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (sy >= 0 && sy < hs && sx >= 0 && sx < ws)
-            v = *reinterpret_cast<const float4 *>(src + ((int64_t(img) * hs + sy) * ws + sx) * lds + c);
-        *reinterpret_cast<float4 *>(dst + (int64_t(row) * wd + x) * ldd + c) = v;
+        bnf4 v = {0.f, 0.f, 0.f, 0.f};
+        if (sy >= 0 && sy < hs && sx >= 0 && sx < ws) v = ld4(src + ((int64_t(img) * hs + sy) * ws + sx) * lds + c);
+        st4(dst + (int64_t(row) * wd + x) * ldd + c, v);
     }
 }
 
@@ -150,10 +150,13 @@ extern "C" int scd_window_copy(scd_nhwc_t src, scd_nhwc_t dst, int32_t oy, int32
         return SCD_ERR_ARG;
     }
     const int quads = dst.w * (dst.c / 4);
-    hipLaunchKernelGGL(window_copy_kernel, dim3(unsigned((quads + 255) / 256), unsigned(rows < 65535 ? rows : 65535)),
-                       dim3(256), 0, as_stream(stream), static_cast<const float *>(src.data), src.h, src.w, src.ldc,
-                       static_cast<float *>(dst.data), dst.h, dst.w, dst.ldc, dst.c, oy, ox, int(rows),
-                       make_fastdiv(uint32_t(dst.c / 4)));
+    const int dt = common_dtype("window_copy", {&src, &dst});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL(window_copy_kernel<T>,
+                                  dim3(unsigned((quads + 255) / 256), unsigned(rows < 65535 ? rows : 65535)), dim3(256),
+                                  0, as_stream(stream), view_ptr<const T>(src), src.h, src.w, src.ldc, view_ptr<T>(dst),
+                                  dst.h, dst.w, dst.ldc, dst.c, oy, ox, int(rows), make_fastdiv(uint32_t(dst.c / 4))));
     return launch_status("scd_window_copy");
 }
 

@@ -48,31 +48,31 @@ static int grid_for(int64_t total, int cap = 4096) {
 // the source planes are read 16 pixels x 4 channels per load.  Otherwise one thread per pixel with scalar stores,
 // so any channel offset works (the early-fusion t2 bands).
 // `bound`: raised to max |value| (one atomic per wave, after the loop every lane reaches).
-template <bool VEC>
+template <bool VEC, class T>
 __global__ void pack_nchw_kernel(const float *__restrict__ src, int c, int hw, int c_begin, int c_count,
-                                 float *__restrict__ dst, int dc, int ldc, float *bound) {
+                                 T *__restrict__ dst, int dc, int ldc, float *bound) {
     const int img = blockIdx.y;
     const float *s = src + (size_t(img) * c + c_begin) * hw;
-    float *d = dst + size_t(img) * hw * ldc;
+    T *d = dst + size_t(img) * hw * ldc;
     float vmax = 0.f;
     if (VEC) {
         const int q4 = dc >> 2;  // float4 groups per pixel
         const int total = hw * q4;
         for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
             const int pix = e / q4, c0 = (e - pix * q4) * 4;
-            float4 v;
+            bnf4 v;
             v.x = c0 + 0 < c_count ? s[size_t(c0 + 0) * hw + pix] : 0.f;
             v.y = c0 + 1 < c_count ? s[size_t(c0 + 1) * hw + pix] : 0.f;
             v.z = c0 + 2 < c_count ? s[size_t(c0 + 2) * hw + pix] : 0.f;
             v.w = c0 + 3 < c_count ? s[size_t(c0 + 3) * hw + pix] : 0.f;
-            *reinterpret_cast<float4 *>(d + size_t(pix) * ldc + c0) = v;
+            st4(d + size_t(pix) * ldc + c0, v);
             vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         }
     } else {
         for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < hw; pix += gridDim.x * blockDim.x)
             for (int cc = 0; cc < dc; ++cc) {
                 const float v = cc < c_count ? s[size_t(cc) * hw + pix] : 0.f;
-                d[size_t(pix) * ldc + cc] = v;
+                st1(d + size_t(pix) * ldc + cc, v);
                 vmax = fmaxf(vmax, fabsf(v));
             }
     }
@@ -139,13 +139,13 @@ __device__ __forceinline__ void pool_pick(float v, int k, float &mx, int &idx) {
 // BN: the input is a conv output read through its BatchNorm-apply + ReLU, max(fma(x, sc, sh), 0) with the
 // coefficients of the image's segment (the expression of bn_relu_apply_kernel, so results are bit-identical
 // to pooling the materialised activation).
-__device__ __forceinline__ float4 bn_relu_f4(float4 v, float4 sc, float4 sh) {
-    return make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
-                       fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
+__device__ __forceinline__ bnf4 bn_relu_f4(bnf4 v, bnf4 sc, bnf4 sh) {
+    return bnf4{fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
+                fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f)};
 }
 
-template <bool BN>
-__global__ void maxpool2_fwd_kernel(const float *__restrict__ x, int hx, int wx, int ldx, float *__restrict__ y,
+template <bool BN, class T>
+__global__ void maxpool2_fwd_kernel(const T *__restrict__ x, int hx, int wx, int ldx, T *__restrict__ y,
                                    int hy, int wy, int ldy, uint8_t *__restrict__ idx, int C, int rows,
                                    FastDiv div_cq, const float *__restrict__ bsc, const float *__restrict__ bsh,
                                    int seg_imgs) {
@@ -157,14 +157,14 @@ __global__ void maxpool2_fwd_kernel(const float *__restrict__ x, int hx, int wx,
     for (int row = blockIdx.y; row < rows; row += gridDim.y) {
         const int img = row / hy, oy = row - img * hy;
         const int64_t p = int64_t(row) * wy + ox;  // output pixel
-        const float *base = x + ((int64_t(img) * hx + 2 * oy) * wx + 2 * ox) * ldx + c;
-        float4 v0 = *reinterpret_cast<const float4 *>(base);
-        float4 v1 = *reinterpret_cast<const float4 *>(base + ldx);
-        float4 v2 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx);
-        float4 v3 = *reinterpret_cast<const float4 *>(base + int64_t(wx) * ldx + ldx);
+        const T *base = x + ((int64_t(img) * hx + 2 * oy) * wx + 2 * ox) * ldx + c;
+        bnf4 v0 = ld4(base);
+        bnf4 v1 = ld4(base + ldx);
+        bnf4 v2 = ld4(base + int64_t(wx) * ldx);
+        bnf4 v3 = ld4(base + int64_t(wx) * ldx + ldx);
         if constexpr (BN) {
             const int o = (img / seg_imgs) * C + c;
-            const float4 sc = *reinterpret_cast<const float4 *>(bsc + o), sh = *reinterpret_cast<const float4 *>(bsh + o);
+            const bnf4 sc = ld4(bsc + o), sh = ld4(bsh + o);
             v0 = bn_relu_f4(v0, sc, sh);
             v1 = bn_relu_f4(v1, sc, sh);
             v2 = bn_relu_f4(v2, sc, sh);
@@ -185,14 +185,15 @@ __global__ void maxpool2_fwd_kernel(const float *__restrict__ x, int hx, int wx,
             o[k] = mx;
             packed |= uint32_t(id) << (8 * k);
         }
-        *reinterpret_cast<float4 *>(y + p * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
+        st4(y + p * ldy + c, bnf4{o[0], o[1], o[2], o[3]});
         *reinterpret_cast<uint32_t *>(idx + p * C + c) = packed;
     }
 }
 
-__global__ void feature_grad_kernel(const float *__restrict__ gy, int hy, int wy, int ldgy,
-                                    const uint8_t *__restrict__ idx, const float *__restrict__ gs, int gsn, int ldgs,
-                                    int skip_mode, float *__restrict__ gx, int hx, int wx, int ldgx, int C,
+template <class T>
+__global__ void feature_grad_kernel(const T *__restrict__ gy, int hy, int wy, int ldgy,
+                                    const uint8_t *__restrict__ idx, const T *__restrict__ gs, int gsn, int ldgs,
+                                    int skip_mode, T *__restrict__ gx, int hx, int wx, int ldgx, int C,
                                     int accumulate, int rows, FastDiv div_cq) {
     const int cq = C / 4;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -202,13 +203,13 @@ __global__ void feature_grad_kernel(const float *__restrict__ gy, int hy, int wy
     for (int row = blockIdx.y; row < rows; row += gridDim.y) {
         const int img = row / hx, yy = row - img * hx;
         const int64_t p = int64_t(row) * wx + x;
-        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        bnf4 r = {0.f, 0.f, 0.f, 0.f};
         if (gy) {
             const int oy = yy >> 1, ox = x >> 1;
             if (oy < hy && ox < wy) {
                 const int64_t q = (int64_t(img) * hy + oy) * wy + ox;
                 const uint32_t pk = *reinterpret_cast<const uint32_t *>(idx + q * C + c);
-                const float4 g = *reinterpret_cast<const float4 *>(gy + q * ldgy + c);
+                const bnf4 g = ld4(gy + q * ldgy + c);
                 const uint32_t want = uint32_t((yy & 1) * 2 + (x & 1));
                 r.x = ((pk >> 0) & 0xff) == want ? g.x : 0.f;
                 r.y = ((pk >> 8) & 0xff) == want ? g.y : 0.f;
@@ -219,26 +220,20 @@ __global__ void feature_grad_kernel(const float *__restrict__ gy, int hy, int wy
         if (gs) {
             const int simg = img % gsn;
             const float sg = (skip_mode == 1 && img < gsn) ? -1.f : 1.f;
-            const float4 s = *reinterpret_cast<const float4 *>(gs + ((int64_t(simg) * hx + yy) * wx + x) * ldgs + c);
+            const bnf4 s = ld4(gs + ((int64_t(simg) * hx + yy) * wx + x) * ldgs + c);
             r.x += sg * s.x;
             r.y += sg * s.y;
             r.z += sg * s.z;
             r.w += sg * s.w;
         }
-        float4 *dst = reinterpret_cast<float4 *>(gx + p * ldgx + c);
-        if (accumulate) {
-            const float4 o = *dst;
-            r.x += o.x;
-            r.y += o.y;
-            r.z += o.z;
-            r.w += o.w;
-        }
-        *dst = r;
+        T *dst = gx + p * ldgx + c;
+        if (accumulate) r += ld4(dst);
+        st4(dst, r);
     }
 }
 
-template <bool BN>
-__global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float *__restrict__ d, int ldd, int C,
+template <bool BN, class T>
+__global__ void siamese_diff_kernel(const T *__restrict__ a, int lda, T *__restrict__ d, int ldd, int C,
                                     int w, int64_t half_pixels, int rows, FastDiv div_cq,
                                     const float *__restrict__ bsc, const float *__restrict__ bsh) {
     const int cq = C / 4;
@@ -248,14 +243,13 @@ __global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float 
     const int c = (e - x * cq) * 4;
     for (int row = blockIdx.y; row < rows; row += gridDim.y) {
         const int64_t p = int64_t(row) * w + x;
-        float4 v1 = *reinterpret_cast<const float4 *>(a + p * lda + c);
-        float4 v2 = *reinterpret_cast<const float4 *>(a + (p + half_pixels) * lda + c);
+        bnf4 v1 = ld4(a + p * lda + c);
+        bnf4 v2 = ld4(a + (p + half_pixels) * lda + c);
         if constexpr (BN) {  // branch t1 = coefficient segment 0, t2 = segment 1
-            v1 = bn_relu_f4(v1, *reinterpret_cast<const float4 *>(bsc + c), *reinterpret_cast<const float4 *>(bsh + c));
-            v2 = bn_relu_f4(v2, *reinterpret_cast<const float4 *>(bsc + C + c),
-                            *reinterpret_cast<const float4 *>(bsh + C + c));
+            v1 = bn_relu_f4(v1, ld4(bsc + c), ld4(bsh + c));
+            v2 = bn_relu_f4(v2, ld4(bsc + C + c), ld4(bsh + C + c));
         }
-        *reinterpret_cast<float4 *>(d + p * ldd + c) = make_float4(v2.x - v1.x, v2.y - v1.y, v2.z - v1.z, v2.w - v1.w);
+        st4(d + p * ldd + c, v2 - v1);
     }
 }
 
@@ -263,8 +257,9 @@ __global__ void siamese_diff_kernel(const float *__restrict__ a, int lda, float 
 // d[b] = a_t2 - a_t1 at full resolution and MaxPool2d(2) of both branches for the next level.  Same per-element
 // expressions as siamese_diff_kernel<true> and maxpool2_fwd_kernel<true>, so results are bit-identical to the
 // two-kernel path.  One thread = one pooled pixel quad of pair b, both branches; rows = pairs * hy.
-__global__ void bn_relu_pool_diff_kernel(const float *__restrict__ x, int hx, int wx, int ldx, float *__restrict__ y,
-                                         int hy, int wy, int ldy, uint8_t *__restrict__ idx, float *__restrict__ d,
+template <class T>
+__global__ void bn_relu_pool_diff_kernel(const T *__restrict__ x, int hx, int wx, int ldx, T *__restrict__ y,
+                                         int hy, int wy, int ldy, uint8_t *__restrict__ idx, T *__restrict__ d,
                                          int ldd, int C, int pairs, int rows, FastDiv div_cq,
                                          const float *__restrict__ bsc, const float *__restrict__ bsh) {
     const int cq = C / 4;
@@ -272,28 +267,26 @@ __global__ void bn_relu_pool_diff_kernel(const float *__restrict__ x, int hx, in
     if (e >= wy * cq) return;
     const int ox = int(fdiv(uint32_t(e), div_cq));
     const int c = (e - ox * cq) * 4;
-    const float4 sc1 = *reinterpret_cast<const float4 *>(bsc + c), sh1 = *reinterpret_cast<const float4 *>(bsh + c);
-    const float4 sc2 = *reinterpret_cast<const float4 *>(bsc + C + c);
-    const float4 sh2 = *reinterpret_cast<const float4 *>(bsh + C + c);
+    const bnf4 sc1 = ld4(bsc + c), sh1 = ld4(bsh + c);
+    const bnf4 sc2 = ld4(bsc + C + c);
+    const bnf4 sh2 = ld4(bsh + C + c);
     const int64_t half = int64_t(pairs) * hx * wx;  // pixels of one branch
     for (int row = blockIdx.y; row < rows; row += gridDim.y) {
         const int b = row / hy, oy = row - b * hy;
         const int64_t q[4] = {(int64_t(b) * hx + 2 * oy) * wx + 2 * ox, (int64_t(b) * hx + 2 * oy) * wx + 2 * ox + 1,
                               (int64_t(b) * hx + 2 * oy + 1) * wx + 2 * ox,
                               (int64_t(b) * hx + 2 * oy + 1) * wx + 2 * ox + 1};
-        float4 v1[4], v2[4];
+        bnf4 v1[4], v2[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            v1[k] = bn_relu_f4(*reinterpret_cast<const float4 *>(x + q[k] * ldx + c), sc1, sh1);
-            v2[k] = bn_relu_f4(*reinterpret_cast<const float4 *>(x + (q[k] + half) * ldx + c), sc2, sh2);
+            v1[k] = bn_relu_f4(ld4(x + q[k] * ldx + c), sc1, sh1);
+            v2[k] = bn_relu_f4(ld4(x + (q[k] + half) * ldx + c), sc2, sh2);
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            *reinterpret_cast<float4 *>(d + q[k] * ldd + c) =
-                make_float4(v2[k].x - v1[k].x, v2[k].y - v1[k].y, v2[k].z - v1[k].z, v2[k].w - v1[k].w);
+        for (int k = 0; k < 4; ++k) st4(d + q[k] * ldd + c, v2[k] - v1[k]);
 #pragma unroll
         for (int br = 0; br < 2; ++br) {
-            const float4 *v = br ? v2 : v1;
+            const bnf4 *v = br ? v2 : v1;
             const float a0[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, a1[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
             const float a2[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, a3[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
             float o[4];
@@ -310,7 +303,7 @@ __global__ void bn_relu_pool_diff_kernel(const float *__restrict__ x, int hx, in
                 packed |= uint32_t(id) << (8 * k);
             }
             const int64_t p = (int64_t(b + br * pairs) * hy + oy) * wy + ox;
-            *reinterpret_cast<float4 *>(y + p * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
+            st4(y + p * ldy + c, bnf4{o[0], o[1], o[2], o[3]});
             *reinterpret_cast<uint32_t *>(idx + p * C + c) = packed;
         }
     }
@@ -322,8 +315,8 @@ __global__ void bn_relu_pool_diff_kernel(const float *__restrict__ x, int hx, in
 // wave, whose loads are all issued before the arithmetic (U x the bytes in flight of one set per iteration).
 // scale / shift (optional): the input is read through the producing BatchNorm + ReLU, relu(fma(x, scale, shift))
 // per segment of pseg pixels (bn_relu_apply_kernel's expression), so that activation never has to be written.
-template <int U>
-__global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restrict__ x, int ldx, int C, int hw,
+template <int U, class T>
+__global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const T *__restrict__ x, int ldx, int C, int hw,
                                                           int64_t npix, const float *__restrict__ w,
                                                           const float *__restrict__ b, int n_out, int G,
                                                           const float *__restrict__ scale,
@@ -341,27 +334,27 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restric
 #pragma unroll
             for (int o = 0; o < 4; ++o) s[u][o] = 0.f;
         for (int qq = q; qq < cq; qq += G) {
-            float4 v[U];
+            bnf4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t p = p0 + u * ppw + pp;
-                v[u] = p < npix ? *reinterpret_cast<const float4 *>(x + p * ldx + 4 * qq) : make_float4(0, 0, 0, 0);
+                v[u] = p < npix ? ld4(x + p * ldx + 4 * qq) : bnf4{0.f, 0.f, 0.f, 0.f};
             }
             if (scale) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int64_t p = p0 + u * ppw + pp;
                     const int64_t so = (p < npix ? p / pseg : 0) * C + 4 * qq;
-                    const float4 sc = *reinterpret_cast<const float4 *>(scale + so);
-                    const float4 sf = *reinterpret_cast<const float4 *>(shift + so);
-                    v[u] = make_float4(fmaxf(fmaf(v[u].x, sc.x, sf.x), 0.f), fmaxf(fmaf(v[u].y, sc.y, sf.y), 0.f),
-                                       fmaxf(fmaf(v[u].z, sc.z, sf.z), 0.f), fmaxf(fmaf(v[u].w, sc.w, sf.w), 0.f));
+                    const bnf4 sc = ld4(scale + so);
+                    const bnf4 sf = ld4(shift + so);
+                    v[u] = bnf4{fmaxf(fmaf(v[u].x, sc.x, sf.x), 0.f), fmaxf(fmaf(v[u].y, sc.y, sf.y), 0.f),
+                                fmaxf(fmaf(v[u].z, sc.z, sf.z), 0.f), fmaxf(fmaf(v[u].w, sc.w, sf.w), 0.f)};
                 }
             }
 #pragma unroll
             for (int o = 0; o < 4; ++o) {
                 if (o < n_out) {
-                    const float4 wv = *reinterpret_cast<const float4 *>(w + int64_t(o) * C + 4 * qq);
+                    const bnf4 wv = ld4(w + int64_t(o) * C + 4 * qq);
 #pragma unroll
                     for (int u = 0; u < U; ++u)
                         s[u][o] = fmaf(v[u].x, wv.x, fmaf(v[u].y, wv.y, fmaf(v[u].z, wv.z, fmaf(v[u].w, wv.w, s[u][o]))));
@@ -389,14 +382,15 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const float *__restric
     }
 }
 
+template <class T>
 __global__ void conv1x1_bwd_dx_kernel(const float *__restrict__ gout, int n_out, int hw, const float *__restrict__ w,
-                                      float *__restrict__ gx, int ldgx, int C, int accumulate, int64_t total) {
+                                      T *__restrict__ gx, int ldgx, int C, int accumulate, int64_t total) {
     const int cq = C / 4;
     for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
         const int c = int(e % cq) * 4;
         const int64_t p = e / cq;
         const int64_t img = p / hw, pix = p % hw;
-        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        bnf4 r = {0.f, 0.f, 0.f, 0.f};
         for (int o = 0; o < n_out; ++o) {
             const float g = gout[(img * n_out + o) * hw + pix];
             const float *wr = w + int64_t(o) * C + c;
@@ -405,15 +399,9 @@ __global__ void conv1x1_bwd_dx_kernel(const float *__restrict__ gout, int n_out,
             r.z = fmaf(g, wr[2], r.z);
             r.w = fmaf(g, wr[3], r.w);
         }
-        float4 *dst = reinterpret_cast<float4 *>(gx + p * ldgx + c);
-        if (accumulate) {
-            const float4 o4 = *dst;
-            r.x += o4.x;
-            r.y += o4.y;
-            r.z += o4.z;
-            r.w += o4.w;
-        }
-        *dst = r;
+        T *dst = gx + p * ldgx + c;
+        if (accumulate) r += ld4(dst);
+        st4(dst, r);
     }
 }
 
@@ -530,7 +518,7 @@ __global__ void pjaccard_bwd_kernel(const float *__restrict__ logits, const floa
 using namespace scd;
 
 // ------------------------------------------------------------------------------------------------
-extern "C" const char *scd_version(void) { return "libscd 0.5.0 (gfx950, ABI 5: per-descriptor conv arithmetic, bounded input pack, h2 input-layer weight grad)"; }
+extern "C" const char *scd_version(void) { return "libscd 0.6.0 (gfx950, ABI 6: bf16 activation storage, per-descriptor conv arithmetic)"; }
 extern "C" const char *scd_last_error(void) { return g_err.c_str(); }
 
 extern "C" int scd_device_check(int device) {
@@ -563,8 +551,8 @@ extern "C" int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, 
         return SCD_ERR_ARG;
     }
     if (n == 0 || hw == 0) return SCD_OK;
-    float *d = static_cast<float *>(dst.data);
-    const bool vec = dst.c % 4 == 0 && dst.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(d) & 15) == 0;
+    const bool vec = dst.c % 4 == 0 && dst.ldc % 4 == 0 &&
+                     (reinterpret_cast<uintptr_t>(dst.data) & (is_bf16(dst) ? 7 : 15)) == 0;
     const int64_t per_img = vec ? int64_t(hw) * (dst.c / 4) : hw;
     if (per_img >= (int64_t(1) << 31)) {
         set_error("pack_nchw: image too large");
@@ -572,12 +560,15 @@ extern "C" int scd_pack_nchw(const float *src, int32_t n, int32_t c, int32_t h, 
     }
     // under a bound at most 64 blocks per image (each block's maximum goes to one address by atomic)
     const dim3 grid(unsigned(std::min<int64_t>((per_img + 255) / 256, bound ? 64 : 4096)), unsigned(n));
-    if (vec)
-        hipLaunchKernelGGL(pack_nchw_kernel<true>, grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
-                           c_count, d, dst.c, dst.ldc, bound);
-    else
-        hipLaunchKernelGGL(pack_nchw_kernel<false>, grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
-                           c_count, d, dst.c, dst.ldc, bound);
+    SCD_WITH_T(dst.dtype, T, {
+        T *d = view_ptr<T>(dst);
+        if (vec)
+            hipLaunchKernelGGL((pack_nchw_kernel<true, T>), grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
+                               c_count, d, dst.c, dst.ldc, bound);
+        else
+            hipLaunchKernelGGL((pack_nchw_kernel<false, T>), grid, dim3(256), 0, as_stream(stream), src, c, hw, c_begin,
+                               c_count, d, dst.c, dst.ldc, bound);
+    });
     return launch_status("scd_pack_nchw");
 }
 
@@ -615,9 +606,12 @@ extern "C" int scd_maxpool2_fwd(scd_nhwc_t x, scd_nhwc_t y, uint8_t *idx, scd_st
         return SCD_ERR_ARG;
     }
     const int64_t rows = int64_t(y.n) * y.h;
-    hipLaunchKernelGGL(maxpool2_fwd_kernel<false>, row_grid(y.w * (y.c / 4), rows), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(x.data), x.h, x.w, x.ldc, static_cast<float *>(y.data), y.h, y.w,
-                       y.ldc, idx, y.c, int(rows), make_fastdiv(uint32_t(y.c / 4)), nullptr, nullptr, 1);
+    const int dt = common_dtype("maxpool2_fwd", {&x, &y});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL((maxpool2_fwd_kernel<false, T>), row_grid(y.w * (y.c / 4), rows), dim3(256), 0,
+                                  as_stream(stream), view_ptr<const T>(x), x.h, x.w, x.ldc, view_ptr<T>(y), y.h, y.w,
+                                  y.ldc, idx, y.c, int(rows), make_fastdiv(uint32_t(y.c / 4)), nullptr, nullptr, 1));
     return launch_status("scd_maxpool2_fwd");
 }
 
@@ -632,9 +626,13 @@ extern "C" int scd_bn_relu_maxpool2_fwd(scd_nhwc_t x, int32_t nseg, const float 
         return SCD_ERR_ARG;
     }
     const int64_t rows = int64_t(y.n) * y.h;
-    hipLaunchKernelGGL(maxpool2_fwd_kernel<true>, row_grid(y.w * (y.c / 4), rows), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(x.data), x.h, x.w, x.ldc, static_cast<float *>(y.data), y.h, y.w,
-                       y.ldc, idx, y.c, int(rows), make_fastdiv(uint32_t(y.c / 4)), scale, shift, x.n / nseg);
+    const int dt = common_dtype("bn_relu_maxpool2_fwd", {&x, &y});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL((maxpool2_fwd_kernel<true, T>), row_grid(y.w * (y.c / 4), rows), dim3(256), 0,
+                                  as_stream(stream), view_ptr<const T>(x), x.h, x.w, x.ldc, view_ptr<T>(y), y.h, y.w,
+                                  y.ldc, idx, y.c, int(rows), make_fastdiv(uint32_t(y.c / 4)), scale, shift,
+                                  x.n / nseg));
     return launch_status("scd_bn_relu_maxpool2_fwd");
 }
 
@@ -658,11 +656,14 @@ extern "C" int scd_feature_grad(scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gs
         }
     }
     const int64_t rows = int64_t(gx.n) * gx.h;
-    hipLaunchKernelGGL(feature_grad_kernel, row_grid(gx.w * (gx.c / 4), rows), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(gy.data), gy.h, gy.w, gy.ldc, idx,
-                       static_cast<const float *>(gskip.data), gskip.n > 0 ? gskip.n : 1, gskip.ldc, skip_mode,
-                       static_cast<float *>(gx.data), gx.h, gx.w, gx.ldc, gx.c, accumulate, int(rows),
-                       make_fastdiv(uint32_t(gx.c / 4)));
+    const int dt = common_dtype("feature_grad", {&gy, &gskip, &gx});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL(feature_grad_kernel<T>, row_grid(gx.w * (gx.c / 4), rows), dim3(256), 0,
+                                  as_stream(stream), view_ptr<const T>(gy), gy.h, gy.w, gy.ldc, idx,
+                                  view_ptr<const T>(gskip), gskip.n > 0 ? gskip.n : 1, gskip.ldc, skip_mode,
+                                  view_ptr<T>(gx), gx.h, gx.w, gx.ldc, gx.c, accumulate, int(rows),
+                                  make_fastdiv(uint32_t(gx.c / 4))));
     return launch_status("scd_feature_grad");
 }
 
@@ -675,9 +676,12 @@ extern "C" int scd_siamese_diff(scd_nhwc_t a, scd_nhwc_t d, scd_stream_t stream)
         return SCD_ERR_ARG;
     }
     const int64_t rows = int64_t(d.n) * d.h;
-    hipLaunchKernelGGL(siamese_diff_kernel<false>, row_grid(d.w * (d.c / 4), rows), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(a.data), a.ldc, static_cast<float *>(d.data), d.ldc, d.c, d.w,
-                       pixels(d), int(rows), make_fastdiv(uint32_t(d.c / 4)), nullptr, nullptr);
+    const int dt = common_dtype("siamese_diff", {&a, &d});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL((siamese_diff_kernel<false, T>), row_grid(d.w * (d.c / 4), rows), dim3(256), 0,
+                                  as_stream(stream), view_ptr<const T>(a), a.ldc, view_ptr<T>(d), d.ldc, d.c, d.w,
+                                  pixels(d), int(rows), make_fastdiv(uint32_t(d.c / 4)), nullptr, nullptr));
     return launch_status("scd_siamese_diff");
 }
 
@@ -692,9 +696,12 @@ extern "C" int scd_bn_relu_siamese_diff(scd_nhwc_t a, const float *scale, const 
         return SCD_ERR_ARG;
     }
     const int64_t rows = int64_t(d.n) * d.h;
-    hipLaunchKernelGGL(siamese_diff_kernel<true>, row_grid(d.w * (d.c / 4), rows), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(a.data), a.ldc, static_cast<float *>(d.data), d.ldc, d.c, d.w,
-                       pixels(d), int(rows), make_fastdiv(uint32_t(d.c / 4)), scale, shift);
+    const int dt = common_dtype("bn_relu_siamese_diff", {&a, &d});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL((siamese_diff_kernel<true, T>), row_grid(d.w * (d.c / 4), rows), dim3(256), 0,
+                                  as_stream(stream), view_ptr<const T>(a), a.ldc, view_ptr<T>(d), d.ldc, d.c, d.w,
+                                  pixels(d), int(rows), make_fastdiv(uint32_t(d.c / 4)), scale, shift));
     return launch_status("scd_bn_relu_siamese_diff");
 }
 
@@ -708,8 +715,9 @@ static int conv1x1_fwd_run(const scd_nhwc_t &x, const float *scale, const float 
     const int64_t waves = (npix + (64 / G) * U - 1) / ((64 / G) * U);
     int blocks = int((waves + 3) / 4);
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(conv1x1_fwd_kernel<U>, dim3(blocks), dim3(256), 0, s, static_cast<const float *>(x.data), x.ldc,
-                       x.c, x.h * x.w, npix, w, b, n_out, G, scale, shift, npix / nseg, out);
+    SCD_WITH_T(x.dtype, T,
+               hipLaunchKernelGGL((conv1x1_fwd_kernel<U, T>), dim3(blocks), dim3(256), 0, s, view_ptr<const T>(x),
+                                  x.ldc, x.c, x.h * x.w, npix, w, b, n_out, G, scale, shift, npix / nseg, out));
     return launch_status("scd_conv1x1_fwd");
 }
 }  // namespace scd
@@ -755,6 +763,7 @@ extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, 
         set_error("conv1x1_bwd: gx shape mismatch");
         return SCD_ERR_ARG;
     }
+    if (common_dtype("conv1x1_bwd", {&x, &gx}) < 0) return SCD_ERR_ARG;
     if ((gw || gb) && (!ws || ws_bytes < scd_conv1x1_workspace_bytes(x, n_out))) {
         set_error("conv1x1_bwd: workspace too small");
         return SCD_ERR_WORKSPACE;
@@ -764,8 +773,9 @@ extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, 
     const int hw = x.h * x.w;
     if (gx.data) {
         const int64_t total = npix * (x.c / 4);
-        hipLaunchKernelGGL(conv1x1_bwd_dx_kernel, dim3(grid_for(total)), dim3(256), 0, s, gout, n_out, hw, w,
-                           static_cast<float *>(gx.data), gx.ldc, x.c, accumulate, total);
+        SCD_WITH_T(gx.dtype, T,
+                   hipLaunchKernelGGL(conv1x1_bwd_dx_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, gout, n_out,
+                                      hw, w, view_ptr<T>(gx), gx.ldc, x.c, accumulate, total));
     }
     float *rec = static_cast<float *>(ws);
     const size_t wbytes = weighted_channel_sum_bytes(x);
@@ -863,9 +873,12 @@ extern "C" int scd_bn_relu_pool_diff(scd_nhwc_t a, const float *scale, const flo
         return SCD_ERR_ARG;
     }
     const int64_t rows = int64_t(d.n) * y.h;
-    hipLaunchKernelGGL(bn_relu_pool_diff_kernel, row_grid(y.w * (y.c / 4), rows), dim3(256), 0, as_stream(stream),
-                       static_cast<const float *>(a.data), a.h, a.w, a.ldc, static_cast<float *>(y.data), y.h, y.w,
-                       y.ldc, idx, static_cast<float *>(d.data), d.ldc, d.c, d.n, int(rows),
-                       make_fastdiv(uint32_t(y.c / 4)), scale, shift);
+    const int dt = common_dtype("bn_relu_pool_diff", {&a, &d, &y});
+    if (dt < 0) return SCD_ERR_ARG;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL(bn_relu_pool_diff_kernel<T>, row_grid(y.w * (y.c / 4), rows), dim3(256), 0,
+                                  as_stream(stream), view_ptr<const T>(a), a.h, a.w, a.ldc, view_ptr<T>(y), y.h, y.w,
+                                  y.ldc, idx, view_ptr<T>(d), d.ldc, d.c, d.n, int(rows),
+                                  make_fastdiv(uint32_t(y.c / 4)), scale, shift));
     return launch_status("scd_bn_relu_pool_diff");
 }

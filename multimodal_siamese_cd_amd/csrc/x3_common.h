@@ -2,6 +2,8 @@
 // exact three-way bf16 split and raw buffer loads.
 #pragma once
 
+#include <type_traits>
+
 #include "conv_common.h"
 
 namespace scd {
@@ -109,6 +111,58 @@ __device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 }
 __device__ __forceinline__ u32x4 bload4u(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+// 8 bytes: one bf16 channel quad (SB: bf16 activation storage)
+__device__ __forceinline__ u32x2 bload2u(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ void gstore2u(void *p, u32x2 v) { *(__attribute__((address_space(1))) u32x2 *)(p) = v; }
+
+// Kernel storage of the activation operands and outputs: fp32 (SB false) or bf16 (SB true: ABI 6 bf16 views, the bf16
+// configs).  A bf16 channel quad is staged as its bits (it is already the bf16 operand), or unpacked for an input
+// transform and rounded back; outputs are rounded once (RNE) and the fused statistics are taken of the stored values.
+template <bool SB>
+using StageT = typename std::conditional<SB, u32x2, f32x4>::type;
+template <bool SB>
+__device__ __forceinline__ StageT<SB> bload_q(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    if constexpr (SB)
+        return bload2u(r, off);
+    else
+        return bload4(r, off);
+}
+// bf16 bits of a staged quad (SB: as loaded; fp32: rounded to nearest)
+template <bool SB>
+__device__ __forceinline__ u32x2 stage_bits(const StageT<SB> &v) {
+    if constexpr (SB)
+        return v;
+    else
+        return u32x2{cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3])};
+}
+template <bool SB>
+__device__ __forceinline__ f32x4 stage_f32(const StageT<SB> &v) {
+    if constexpr (SB)
+        return unpk_bf16x4(v);
+    else
+        return v;
+}
+// Store one output channel quad at element offset e of `dst` (fp32 or bf16); returns the stored value.
+template <bool SB>
+__device__ __forceinline__ f32x4 store_q(float *dst, size_t e, f32x4 v) {
+    if constexpr (SB) {
+        const u32x2 pk = pk_bf16x4(v);
+        gstore2u(reinterpret_cast<bf16_t *>(dst) + e, pk);
+        return unpk_bf16x4(pk);
+    } else {
+        *(__attribute__((address_space(1))) f32x4 *)(dst + e) = v;
+        return v;
+    }
+}
+template <bool SB>
+__device__ __forceinline__ f32x4 load_q(const float *src, size_t e) {
+    if constexpr (SB)
+        return ld4(reinterpret_cast<const bf16_t *>(src) + e);
+    else
+        return *(const __attribute__((address_space(1))) f32x4 *)(src + e);
 }
 
 

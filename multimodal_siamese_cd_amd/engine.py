@@ -172,6 +172,53 @@ def _empty(shape, like: torch.Tensor, dtype=_F32):
     return torch.empty(shape, device=like.device, dtype=dtype)
 
 
+def _act(shape, like: torch.Tensor):
+    """An activation / gradient buffer in the storage type of `like` (fp32, or bf16 under bf16 storage)."""
+    return torch.empty(shape, device=like.device, dtype=like.dtype)
+
+
+# Activation and gradient storage of the model being run (act_storage_for / storage_scope): the input packing creates
+# its NHWC tensors in this type, and every buffer downstream inherits the type of the activation it derives from.
+_STORAGE = contextvars.ContextVar('scd_act_storage', default=_F32)
+
+
+@contextlib.contextmanager
+def storage_scope(dtype):
+    tok = _STORAGE.set(dtype)
+    try:
+        yield
+    finally:
+        _STORAGE.reset(tok)
+
+
+def act_storage_for(cfg, math: str | None = None):
+    """torch dtype of a model's activations and gradients in HBM: bf16 for the bf16 arithmetic when every conv of the
+    model has a bf16-storage kernel (TOPOLOGY channel counts multiples of 64, input bands <= 16: the bf16 halo16, c16,
+    gather16 and ConvTranspose weight-grad kernels), else fp32.  MODEL.ACT_STORAGE ('fp32' / 'bf16') overrides."""
+    math = math or conv_math_for(cfg)
+    want = str(cfg.MODEL.get('ACT_STORAGE', '') or '').lower()
+    if want in ('fp32', 'f32', 'float32'):
+        return _F32
+    ok = math == 'bf16' and all(int(c) % 64 == 0 for c in cfg.MODEL.TOPOLOGY)
+    if want in ('bf16', 'bfloat16'):
+        if not ok:
+            raise ValueError("MODEL.ACT_STORAGE bf16 needs MODEL.PRECISION bf16 and TOPOLOGY channels in multiples "
+                             "of 64")
+        return torch.bfloat16
+    if want:
+        raise ValueError(f"MODEL.ACT_STORAGE {want!r}: expected 'fp32' or 'bf16'")
+    return torch.bfloat16 if ok else _F32
+
+
+def storage_for_input(dtype, h: int, w: int, levels: int):
+    """The storage a forward on (h, w) tiles runs in: bf16 storage needs every level's map tiled by the bf16 kernels
+    (the deepest, h / 2^(levels - 1), a multiple of 16 both ways); other tiles (e.g. full-AOI evaluation) run fp32."""
+    if dtype == _F32:
+        return _F32
+    g = 16 << max(levels - 1, 0)
+    return dtype if h % g == 0 and w % g == 0 else _F32
+
+
 def _ws(nbytes: int, like: torch.Tensor):
     return torch.empty(int(nbytes), device=like.device, dtype=torch.uint8)
 
@@ -349,7 +396,7 @@ def _conv3x3_stats(x: torch.Tensor, wpk: torch.Tensor, bias, n_out: int, want: b
     `in_bn` = (scale, shift, nseg): x is the previous conv's output, read through its BatchNorm + ReLU.
     `src_bound` (h2): the bound of x as read."""
     n, h, w, _ = x.shape
-    y = _empty((n, h, w, n_out), x) if y is None else y
+    y = _act((n, h, w, n_out), x) if y is None else y
     tiles = None
     if want:
         ntiles, tpx = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(y), src_bound=src_bound)
@@ -390,7 +437,7 @@ def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool, mate
     st0 = _bn_forward(y0, bn0, nseg, training, t0, b0)
     wpk1 = packed_conv3x3(conv1.weight, 0)
     n, h, w, _ = y0.shape
-    y1 = _empty((n, h, w, conv1.out_channels), y0)
+    y1 = _act((n, h, w, conv1.out_channels), y0)
     if _can_fuse_input_bn(y0, wpk1, y1, st0, save, b0):
         a0 = None  # never materialised: conv1 and its weight grad apply BN0 + ReLU while staging y0
         y1, t1 = _conv3x3_stats(y0, wpk1, conv1.bias, conv1.out_channels, _bn_uses_batch_stats(bn1, training),
@@ -492,7 +539,7 @@ def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Te
     offers them.  Returns (ga0, tiles or None, bound of ga0 or None).  `pool` (h2): the epilogue also raises a bound
     of ga0 where the kernel runs h2 (for a consumer that forms BN0's dy itself, _bn_backward_coef)."""
     n, h, w, _ = dy1.shape
-    ga0 = _empty((n, h, w, n_out), dy1)
+    ga0 = _act((n, h, w, n_out), dy1)
     gb = None
     if pool is not None and hip.igemm_arith(nhwc(dy1), h, w, 1, TAPS_3X3, wpk, n_out, nhwc(ga0),
                                             src_bound=src_bound) == 'h2':
@@ -548,7 +595,7 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None):
         if x.shape[3] != conv0.in_channels:
             raise RuntimeError("input-gradient through a channel-padded first layer is not supported")
         n, h, w, _ = dy0.shape
-        gx = _empty((n, h, w, conv0.in_channels), dy0)
+        gx = _act((n, h, w, conv0.in_channels), dy0)
         wd = packed_conv3x3(conv0.weight, 1)
         # h2: the kernel raises gx's bound as it stores (the decoder's ConvT data grad reads gx through it)
         gxb = None
@@ -588,7 +635,7 @@ def pack_pair(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_count:
         raise NotImplementedError("input gradients are not computed by the HIP path")
     b, c, h, w = x_t1.shape
     c_count = c - c_begin if c_count is None else c_count
-    out = torch.empty((2 * b, h, w, pad_in(c_count)), device=x_t1.device, dtype=_F32)
+    out = torch.empty((2 * b, h, w, pad_in(c_count)), device=x_t1.device, dtype=_STORAGE.get())
     bound = _input_bound(out)
     hip.pack_nchw(x_t1.float(), c_begin, c_count, out[:b], bound=bound)
     hip.pack_nchw(x_t2.float(), c_begin, c_count, out[b:], bound=bound)
@@ -603,7 +650,7 @@ def pack_stream(x_t1: torch.Tensor, x_t2: torch.Tensor, c_begin: int = 0, c_coun
     b, c, h, w = x_t1.shape
     c_count = c - c_begin if c_count is None else c_count
     cp = pad_in(2 * c_count)
-    out = torch.empty((b, h, w, cp), device=x_t1.device, dtype=_F32)
+    out = torch.empty((b, h, w, cp), device=x_t1.device, dtype=_STORAGE.get())
     # t1 bands -> channels [0, nb) (zero-padding the rest), then t2 bands -> [nb, 2nb)
     bound = _input_bound(out)
     hip.pack_nchw(x_t1.float(), c_begin, c_count, out, 0, cp, bound=bound)  # t1 bands -> [0, nb), zero-pad to cp
@@ -657,7 +704,7 @@ class EncoderLevelFn(torch.autograd.Function):
         outs, idx = (a,), None
         if not meta.last:
             n, h, w, c = a.shape
-            nxt = _empty((n, h // 2, w // 2, c), a)
+            nxt = _act((n, h // 2, w // 2, c), a)
             idx = _empty((n, h // 2, w // 2, c), a, dtype=torch.uint8)
             hip.maxpool2_fwd(nhwc(a), nhwc(nxt), idx)  # the pooled map keeps the level's bound
             outs = (a, nxt)
@@ -724,12 +771,12 @@ class SiameseLevelFn(torch.autograd.Function):
                                             pool=meta.pool, x_bound=meta.x_bound)
         meta.out_bound = bound
         n2, h, w, c = y1.shape
-        buf = _empty((n2 // 2, h, w, c + meta.extra), y1)
+        buf = _act((n2 // 2, h, w, c + meta.extra), y1)
         d = buf[..., :c] if meta.extra else buf
         sc, sh = _two_seg(st1)
         idx = nxt = None
         if not meta.last:
-            nxt = _empty((n2, h // 2, w // 2, c), y1)
+            nxt = _act((n2, h // 2, w // 2, c), y1)
             idx = _empty((n2, h // 2, w // 2, c), y1, dtype=torch.uint8)
         if nxt is not None and h % 2 == 0 and w % 2 == 0 and _OPTS['pool_diff']:
             hip.bn_relu_pool_diff(nhwc(y1), sc, sh, nhwc(buf, 0, c), nhwc(nxt), idx)  # one read of y1
@@ -784,14 +831,14 @@ class SiameseDiffFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, feat):
         n2, h, w, c = feat.shape
-        d = _empty((n2 // 2, h, w, c), feat)
+        d = _act((n2 // 2, h, w, c), feat)
         hip.siamese_diff(nhwc(feat), nhwc(d))
         ctx.shape = feat.shape
         return d
 
     @staticmethod
     def backward(ctx, g):
-        gf = _empty(tuple(ctx.shape), g)
+        gf = _act(tuple(ctx.shape), g)
         hip.feature_grad(hip._NULL, None, nhwc(g), 1, nhwc(gf))
         return gf
 
@@ -833,7 +880,7 @@ class DecoderFn(torch.autograd.Function):
                     and skip.stride(2) == cs + cto):
                 cat = buf  # the encoder wrote the skip into channels [0, cs) already (zero-copy cat)
             else:
-                cat = _empty((b, h, w, cs + cto), skip)
+                cat = _act((b, h, w, cs + cto), skip)
                 hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
             wT = hip.pack_convT2x2(convT.weight.detach(), 0)
             # h2: the concat's own bound, seeded with the skip's and raised by the ConvT epilogue to max |up| (F.pad's
@@ -848,7 +895,7 @@ class DecoderFn(torch.autograd.Function):
             epi_bound = cat_bound if hip.conv_math() != 'f32' and cu % 16 == 0 else None
             if pad_y or pad_x:
                 # ConvT into its own map, then F.pad's zero border and placement in one window copy
-                upm = _empty((b, 2 * hc, 2 * wc, cto), skip)
+                upm = _act((b, 2 * hc, 2 * wc, cto), skip)
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(upm), store_mode=1,
                                src_bound=cur_bound, dst_bound=epi_bound)
                 hip.window_copy(nhwc(upm), nhwc(cat, cs, cto), -(pad_y // 2), -(pad_x // 2))
@@ -915,7 +962,7 @@ class DecoderFn(torch.autograd.Function):
             b, hc, wc, cu = cur.shape
             bb, hh, ww, _ = g_cat.shape
             if (hh, ww) != (2 * hc, 2 * wc):  # backward of F.pad: crop the ConvT's window out of g_cat
-                g_up_t = _empty((b, 2 * hc, 2 * wc, cto), g_cat)
+                g_up_t = _act((b, 2 * hc, 2 * wc, cto), g_cat)
                 hip.window_copy(nhwc(g_cat, cs, cto), nhwc(g_up_t), (hh - 2 * hc) // 2, (ww - 2 * wc) // 2)
                 g_up = nhwc(g_up_t)
                 hh, ww = 2 * hc, 2 * wc
@@ -1054,7 +1101,7 @@ class BlockFn(torch.autograd.Function):
         cur, idx = x, None
         if meta.maxpool:
             n, h, w, c = x.shape
-            cur = _empty((n, h // 2, w // 2, c), x)
+            cur = _act((n, h // 2, w // 2, c), x)
             idx = _empty((n, h // 2, w // 2, c), x, dtype=torch.uint8)
             hip.maxpool2_fwd(nhwc(x), nhwc(cur), idx)
         a, sv, _, _, _ = _dc_forward(cur, meta.dc, 1, meta.training, meta.save, pool=pool)
@@ -1072,7 +1119,7 @@ class BlockFn(torch.autograd.Function):
             need_dx = ctx.needs_input_grad[0]
             gx, pg = _dc_backward(g.contiguous(), sv, meta.dc, need_dx=need_dx, pool=_bounds(g))
             if need_dx and meta.maxpool:  # MaxPool2d backward through the argmax bytes
-                gfull = _empty(xshape, g)
+                gfull = _act(xshape, g)
                 hip.feature_grad(nhwc(gx), idx, hip._NULL, 0, nhwc(gfull))
                 gx = gfull
         ctx.saved = None
@@ -1099,7 +1146,7 @@ class CatFn(torch.autograd.Function):
     def forward(ctx, *xs):
         n, h, w, _ = xs[0].shape
         cs = [x.shape[3] for x in xs]
-        out = _empty((n, h, w, sum(cs)), xs[0])
+        out = _act((n, h, w, sum(cs)), xs[0])
         off = 0
         for x, c in zip(xs, cs):
             hip.feature_grad(hip._NULL, None, nhwc(x), 0, nhwc(out, off, c))

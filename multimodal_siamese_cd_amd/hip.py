@@ -18,9 +18,15 @@ LIB_PATH = os.environ.get("SCD_LIB") or os.path.join(os.path.dirname(os.path.abs
 
 
 class NHWC(ctypes.Structure):
-    """scd_nhwc_t: channel-slice view of an NHWC fp32 tensor."""
+    """scd_nhwc_t: channel-slice view of an NHWC fp32 or bf16 tensor (dtype: SCD_DT_F32 0 / SCD_DT_BF16 1, ABI 6)."""
 
-    _fields_ = [("data", c_void_p), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32), ("ldc", c_int32)]
+    _fields_ = [("data", c_void_p), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32), ("ldc", c_int32),
+                ("dtype", c_int32)]
+
+
+# element types of NHWC views (enum scd_dtype); activations and gradients of the bf16 configs are stored as bf16
+DT_F32, DT_BF16 = 0, 1
+_VIEW_DTYPES = {torch.float32: (DT_F32, 4), torch.bfloat16: (DT_BF16, 2)}
 
 
 class BNBWD(ctypes.Structure):
@@ -88,7 +94,7 @@ TAPS_3X3 = ([-1, -1, -1, 0, 0, 0, 1, 1, 1], [-1, 0, 1, -1, 0, 1, -1, 0, 1])  # t
 TAPS_1 = ([0], [0])
 TAPS_2X2 = ([0, 0, 1, 1], [0, 1, 0, 1])  # t = i*2 + j
 
-_NULL = NHWC(None, 0, 0, 0, 0, 0)
+_NULL = NHWC(None, 0, 0, 0, 0, 0, 0)
 
 _lib = None
 _dev_checked: set = set()
@@ -189,7 +195,7 @@ _SIGS = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
-ABI_VERSION = 5  # SCD_ABI_VERSION of include/scd.h
+ABI_VERSION = 6  # SCD_ABI_VERSION of include/scd.h
 
 
 def load_library(path: str = LIB_PATH):
@@ -252,18 +258,20 @@ def _ptr(t):
 
 
 def nhwc(t: torch.Tensor, c_off: int = 0, c: int | None = None) -> NHWC:
-    """View a 4-D [n, h, w, C] tensor (stride(3) == 1, rows of ldc = stride(2)) as scd_nhwc_t."""
+    """View a 4-D [n, h, w, C] fp32 or bf16 tensor (stride(3) == 1, rows of ldc = stride(2)) as scd_nhwc_t."""
     if t is None:
         return _NULL
-    if t.dim() != 4 or t.dtype != torch.float32 or t.stride(3) != 1:
-        raise ValueError(f"expected fp32 NHWC tensor with unit channel stride, got {tuple(t.shape)} {t.stride()}")
+    if t.dim() != 4 or t.dtype not in _VIEW_DTYPES or t.stride(3) != 1:
+        raise ValueError(f"expected an fp32 / bf16 NHWC tensor with unit channel stride, got {tuple(t.shape)} "
+                         f"{t.dtype} {t.stride()}")
     n, h, w, cc = t.shape
     ldc = t.stride(2)
     if (h > 1 and t.stride(1) != w * ldc) or (n > 1 and t.stride(0) != h * w * ldc):
         raise ValueError(f"tensor is not an NHWC channel slice: shape {tuple(t.shape)} stride {t.stride()}")
     if c is None:
         c = cc - c_off
-    v = NHWC(t.data_ptr() + 4 * c_off, n, h, w, c, ldc)
+    dt, eb = _VIEW_DTYPES[t.dtype]
+    v = NHWC(t.data_ptr() + eb * c_off, n, h, w, c, ldc, dt)
     v._owner = t  # keep the storage alive at least until the view has been handed to a launch
     return v
 
@@ -284,7 +292,8 @@ def pack_nchw(src: torch.Tensor, c_begin: int, c_count: int, dst: torch.Tensor, 
     n, c, h, w = src.shape
     src = src.contiguous()
     cc = dst.shape[3] - dst_c_off if dst_c is None else dst_c
-    v = NHWC(dst.data_ptr() + 4 * dst_c_off, dst.shape[0], dst.shape[1], dst.shape[2], cc, dst.stride(2))
+    dt, eb = _VIEW_DTYPES[dst.dtype]
+    v = NHWC(dst.data_ptr() + eb * dst_c_off, dst.shape[0], dst.shape[1], dst.shape[2], cc, dst.stride(2), dt)
     _check(lib().scd_pack_nchw(src.data_ptr(), n, c, h, w, c_begin, c_count, v, _ptr(bound), _stream()),
            "scd_pack_nchw")
 

@@ -147,11 +147,14 @@ class _HipNet(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.conv_math = engine.conv_math_for(cfg)
+        # activations / gradients in HBM: bf16 for the bf16 configs (engine.act_storage_for), fp32 otherwise
+        self.act_storage = engine.act_storage_for(cfg, self.conv_math)
         object.__setattr__(self, '_twin_topo', _padded_topology(cfg))
         object.__setattr__(self, '_twin', None)
 
     def forward(self, x_t1, x_t2):
-        with hip.conv_scope(self.conv_math):
+        st = engine.storage_for_input(self.act_storage, x_t1.shape[-2], x_t1.shape[-1], len(self.cfg.MODEL.TOPOLOGY))
+        with hip.conv_scope(self.conv_math), engine.storage_scope(st):
             if self._twin_topo is not None:
                 return self._twin_forward(x_t1, x_t2)
             return self._forward(x_t1, x_t2)

@@ -246,18 +246,19 @@ def r16(t):
 
 class _Conv16(torch.autograd.Function):
     """A 3x3 conv with the bf16 kernels' arithmetic: bf16-rounded operands in forward, data-grad and weight-grad,
-    exact products, fp32 (here double) accumulation."""
+    exact products, fp32 (here double) accumulation; the output and the data grad rounded to bf16 as bf16 storage
+    (engine.act_storage_for) keeps them in HBM."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
-        return _CONV2D(r16(x).double(), r16(w).double(), None, padding=1).float() + b[None, :, None, None]
+        return r16(_CONV2D(r16(x).double(), r16(w).double(), None, padding=1).float() + b[None, :, None, None])
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         g16 = r16(gy).double()
-        gx = torch.nn.grad.conv2d_input(x.shape, r16(w).double(), g16, padding=1).float()
+        gx = r16(torch.nn.grad.conv2d_input(x.shape, r16(w).double(), g16, padding=1).float())
         gw = torch.nn.grad.conv2d_weight(r16(x).double(), w.shape, g16, padding=1).float()
         return gx, gw, gy.sum((0, 2, 3))
 

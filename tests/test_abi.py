@@ -64,7 +64,7 @@ def test_struct_layout_matches_c_compiler(tmp_path):
     if cc is None:
         pytest.skip('no host C compiler')
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    fields = {'scd_nhwc_t': (hip.NHWC, ['data', 'n', 'h', 'w', 'c', 'ldc']),
+    fields = {'scd_nhwc_t': (hip.NHWC, ['data', 'n', 'h', 'w', 'c', 'ldc', 'dtype']),
               'scd_igemm_t': (hip.IGEMM, [f[0] for f in hip.IGEMM._fields_]),
               'scd_wgrad_t': (hip.WGRAD, [f[0] for f in hip.WGRAD._fields_])}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "scd.h"', 'int main(void) {']
