@@ -43,6 +43,18 @@ def _checked_loss(value: float, cfg, step: int) -> float:
     return value
 
 
+def _check_finite(bad, cfg, step: int, device) -> None:
+    """Raise on every rank when any step since the last check produced a non-finite loss on any rank: the flag is
+    max-all-reduced, so no rank is left waiting in a DDP collective while another one stops."""
+    flag = torch.zeros(1, device=device) if bad is None else bad.float().reshape(1)
+    if parallel.is_distributed():
+        torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+    if flag.item() > 0:
+        raise FloatingPointError(f"non-finite training loss within the {int(cfg.LOG_FREQ)} steps up to step {step} "
+                                 f"(conv arithmetic {engine.conv_math_for(cfg)!r}; MODEL.CONV_MATH x3 is the bound-free "
+                                 "fp32-class alternative)")
+
+
 def run_training(cfg, device, max_steps: int | None = None):
     rank, _, world = parallel.env_rank()
     net = networks.create_network(cfg)
@@ -64,6 +76,7 @@ def run_training(cfg, device, max_steps: int | None = None):
         loader = datasets.DeviceDataLoader(ds, int(cfg.TRAINER.BATCH_SIZE), device, shuffle=bool(cfg.DATALOADER.SHUFFLE),
                                            num_workers=int(cfg.DATALOADER.get('NUM_WORKER', 0)))
         steps_per_epoch = len(loader)
+    bad = None
     for epoch in range(1, epochs + 1):
         start = timeit.default_timer()
         losses = []
@@ -80,11 +93,16 @@ def run_training(cfg, device, max_steps: int | None = None):
             loss.backward()
             optimizer.step()
             losses.append(loss.detach())
+            # device-side non-finite flag of every step (no host sync); checked on every rank at the log step
+            bad = ~torch.isfinite(loss.detach()) if bad is None else bad | ~torch.isfinite(loss.detach())
             global_step += 1
             epoch_float = global_step / steps_per_epoch
             if cfg.DEBUG:
                 _evaluate(net, cfg, device, ('test',), epoch_float, global_step, rank)
                 break
+            if global_step % int(cfg.LOG_FREQ) == 0:
+                _check_finite(bad, cfg, global_step, device)  # every rank raises together (max over ranks)
+                bad = None
             if global_step % int(cfg.LOG_FREQ) == 0 and rank == 0:
                 t = timeit.default_timer() - start
                 mean_loss = _checked_loss(torch.stack(losses).mean().item(), cfg, global_step)

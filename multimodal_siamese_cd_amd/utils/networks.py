@@ -202,11 +202,13 @@ class _HipNet(nn.Module):
             object.__setattr__(self, '_twin', tw)
             object.__setattr__(self, '_twin_maps', None)
         if next(tw.buffers()).device != torch.device(dev):
-            tw.to(dev)
+            tw.to(dev)  # buffers only: the twin's parameters are plain attributes, set per forward
             object.__setattr__(self, '_twin_maps', None)
         if self._twin_maps is None:
-            tp = dict(tw.named_parameters())
-            tw_params = {k: tuple(v.shape) for k, v in tp.items()}
+            tw_params = getattr(self, '_twin_shapes', None)
+            if tw_params is None:  # first build: record the twin's parameter shapes (device-independent)
+                tw_params = {k: tuple(v.shape) for k, v in tw.named_parameters()}
+                object.__setattr__(self, '_twin_shapes', tw_params)
             for mod in tw.modules():  # from now on the twin's parameters are plain tensor attributes set per forward
                 for k in list(mod._parameters):
                     v = mod._parameters.pop(k)

@@ -352,3 +352,34 @@ def test_bench_distributed_fields_world2():
         assert r['marks'] == r['n_params']  # every parameter's gradient stamped once per backward
         for e in r['exposed']:
             assert 0.0 < e['last_grad_ms'] <= e['backward_ms']
+
+
+def _worker_nonfinite(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    parallel.init_distributed('gloo')
+    from multimodal_siamese_cd_amd import train_supervised
+    from multimodal_siamese_cd_amd.utils import experiment_manager as em
+    cfg = em.load_cfg('debug')
+    dev = torch.device('cpu')
+    train_supervised._check_finite(torch.tensor(False), cfg, 10, dev)  # all finite: no raise
+    bad = torch.tensor(rank == 1)  # only rank 1 saw a NaN loss
+    raised = False
+    try:
+        train_supervised._check_finite(bad, cfg, 20, dev)
+    except FloatingPointError:
+        raised = True
+    torch.save({'raised': raised}, os.path.join(out_dir, f'rank{rank}.pt'))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_nonfinite_loss_stops_every_rank_world2():
+    """train_supervised's per-step non-finite flag is max-all-reduced at the log step: a NaN loss on one rank stops
+    every rank together (none is left blocked in a DDP collective)."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_nonfinite, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+    assert all(r['raised'] for r in res)

@@ -1057,3 +1057,31 @@ def test_batched_weight_pack_equals_standalone(dev, arith):
                 assert torch.equal(a, b), (tuple(w.shape), mode)
     finally:
         hip.set_conv_math(prev)
+
+
+@pytest.mark.parametrize('math', ['h2', 'bf16'])
+def test_wgrad_repeat_runs_identical(dev, math):
+    """The surviving halo weight grads (the 16x16x32 kernels) run to run: eight launches per plan, each into a freshly
+    NaN-filled slab workspace, write every slab element and produce bit-identical slabs (the closed round-2 hunt on
+    the deleted 32x32 kernel, DESIGN 7: a block that skipped part of its slab range, or an LDS reuse race, would show
+    here as a NaN or a changed bit).  A bounded check, not a repeat-until-fail hunt."""
+    from multimodal_siamese_cd_amd import hip
+    for n, h, w, ci, co in [(2, 16, 32, 128, 128), (3, 6, 16, 128, 192)]:
+        g = torch.Generator().manual_seed(ci + co + h)
+        xd = torch.randn(n, h, w, ci, generator=g).to(dev)
+        dyd = torch.randn(n, h, w, co, generator=g).to(dev)
+        bx = by = None
+        if math == 'h2':
+            bx, by = xd.abs().max().reshape(1).clone(), dyd.abs().max().reshape(1).clone()
+        first = None
+        with hip.conv_scope(math):
+            for _ in range(8):
+                d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dyd), hip.nhwc(xd), 1, hip.TAPS_3X3, None, by, bx)
+                slabs = torch.full((nbytes // 4,), float('nan'), device=dev)
+                hip.conv_wgrad(d, slabs)
+                torch.cuda.synchronize()
+                assert not torch.isnan(slabs).any(), (n, h, w, ci, co)
+                if first is None:
+                    first = slabs.clone()
+                else:
+                    assert torch.equal(slabs, first), (n, h, w, ci, co)

@@ -361,3 +361,22 @@ def test_reference_fixtures_reach_the_h2_kernels(dev, monkeypatch, name):
     h2 = [s for s in seen if s[3] == 9 and s[1] % 32 == 0 and s[2] % 64 == 0]
     assert h2 and all(s[4] == 'h2' for s in h2), [s for s in h2 if s[4] != 'h2']
     print(f'{sum(s[4] == "h2" for s in seen)} of {len(seen)} conv launches run h2')
+
+
+def test_padded_twin_survives_a_device_change(dev):
+    """A TOPOLOGY off the channel granule (here [12, 20]) runs a zero-padded twin whose parameters are plain attributes
+    after the first build; moving the twin to another device and back rebuilds only the index maps (the parameter
+    shapes are kept from the first build) and the forward gives the same logits."""
+    from multimodal_siamese_cd_amd.utils import experiment_manager as em, networks
+    cfg = em.load_cfg('debug')
+    cfg.MODEL.TOPOLOGY = [12, 20]
+    torch.manual_seed(0)
+    net = networks.create_network(cfg).to(dev).eval()
+    g = torch.Generator(device=dev).manual_seed(2)
+    x1 = torch.rand(2, 5, 32, 32, device=dev, generator=g)
+    x2 = torch.rand(2, 5, 32, 32, device=dev, generator=g)
+    with torch.no_grad():
+        out0 = net(x1, x2).clone()
+        net.module._twin_ready(torch.device('cpu'))  # the twin moves away: maps rebuilt without its parameters
+        out1 = net(x1, x2)  # and back to the GPU
+    assert torch.equal(out0, out1)
