@@ -175,6 +175,8 @@ int scd_abi_version(void);
 #define SCD_TUNE_HALO16_LATE_LOAD (1u << 27)  /* single-buffered halo16: next chunk's halo loaded at the last tap  */
 #define SCD_TUNE_H2_TILE64_128    (1u << 28)  /* h2, 64..127 outputs of 64-channel sources: 128 x 64 tiles instead
                                                  of 256 x 64 (2x2 waves of 128 px x 32 ch)                          */
+#define SCD_TUNE_HALO16_WS        (1u << 29)  /* h2 1 x N tiles as warp-specialized blocks: one producer wave stages
+                                                 the halo, the compute waves load only weights (128 px tiles)        */
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);

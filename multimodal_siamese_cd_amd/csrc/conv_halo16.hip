@@ -437,6 +437,342 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Warp-specialized h2 halo forward / data grad (SCD_TUNE_HALO16_WS): WAVES_N compute waves of 128 px x 32 ch (the
+// 1 x N wave tiles of igemm_halo16_x3) plus one producer wave per block.  The producer alone loads each 32-channel
+// chunk's halo, applies the input transform, splits it into the fp16 h / pre-scaled m planes and writes them into the
+// other of two LDS buffers while the compute waves run the current chunk.  The compute waves' only vector-memory stream
+// is their own weight fragments, one k-step ahead: vmcnt retires in order per wave, so in igemm_halo16_x3 every weight
+// wait also drained the next chunk's halo loads (about one k-step of MFMAs to hide an HBM latency); here those loads
+// belong to a wave that waits for nothing else.  One barrier per chunk.  Same products, reduction order and epilogue as
+// igemm_halo16_x3<..., NP = 4> (bit-identical outputs and records).
+// ------------------------------------------------------------------------------------------------
+template <int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN>
+__global__ __launch_bounds__(64 * (WAVES_N + 1), OCC) void igemm_halo16_ws(IgemmArgs a) {
+    constexpr int NT = 64 * (WAVES_N + 1);
+    constexpr int WPX = TM * 16, WCH = TN * 16;
+    constexpr int BM = WPX, BN = WAVES_N * WCH;
+    constexpr int TR = BM / TW;
+    constexpr int HWD = TW + 2;
+    constexpr int HR = (TR + 2) * HWD;
+    constexpr int A_CH = HR * 8;               // 16-byte (4-channel) pieces of one 32-channel chunk
+    constexpr int P_PER = (A_CH + 63) / 64;    // per producer lane
+    constexpr int PA = HR * 64;                // one plane
+    constexpr int BUF = 2 * PA;                // h and m planes
+    constexpr int RG = TM >= 8 ? TM / 4 : 1;   // reduction groups per wave (igemm_halo16_x3's order)
+    constexpr int TMG = TM / RG;
+    constexpr int WME = RG;                    // reduction rows of the block (one wave row)
+    constexpr int RED = 2 * WME * BN * 4;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF > RED ? 2 * BUF : RED];
+    float xs = 1.f, xs_inv = 1.f;
+    h2_scale(*a.src_bound, xs, xs_inv);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the role branch is scalar
+    const bool producer = wid == WAVES_N;
+    const int wn = producer ? 0 : wid;
+    const int g = lane >> 4, l16 = lane & 15;
+    int mt, nt;
+    if (a.remap == 2) {
+        const uint32_t L = xcd_swizzle(blockIdx.x, uint32_t(a.grid_m * a.grid_n));
+        nt = int(L / uint32_t(a.grid_m));
+        mt = int(L - uint32_t(nt) * uint32_t(a.grid_m));
+    } else if (a.remap) {
+        const uint32_t L = xcd_swizzle(blockIdx.x, uint32_t(a.grid_m * a.grid_n));
+        mt = int(L / uint32_t(a.grid_n));
+        nt = int(L - uint32_t(mt) * uint32_t(a.grid_n));
+    } else {
+        mt = int(blockIdx.x % uint32_t(a.grid_m));
+        nt = int(blockIdx.x / uint32_t(a.grid_m));
+    }
+    const int tiles_x = a.wo / TW, tiles_y = a.ho / TR;
+    const int img = mt / (tiles_x * tiles_y);
+    const int trem = mt - img * tiles_x * tiles_y;
+    const int ty = trem / tiles_x;
+    const int y0 = ty * TR, x0 = (trem - ty * tiles_x) * TW;
+    const int n0 = nt * BN;
+    const int cpk = a.c / 32;
+    const int nsteps = cpk * a.ntaps;
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (producer) {
+        // ---- the producer: halo of chunk cc + 1 while the compute waves run chunk cc
+        auto soff = [](int row, int col) { return row * 64 + ((((col >> 1) ^ (row >> 1)) & 3) << 4) + ((col & 1) << 3); };
+        const int col = lane & 7;  // the channel piece of every piece of this lane (e = lane + 64 i)
+        uint32_t p_boff[P_PER];
+        int p_off[P_PER];
+#pragma unroll
+        for (int i = 0; i < P_PER; ++i) {
+            const int e = lane + i * 64;
+            const bool in = e < A_CH;
+            const int hp = in ? (e >> 3) : 0;
+            const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
+            const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
+            const bool ok = in && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+            p_boff[i] = ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * 4u : kOOB;
+            p_off[i] = in ? soff(hp, col) : -1;
+        }
+        const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
+        f32x4 ra[P_PER];
+        f32x4 in_sc, in_sh;
+        auto pload = [&](int cc) {
+#pragma unroll
+            for (int i = 0; i < P_PER; ++i) ra[i] = bload4(rs_src, p_boff[i] == kOOB ? kOOB : p_boff[i] + cc * 128u);
+            if constexpr (IN_BN) {
+                const int ch = (img / a.in_seg_imgs) * a.c + cc * 32 + col * 4;
+                in_sc = gload4(a.in_scale + ch) * xs;  // fma(y, sc s, sh s) == s fma(y, sc, sh): s a power of two
+                in_sh = gload4(a.in_shift + ch) * xs;
+            }
+        };
+        auto pstore = [&](int buf) {
+            unsigned char *const sb = smem + buf * BUF;
+#pragma unroll
+            for (int i = 0; i < P_PER; ++i)
+                if ((A_CH % 64 == 0) || p_off[i] >= 0) {
+                    f32x4 x = ra[i];
+                    if constexpr (IN_BN) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            x[q] = p_boff[i] == kOOB ? 0.f : fmaxf(fmaf(x[q], in_sc[q], in_sh[q]), 0.f);
+                    } else {
+                        x *= xs;
+                    }
+                    u32x2 h, m;
+                    split2h_pre(x, h, m);
+                    *reinterpret_cast<u32x2 *>(sb + p_off[i]) = h;
+                    *reinterpret_cast<u32x2 *>(sb + PA + p_off[i]) = m;
+                }
+        };
+        pload(0);
+        pstore(0);
+        __syncthreads();  // buffer 0 holds chunk 0
+        for (int cc = 0; cc < cpk; ++cc) {
+            if (cc + 1 < cpk) {
+                pload(cc + 1);
+                pstore((cc + 1) & 1);  // the buffer chunk cc - 1 used: every compute wave left it (last barrier)
+            }
+            __syncthreads();  // end of chunk cc
+        }
+    } else {
+        // ---- a compute wave: 128 px x 32 ch, weights one k-step ahead in registers
+        const int KS16 = a.K / 16, NB32 = (a.n_out + 31) / 32;
+        const uint32_t wplane_b = uint32_t(a.wplane) * 2u;
+        uint32_t w_base[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int cb = (n0 >> 4) + wn * TN + j;
+            const int nb = cb >> 1;
+            w_base[j] = nb < NB32 ? uint32_t(nb * KS16 + (g >> 1)) * 1024u +
+                                        uint32_t(16 * (cb & 1) + l16 + 32 * (g & 1)) * 16u
+                                  : kOOB;
+        }
+        const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, 2u * wplane_b);
+        auto load_W = [&](int cc, int t, u32x4 (&wq)[2][TN]) {
+            const uint32_t ko = uint32_t(t * cpk + cc) * 2048u;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    wq[p][j] = bload4u(rs_w, w_base[j] == kOOB ? kOOB : w_base[j] + ko + uint32_t(p) * wplane_b);
+        };
+        int a_hr[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int p = i * 16 + l16;
+            a_hr[i] = (p / TW + 1) * HWD + (p % TW) + 1;
+        }
+        u32x4 wq[2][TN];
+        load_W(0, 0, wq);
+        __syncthreads();  // buffer 0 holds chunk 0
+        int cc = 0, t = 0;
+        for (int s = 0; s < nsteps; ++s) {
+            int t1 = t + 1, cc1 = cc;
+            if (t1 == a.ntaps) {
+                t1 = 0;
+                cc1 = cc + 1;
+            }
+            const unsigned char *const sbuf = smem + (cc & 1) * BUF;
+            const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
+            u32x4 wh[TN], wm_[TN], wl[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                wh[j] = wq[0][j];
+                wm_[j] = wq[1][j];
+                wl[j] = f16_down11(wh[j]);
+            }
+            if (s + 1 < nsteps) load_W(cc1, t1, wq);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int hr = a_hr[i] + toff;
+                const int ad = hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
+                const u32x4 xh = *reinterpret_cast<const u32x4 *>(sbuf + ad);
+                const u32x4 xm = *reinterpret_cast<const u32x4 *>(sbuf + PA + ad);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[j][i] = mfma16_f16(wl[j], xm, acc[j][i]);
+                    acc[j][i] = mfma16_f16(wm_[j], xh, acc[j][i]);
+                    acc[j][i] = mfma16_f16(wh[j], xh, acc[j][i]);
+                }
+            }
+            if (t1 == 0) __syncthreads();  // end of chunk cc: the producer has written chunk cc + 1
+            t = t1;
+            cc = cc1;
+        }
+        // undo the operand scales: per-channel weight inverse scales after the planes
+        const float *winv = reinterpret_cast<const float *>(reinterpret_cast<const unsigned char *>(a.wsplit) +
+                                                            2u * wplane_b);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WCH + j * 16 + 4 * g;
+            const f32x4 sc = (n < NB32 * 32 ? gload4(winv + n) : f32x4{0.f, 0.f, 0.f, 0.f}) * xs_inv;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[j][i] *= sc;
+        }
+    }
+
+    // ---- epilogue (igemm_halo16_x3's, the producer joining its barriers only)
+    f32x4 bias4[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WCH + j * 16 + 4 * g;
+        bias4[j] = (!producer && a.bias && n < a.n_out) ? *reinterpret_cast<const f32x4 *>(a.bias + n)
+                                                        : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float omax = 0.f;
+    if (!producer) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int p = i * 16 + l16;
+            const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wn * WCH + j * 16 + 4 * g;
+                if (n < a.n_out) {
+                    const f32x4 v = acc[j][i] + bias4[j];
+                    gstore4(a.dst + pix * a.ldc_d + n, v);
+                    omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+                }
+            }
+        }
+    }
+    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform per wave; the producer adds 0
+
+    if (a.stat_rec) {
+        float *red1 = reinterpret_cast<float *>(smem);  // [WME][BN] sums
+        float *red2 = red1 + WME * BN;                  // [WME][BN] M2
+        if (!producer) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int q = 0; q < RG; ++q) {
+                        float sm = 0.f;
+#pragma unroll
+                        for (int i = q * TMG; i < (q + 1) * TMG; ++i) sm += acc[j][i][r] + bias4[j][r];
+                        sm = row16_sum(sm);
+                        if (l16 == 0) red1[q * BN + wn * WCH + j * 16 + 4 * g + r] = sm;
+                    }
+        }
+        __syncthreads();
+        if (!producer) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int nl = wn * WCH + j * 16 + 4 * g + r;
+                    float sm = 0.f;
+#pragma unroll
+                    for (int w = 0; w < WME; ++w) sm += red1[w * BN + nl];
+                    const float mean = sm * (1.f / float(BM));
+#pragma unroll
+                    for (int qg = 0; qg < RG; ++qg) {
+                        float q = 0.f;
+#pragma unroll
+                        for (int i = qg * TMG; i < (qg + 1) * TMG; ++i) {
+                            const float d = (acc[j][i][r] + bias4[j][r]) - mean;
+                            q = fmaf(d, d, q);
+                        }
+                        q = row16_sum(q);
+                        if (l16 == 0) red2[qg * BN + nl] = q;
+                    }
+                }
+        }
+        __syncthreads();
+        for (int nl = tid; nl < BN; nl += NT) {
+            if (n0 + nl >= a.n_out) continue;
+            float sm = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < WME; ++w) {
+                sm += red1[w * BN + nl];
+                m2 += red2[w * BN + nl];
+            }
+            float *rec = a.stat_rec + (size_t(mt) * a.n_out + n0 + nl) * 2;
+            rec[0] = sm * (1.f / float(BM));
+            rec[1] = m2;
+        }
+    }
+
+    if (a.bb_rec) {
+        float *red1 = reinterpret_cast<float *>(smem);
+        float *red2 = red1 + WME * BN;
+        if (!producer) {
+            const int co = (img / a.bb_seg_imgs) * a.n_out;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wn * WCH + j * 16 + 4 * g;
+                const bool nok = n < a.n_out;
+                const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+                const f32x4 mu = nok ? gload4(a.bb_mean + co + n) : z4, iv = nok ? gload4(a.bb_inv + co + n) : z4;
+                const f32x4 sc = nok ? gload4(a.bb_scale + co + n) : z4, sf = nok ? gload4(a.bb_shift + co + n) : z4;
+#pragma unroll
+                for (int qg = 0; qg < RG; ++qg) {
+                    f32x4 s1 = z4, s2 = z4;
+#pragma unroll
+                    for (int i = qg * TMG; i < (qg + 1) * TMG; ++i) {
+                        const int p = i * 16 + l16;
+                        const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+                        const f32x4 y4 = nok ? gload4(a.bb_y + pix * a.bb_ldy + n) : z4;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float dz = fmaf(y4[r], sc[r], sf[r]) > 0.f ? acc[j][i][r] : 0.f;
+                            s1[r] += dz;
+                            s2[r] += dz * ((y4[r] - mu[r]) * iv[r]);
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float t1 = row16_sum(s1[r]), t2 = row16_sum(s2[r]);
+                        if (l16 == 0) {
+                            red1[qg * BN + wn * WCH + j * 16 + 4 * g + r] = t1;
+                            red2[qg * BN + wn * WCH + j * 16 + 4 * g + r] = t2;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (int nl = tid; nl < BN; nl += NT) {
+            if (n0 + nl >= a.n_out) continue;
+            float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+            for (int w = 0; w < WME; ++w) {
+                t1 += red1[w * BN + nl];
+                t2 += red2[w * BN + nl];
+            }
+            float *rec = a.bb_rec + (size_t(n0 + nl) * a.bb_ntiles + mt) * 2;
+            rec[0] = t1;
+            rec[1] = t2;
+        }
+    }
+}
+
 namespace {
 
 struct H16Cfg {
@@ -572,6 +908,29 @@ bool wide_1xn_ok(const IgemmArgs &a) {
     return a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune);
 }
 
+// The warp-specialized form of the 1 x N tiles (igemm_halo16_ws): WN compute waves + one producer wave per block.
+template <int WN, int TM, int TN, int OCC, bool IN_BN>
+void launch_ws_b(const IgemmArgs &a, int tw, hipStream_t s) {
+    constexpr int BM = TM * 16, BN = WN * TN * 16;
+    IgemmArgs b = a;
+    b.grid_m = a.n_img * (a.ho / (BM / tw)) * (a.wo / tw);
+    b.grid_n = (a.n_out + BN - 1) / BN;
+    b.remap = halo_remap(a.tune);
+    const dim3 grid(b.grid_m * b.grid_n), block(64 * (WN + 1));
+    (void)tw;  // 16: halo16_ws only takes maps tiled by 16-wide tiles (halo16_pick's first choice)
+    hipLaunchKernelGGL((igemm_halo16_ws<WN, TM, TN, 16, OCC, IN_BN>), grid, block, 0, s, b);
+}
+template <int WN, int TM, int TN, int OCC>
+void launch_ws(const IgemmArgs &a, int tw, hipStream_t s) {
+    if (a.in_scale)
+        launch_ws_b<WN, TM, TN, OCC, true>(a, tw, s);
+    else
+        launch_ws_b<WN, TM, TN, OCC, false>(a, tw, s);
+}
+bool halo16_ws(const IgemmArgs &a) {
+    return (a.tune & SCD_TUNE_HALO16_WS) && wide_1xn_ok(a) && !a.sb && a.wo % 16 == 0 && a.ho % 8 == 0;
+}
+
 }  // namespace
 
 // 0 when `a` does not take this kernel, else 1 + config id; *bm = pixels per tile, *tw = tile width.
@@ -596,6 +955,7 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     else
         return 0;
     if (id < 0 || id > 5 || (id > 2 && !wide_1xn_ok(a))) return 0;
+    if (id == 5 && halo16_ws(a)) id = 4;  // the warp-specialized blocks tile 128 pixels
     for (;;) {
         *bm = kCfg[id].bm;
         const int pref = 16;  // preferred tile width, the smallest halo per pixel (180 rows for 128 px)
@@ -613,8 +973,18 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
     switch (cfg - 1) {
         case 0: launch16<2, 2, 4, 4, 2>(a, tw, s); break;
         case 1: launch16<2, 2, 4, 2, 3>(a, tw, s); break;
-        case 3: launch16_1xn<1, 4, 8, 2, 2>(a, tw, s); break;
-        case 4: launch16_1xn<1, 2, 8, 2, 2>(a, tw, s); break;
+        case 3:
+            if (halo16_ws(a))
+                launch_ws<4, 8, 2, 2>(a, tw, s);
+            else
+                launch16_1xn<1, 4, 8, 2, 2>(a, tw, s);
+            break;
+        case 4:
+            if (halo16_ws(a))
+                launch_ws<2, 8, 2, 3>(a, tw, s);
+            else
+                launch16_1xn<1, 2, 8, 2, 2>(a, tw, s);
+            break;
         case 5: launch16_1xn<2, 2, 8, 2, 2>(a, tw, s); break;
         default: launch16<2, 2, 2, 4, 3>(a, tw, s); break;
     }

@@ -408,6 +408,7 @@ TUNE_NO_HALO16_C16 = 1 << 25
 TUNE_NO_HALO = 1 << 26
 TUNE_HALO16_LATE_LOAD = 1 << 27
 TUNE_H2_TILE64_128 = 1 << 28
+TUNE_HALO16_WS = 1 << 29
 
 
 def tune_halo16_cfg(tile_id: int) -> int:

@@ -500,7 +500,7 @@ def test_halo16_dst_bound(dev, h2):
         hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, None, hip.nhwc(y), dst_bound=bound)
 
 
-@pytest.mark.parametrize('env', ['TUNE_H2_TILE64_2X2', 'TUNE_H2_TILE_2X2'])
+@pytest.mark.parametrize('env', ['TUNE_H2_TILE64_2X2', 'TUNE_H2_TILE_2X2', 'TUNE_HALO16_WS'])
 @pytest.mark.parametrize('ci,co,mode', [(64, 64, 'stats'), (32, 64, 'bn_bwd'), (64, 64, 'in_bn'), (128, 128, 'stats'),
                                         (64, 128, 'bn_bwd'), (64, 96, 'plain')])
 def test_h2_tile_layouts_bit_identical(dev, h2, env, ci, co, mode):
@@ -587,3 +587,27 @@ def test_h2_tile64_256_matches_128(dev, h2, ci, mode):
     if outs[0][1] is not None:
         a, b = outs[0][1], outs[1][1]
         assert ((a - b).abs().max() / b.abs().max()).item() < 1e-5
+
+
+def test_halo16_ws_training_step_bit_identical(dev, h2):
+    """The warp-specialized h2 halo kernel (SCD_TUNE_HALO16_WS: a producer wave stages the halo) inside a whole
+    training step of SiameseUNet [64, 128, 256] at 64x64: logits, loss and every gradient bit-identical to the
+    default kernels."""
+    from multimodal_siamese_cd_amd import hip, trainers
+    from multimodal_siamese_cd_amd.utils import datasets, experiment_manager as em, networks
+    cfg = em.load_cfg('debug')
+    cfg.MODEL.TOPOLOGY = [64, 128, 256]
+    gen = torch.Generator(device=dev).manual_seed(6)
+    b = datasets.synthetic_batch(cfg, 4, dev, gen, 64)
+    res = []
+    for tune in (0, hip.TUNE_HALO16_WS):
+        torch.manual_seed(0)
+        net = networks.create_network(cfg).to(dev).train()
+        with hip.conv_scope(tune=tune):
+            out = net(b['x_t1'], b['x_t2'])
+            loss = trainers.step_loss(cfg, out, b, net)
+            loss.backward()
+        res.append((out.detach(), loss.detach(), [p.grad.clone() for p in net.parameters()]))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for g0, g1 in zip(res[0][2], res[1][2]):
+        assert torch.equal(g0, g1)
