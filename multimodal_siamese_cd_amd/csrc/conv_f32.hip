@@ -843,7 +843,12 @@ static int conv_igemm_run(const scd_igemm_t *d, hipStream_t s, int bb_ntiles_tot
     if (math_split(a.math) && launch_igemm_x3(a, s)) return launch_status("scd_conv_igemm");
     if (a.sb) {
         set_error("igemm: bf16 views need the bf16 halo16 / c16 / gather16 kernels; this shape takes none "
-                  "(check scd_igemm_arith)");
+                  "(check scd_igemm_arith): n=%d c=%d %dx%d -> %dx%d n_out=%d ldc=%d taps=%d stride=%d store=%d "
+                  "K=%d wsplit=%d src_bytes=%u dst%%16=%d bias%%16=%d in_bn=%d bn_bwd=%d math=%d",
+                  a.n_img, a.c, a.hs, a.ws, a.ho, a.wo, a.n_out, a.ldc_d, a.ntaps, a.stride, a.store_mode, a.K,
+                  a.wsplit ? 1 : 0, a.src_bytes, int(reinterpret_cast<uintptr_t>(a.dst) & 15),
+                  a.bias ? int(reinterpret_cast<uintptr_t>(a.bias) & 15) : -1, a.in_scale ? 1 : 0, a.bb_rec ? 1 : 0,
+                  a.math);
         return SCD_ERR_ARG;
     }
     if (a.dst_bound) {

@@ -153,7 +153,9 @@ class _HipNet(nn.Module):
         object.__setattr__(self, '_twin', None)
 
     def forward(self, x_t1, x_t2):
-        st = engine.storage_for_input(self.act_storage, x_t1.shape[-2], x_t1.shape[-1], len(self.cfg.MODEL.TOPOLOGY))
+        # levels: the input map and one per Down (Encoder: len(TOPOLOGY) of them)
+        st = engine.storage_for_input(self.act_storage, x_t1.shape[-2], x_t1.shape[-1],
+                                      len(self.cfg.MODEL.TOPOLOGY) + 1)
         with hip.conv_scope(self.conv_math), engine.storage_scope(st):
             if self._twin_topo is not None:
                 return self._twin_forward(x_t1, x_t2)

@@ -361,6 +361,10 @@ def test_pool_and_difference_kernels(dev):
         hip.window_copy(nhwc(yy), nhwc(wc), -1, -2)
         res[dt] = dict(p=p, i0=i0, pb=pb, i1=i1, d=d[..., :c], pd=pd, i2=i2, d2=d2, d3=d3, gx=gx, wc=wc)
     a, b = res[torch.bfloat16], res[torch.float32]
+    # the feature grad's fp32 twin reads the bf16 run's (rounded) gradients: its output is then one rounding away
+    gx = torch.empty_like(y)
+    hip.feature_grad(nhwc(a['p'].float()), a['i0'], nhwc(a['d2'].float()), 1, nhwc(gx))
+    b['gx'] = gx
     for k in ('i0', 'i1', 'i2'):
         assert torch.equal(a[k], b[k]), k
     for k in ('p', 'pb', 'd', 'pd', 'd2', 'd3', 'gx', 'wc'):
@@ -434,7 +438,7 @@ def test_bf16_models_store_bf16_activations(dev):
     hip.conv_igemm = spy
     try:
         gen = torch.Generator(device=dev).manual_seed(1)
-        b = datasets.synthetic_batch(cfg, 2, dev, gen, 128)
+        b = datasets.synthetic_batch(cfg, 2, dev, gen, 256)  # deepest level 16 x 16
         loss = trainers.step_loss(cfg, net(b['x_t1'], b['x_t2']), b, net)
         loss.backward()
         assert torch.isfinite(loss)
@@ -442,7 +446,7 @@ def test_bf16_models_store_bf16_activations(dev):
         seen.clear()
         with torch.no_grad():
             net.eval()
-            net(b['x_t1'][:, :, :120, :120].contiguous(), b['x_t2'][:, :, :120, :120].contiguous())
-        assert seen and all(d == hip.DT_F32 for d in seen)  # 120 / 8 is not a multiple of 16: fp32 storage
+            net(b['x_t1'][:, :, :128, :128].contiguous(), b['x_t2'][:, :, :128, :128].contiguous())
+        assert seen and all(d == hip.DT_F32 for d in seen)  # deepest level 8 x 8, not tiled: fp32 storage
     finally:
         hip.conv_igemm = orig

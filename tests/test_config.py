@@ -172,3 +172,18 @@ def test_padded_twin_maps_on_cpu(mtype, topo):
             assert torch.equal(networks._gather(big, [m[0]])[:, shape[1] // 2], p.detach()[:, h])
     for k, b in net.named_buffers():
         assert k in bufs
+
+
+def test_bf16_storage_needs_every_level_tiled():
+    """bf16 storage runs only where every level's map (the input and one per Down: len(TOPOLOGY) + 1 levels) is
+    tiled by the bf16 kernels, the deepest a multiple of 16 both ways; other tiles (e.g. full-AOI evaluation) run
+    fp32.  The models ask with len(TOPOLOGY) + 1 levels."""
+    from multimodal_siamese_cd_amd import engine
+    bf, f32 = torch.bfloat16, torch.float32
+    assert engine.storage_for_input(bf, 256, 256, 5) == bf  # [64, 128, 256, 512]: deepest 16 x 16
+    assert engine.storage_for_input(bf, 128, 128, 5) == f32  # deepest 8 x 8: not tiled
+    assert engine.storage_for_input(bf, 128, 128, 4) == bf
+    assert engine.storage_for_input(bf, 256, 240, 5) == f32
+    assert engine.storage_for_input(f32, 256, 256, 5) == f32
+    src = Path(__file__).resolve().parents[1] / 'multimodal_siamese_cd_amd' / 'utils' / 'networks.py'
+    assert 'len(self.cfg.MODEL.TOPOLOGY) + 1' in src.read_text()

@@ -589,9 +589,10 @@ def test_h2_tile64_256_matches_128(dev, h2, ci, mode):
         assert ((a - b).abs().max() / b.abs().max()).item() < 1e-5
 
 
-def test_halo16_ws_training_step_bit_identical(dev, h2):
-    """The warp-specialized h2 halo kernel (SCD_TUNE_HALO16_WS: a producer wave stages the halo) inside a whole
-    training step of SiameseUNet [64, 128, 256] at 64x64: logits, loss and every gradient bit-identical to the
+@pytest.mark.parametrize('variant,base', [('TUNE_HALO16_WS', 'TUNE_H2_TILE64_128')])
+def test_halo16_variant_training_step_bit_identical(dev, h2, variant, base):
+    """The warp-specialized h2 halo kernel (SCD_TUNE_HALO16_WS: a producer wave stages the halo; both runs on
+    128-pixel tiles, the only ones it has) inside a whole training step of SiameseUNet [64, 128, 256] at 64x64: logits, loss and every gradient bit-identical to the
     default kernels."""
     from multimodal_siamese_cd_amd import hip, trainers
     from multimodal_siamese_cd_amd.utils import datasets, experiment_manager as em, networks
@@ -600,7 +601,8 @@ def test_halo16_ws_training_step_bit_identical(dev, h2):
     gen = torch.Generator(device=dev).manual_seed(6)
     b = datasets.synthetic_batch(cfg, 4, dev, gen, 64)
     res = []
-    for tune in (0, hip.TUNE_HALO16_WS):
+    t0 = getattr(hip, base) if base else 0
+    for tune in (t0, t0 | getattr(hip, variant)):
         torch.manual_seed(0)
         net = networks.create_network(cfg).to(dev).train()
         with hip.conv_scope(tune=tune):
