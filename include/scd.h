@@ -315,6 +315,11 @@ typedef struct scd_wgrad {
     const float *rows_mean, *rows_invstd, *rows_gamma, *rows_scale, *rows_shift, *rows_coef;
     int32_t math;  /* enum scd_conv_math: the arithmetic of this launch */
     uint32_t tune; /* SCD_TUNE_* kernel-variant bits, 0 = defaults */
+    /* Optional [nsplit][ntaps * src.c] (nsplit from scd_wgrad_plan): per K-split, the sum over its pixels of every
+     * gathered src column (tap t, channel c), summed as staged.  For a ConvTranspose2d weight grad (src = dOut,
+     * every output pixel gathered by exactly one tap) scd_wgrad_colsum_finalize turns it into the bias grad, so dOut
+     * is not read again for it.  NULL = off.  Only where scd_wgrad_colsum_supported() returns 1. */
+    float *src_colsum;
 } scd_wgrad_t;
 
 /* Number of K-splits the library will use and the slab bytes it needs. */
@@ -334,6 +339,13 @@ int scd_wgrad_rows_bn_supported(const scd_wgrad_t *d);
  * mode 1: out ConvT [R][C][2][2]       (slab cols (i*2+j)*C + c)                                  */
 int scd_wgrad_finalize(float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C, int32_t mode,
                        int32_t c_valid, float *out, scd_stream_t stream);
+/* 1 if the weight-grad kernel for `d` writes src_colsum (the generic split-arithmetic kernel), else 0. */
+int scd_wgrad_colsum_supported(const scd_wgrad_t *d);
+/* out[c] = sum over splits s and taps t of colsum[s][t*C + c], in a fixed order (the ConvTranspose bias grad from
+ * scd_wgrad_t.src_colsum; colsum is scratch and is overwritten; ntaps <= 9).  replaces: the bias-grad reduction of
+ * convolution_backward for ConvTranspose2d. */
+int scd_wgrad_colsum_finalize(float *colsum, int32_t nsplit, int32_t ntaps, int32_t C, float *out,
+                              scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * BatchNorm2d (train: batch statistics per segment; eval: running statistics) + ReLU.

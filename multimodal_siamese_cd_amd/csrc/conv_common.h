@@ -109,6 +109,9 @@ struct WgradArgs {
     int math;       // SCD_MATH_* of this launch (scd_wgrad_t.math)
     uint32_t tune;  // SCD_TUNE_* bits (scd_wgrad_t.tune)
     int sb;         // 1: rows, src and rows_y are bf16 views (ABI 6)
+    // optional [split][Ng] column sums of the staged src (generic weight grad: the ConvTranspose bias grad), written
+    // by the blocks of row tile 0
+    float *colsum;
 };
 
 // Split-bf16 ("x3") launchers, conv_x3.hip.  Return false when the shape is not supported by the x3 kernels

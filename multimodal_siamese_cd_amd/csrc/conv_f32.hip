@@ -1058,7 +1058,17 @@ static void wgrad_split(const scd_wgrad_t *d, int *nsplit, int *kchunk) {
 
 namespace scd {
 static bool wgrad_src_bn_ok(const scd_wgrad_t *d) { return wgrad_halo_ok(d) || wgrad_c16_ok(d); }
+// The generic split-arithmetic weight grad (wgrad_x3: the ConvTranspose weight grad) also writes src column sums.
+static bool wgrad_colsum_ok(const scd_wgrad_t *d) {
+    return math_split(d->math) && !wgrad_halo_ok(d) && !wgrad_c16_ok(d) && d->src.c % 4 == 0;
+}
 }  // namespace scd
+
+extern "C" int scd_wgrad_colsum_supported(const scd_wgrad_t *d) {
+    clear_error();
+    if (wgrad_validate(d) != SCD_OK) return 0;
+    return wgrad_colsum_ok(d) ? 1 : 0;
+}
 
 extern "C" int scd_wgrad_src_bn_supported(const scd_wgrad_t *d) {
     clear_error();
@@ -1173,7 +1183,8 @@ extern "C" int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_by
     }
     size_t used = 0;  // slabs written by the previous chunks
     for (int img0 = 0; img0 < d->rows.n; img0 += chunk) {
-        const scd_wgrad_t c = wgrad_slice(d, img0, std::min(chunk, d->rows.n - img0));
+        scd_wgrad_t c = wgrad_slice(d, img0, std::min(chunk, d->rows.n - img0));
+        if (d->src_colsum) c.src_colsum = d->src_colsum + used * size_t(d->ntaps) * d->src.c;
         int ns, kc;
         wgrad_split(&c, &ns, &kc);
         SCD_TRY(conv_wgrad_run(&c, slabs + used * slab, (size_t(ns)) * slab * sizeof(float), as_stream(stream)));
@@ -1195,6 +1206,11 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     WgradArgs a;
     a.sb = wgrad_sb(d) ? 1 : 0;
     const int eb = elem_size(a.sb);
+    if (d->src_colsum && !wgrad_colsum_ok(d)) {
+        set_error("wgrad: src_colsum needs the generic split-arithmetic weight grad (check scd_wgrad_colsum_supported)");
+        return SCD_ERR_ARG;
+    }
+    a.colsum = d->src_colsum;
     if (a.sb && !wgrad_halo_ok(d) && !wgrad_c16_ok(d) && !wgrad_generic_bf16(d)) {
         set_error("wgrad: bf16 views need the bf16 halo16 / c16 / ConvTranspose weight-grad kernels; this shape takes "
                   "none (check scd_wgrad_arith)");
@@ -1316,6 +1332,59 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
     return launch_status("scd_conv_wgrad");
 }
 }  // namespace scd
+
+namespace scd {
+// scd_wgrad_colsum_finalize, two fixed-order stages: (1) in place, split group g's 16 rows summed in split order into
+// its first row, one thread per column (coalesced); (2) per channel, the group rows in order, then the taps in order.
+constexpr int kColsumGroup = 16;
+__global__ __launch_bounds__(256) void colsum_group_kernel(float *__restrict__ colsum, int nsplit, int Ng) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= Ng) return;
+    const int s0 = blockIdx.y * kColsumGroup, s1 = min(s0 + kColsumGroup, nsplit);
+    float v[kColsumGroup];
+#pragma unroll
+    for (int u = 0; u < kColsumGroup; ++u) v[u] = s0 + u < s1 ? colsum[size_t(s0 + u) * Ng + j] : 0.f;
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < kColsumGroup; ++u) acc += v[u];
+    colsum[size_t(s0) * Ng + j] = acc;
+}
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float *__restrict__ colsum, int nsplit, int ntaps,
+                                                           int C, float *__restrict__ out) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    const int Ng = ntaps * C;
+    float tap[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) tap[t] = 0.f;
+#pragma unroll 4
+    for (int s = 0; s < nsplit; s += kColsumGroup)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            if (t < ntaps) tap[t] += colsum[size_t(s) * Ng + t * C + c];
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+        if (t < ntaps) acc += tap[t];
+    out[c] = acc;
+}
+}  // namespace scd
+
+extern "C" int scd_wgrad_colsum_finalize(float *colsum, int32_t nsplit, int32_t ntaps, int32_t C, float *out,
+                                         scd_stream_t stream) {
+    clear_error();
+    if (!colsum || !out || nsplit < 1 || ntaps < 1 || ntaps > 9 || C < 1) {
+        set_error("wgrad_colsum_finalize: colsum/out non-null, nsplit=%d >= 1, ntaps=%d in [1, 9], C=%d >= 1", nsplit,
+                  ntaps, C);
+        return SCD_ERR_ARG;
+    }
+    const hipStream_t s = as_stream(stream);
+    const int Ng = ntaps * C;
+    hipLaunchKernelGGL(colsum_group_kernel, dim3((Ng + 255) / 256, (nsplit + kColsumGroup - 1) / kColsumGroup),
+                       dim3(256), 0, s, colsum, nsplit, Ng);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 255) / 256), dim3(256), 0, s, colsum, nsplit, ntaps, C, out);
+    return launch_status("scd_wgrad_colsum_finalize");
+}
 
 extern "C" int scd_wgrad_finalize(float *slabs, int32_t nsplit, int32_t R, int32_t ntaps, int32_t C,
                                   int32_t mode, int32_t c_valid, float *out, scd_stream_t stream) {

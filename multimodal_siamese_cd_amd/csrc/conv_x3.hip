@@ -759,6 +759,12 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
     }
 
     StageT<SB> ra[A_PER], rb[B_PER];
+    // colsum: the blocks of row tile 0 also sum every src element they stage, per column (as loaded: before the
+    // split and the h2 scale), so the ConvTranspose bias grad needs no pass of its own over dOut
+    const bool col_sums = a.colsum != nullptr && r0 == 0;
+    f32x4 cs[B_PER];
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) cs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
     auto load_stage = [&](int kb) {
@@ -815,6 +821,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
             if (B_FULL || b_in[i]) {
+                if (col_sums) cs[i] += stage_f32<SB>(rb[i]);
                 u32x2 h, m, l;
                 if constexpr (H2) {
                     split2h_pre(rb[i] * ssc, h, m);
@@ -909,6 +916,26 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void wgrad_x3(WgradArgs a) {
             }
             if (more) store_stage((s + 1) & 1);
             __syncthreads();
+        }
+    }
+
+    if (col_sums) {  // uniform per block; the loop's last barrier has released the stage buffers
+        // piece ch = tid + i * NT is (pixel row b_k, column quad ch % BQ): each quad's 16 rows summed in row order
+        static_assert(B_CH * 16 <= 2 * STAGE, "column-sum rows fit the stage buffers");
+        f32x4 *red = reinterpret_cast<f32x4 *>(smem);
+#pragma unroll
+        for (int i = 0; i < B_PER; ++i)
+            if (B_FULL || b_in[i]) red[tid + i * NT] = cs[i];
+        __syncthreads();
+        for (int q = tid; q < BQ; q += NT) {
+            f32x4 v = red[q];
+#pragma unroll
+            for (int k = 1; k < BK; ++k) v += red[k * BQ + q];
+            const int j = j0 + q * 4;
+            float *o = a.colsum + size_t(split) * a.Ng + j;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (j + e < a.Ng) o[e] = v[e];
         }
     }
 

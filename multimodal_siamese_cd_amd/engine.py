@@ -32,7 +32,8 @@ _F32 = torch.float32
 
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
-         'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True, 'defer_bn_bwd': True, 'fuse_head': True}
+         'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True, 'defer_bn_bwd': True, 'fuse_head': True,
+         'convT_bias_in_wgrad': True}
 
 
 def conv_math_for(cfg) -> str:
@@ -975,13 +976,21 @@ class DecoderFn(torch.autograd.Function):
             hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, hip.pack_convT2x2(convT.weight.detach(), 1), cu, None,
                            nhwc(g_cur), src_bound=gcat_bound)
             # ConvT weight grad: rows = convT input, src = g_up gathered with stride 2 (h2: both bounds)
+            # (and its bias grad: the kernel sums the g_up columns it stages, scd_wgrad_t.src_colsum)
             d, nsplit, nbytes = hip.wgrad_plan(nhwc(cur), g_up, 2, TAPS_2X2, None, cur_bound, gcat_bound)
             slabs = _empty((nbytes // 4,), cur)
+            colsum = None
+            if _OPTS['convT_bias_in_wgrad'] and hip.wgrad_colsum_supported(d):
+                colsum = _empty((nsplit * 4 * cto,), cur)
+                d.src_colsum = colsum.data_ptr()
             hip.conv_wgrad(d, slabs)
             gwT = torch.empty_like(convT.weight)
             hip.wgrad_finalize(slabs, nsplit, cu, 4, cto, 1, cto, gwT)
             gbT = _empty((cto,), cur)
-            hip.channel_sum(g_up, gbT, _ws(hip.bn_workspace_bytes(bb, hh, ww, cto, 1), cur))
+            if colsum is not None:
+                hip.wgrad_colsum_finalize(colsum, nsplit, 4, cto, gbT)
+            else:
+                hip.channel_sum(g_up, gbT, _ws(hip.bn_workspace_bytes(bb, hh, ww, cto, 1), cur))
             grads[10 * k:10 * k + 10] = [gwT, gbT] + pg
             g = g_cur
         ctx.saved = None

@@ -86,6 +86,7 @@ class WGRAD(ctypes.Structure):
         ("rows_coef", c_void_p),
         ("math", c_int32),
         ("tune", c_uint32),
+        ("src_colsum", c_void_p),
     ]
 
 
@@ -125,6 +126,8 @@ _SIGS = {
     "scd_wgrad_rows_per_block": ([POINTER(WGRAD)], c_int),
     "scd_wgrad_rows_bn_supported": ([POINTER(WGRAD)], c_int),
     "scd_wgrad_finalize": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
+    "scd_wgrad_colsum_supported": ([POINTER(WGRAD)], c_int),
+    "scd_wgrad_colsum_finalize": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_bn_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32], c_size_t),
     "scd_bn_train_stats": (
         [NHWC, c_int32, c_void_p, c_void_p, c_float, c_float, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -630,6 +633,17 @@ def conv_wgrad(d: WGRAD, slabs: torch.Tensor):
 def wgrad_finalize(slabs, nsplit, R, ntaps, C, mode, c_valid, out: torch.Tensor):
     _check(lib().scd_wgrad_finalize(slabs.data_ptr(), nsplit, R, ntaps, C, mode, c_valid, out.data_ptr(), _stream()),
            "scd_wgrad_finalize")
+
+
+def wgrad_colsum_supported(d: 'WGRAD') -> bool:
+    """Whether the weight-grad kernel for `d` also writes the src column sums (scd_wgrad_t.src_colsum)."""
+    return bool(lib().scd_wgrad_colsum_supported(ctypes.byref(d)))
+
+
+def wgrad_colsum_finalize(colsum: torch.Tensor, nsplit: int, ntaps: int, C: int, out: torch.Tensor):
+    """out[c] = sum over splits and taps of colsum[s][t*C + c] (the ConvTranspose bias grad)."""
+    _check(lib().scd_wgrad_colsum_finalize(colsum.data_ptr(), nsplit, ntaps, C, out.data_ptr(), _stream()),
+           "scd_wgrad_colsum_finalize")
 
 
 def bn_workspace_bytes(n, h, w, c, nseg) -> int:

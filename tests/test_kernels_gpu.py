@@ -222,6 +222,58 @@ def test_convT2x2_backward(dev, math, n, h, w, c, cs):
     assert rel(gb, b.grad) < TOL
 
 
+@pytest.mark.parametrize('arith', ['h2', 'x3', 'bf16'])
+@pytest.mark.parametrize('n,h,w,c,cs', [(2, 8, 8, 16, 16), (4, 16, 16, 64, 64), (2, 4, 6, 512, 512), (32, 64, 64, 128, 64)])
+def test_convT_bias_grad_from_weight_grad_staging(dev, arith, n, h, w, c, cs):
+    """The ConvTranspose bias grad from the weight grad's column sums (scd_wgrad_t.src_colsum, every split's slab
+    written: NaN-prefilled) == the float64 sum of dOut over the concat slice, as scd_channel_sum, in each arithmetic
+    (bf16: bf16 storage of dOut and x).  The weight grad itself is unchanged by the extra output."""
+    from multimodal_siamese_cd_amd import hip
+    st = torch.bfloat16 if arith == 'bf16' else torch.float32
+    g = torch.Generator().manual_seed(5 + c + n)
+    gd = torch.randn(n, 2 * h, 2 * w, cs + c, generator=g).to(dev).to(st)
+    xd = torch.randn(n, h, w, c, generator=g).to(dev).to(st)
+    gup = hip.nhwc(gd, cs, c)
+    with hip.conv_scope(arith):
+        bounds = (xd.float().abs().max().reshape(1), gd.float().abs().max().reshape(1)) if arith == 'h2' else (None, None)
+        outs = []
+        for with_cs in (False, True):
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(xd), gup, 2, hip.TAPS_2X2, None, *bounds)
+            assert hip.wgrad_colsum_supported(d)
+            colsum = torch.full((nsplit * 4 * c,), float('nan'), device=dev)
+            if with_cs:
+                d.src_colsum = colsum.data_ptr()
+            slabs = torch.empty(nbytes // 4, device=dev)
+            hip.conv_wgrad(d, slabs)
+            gw = torch.empty(c, c, 2, 2, device=dev)
+            hip.wgrad_finalize(slabs, nsplit, c, 4, c, 1, c, gw)
+            outs.append(gw)
+        assert torch.equal(outs[0], outs[1])
+        assert bool(torch.isfinite(colsum).all())
+        gb = torch.empty(c, device=dev)
+        hip.wgrad_colsum_finalize(colsum, nsplit, 4, c, gb)
+    exact = gd[..., cs:].double().sum((0, 1, 2)).cpu()
+    scale = gd[..., cs:].double().abs().sum((0, 1, 2)).max().item()
+    assert (gb.double().cpu() - exact).abs().max().item() / scale < 1e-6
+    ref = torch.empty(c, device=dev)
+    hip.channel_sum(gup, ref, torch.empty(hip.bn_workspace_bytes(n, 2 * h, 2 * w, c, 1), dtype=torch.uint8, device=dev))
+    assert (ref.double().cpu() - exact).abs().max().item() / scale < 1e-6
+
+
+def test_convT_bias_colsum_refused_off_the_generic_kernel(dev):
+    """A 3x3 weight grad on the halo kernels has no column sums: setting src_colsum there is refused."""
+    from multimodal_siamese_cd_amd import hip
+    x = torch.randn(2, 16, 16, 64, device=dev)
+    dy = torch.randn(2, 16, 16, 64, device=dev)
+    with hip.conv_scope('x3'):
+        d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dy), hip.nhwc(x), 1, hip.TAPS_3X3)
+        assert not hip.wgrad_colsum_supported(d)
+        colsum = torch.empty(nsplit * 9 * 64, device=dev)
+        d.src_colsum = colsum.data_ptr()
+        with pytest.raises(RuntimeError, match='src_colsum'):
+            hip.conv_wgrad(d, torch.empty(nbytes // 4, device=dev))
+
+
 @pytest.mark.parametrize('n,h,w,ci,co,nseg', [(4, 32, 32, 64, 128, 2), (4, 16, 16, 32, 64, 2), (2, 64, 64, 16, 32, 1),
                                               (2, 16, 16, 512, 512, 1)])
 def test_conv_fused_bn_stats(dev, n, h, w, ci, co, nseg):
