@@ -177,6 +177,8 @@ int scd_abi_version(void);
                                                  of 256 x 64 (2x2 waves of 128 px x 32 ch)                          */
 #define SCD_TUNE_HALO16_WS        (1u << 29)  /* h2 1 x N tiles as warp-specialized blocks: one producer wave stages
                                                  the halo, the compute waves load only weights (128 px tiles)        */
+#define SCD_TUNE_GATHER16_PERSIST (1u << 30)  /* ConvTranspose gather kernel as persistent blocks: each walks tiles, the
+                                                 next tile's first stage loaded behind the current tile's last one   */
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);
@@ -411,12 +413,16 @@ int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx,
                                 size_t ws_bytes, scd_stream_t stream);
 /* scd_bn_relu_backward whose incoming gradient is the 1x1 head's input gradient, formed on the fly:
  *   da[p][c] = sum_o gout[img][o][pix] * w_head[o][c]   (gout NCHW [n][n_out][h][w], n_out <= 4)
- * -- what scd_conv1x1_bwd would write into gx (same fma chain, bit-identical results); y.n * y.h * y.w < 2^31. */
+ * -- what scd_conv1x1_bwd would write into gx (same fma chain, bit-identical results); y.n * y.h * y.w < 2^31.
+ * w_grad (optional, [n_out][C]): also the head's weight grad, sum_p gout[o](p) * relu(fma(y, scale, shift)), from
+ * the same partial pass over y (scd_conv1x1_bwd_bn then needs no gw); workspace scd_bn_head_workspace_bytes, else
+ * scd_bn_workspace_bytes. */
+size_t scd_bn_head_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t c, int32_t nseg, int32_t n_out);
 int scd_bn_relu_backward_head(scd_nhwc_t y, const float *gout, const float *w_head, int32_t n_out, int32_t nseg,
                               const float *save_mean, const float *save_invstd, const float *gamma,
                               const float *scale, const float *shift, float *dgamma, float *dbeta,
-                              float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws, size_t ws_bytes,
-                              scd_stream_t stream);
+                              float *dbias_prev, scd_nhwc_t dy, float *dy_bound, float *w_grad, void *ws,
+                              size_t ws_bytes, scd_stream_t stream);
 /* scd_bn_relu_backward with the partial sums taken from conv-epilogue tile records (scd_bn_bwd_tiles_t.rec,
  * ntiles tiles, image-major, split evenly into nseg segments) instead of a pass over (y, da). */
 int scd_bn_relu_backward_tiles(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, const float *save_mean,

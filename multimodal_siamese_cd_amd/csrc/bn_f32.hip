@@ -822,6 +822,111 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const T *__restrict
     }
 }
 
+// bn_bwd_partial for the head's BatchNorm (DaHead) that also takes the 1x1 head's weight grad from the same pass:
+//   hrec[o][c][chunk] = sum_p gout[o](p) * relu(fma(y, scale, shift))(p, c)
+// (what weighted_channel_sum's chan_sum_partial summed in a pass of its own over y; same chunks, per-thread order and
+// tree).  The gradient values g_o(p) are loaded once per pixel for both the head's dL/da and the weight grad.
+template <class T>
+__global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial_head(const T *__restrict__ y, int ldy, DaHead da, int C,
+                                                                  int64_t pseg, int ncps, int chunk, int nrec, int qpb,
+                                                                  const float *smean, const float *sinv,
+                                                                  const float *scale, const float *shift,
+                                                                  float *__restrict__ rec, float *__restrict__ hrec) {
+    __shared__ f4 sh1[BN_THREADS], sh2[BN_THREADS], shh[4][BN_THREADS];
+    const int tid = threadIdx.x;
+    const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
+    const int c = (blockIdx.y * qpb + q) * 4;
+    const Chunk ch = chunk_of(pseg, ncps, chunk);
+    const f4 zero = {0.f, 0.f, 0.f, 0.f};
+    f4 s1 = zero, s2 = zero, hw[4] = {zero, zero, zero, zero};
+    if (c < C) {
+        const int o = ch.seg * C + c;
+        const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
+        f4 w4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w4[k] = k < da.n_out ? ld4(da.w + int64_t(k) * C + c) : zero;
+        // one pixel: its n_out gradient values, dL/da (DaHead's fma chain) and the activation
+        auto px = [&](int64_t p, f4 yv, f4 (&gk)[4]) {
+            const uint32_t img = fdiv(uint32_t(p), da.div_hw);
+            const int pix = int(uint32_t(p) - img * uint32_t(da.hw));
+            f4 r = zero;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float gv = k < da.n_out ? da.g[(int64_t(img) * da.n_out + k) * da.hw + pix] : 0.f;
+                gk[k] = f4{gv, gv, gv, gv};
+                if (k < da.n_out) {
+                    r.x = fmaf(gv, w4[k].x, r.x);
+                    r.y = fmaf(gv, w4[k].y, r.y);
+                    r.z = fmaf(gv, w4[k].z, r.z);
+                    r.w = fmaf(gv, w4[k].w, r.w);
+                }
+            }
+            return r;
+        };
+        int64_t p = ch.beg + pl;
+        for (; p + 3 * npl < ch.end; p += 4 * npl) {
+            f4 y0 = ld4(y + p * ldy + c), y1 = ld4(y + (p + npl) * ldy + c);
+            f4 y2 = ld4(y + (p + 2 * npl) * ldy + c), y3 = ld4(y + (p + 3 * npl) * ldy + c);
+            f4 k0[4], k1[4], k2[4], k3[4];
+            f4 g0 = px(p, y0, k0), g1 = px(p + npl, y1, k1);
+            f4 g2 = px(p + 2 * npl, y2, k2), g3 = px(p + 3 * npl, y3, k3);
+            PIN4(y0, y1, y2, y3);
+            PIN4(g0, g1, g2, g3);
+            const f4 z0 = relu_mask(y0, sc, sf, g0), z1 = relu_mask(y1, sc, sf, g1);
+            const f4 z2 = relu_mask(y2, sc, sf, g2), z3 = relu_mask(y3, sc, sf, g3);
+            s1 += (z0 + z1) + (z2 + z3);
+            s2 += (z0 * ((y0 - mu) * iv) + z1 * ((y1 - mu) * iv)) + (z2 * ((y2 - mu) * iv) + z3 * ((y3 - mu) * iv));
+            const f4 a0 = bn_relu4(y0, sc, sf), a1 = bn_relu4(y1, sc, sf);
+            const f4 a2 = bn_relu4(y2, sc, sf), a3 = bn_relu4(y3, sc, sf);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < da.n_out) hw[k] += (a0 * k0[k] + a1 * k1[k]) + (a2 * k2[k] + a3 * k3[k]);
+        }
+        for (; p < ch.end; p += npl) {
+            const f4 y0 = ld4(y + p * ldy + c);
+            f4 k0[4];
+            const f4 z0 = relu_mask(y0, sc, sf, px(p, y0, k0));
+            s1 += z0;
+            s2 += z0 * ((y0 - mu) * iv);
+            const f4 a0 = bn_relu4(y0, sc, sf);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < da.n_out) hw[k] += a0 * k0[k];
+        }
+    }
+    sh1[tid] = s1;
+    sh2[tid] = s2;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) shh[k][tid] = hw[k];
+    __syncthreads();
+    for (int off = npl / 2; off > 0; off >>= 1) {
+        if (pl < off) {
+            sh1[tid] += sh1[tid + off * qpb];
+            sh2[tid] += sh2[tid + off * qpb];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < da.n_out) shh[k][tid] += shh[k][tid + off * qpb];
+        }
+        __syncthreads();
+    }
+    if (pl == 0 && c < C) {
+        const f4 a = sh1[tid], b = sh2[tid];
+        const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float *r = rec + (size_t(c + k) * nrec + blockIdx.x) * 2;
+            r[0] = av[k];
+            r[1] = bv[k];
+        }
+        for (int o = 0; o < da.n_out; ++o) {
+            const f4 h = shh[o][tid];
+            const float hv[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hrec[(size_t(o) * C + c + k) * nrec + blockIdx.x] = hv[k];
+        }
+    }
+}
+
 // Upper bound of |dy| = |gamma*invstd*(dz - k1 - xhat*k2)| over one segment and channel of n values from the statistics
 // alone (the SCD_MATH_H2 operand bound of a weight grad that forms dy itself, scd_wgrad_t.rows_y): |dz| <= the bound
 // of the incoming gradient, |xhat| <= sqrt(n - 1) (as bn_act_bound) plus the rounding of (y - mean) * invstd in fp32;
@@ -1237,6 +1342,31 @@ static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *s
                        dbias_prev ? brec : nullptr, dy_bound);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
 }
+// The head's BatchNorm backward (DaHead) with the head's weight grad from the same partial pass (w_grad non-null):
+// hrec after the usual records (scd_bn_head_workspace_bytes).
+template <class T>
+static void bn_backward_run_head(const scd_nhwc_t &y, const DaHead &da, int nseg, const float *save_mean,
+                                 const float *save_invstd, const float *gamma, const float *scale, const float *shift,
+                                 float *dgamma, float *dbeta, float *dbias_prev, const scd_nhwc_t &dy, float *dy_bound,
+                                 float *w_grad, void *ws, hipStream_t s) {
+    const BnGeom g = bn_geom(y, nseg);
+    float *rec = static_cast<float *>(ws);
+    float *brec = rec + size_t(g.nrec) * y.c * 2;
+    float *coef = brec + size_t(g.nrec) * y.c;
+    float *hrec = reinterpret_cast<float *>(static_cast<unsigned char *>(ws) +
+                                            scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg));
+    hipLaunchKernelGGL(bn_bwd_partial_head<T>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       view_ptr<const T>(y), y.ldc, da, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb,
+                       save_mean, save_invstd, scale, shift, rec, hrec);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
+                       coef, dgamma, dbeta);
+    hipLaunchKernelGGL((bn_bwd_apply<T, DaHead>), dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       view_ptr<const T>(y), y.ldc, da, view_ptr<T>(dy), dy.ldc, y.c,
+                       g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
+                       dbias_prev ? brec : nullptr, dy_bound);
+    if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
+    hipLaunchKernelGGL(sum_records, dim3(da.n_out * y.c), dim3(BN_THREADS), 0, s, hrec, g.nrec, w_grad);
+}
 // The encoder levels' BatchNorm backward with the pooled gradient (DaPooled) over 2x2 cells.  The chunks partition
 // each segment's cells into at most bn_geom's chunk count, so the records fit the same workspace.
 // Building with -DSCD_BN_POOLED_CELLS=0 runs the per-pixel kernels instead (A/B experiments; bit-identical).
@@ -1323,11 +1453,19 @@ extern "C" int scd_bn_relu_backward(scd_nhwc_t y, scd_nhwc_t da, int32_t nseg, c
     return launch_status("scd_bn_relu_backward");
 }
 
+extern "C" size_t scd_bn_head_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t c, int32_t nseg,
+                                              int32_t n_out) {
+    if (nseg < 1) nseg = 1;
+    scd_nhwc_t v{nullptr, n, h, w, c, c};
+    const BnGeom g = bn_geom(v, nseg);
+    return scd_bn_workspace_bytes(n, h, w, c, nseg) + size_t(n_out > 0 ? n_out : 1) * c * g.nrec * sizeof(float);
+}
+
 extern "C" int scd_bn_relu_backward_head(scd_nhwc_t y, const float *gout, const float *w_head, int32_t n_out,
                                          int32_t nseg, const float *save_mean, const float *save_invstd,
                                          const float *gamma, const float *scale, const float *shift, float *dgamma,
-                                         float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws,
-                                         size_t ws_bytes, scd_stream_t stream) {
+                                         float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound,
+                                         float *w_grad, void *ws, size_t ws_bytes, scd_stream_t stream) {
     clear_error();
     SCD_TRY(bn_check(y, nseg));
     SCD_TRY(check_view(dy, "bn_bwd_head.dy"));
@@ -1336,16 +1474,24 @@ extern "C" int scd_bn_relu_backward_head(scd_nhwc_t y, const float *gout, const 
         set_error("bn_relu_backward_head: shape mismatch / null / n_out not in [1,4] / 2^31 pixels or more");
         return SCD_ERR_ARG;
     }
-    if (!ws || ws_bytes < scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg)) {
-        set_error("bn_relu_backward_head: workspace too small");
+    const size_t need = w_grad ? scd_bn_head_workspace_bytes(y.n, y.h, y.w, y.c, nseg, n_out)
+                               : scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg);
+    if (!ws || ws_bytes < need) {
+        set_error("bn_relu_backward_head: workspace %zu < %zu bytes", ws_bytes, need);
         return SCD_ERR_WORKSPACE;
     }
     const DaHead da{gout, w_head, n_out, y.c, y.h * y.w, make_fastdiv(uint32_t(y.h * y.w))};
     const int dt = common_dtype("bn_relu_backward_head", {&y, &dy});
     if (dt < 0) return SCD_ERR_ARG;
-    SCD_WITH_T(dt, T,
-               bn_backward_run<T>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta, dbias_prev,
-                                  dy, dy_bound, ws, as_stream(stream)));
+    if (w_grad) {
+        SCD_WITH_T(dt, T,
+                   bn_backward_run_head<T>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta,
+                                           dbias_prev, dy, dy_bound, w_grad, ws, as_stream(stream)));
+    } else {
+        SCD_WITH_T(dt, T,
+                   bn_backward_run<T>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta,
+                                      dbias_prev, dy, dy_bound, ws, as_stream(stream)));
+    }
     return launch_status("scd_bn_relu_backward_head");
 }
 

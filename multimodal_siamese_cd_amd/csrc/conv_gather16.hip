@@ -22,7 +22,10 @@
 namespace scd {
 
 // SB: bf16 storage of src and dst (bf16 arithmetic only).
-template <int WM, int WN, int TM, int TN, int SK, int OCC, int NP, bool SB = false>
+// P: persistent blocks (SCD_TUNE_GATHER16_PERSIST): block b walks tiles b, b + gridDim.x, ... as one stream of stages,
+// so the next tile's first stage is loaded while the current tile's last stage computes and its epilogue stores (the
+// ConvTranspose forward has one or two stages per tile: one tile per block leaves every block's load latency exposed).
+template <int WM, int WN, int TM, int TN, int SK, int OCC, int NP, bool SB = false, bool P = false>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a) {
     static_assert(NP == 1 || NP == 4, "bf16 or h2");
     static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
@@ -37,22 +40,32 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
     constexpr int A_PER = BM * 8 / NT;   // 16-byte (4-channel) pieces per thread and k-step
     static_assert((BM * 8) % NT == 0 && NT % 8 == 0, "pieces tile the block");
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STG];
+    // the epilogue's per-channel scale and bias of the block's BN channels, per tile parity (P: a tile's are written
+    // at its start, while the other half may still be read by the previous tile's epilogue)
+    __shared__ __attribute__((aligned(16))) float ep_sc[2][BN], ep_b[2][BN];
     float xs = 1.f, xs_inv = 1.f;
     if constexpr (H2) h2_scale(*a.src_bound, xs, xs_inv);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid % WM, wn = wid / WM;
     const int g = lane >> 4, l16 = lane & 15;
-    int mt, nt;
-    if (a.remap) {  // N fastest: the n-tiles of one pixel tile (sharing its gathered rows) under one L2
-        const uint32_t L = xcd_swizzle(blockIdx.x, uint32_t(a.grid_m * a.grid_n));
-        mt = int(L / uint32_t(a.grid_n));
-        nt = int(L - uint32_t(mt) * uint32_t(a.grid_n));
-    } else {
-        mt = int(blockIdx.x % uint32_t(a.grid_m));
-        nt = int(blockIdx.x / uint32_t(a.grid_m));
-    }
-    const int m0 = mt * BM, n0 = nt * BN;
+    const uint32_t ntile = uint32_t(a.grid_m * a.grid_n);
+    auto tile_of = [&](uint32_t q, int &m0_, int &n0_) {
+        int mt, nt;
+        if (a.remap) {  // N fastest: the n-tiles of one pixel tile (sharing its gathered rows) under one L2
+            const uint32_t L = xcd_swizzle(q, ntile);
+            mt = int(L / uint32_t(a.grid_n));
+            nt = int(L - uint32_t(mt) * uint32_t(a.grid_n));
+        } else {
+            mt = int(q % uint32_t(a.grid_m));
+            nt = int(q / uint32_t(a.grid_m));
+        }
+        m0_ = mt * BM;
+        n0_ = nt * BN;
+    };
+    uint32_t q = blockIdx.x;
+    int m0, n0;
+    tile_of(q, m0, n0);
 
     auto soff = [](int row, int col) { return row * 64 + ((((col >> 1) ^ (row >> 1)) & 3) << 4) + ((col & 1) << 3); };
 
@@ -61,31 +74,38 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
     const ST *a_base[A_PER];
     int a_sy[A_PER], a_sx[A_PER], a_off[A_PER];
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-        const int row = (tid >> 3) + i * (NT / 8);
-        const int m = m0 + row;
-        const bool ok = m < a.M;
-        const uint32_t mm = ok ? uint32_t(m) : 0u;
-        const uint32_t img = fdiv(mm, a.div_hw);
-        const uint32_t r = mm - img * uint32_t(a.ho * a.wo);
-        const uint32_t oy = fdiv(r, a.div_w);
-        const uint32_t ox = r - oy * uint32_t(a.wo);
-        a_sy[i] = ok ? int(oy) * a.stride : -(1 << 20);
-        a_sx[i] = int(ox) * a.stride;
-        a_base[i] = reinterpret_cast<const ST *>(a.src) + (size_t(int(img) * a.hs + (ok ? a_sy[i] : 0)) * a.ws + a_sx[i]) * a.ldc_s +
-                    col * 4;
-        a_off[i] = soff(row, col);
-    }
+    for (int i = 0; i < A_PER; ++i) a_off[i] = soff((tid >> 3) + i * (NT / 8), col);
+    auto set_rows = [&](int m0_) {
+#pragma unroll
+        for (int i = 0; i < A_PER; ++i) {
+            const int m = m0_ + (tid >> 3) + i * (NT / 8);
+            const bool ok = m < a.M;
+            const uint32_t mm = ok ? uint32_t(m) : 0u;
+            const uint32_t img = fdiv(mm, a.div_hw);
+            const uint32_t r = mm - img * uint32_t(a.ho * a.wo);
+            const uint32_t oy = fdiv(r, a.div_w);
+            const uint32_t ox = r - oy * uint32_t(a.wo);
+            a_sy[i] = ok ? int(oy) * a.stride : -(1 << 20);
+            a_sx[i] = int(ox) * a.stride;
+            a_base[i] = reinterpret_cast<const ST *>(a.src) +
+                        (size_t(int(img) * a.hs + (ok ? a_sy[i] : 0)) * a.ws + a_sx[i]) * a.ldc_s + col * 4;
+        }
+    };
+    set_rows(m0);
     const int KS16 = a.K / 16, NB32 = (a.n_out + 31) / 32;
     const uint32_t wplane_b = uint32_t(a.wplane) * 2u;
     uint32_t w_base[TN];
+    auto set_wbase = [&](int n0_) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int cb = (n0 >> 4) + wn * TN + j;  // 16-channel block
-        const int nb = cb >> 1;
-        w_base[j] = nb < NB32 ? uint32_t(nb * KS16 + (g >> 1)) * 1024u + uint32_t(16 * (cb & 1) + l16 + 32 * (g & 1)) * 16u
-                              : kOOB;
-    }
+        for (int j = 0; j < TN; ++j) {
+            const int cb = (n0_ >> 4) + wn * TN + j;  // 16-channel block
+            const int nb = cb >> 1;
+            w_base[j] = nb < NB32 ? uint32_t(nb * KS16 + (g >> 1)) * 1024u +
+                                        uint32_t(16 * (cb & 1) + l16 + 32 * (g & 1)) * 16u
+                                  : kOOB;
+        }
+    };
+    set_wbase(n0);
     const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(a.wsplit, uint32_t(XP) * wplane_b);
 
     const int cpk = a.c / 32;
@@ -135,10 +155,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
     };
 
     f32x4 acc[TN][TM];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     int x_rd[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -147,14 +163,41 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
     }
 
     const int nst = nk / SK;
+    const float *winv = reinterpret_cast<const float *>(reinterpret_cast<const unsigned char *>(a.wsplit) + 2u * wplane_b);
+    float omax = 0.f;
     load_stage(0);
     load_W(0);
     store_stage(0);
     __syncthreads();
+    int buf = 0;   // stage buffer of the current stage (stages run on across the tiles of a persistent block)
+    int tpar = 0;  // tile parity (epilogue constants)
+    for (;;) {
+    const uint32_t qn = q + gridDim.x;
+    const bool has_next = P && qn < ntile;
+    int nm0 = 0, nn0 = 0;
+    if (has_next) tile_of(qn, nm0, nn0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the epilogue's per-channel scale and bias into LDS now, before any of the next tile's stage loads (vmcnt retires
+    // in order: loaded in the epilogue they would wait for those); read after at least one stage barrier
+    for (int c = tid; c < BN; c += NT) {
+        const int n = n0 + c;
+        const int oc = a.store_mode == 1 ? n - (n / a.cout) * a.cout : n;
+        const bool nok = n < a.n_out;
+        ep_sc[tpar][c] = H2 && nok ? winv[n] * xs_inv : 1.f;
+        ep_b[tpar][c] = a.bias && nok ? a.bias[oc] : 0.f;
+    }
     for (int st = 0; st < nst; ++st) {
         const bool more = st + 1 < nst;
-        if (more) load_stage(st + 1);
-        const unsigned char *const sb = smem + (st & 1) * STG;
+        if (more) {
+            load_stage(st + 1);
+        } else if (has_next) {  // the next tile's first stage, behind this tile's last MFMAs and its epilogue
+            set_rows(nm0);
+            load_stage(0);
+        }
+        const unsigned char *const sb = smem + buf * STG;
 #pragma unroll
         for (int s = 0; s < SK; ++s) {
             u32x4 xh[TM], xm[TM];
@@ -181,21 +224,26 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
                                                                             acc[j][i], 0, 0, 0);
                 }
             }
-            if (st * SK + s + 1 < nk) load_W(st * SK + s + 1);  // next k-step's fragments (L2), one step ahead
+            if (st * SK + s + 1 < nk) {
+                load_W(st * SK + s + 1);  // next k-step's fragments (L2), one step ahead
+            } else if (has_next) {
+                set_wbase(nn0);
+                load_W(0);
+            }
         }
         // the other buffer was last read in stage st - 1, which every wave has left (barrier below)
-        if (more) store_stage((st + 1) & 1);
+        if (more || has_next) store_stage(buf ^ 1);
         __syncthreads();
+        buf ^= 1;
     }
 
     // h2: undo the operand scales (powers of two: exact); add the bias, store 4 channels per lane
-    const float *winv = reinterpret_cast<const float *>(reinterpret_cast<const unsigned char *>(a.wsplit) + 2u * wplane_b);
-    float omax = 0.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * WCH + j * 16 + 4 * g;
         if (n >= a.n_out) continue;  // n_out % 4 == 0: a lane's 4 channels are all in or all out
-        const f32x4 sc = H2 ? gload4(winv + n) * xs_inv : f32x4{1.f, 1.f, 1.f, 1.f};
+        const int nl = wn * WCH + j * 16 + 4 * g;
+        const f32x4 sc = *reinterpret_cast<const f32x4 *>(&ep_sc[tpar][nl]);
         int oc = n, di = 0, dj = 0;
         if (a.store_mode == 1) {
             const int ij = n / a.cout;
@@ -203,7 +251,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
             di = ij >> 1;
             dj = ij & 1;
         }
-        const f32x4 b4 = a.bias ? gload4(a.bias + oc) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 b4 = *reinterpret_cast<const f32x4 *>(&ep_b[tpar][nl]);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int m = m0 + wm * WPX + i * 16 + l16;
@@ -221,6 +269,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
             omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
         }
     }
+    if (!has_next) break;
+    q = qn;
+    m0 = nm0;
+    n0 = nn0;
+    tpar ^= 1;
+    }
     if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the wave takes part
 }
 
@@ -229,6 +283,22 @@ namespace {
 constexpr int kSK = 2;  // 32-channel k-steps per stage
 
 int gather16_enabled(uint32_t tune) { return (tune & SCD_TUNE_NO_GATHER16) ? 0 : 1; }
+int gather16_persist(uint32_t tune) { return (tune & SCD_TUNE_GATHER16_PERSIST) ? 1 : 0; }
+
+// Resident blocks of `fn` on the device (occupancy x CUs), cached per kernel by the caller.
+int resident_blocks(const void *fn, int threads, int *cache) {
+    if (*cache > 0) return *cache;
+    int per_cu = 0, cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess || per_cu < 1 || cus < 1) {
+        (void)hipGetLastError();
+        per_cu = 2;
+        cus = 256;
+    }
+    *cache = per_cu * cus;
+    return *cache;
+}
 
 template <int WM, int WN, int TM, int TN, int OCC, int NP, bool SB = false>
 void launch_g16(const IgemmArgs &a, hipStream_t s) {
@@ -237,8 +307,17 @@ void launch_g16(const IgemmArgs &a, hipStream_t s) {
     b.grid_m = (a.M + BM - 1) / BM;
     b.grid_n = (a.n_out + BN - 1) / BN;
     b.remap = xcd_remap_enabled(a.tune);
-    hipLaunchKernelGGL((igemm_gather16<WM, WN, TM, TN, kSK, OCC, NP, SB>), dim3(b.grid_m * b.grid_n), dim3(64 * WM * WN),
-                       0, s, b);
+    const uint32_t ntile = uint32_t(b.grid_m * b.grid_n);
+    if (gather16_persist(a.tune)) {
+        // as many blocks as are resident (a multiple of 8: a block's tiles q, q + grid, ... stay on its XCD)
+        const auto fn = igemm_gather16<WM, WN, TM, TN, kSK, OCC, NP, SB, true>;
+        static int cap = 0;
+        uint32_t nb = uint32_t(resident_blocks(reinterpret_cast<const void *>(fn), 64 * WM * WN, &cap));
+        nb = ntile <= nb ? ntile : (nb >= 8 ? nb & ~7u : nb);
+        hipLaunchKernelGGL(fn, dim3(nb), dim3(64 * WM * WN), 0, s, b);
+        return;
+    }
+    hipLaunchKernelGGL((igemm_gather16<WM, WN, TM, TN, kSK, OCC, NP, SB>), dim3(ntile), dim3(64 * WM * WN), 0, s, b);
 }
 
 // h2 with the h2 weight split and a source bound; bf16 on plane 0 of the bf16 weight split (no bound needed)

@@ -33,7 +33,7 @@ _F32 = torch.float32
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
          'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True, 'defer_bn_bwd': True, 'fuse_head': True,
-         'convT_bias_in_wgrad': True}
+         'convT_bias_in_wgrad': True, 'head_wgrad_in_bn_bwd': True}
 
 
 def conv_math_for(cfg) -> str:
@@ -490,6 +490,7 @@ class _HeadGrad:
     g: torch.Tensor
     w2: torch.Tensor
     n_out: int
+    w_grad: torch.Tensor | None = None  # also the head's weight grad ([n_out][C]) from the same pass
 
 
 def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, dy_bound=None):
@@ -503,8 +504,10 @@ def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, dy_bo
     n, h, w, _ = y.shape
     ws = _ws(hip.bn_workspace_bytes(n, h, w, c, st.nseg), y)
     if isinstance(g, _HeadGrad):
+        if g.w_grad is not None:
+            ws = _ws(hip.bn_head_workspace_bytes(n, h, w, c, st.nseg, g.n_out), y)
         hip.bn_relu_backward_head(nhwc(y), g.g, g.w2, g.n_out, st.nseg, st.smean, st.sinv, bn.weight, st.scale,
-                                  st.shift, dgamma, dbeta, dbias, nhwc(dy), ws, dy_bound)
+                                  st.shift, dgamma, dbeta, dbias, nhwc(dy), ws, dy_bound, g.w_grad)
     elif isinstance(g, _PooledGrad):
         hip.bn_relu_backward_pooled(nhwc(y), nhwc(g.gy) if g.gy is not None else hip._NULL, g.idx,
                                     nhwc(g.gskip) if g.gskip is not None else hip._NULL, g.skip_mode, st.nseg,
@@ -949,9 +952,12 @@ class DecoderFn(torch.autograd.Function):
             gw = _empty(tuple(wshape), y1)
             gb = _empty((n_out,), y1) if has_bias else None
             ws = _ws(hip.conv1x1_workspace_bytes(nhwc(y1), n_out), y1)
-            hip.conv1x1_bwd_bn(nhwc(y1), st1.scale, st1.shift, st1.nseg, w2, g, n_out, gw, gb, ws)
+            # the head's weight grad comes from its BatchNorm's backward pass over y1 (scd_bn_relu_backward_head
+            # w_grad); here only its bias grad
+            fold = _OPTS['head_wgrad_in_bn_bwd']
+            hip.conv1x1_bwd_bn(nhwc(y1), st1.scale, st1.shift, st1.nseg, w2, g, n_out, None if fold else gw, gb, ws)
             head_grads = [gw, gb]
-            g = _HeadGrad(g, w2, n_out)
+            g = _HeadGrad(g, w2, n_out, gw if fold else None)
             ctx.head = None
         for k in range(n - 1, -1, -1):
             up = ups[k]

@@ -150,9 +150,10 @@ _SIGS = {
     "scd_bn_relu_backward_pooled": ([NHWC, NHWC, c_void_p, NHWC, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p,
                                      c_size_t, c_void_p], c_int),
+    "scd_bn_head_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32, c_int32], c_size_t),
     "scd_bn_relu_backward_head": ([NHWC, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
-                                   c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_size_t,
-                                   c_void_p], c_int),
+                                   c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_void_p,
+                                   c_size_t, c_void_p], c_int),
     "scd_bn_relu_backward_tiles": (
         [NHWC, NHWC, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
          c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_size_t, c_void_p],
@@ -412,6 +413,7 @@ TUNE_NO_HALO = 1 << 26
 TUNE_HALO16_LATE_LOAD = 1 << 27
 TUNE_H2_TILE64_128 = 1 << 28
 TUNE_HALO16_WS = 1 << 29
+TUNE_GATHER16_PERSIST = 1 << 30
 
 
 def tune_halo16_cfg(tile_id: int) -> int:
@@ -709,15 +711,20 @@ def bn_relu_backward_pooled(y: NHWC, gy: NHWC, idx, gskip: NHWC, skip_mode: int,
         "scd_bn_relu_backward_pooled")
 
 
+def bn_head_workspace_bytes(n, h, w, c, nseg, n_out) -> int:
+    return lib().scd_bn_head_workspace_bytes(n, h, w, c, nseg, n_out)
+
+
 def bn_relu_backward_head(y: NHWC, gout: torch.Tensor, w_head: torch.Tensor, n_out: int, nseg, smean, sinv, gamma,
-                          scale, shift, dgamma, dbeta, dbias, dy: NHWC, ws, dy_bound=None):
+                          scale, shift, dgamma, dbeta, dbias, dy: NHWC, ws, dy_bound=None, w_grad=None):
     """bn_relu_backward of da = gout . w_head, the 1x1 head's input gradient (conv1x1_bwd's gx, never materialised);
-    gout NCHW [n][n_out][h][w], w_head [n_out][C]."""
+    gout NCHW [n][n_out][h][w], w_head [n_out][C].  `w_grad` ([n_out][C]): also the head's weight grad from the same
+    pass (workspace bn_head_workspace_bytes)."""
     _check(
         lib().scd_bn_relu_backward_head(y, gout.data_ptr(), w_head.data_ptr(), n_out, nseg, smean.data_ptr(),
                                         sinv.data_ptr(), _ptr(gamma), scale.data_ptr(), shift.data_ptr(), _ptr(dgamma),
-                                        _ptr(dbeta), _ptr(dbias), dy, _ptr(dy_bound), ws.data_ptr(), ws.numel(),
-                                        _stream()),
+                                        _ptr(dbeta), _ptr(dbias), dy, _ptr(dy_bound), _ptr(w_grad), ws.data_ptr(),
+                                        ws.numel(), _stream()),
         "scd_bn_relu_backward_head")
 
 

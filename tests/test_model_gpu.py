@@ -293,7 +293,7 @@ def test_fused_head_bit_identical(dev, name):
     fx = Fixture(name)
     res = []
     for fused in (True, False):
-        prev = engine.set_options(fuse_head=fused)
+        prev = engine.set_options(fuse_head=fused, head_wgrad_in_bn_bwd=False)
         try:
             cfg, net = _build(fx, dev)
             net.train()
@@ -315,6 +315,42 @@ def test_fused_head_bit_identical(dev, name):
     assert g1.keys() == g0.keys()
     for k in g0:
         assert torch.equal(g1[k], g0[k]), k
+
+
+@pytest.mark.parametrize('name', ['siamese_t8-16', 'siamese_t8-16-32_odd', 'dtsiamese_t8-16'])
+def test_head_weight_grad_from_bn_backward(dev, name):
+    """The fused head's weight grad taken in its BatchNorm's partial pass (engine head_wgrad_in_bn_bwd:
+    scd_bn_relu_backward_head w_grad) vs its own weighted channel sum (scd_conv1x1_bwd_bn gw): logits, loss and every
+    other gradient bit-identical, the head weights' within 1e-6 (same chunks and tree, the products' rounding may
+    contract differently)."""
+    from multimodal_siamese_cd_amd import engine, trainers
+    fx = Fixture(name)
+    res = []
+    for fold in (True, False):
+        prev = engine.set_options(fuse_head=True, head_wgrad_in_bn_bwd=fold)
+        try:
+            cfg, net = _build(fx, dev)
+            net.train()
+            batch = {k: v.to(dev) for k, v in fx.batch().items()}
+            out = net(batch['x_t1'], batch['x_t2'])
+            loss = trainers.step_loss(cfg, out, batch)
+            loss.backward()
+            res.append(([o.detach().cpu() for o in _outs(out)], loss.item(),
+                        {k: p.grad.cpu() for k, p in net.module.named_parameters() if p.grad is not None}))
+        finally:
+            engine.set_options(**prev)
+    (o1, l1, g1), (o0, l0, g0) = res
+    assert l1 == l0
+    for a, b in zip(o1, o0):
+        assert torch.equal(a, b)
+    assert g1.keys() == g0.keys()
+    heads = [k for k in g0 if k.startswith('outc') and k.endswith('weight')]
+    assert heads
+    for k in g0:
+        if k in heads:
+            assert ((g1[k] - g0[k]).abs().max() / g0[k].abs().max()).item() < 1e-6, k
+        else:
+            assert torch.equal(g1[k], g0[k]), k
 
 
 @pytest.mark.parametrize('name', ['siamese_t8-16', 'siamese_t8-16-32_odd', 'whatevernet_t8-16'])

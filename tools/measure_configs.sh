@@ -13,5 +13,6 @@ run --config baseline_siamese --math x5
 run --config baseline_siamese --math bf16
 run --config baseline_siamese --math bf16 --batch 64
 run --config baseline_dualstream
+run --config baseline_dualstream --batch 64
 run --config dtsiamese
 run --config siamese_mmcr_alpha0500 --batch 16

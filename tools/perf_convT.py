@@ -37,11 +37,14 @@ def main():
     ap.add_argument('--plain', action='store_true', help='also time the forward GEMM with plain stores')
     ap.add_argument('--math', default='x3', choices=['x3', 'h2'])
     ap.add_argument('--dst-bound', action='store_true', help='forward raises a dst bound (h2 engine path)')
+    ap.add_argument('--tunes', default=None, help='comma list of raw SCD_TUNE_* values to compare instead of --tiles '
+                                                  '(e.g. 0,0x40000000)')
     args = ap.parse_args()
     hip.load_library()
     hip.set_conv_math(args.math)
     dev = torch.device('cuda:0')
-    tiles = args.tiles.split(',')
+    tiles = args.tunes.split(',') if args.tunes else args.tiles.split(',')
+    tune_of = (lambda t: int(t, 0)) if args.tunes else (lambda t: hip.tune_x3_tile(int(t)))
     # (level, input size, ConvT channels (in == out, networks.py Up), skip channels) of SiameseUNet [64,128,256,512]
     # at 256^2
     levels = [('up4', 16, 512, 512, 512), ('up3', 32, 256, 256, 256), ('up2', 64, 128, 128, 128),
@@ -65,7 +68,7 @@ def main():
             if args.dst_bound:
                 db = torch.zeros(1, device=dev)
         for t in tiles:
-            hip.set_tune(hip.tune_x3_tile(int(t)))  # 0: automatic
+            hip.set_tune(tune_of(t))  # tiles: 0 = automatic
             f = timeit(lambda: hip.conv_igemm(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, bias, gup,
                                               store_mode=1, src_bound=xb, dst_bound=db), args.reps)
             d = timeit(lambda: hip.conv_igemm(gup, hc, hc, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx), src_bound=gb),
@@ -77,8 +80,9 @@ def main():
                 print(f'{name} tile {t}: fwd plain-store {fp * 1e3:7.1f} us', flush=True)
             tot[t][0] += f
             tot[t][1] += d
-            print(f'{name} hc={hc:4d} ci={ci:4d} co={co:4d} tile {t}: fwd {f * 1e3:7.1f} us  dgrad {d * 1e3:7.1f} us',
-                  flush=True)
+            gb_ = 4 * b * hc * hc * ci * 5 / 1e9  # fp32 bytes: fwd reads x, writes 4x its pixels; dgrad the reverse
+            print(f'{name} hc={hc:4d} ci={ci:4d} co={co:4d} {"tune" if args.tunes else "tile"} {t}: fwd {f * 1e3:7.1f} us '
+                  f'({gb_ / f:5.2f} TB/s)  dgrad {d * 1e3:7.1f} us ({gb_ / d:5.2f} TB/s)', flush=True)
     hip.set_tune(0)
     for t, (f, d) in tot.items():
         print(f'tile {t}: fwd {f * 1e3:7.1f} us  dgrad {d * 1e3:7.1f} us  sum {(f + d) * 1e3:7.1f} us')
