@@ -103,6 +103,12 @@ int scd_pack_conv3x3(const float *w, int32_t co, int32_t ci, int32_t ci_pad, int
  *   mode 1 (data grad): [ci][(i*2+j)*co + o]
  * replaces: nn.ConvTranspose2d(C,C,2,stride=2) parameter layout (networks.py:433). */
 int scd_pack_convT2x2(const float *w, int32_t ci, int32_t co, int32_t mode, float *out, scd_stream_t stream);
+/* Several ConvTranspose2d weights in three launches: per job (scd_pack_job_t: w [ci][co][2][2], out as
+ * scd_pack_convT2x2 mode 0 / 1, ci_pad ignored) the packed layout and, with `split`, its fragment-order split in the
+ * format the conv reading it expects under job.math (scd_split_h2_frag where h2_weight_format applies -- 1 tap over ci
+ * channels (mode 0) or 4 taps over co (mode 1), a multiple of 32 -- else scd_split_bf16x3_frag; K % 16 == 0).
+ * Results equal the one-weight calls. */
+int scd_pack_convT2x2_multi(const scd_pack_job_t *jobs, int32_t n, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Conv arithmetic, chosen per launch by scd_igemm_t.math / scd_wgrad_t.math (and scd_pack_job_t.math for the

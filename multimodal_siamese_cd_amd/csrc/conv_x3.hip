@@ -1306,6 +1306,161 @@ __global__ void h2_split_frag_kernel(const float *__restrict__ w, int n_out, int
 }
 }  // namespace scd
 
+namespace scd {
+// ------------------------------------------------------------------------------------------------
+// Batched ConvTranspose2d(2, s2) weight preparation (scd_pack_convT2x2_multi): the packed layouts of
+// scd_pack_convT2x2 and their fragment-order splits (h2 or bf16x3) for up to kConvTJobs weights in three launches
+// (pack, h2 row scales, split) instead of three per weight.  Same index maps and split arithmetic as the one-weight
+// path (pack_convT_kernel, h2_rowscale_kernel, h2_split_frag_kernel / split_frag_kernel).
+// ------------------------------------------------------------------------------------------------
+constexpr int kConvTJobs = 8;
+struct ConvTJobs {
+    const float *w[kConvTJobs];
+    float *out[kConvTJobs];
+    uint16_t *split[kConvTJobs];
+    int ci[kConvTJobs], co[kConvTJobs], mode[kConvTJobs];
+    int fmt[kConvTJobs];                // 0 no split, 1 bf16x3, 2 h2
+    int64_t first_e[kConvTJobs + 1];    // packed elements (ci * co * 4), prefix sums
+    int first_rs[kConvTJobs + 1];       // h2 jobs: padded split rows, prefix sums
+    int64_t first_f[kConvTJobs + 1];    // split jobs: fragment lanes (NB * K/16 * 64), prefix sums
+    int n;
+};
+__device__ __forceinline__ int convT_job(const int64_t *first, int n, int64_t e) {
+    int q = 0;
+    while (q + 1 < n && e >= first[q + 1]) ++q;
+    return q;
+}
+__device__ __forceinline__ void convT_dims(const ConvTJobs &J, int q, int &n_out, int &K) {
+    n_out = J.mode[q] == 0 ? 4 * J.co[q] : J.ci[q];
+    K = J.mode[q] == 0 ? J.ci[q] : 4 * J.co[q];
+}
+__global__ void convT_pack_multi_kernel(ConvTJobs J) {
+    const int64_t total = J.first_e[J.n];
+    for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < total; g += int64_t(gridDim.x) * blockDim.x) {
+        const int q = convT_job(J.first_e, J.n, g);
+        const int64_t e = g - J.first_e[q];
+        const int ci = J.ci[q], co = J.co[q];
+        if (J.mode[q] == 0) {  // out[(t*co + o)][c]
+            const int c = int(e % ci);
+            const int r = int(e / ci);
+            const int t = r / co, o = r % co;
+            J.out[q][e] = J.w[q][(int64_t(c) * co + o) * 4 + t];
+        } else {  // out[c][t*co + o]
+            const int col = int(e % (4 * co));
+            const int c = int(e / (4 * co));
+            const int t = col / co, o = col % co;
+            J.out[q][e] = J.w[q][(int64_t(c) * co + o) * 4 + t];
+        }
+    }
+}
+__global__ __launch_bounds__(256) void convT_rowscale_multi_kernel(ConvTJobs J) {
+    const int wave = int(blockIdx.x) * 4 + int(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (wave >= J.first_rs[J.n]) return;
+    int q = 0;
+    while (q + 1 < J.n && wave >= J.first_rs[q + 1]) ++q;
+    int n_out, K;
+    convT_dims(J, q, n_out, K);
+    const int r = wave - J.first_rs[q];
+    float mx = 0.f;
+    if (r < n_out)
+        for (int k = lane; k < K; k += 64) mx = fmaxf(mx, fabsf(J.out[q][size_t(r) * K + k]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    if (lane == 0) {
+        float sc, inv;
+        h2_scale(mx, sc, inv);
+        h2_row_inv(J.split[q], int64_t((n_out + 31) / 32) * 32 * K)[r] = inv;
+    }
+}
+__global__ void convT_split_multi_kernel(ConvTJobs J) {
+    const int64_t total = J.first_f[J.n];
+    for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < total; g += int64_t(gridDim.x) * blockDim.x) {
+        const int q = convT_job(J.first_f, J.n, g);
+        if (!J.fmt[q]) continue;
+        const int64_t e = g - J.first_f[q];
+        int n_out, K;
+        convT_dims(J, q, n_out, K);
+        const int KS = K / 16, NB = (n_out + 31) / 32;
+        const int64_t plane = int64_t(NB) * KS * 64 * 8;
+        const int lane = int(e & 63);
+        const int64_t fk = e >> 6;
+        const int nb = int(fk / KS), ks = int(fk - int64_t(nb) * KS);
+        const int n = nb * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
+        const float *w = J.out[q];
+        uint16_t *o = J.split[q] + e * 8;
+        f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+        if (J.fmt[q] == 2) {
+            if (n < n_out) {
+                const float sc = 1.f / h2_row_inv(J.split[q], plane)[n];
+                v0 = gload4(w + size_t(n) * K + k0) * sc;
+                v1 = gload4(w + size_t(n) * K + k0 + 4) * sc;
+            }
+            u32x2 h0, m0, h1, m1;
+            split2h(v0, h0, m0);
+            split2h(v1, h1, m1);
+            *reinterpret_cast<u32x4 *>(o) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+            *reinterpret_cast<u32x4 *>(o + plane) = u32x4{m0[0], m0[1], m1[0], m1[1]};
+        } else {
+            if (n < n_out) {
+                v0 = gload4(w + size_t(n) * K + k0);
+                v1 = gload4(w + size_t(n) * K + k0 + 4);
+            }
+            u32x2 h0, m0, l0, h1, m1, l1;
+            split3(v0, h0, m0, l0);
+            split3(v1, h1, m1, l1);
+            *reinterpret_cast<u32x4 *>(o) = u32x4{h0[0], h0[1], h1[0], h1[1]};
+            *reinterpret_cast<u32x4 *>(o + plane) = u32x4{m0[0], m0[1], m1[0], m1[1]};
+            *reinterpret_cast<u32x4 *>(o + 2 * plane) = u32x4{l0[0], l0[1], l1[0], l1[1]};
+        }
+    }
+}
+}  // namespace scd
+
+extern "C" int scd_pack_convT2x2_multi(const scd_pack_job_t *jobs, int32_t n, scd_stream_t stream) {
+    clear_error();
+    if (!jobs || n < 0) {
+        set_error("pack_convT2x2_multi: bad arguments");
+        return SCD_ERR_ARG;
+    }
+    const hipStream_t s = as_stream(stream);
+    auto grid = [](int64_t total) { return dim3(unsigned(std::min<int64_t>((total + 255) / 256, 8192))); };
+    for (int base = 0; base < n; base += kConvTJobs) {
+        ConvTJobs J;
+        J.n = std::min(kConvTJobs, n - base);
+        J.first_e[0] = 0;
+        J.first_rs[0] = 0;
+        J.first_f[0] = 0;
+        for (int i = 0; i < J.n; ++i) {
+            const scd_pack_job_t &P = jobs[base + i];
+            const int n_out = P.mode == 0 ? 4 * P.co : P.ci, K = P.mode == 0 ? P.ci : 4 * P.co;
+            if (!P.w || !P.out || P.co < 1 || P.ci < 1 || (P.mode != 0 && P.mode != 1) ||
+                (P.split && (K % 16 || !aligned16(P.split) || !aligned16(P.out)))) {
+                set_error("pack_convT2x2_multi: job %d: bad arguments (split needs K %% 16 == 0, 16-byte alignment)",
+                          base + i);
+                return SCD_ERR_ARG;
+            }
+            J.w[i] = P.w;
+            J.out[i] = P.out;
+            J.split[i] = P.split;
+            J.ci[i] = P.ci;
+            J.co[i] = P.co;
+            J.mode[i] = P.mode;
+            const int c = P.mode == 0 ? P.ci : P.co;  // source channels of the conv reading this layout
+            J.fmt[i] = !P.split ? 0 : h2_weight_format(P.math, P.mode == 0 ? 1 : 4, c) ? 2 : 1;
+            const int NB = (n_out + 31) / 32;
+            J.first_e[i + 1] = J.first_e[i] + int64_t(P.ci) * P.co * 4;
+            J.first_rs[i + 1] = J.first_rs[i] + (J.fmt[i] == 2 ? NB * 32 : 0);
+            J.first_f[i + 1] = J.first_f[i] + (J.fmt[i] ? int64_t(NB) * (K / 16) * 64 : 0);
+        }
+        hipLaunchKernelGGL(convT_pack_multi_kernel, grid(J.first_e[J.n]), dim3(256), 0, s, J);
+        if (J.first_rs[J.n] > 0)
+            hipLaunchKernelGGL(convT_rowscale_multi_kernel, dim3((J.first_rs[J.n] + 3) / 4), dim3(256), 0, s, J);
+        if (J.first_f[J.n] > 0) hipLaunchKernelGGL(convT_split_multi_kernel, grid(J.first_f[J.n]), dim3(256), 0, s, J);
+        SCD_TRY(launch_status("scd_pack_convT2x2_multi"));
+    }
+    return SCD_OK;
+}
+
 extern "C" int scd_split_h2_frag(const float *w, int32_t n_out, int32_t K, uint16_t *dst, scd_stream_t stream) {
     clear_error();
     if (!w || !dst || n_out < 1 || K < 16 || K % 16 || !aligned16(w) || !aligned16(dst)) {

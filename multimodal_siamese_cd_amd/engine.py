@@ -105,8 +105,9 @@ class _IdentityMap:
 
 
 class _WeightGroup:
-    def __init__(self, weights):
-        self.refs = [weakref.ref(w) for w in weights]
+    def __init__(self, weights, convT_weights=()):
+        self.refs = [weakref.ref(w) for w in weights]  # 3x3 conv weights
+        self.trefs = [weakref.ref(w) for w in convT_weights]  # ConvTranspose2d(2, s2) weights
         self.gen = 0
 
 
@@ -116,8 +117,9 @@ _PACKED = _IdentityMap()  # weight Parameter -> {key: (generation, data_ptr, pac
 
 def register_weight_group(model: torch.nn.Module):
     convs = [m for m in model.modules() if isinstance(m, torch.nn.Conv2d) and m.kernel_size == (3, 3)]
-    group = _WeightGroup([c.weight for c in convs])
-    for c in convs:
+    convTs = [m for m in model.modules() if isinstance(m, torch.nn.ConvTranspose2d) and m.kernel_size == (2, 2)]
+    group = _WeightGroup([c.weight for c in convs], [c.weight for c in convTs])
+    for c in convs + convTs:
         _GROUPS.setdefault(c.weight, group)
 
     def new_generation(_module, _args):
@@ -166,6 +168,29 @@ def packed_conv3x3(weight: torch.Tensor, mode: int, ci_pad: int | None = None) -
         packs = hip.pack_conv3x3_multi([(w.detach(), mode, cp) for w, cp in todo])
     for (w, cp), pk in zip(todo, packs):
         _PACKED.setdefault(w, {})[_pack_key(mode, cp)] = (group.gen, w.data_ptr(), pk)
+    return packs[0]
+
+
+def packed_convT2x2(weight: torch.Tensor, mode: int) -> torch.Tensor:
+    """hip.pack_convT2x2(weight, mode) through the per-forward group cache: the first request of a forward packs (and
+    splits) every ConvTranspose weight of the model in that layout in one batched call (scd_pack_convT2x2_multi)."""
+    group = _GROUPS.get(weight)
+    if not _OPTS['pack_cache'] or group is None or not any(r() is weight for r in group.trefs):
+        return hip.pack_convT2x2(weight.detach(), mode)
+    key = ('convT', mode, hip.conv_math())
+    hit = _cached(weight, key, group)
+    if hit is not None:
+        return hit
+    todo = [weight]
+    if _OPTS['batch_pack']:
+        for r in group.trefs:
+            w = r()
+            if w is not None and w is not weight and w.device == weight.device and _cached(w, key, group) is None:
+                todo.append(w)
+    with torch.no_grad():
+        packs = hip.pack_convT2x2_multi([(w.detach(), mode) for w in todo])
+    for w, pk in zip(todo, packs):
+        _PACKED.setdefault(w, {})[key] = (group.gen, w.data_ptr(), pk)
     return packs[0]
 
 
@@ -886,7 +911,7 @@ class DecoderFn(torch.autograd.Function):
             else:
                 cat = _act((b, h, w, cs + cto), skip)
                 hip.feature_grad(hip._NULL, None, nhwc(skip), 0, nhwc(cat, 0, cs))  # skip -> cat[..., :cs]
-            wT = hip.pack_convT2x2(convT.weight.detach(), 0)
+            wT = packed_convT2x2(convT.weight, 0)
             # h2: the concat's own bound, seeded with the skip's and raised by the ConvT epilogue to max |up| (F.pad's
             # zero border adds nothing); the skip's bound, also read by the encoder's weight grads, stays as it is.
             # The ConvT reads cur through cur's bound.
@@ -979,7 +1004,7 @@ class DecoderFn(torch.autograd.Function):
             # DoubleConv data grad that wrote it)
             g_cur = torch.empty_like(cur)
             gcat_bound = _bound_of(g_cat, pool)
-            hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, hip.pack_convT2x2(convT.weight.detach(), 1), cu, None,
+            hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, packed_convT2x2(convT.weight, 1), cu, None,
                            nhwc(g_cur), src_bound=gcat_bound)
             # ConvT weight grad: rows = convT input, src = g_up gathered with stride 2 (h2: both bounds)
             # (and its bias grad: the kernel sums the g_up columns it stages, scd_wgrad_t.src_colsum)

@@ -108,6 +108,7 @@ _SIGS = {
     "scd_pack_nchw": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, NHWC, c_void_p, c_void_p], c_int),
     "scd_pack_conv3x3": ([c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_pack_conv3x3_multi": ([c_void_p, c_int32, c_void_p], c_int),
+    "scd_pack_convT2x2_multi": ([c_void_p, c_int32, c_void_p], c_int),
     "scd_pack_convT2x2": ([c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p], c_int),
     "scd_split_bf16x3": ([c_void_p, c_int64, c_void_p, c_void_p], c_int),
     "scd_split_frag_bytes": ([c_int32, c_int32], c_size_t),
@@ -346,6 +347,30 @@ def pack_convT2x2(w: torch.Tensor, mode: int) -> torch.Tensor:
     _check(lib().scd_pack_convT2x2(w.contiguous().data_ptr(), ci, co, mode, out.data_ptr(), _stream()),
            "scd_pack_convT2x2")
     return _attach_split(out, 4 * co, ci, 1) if mode == 0 else _attach_split(out, ci, 4 * co, 4)
+
+
+def pack_convT2x2_multi(jobs) -> list:
+    """jobs: [(weight [ci][co][2][2], mode)] -> packed tensors as pack_convT2x2 returns them (split planes attached
+    under the split conv arithmetics), all prepared in three launches per 8 weights."""
+    if not jobs:
+        return []
+    split = conv_math() != 'f32'
+    m = _MATH_NAMES[conv_math()]
+    outs, keep, arr = [], [], (PACKJOB * len(jobs))()
+    for i, (w, mode) in enumerate(jobs):
+        ci, co = w.shape[0], w.shape[1]
+        w = w.contiguous()
+        n_out, K = (4 * co, ci) if mode == 0 else (ci, 4 * co)
+        out = torch.empty(ci * co * 4, device=w.device, dtype=torch.float32)
+        sp = None
+        if split and K % 16 == 0:
+            sp = torch.empty(lib().scd_split_frag_bytes(n_out, K) // 2, dtype=torch.int16, device=w.device)
+            out._x3 = sp
+        keep.append(w)
+        arr[i] = PACKJOB(w.data_ptr(), out.data_ptr(), _ptr(sp), co, ci, ci, mode, m)
+        outs.append(out)
+    _check(lib().scd_pack_convT2x2_multi(ctypes.cast(arr, c_void_p), len(jobs), _stream()), "scd_pack_convT2x2_multi")
+    return outs
 
 
 def split_bf16x3(src: torch.Tensor) -> torch.Tensor:

@@ -1137,3 +1137,31 @@ def test_wgrad_repeat_runs_identical(dev, math):
                     first = slabs.clone()
                 else:
                     assert torch.equal(slabs, first), (n, h, w, ci, co)
+
+
+@pytest.mark.parametrize('arith', ['x3', 'h2', 'bf16'])
+def test_batched_convT_pack_equals_standalone(dev, arith):
+    """scd_pack_convT2x2_multi (three launches for every job) writes the packed layouts and the split bytes (h2 where
+    the format applies: 32-channel multiples; bf16x3 otherwise) of the one-weight pack_convT2x2, both modes, with more
+    jobs than one launch holds (8)."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(9)
+    shapes = [(512, 512), (256, 256), (128, 128), (64, 64), (48, 48), (16, 16), (96, 32), (32, 80), (8, 8)]
+    jobs = []
+    for ci, co in shapes:
+        w = (torch.randn(ci, co, 2, 2, generator=g) * 10 ** (2 * torch.rand(ci, 1, 1, 1, generator=g) - 1)).to(dev)
+        jobs += [(w, 0), (w, 1)]
+    with hip.conv_scope(arith):
+        multi = hip.pack_convT2x2_multi(jobs)
+        for (w, mode), got in zip(jobs, multi):
+            ref = hip.pack_convT2x2(w, mode)
+            assert torch.equal(got, ref), (tuple(w.shape), mode)
+            a, b = getattr(got, '_x3', None), getattr(ref, '_x3', None)
+            assert (a is None) == (b is None), (tuple(w.shape), mode)
+            if a is not None:
+                ci, co = w.shape[0], w.shape[1]
+                rows, K, taps = (4 * co, ci, 1) if mode == 0 else (ci, 4 * co, 4)
+                if hip.h2_weight_format(K, taps):  # two fp16 planes and the row scales; the rest is not written
+                    n = 2 * ((rows + 31) // 32 * 32) * K + 2 * ((rows + 31) // 32 * 32)
+                    a, b = a[:n], b[:n]
+                assert torch.equal(a, b), (tuple(w.shape), mode)
