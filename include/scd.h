@@ -185,6 +185,8 @@ int scd_abi_version(void);
                                                  the halo, the compute waves load only weights (128 px tiles)        */
 #define SCD_TUNE_GATHER16_PERSIST (1u << 30)  /* ConvTranspose gather kernel as persistent blocks: each walks tiles, the
                                                  next tile's first stage loaded behind the current tile's last one   */
+#define SCD_TUNE_WGRAD16_DB       (1u << 31)  /* h2 halo weight grad with two patch buffers, one barrier per patch and
+                                                 (128-row blocks) the two wave groups staggered                      */
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.
  * n % 8 == 0, src and dst 16-byte aligned. */
 int scd_split_bf16x3(const float *src, int64_t n, uint16_t *dst, scd_stream_t stream);

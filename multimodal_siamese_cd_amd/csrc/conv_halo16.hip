@@ -1487,7 +1487,11 @@ __device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][W16L<LC>::CB][W16L<LC>
 // RG = 2 (LC 1 only): a block of 8 waves owns 128 rows r x 64 channels c; the two 4-wave groups share the
 // staged X halo, which is then split and stored once per 128 rows instead of per 64 (the staging per MFMA,
 // a third of the kernel's time at RG 1, drops by ~35%).
-template <int NP, int LC, int RG, bool SB = false>
+// DB (SCD_TUNE_WGRAD16_DB): two patch buffers, one barrier per patch; with RG 2 the second 4-wave group (waves 4-7,
+// the partners of waves 0-3 on their SIMDs) stores the next patch BEFORE its MFMAs while the first group stores it
+// after them, so one wave of each SIMD pair stages while the other computes (a stagger: without it both reach
+// their split + LDS writes, and the matrix cores idle, together).
+template <int NP, int LC, int RG, bool SB = false, bool DB = false>
 __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a) {
     static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
     constexpr uint32_t EB = SB ? 2u : 4u;
@@ -1505,7 +1509,8 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
     constexpr bool H2 = NP == 2 || NP == 4;
     constexpr int DP = w16_dp<NP>();  // dY planes
     constexpr int XP = w16_xp<NP>();  // X planes
-    __shared__ __attribute__((aligned(16))) unsigned char smem[DP * PA + XP * PB];
+    constexpr int STAGE = DP * PA + XP * PB;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[(DB ? 2 : 1) * STAGE];
     float ds = 1.f, ds_inv = 1.f, xs = 1.f, xs_inv = 1.f;  // h2: power-of-two operand scales
     if constexpr (H2) {
         h2_scale(*a.rows_bound, ds, ds_inv);
@@ -1558,7 +1563,8 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
             rb[i] = bload_q<SB>(rs_src, v ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + cq * 4) * EB : kOOB);
         }
     };
-    auto store_patch = [&]() {
+    auto store_patch = [&](int buf) {
+        unsigned char *const smem_b = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * NT;
@@ -1569,15 +1575,15 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
                     split2h_pre(ra[i] * ds, h, m);
                 else
                     split2h(ra[i] * ds, h, m);
-                *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
+                *reinterpret_cast<u32x2 *>(smem_b + PA + o) = m;
             } else if constexpr (DP == 3) {
                 split3(ra[i], h, m, l);
-                *reinterpret_cast<u32x2 *>(smem + PA + o) = m;
-                *reinterpret_cast<u32x2 *>(smem + 2 * PA + o) = l;
+                *reinterpret_cast<u32x2 *>(smem_b + PA + o) = m;
+                *reinterpret_cast<u32x2 *>(smem_b + 2 * PA + o) = l;
             } else {
                 h = stage_bits<SB>(ra[i]);
             }
-            *reinterpret_cast<u32x2 *>(smem + o) = h;
+            *reinterpret_cast<u32x2 *>(smem_b + o) = h;
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i)
@@ -1592,7 +1598,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
                         h = pk_bf16x4(x);
                     }
                     const int e = tid + i * NT;
-                    *reinterpret_cast<u32x2 *>(smem + DP * PA + (e >> 4) * RS + (e & 15) * 8) = h;
+                    *reinterpret_cast<u32x2 *>(smem_b + DP * PA + (e >> 4) * RS + (e & 15) * 8) = h;
                 }
             } else if (tid + i * NT < B_CH) {
                 u32x2 h, m, l;
@@ -1607,16 +1613,16 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
                 const int o = DP * PA + (e >> 4) * RS + (e & 15) * 8;
                 if constexpr (H2) {
                     split2h(rb[i], h, m);
-                    *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
+                    *reinterpret_cast<u32x2 *>(smem_b + PB + o) = m;
                 } else if constexpr (XP >= 2) {
                     split3(rb[i], h, m, l);  // x5: the l term is not needed (dead code)
-                    *reinterpret_cast<u32x2 *>(smem + PB + o) = m;
-                    if constexpr (XP == 3) *reinterpret_cast<u32x2 *>(smem + 2 * PB + o) = l;
+                    *reinterpret_cast<u32x2 *>(smem_b + PB + o) = m;
+                    if constexpr (XP == 3) *reinterpret_cast<u32x2 *>(smem_b + 2 * PB + o) = l;
                 } else {
                     h[0] = cvt_pk_bf16(rb[i][0], rb[i][1]);
                     h[1] = cvt_pk_bf16(rb[i][2], rb[i][3]);
                 }
-                *reinterpret_cast<u32x2 *>(smem + o) = h;
+                *reinterpret_cast<u32x2 *>(smem_b + o) = h;
             }
     };
 
@@ -1636,21 +1642,36 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
     const uint32_t xbase = lds_addr(smem) + DP * PA + (py * HW_ + pxq) * RS + (16 * NCB * wj + 4 * (w16 & 3)) * 2;
 
     if (pbeg < pend) {
+        // DB, RG 2: waves 4-7 stage the next patch before their MFMAs (loads two patches ahead), waves 0-3 after
+        const bool early = DB && RG == 2 && __builtin_amdgcn_readfirstlane(wid) >= 4;
         load_patch(pbeg);
-        store_patch();
+        store_patch(0);
+        if (early && pbeg + 1 < pend) load_patch(pbeg + 1);
         __syncthreads();
+        int buf = 0;
         for (int pi = pbeg; pi < pend; ++pi) {
             const bool more = pi + 1 < pend;
-            if (more) load_patch(pi + 1);
+            if (early) {
+                // the buffer of patch pi + 1 was last read in the previous patch, which the barrier closed
+                if (more) store_patch(buf ^ 1);
+                if (pi + 2 < pend) load_patch(pi + 2);
+            } else if (more) {
+                load_patch(pi + 1);
+            }
+            const uint32_t bo = uint32_t(buf * STAGE);
             bf16x8 dv[3][NRB];
-            w16_read_dy<0, PA, NRB, DP, RSD>(dv, dbase);
+            w16_read_dy<0, PA, NRB, DP, RSD>(dv, dbase + bo);
             s16x4 f0[6], f1[6];
-            w16_read_x<0 / NCB, 0 % NCB, PB, HW_, NP>(f0, xbase);
-            w16_read_x<1 / NCB, 1 % NCB, PB, HW_, NP>(f1, xbase);
-            w16_chain<0, PB, HW_, NP, LC>(acc, dv, f0, f1, xbase);
-            if (more) {
+            w16_read_x<0 / NCB, 0 % NCB, PB, HW_, NP>(f0, xbase + bo);
+            w16_read_x<1 / NCB, 1 % NCB, PB, HW_, NP>(f1, xbase + bo);
+            w16_chain<0, PB, HW_, NP, LC>(acc, dv, f0, f1, xbase + bo);
+            if constexpr (DB) {
+                if (!early && more) store_patch(buf ^ 1);
+                __syncthreads();  // patch pi + 1 is staged; every wave is done with patch pi
+                buf ^= 1;
+            } else if (more) {
                 __syncthreads();  // every wave is done with this patch
-                store_patch();
+                store_patch(0);
                 __syncthreads();
             }
         }
@@ -2010,6 +2031,15 @@ static const void *w16_kernel(int lc, int rb) {
 }
 template <int NP, bool SB = false>
 static void w16_launch(int lc, int rb, const WgradArgs &a, dim3 grid, hipStream_t s) {
+    if constexpr (NP == 4 && !SB) {
+        if ((a.tune & SCD_TUNE_WGRAD16_DB) && lc) {
+            if (rb == 128)
+                hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 2, false, true>), grid, dim3(512), 0, s, a);
+            else
+                hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 1, false, true>), grid, dim3(256), 0, s, a);
+            return;
+        }
+    }
     if (rb == 128)
         hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 2, SB>), grid, dim3(512), 0, s, a);
     else if (lc)

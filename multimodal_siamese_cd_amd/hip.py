@@ -439,6 +439,7 @@ TUNE_HALO16_LATE_LOAD = 1 << 27
 TUNE_H2_TILE64_128 = 1 << 28
 TUNE_HALO16_WS = 1 << 29
 TUNE_GATHER16_PERSIST = 1 << 30
+TUNE_WGRAD16_DB = 1 << 31
 
 
 def tune_halo16_cfg(tile_id: int) -> int:

@@ -649,3 +649,35 @@ def test_gather16_persistent_bit_identical(dev, arith, b, hc, ci, co):
     assert torch.equal(outs[0][1], outs[1][1])
     if outs[0][2] is not None:
         assert torch.equal(outs[0][2], outs[1][2])
+
+
+@pytest.mark.parametrize('n,h,w,ci,co,src_bn', [(4, 32, 32, 64, 128, False), (3, 16, 48, 128, 256, True),
+                                                 (2, 32, 32, 128, 64, False), (5, 8, 64, 64, 64, True),
+                                                 (1, 2, 16, 64, 128, False)])
+def test_wgrad_double_buffered_bit_identical(dev, h2, n, h, w, ci, co, src_bn):
+    """The double-buffered h2 halo weight grad (SCD_TUNE_WGRAD16_DB: two patch buffers, one barrier per patch, the two
+    wave groups of a 128-row block staggered) against the default: identical split plan, slabs written in full
+    (NaN-prefilled) and bit-identical, with and without the source BatchNorm transform, on 128- and 64-row blocks,
+    including a split of a single patch."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * co + ci + int(src_bn))
+    xd = torch.randn(n, h, w, ci, generator=g).to(dev)
+    dyd = (torch.randn(n, h, w, co, generator=g) * 10 ** (2 * torch.rand(n, h, w, co, generator=g) - 1)).to(dev)
+    bn = None
+    if src_bn:
+        sc = (torch.rand(ci, generator=g) + 0.5).to(dev)
+        sh = (torch.randn(ci, generator=g) * 0.1).to(dev)
+        bn = (sc, sh, 1)
+    xb = (xd * (2.0 if src_bn else 1.0)).abs().max().reshape(1)
+    db = dyd.abs().max().reshape(1)
+    res = []
+    for tune in (0, hip.TUNE_WGRAD16_DB):
+        with hip.conv_scope(tune=tune):
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(dyd), hip.nhwc(xd), 1, hip.TAPS_3X3, bn, db, xb)
+            assert hip.wgrad_arith(d) == 'h2'
+            slabs = torch.full((nbytes // 4,), float('nan'), device=dev)
+            hip.conv_wgrad(d, slabs)
+            res.append((nsplit, hip.wgrad_rows_per_block(d), slabs.cpu()))
+    assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
+    assert bool(torch.isfinite(res[1][2]).all())
+    assert torch.equal(res[0][2], res[1][2])
