@@ -907,6 +907,18 @@ void launch16_1xn(const IgemmArgs &a, int tw, hipStream_t s) {
 bool wide_1xn_ok(const IgemmArgs &a) {
     return a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune);
 }
+// The bf16 arithmetic on the 1 x N tiles (SCD_TUNE_BF16_1XN, A/B): one wave per weight fragment, no fragment loaded by
+// two waves (the 2 x 2 tiles' duplicate L2 weight loads per MFMA bound the one-product bf16 steps).
+bool bf16_1xn(const IgemmArgs &a) { return (a.tune & SCD_TUNE_BF16_1XN) && a.math == SCD_MATH_BF16; }
+
+// The 1 x N tiles in the bf16 arithmetic (fp32 or bf16 storage, double-buffered: one plane always fits).
+template <int WM, int WN, int TM, int TN, int OCC>
+void launch16_1xn_bf16(const IgemmArgs &a, int tw, hipStream_t s) {
+    if (halo16_db(a.tune, false))
+        launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
+    else
+        launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
+}
 
 // The warp-specialized form of the 1 x N tiles (igemm_halo16_ws): WN compute waves + one producer wave per block.
 template <int WN, int TM, int TN, int OCC, bool IN_BN>
@@ -946,15 +958,17 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     else if (a.n_out >= 128)
         // 128 x 128 at 2 waves/SIMD: +4..17% over the 32x32x16 halo kernel on the 128..512-channel layers; under h2
         // as 1 x 4 waves of 128 px x 32 ch (no weight fragment loaded by two waves; SCD_H2_TILE=0: 2 x 2)
-        id = (wide_1xn_ok(a) && h2_wide_tile(a.tune)) ? 3 : 0;
+        id = ((wide_1xn_ok(a) && h2_wide_tile(a.tune)) || bf16_1xn(a)) ? 3 : 0;
     else if (a.n_out >= 64)
         // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
         // h2 on 1 x 2 waves; 64-channel sources (K = 576, two 32-channel chunks) on the 256 x 64 tile of 2 x 2 such
         // waves (enc0b fwd / dgrad -4..-5%, up2b -2%; 128- and 256-channel sources measured neutral or slower)
-        id = (wide_1xn_ok(a) && h2_tile64(a.tune)) ? ((a.c == 64 && !(a.tune & SCD_TUNE_H2_TILE64_128)) ? 5 : 4) : 1;
+        id = ((wide_1xn_ok(a) && h2_tile64(a.tune)) || bf16_1xn(a))
+                 ? ((a.c == 64 && !(a.tune & SCD_TUNE_H2_TILE64_128)) ? 5 : 4)
+                 : 1;
     else
         return 0;
-    if (id < 0 || id > 5 || (id > 2 && !wide_1xn_ok(a))) return 0;
+    if (id < 0 || id > 5 || (id > 2 && !wide_1xn_ok(a) && !bf16_1xn(a))) return 0;
     if (id == 5 && halo16_ws(a)) id = 4;  // the warp-specialized blocks tile 128 pixels
     for (;;) {
         *bm = kCfg[id].bm;
@@ -970,6 +984,13 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
 }
 
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
+    if (cfg >= 4 && bf16_1xn(a)) {
+        switch (cfg - 1) {
+            case 3: launch16_1xn_bf16<1, 4, 8, 2, 3>(a, tw, s); return;
+            case 4: launch16_1xn_bf16<1, 2, 8, 2, 3>(a, tw, s); return;
+            default: launch16_1xn_bf16<2, 2, 8, 2, 3>(a, tw, s); return;
+        }
+    }
     switch (cfg - 1) {
         case 0: launch16<2, 2, 4, 4, 2>(a, tw, s); break;
         case 1: launch16<2, 2, 4, 2, 3>(a, tw, s); break;

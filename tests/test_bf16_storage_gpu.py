@@ -450,3 +450,45 @@ def test_bf16_models_store_bf16_activations(dev):
         assert seen and all(d == hip.DT_F32 for d in seen)  # deepest level 8 x 8, not tiled: fp32 storage
     finally:
         hip.conv_igemm = orig
+
+
+@pytest.mark.parametrize('st', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('ci,co,mode', [(64, 64, 'stats'), (128, 128, 'stats'), (64, 128, 'bn_bwd'), (64, 64, 'in_bn'),
+                                        (256, 64, 'plain')])
+def test_bf16_1xn_tiles_bit_identical(dev, st, ci, co, mode):
+    """The bf16 arithmetic on the 1 x N wave tiles (SCD_TUNE_BF16_1XN) against its 2 x 2 tiles, both on 128-pixel tiles
+    (SCD_TUNE_H2_TILE64_128): every output accumulates the same products in the same order and the epilogue reduces
+    in 64-pixel groups in both, so outputs and statistics / BatchNorm-backward records are bit-identical (bf16 and
+    fp32 storage)."""
+    n, h, w, nseg = 4, 32, 32, 2
+    g = torch.Generator(device=dev).manual_seed(ci + co + 3)
+    x = torch.randn(n, h, w, ci, device=dev, generator=g).to(st)
+    outs = []
+    for tune in (hip.TUNE_H2_TILE64_128, hip.TUNE_H2_TILE64_128 | hip.TUNE_BF16_1XN):
+        with hip.conv_scope('bf16', tune=tune):
+            gw = torch.Generator(device=dev).manual_seed(ci * co)
+            wpk = hip.pack_conv3x3(torch.randn(co, ci, 3, 3, device=dev, generator=gw) / (3 * ci ** 0.5), 0)
+            sc = torch.rand(nseg * ci, device=dev, generator=gw) + 0.5
+            sh = torch.randn(nseg * ci, device=dev, generator=gw) * 0.1
+            yb = torch.randn(n, h, w, co, device=dev, generator=gw).to(st)
+            mu = torch.randn(nseg * co, device=dev, generator=gw) * 0.1
+            iv = torch.rand(nseg * co, device=dev, generator=gw) + .5
+            bsc = torch.rand(nseg * co, device=dev, generator=gw) + 0.5
+            bsh = torch.randn(nseg * co, device=dev, generator=gw)
+            y = torch.full((n, h, w, co), 7.0, device=dev).to(st)
+            extra, rec = {}, None
+            if mode == 'in_bn':
+                extra['in_bn'] = (sc, sh, nseg)
+            elif mode == 'stats':
+                nt, _ = hip.igemm_stat_tiles(nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, nhwc(y))
+                rec = extra['stat_rec'] = torch.full((nt * co * 2,), 9.0, device=dev)
+            elif mode == 'bn_bwd':
+                nt, _ = hip.igemm_bn_bwd_tiles(nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, nhwc(y))
+                rec = torch.full((co * nt * 2,), 9.0, device=dev)
+                extra['bn_bwd'] = (yb, nseg, mu, iv, bsc, bsh, rec)
+            assert hip.igemm_arith(nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, nhwc(y)) == 'bf16'
+            hip.conv_igemm(nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, None, nhwc(y), **extra)
+            outs.append((y.cpu(), None if rec is None else rec.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[1][1])
