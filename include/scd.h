@@ -159,6 +159,7 @@ int scd_abi_version(void);
 #define SCD_TUNE_HALO16_CFG(id)   ((uint32_t)((id) + 1))  /* force 16x16x32 halo tile id 0..5 (3-5: h2 only) */
 #define SCD_TUNE_HALO16_OFF       0xFu                    /* the 32x32x16 halo kernel instead                     */
 #define SCD_TUNE_HALO16_MASK      0xFu
+#define SCD_TUNE_HALO16_WRING     0x8u                    /* automatic tiles; h2 1xN tiles' weights via an LDS ring */
 #define SCD_TUNE_H2_TILE_2X2      (1u << 4)   /* h2, >= 128 outputs: 2x2 waves instead of 1x4                     */
 #define SCD_TUNE_H2_TILE64_2X2    (1u << 5)   /* h2, 64..127 outputs: 2x2 waves instead of 1x2                    */
 #define SCD_TUNE_H2_NO_PRESCALE   (1u << 6)   /* h2 without the 2^11 pre-scaled low term (narrower range)         */

@@ -50,9 +50,31 @@ __device__ __forceinline__ void gstore4(float *p, f32x4 v) { *(__attribute__((ad
 // scaled by the power of two of *src_bound while staged, the weights come pre-scaled per output channel, and the
 // epilogue multiplies both inverse scales back out -- exact, powers of two).
 // SB: bf16 storage of src / dst / the BatchNorm-backward y (bf16 arithmetic only, StageT in x3_common.h).
-template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP, bool SB = false>
+// WL (SCD_TUNE_HALO16_WRING, h2 single-buffered 3x3 only): the weight fragments go through a 3-slot LDS ring instead of
+// straight into registers.  Each k-step's BN x 32 x 2-plane weights (8 or 16 KB) are copied global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, 1 KB per wave-instruction, split over the block's waves) two steps ahead; a step starts with
+// a counted vmcnt wait for this wave's pieces of the step plus one barrier, then reads its fragments with ds_read_b128.
+// What it changes: (1) a weight fragment shared by two waves (the 2 x 2 tile) is fetched once; (2) the next chunk's
+// halo loads, issued after the DMA of step T+2, are waited for only at step T+3 (vmcnt counts them as younger than the
+// DMA pieces of steps T+1 and T+2), two k-steps later than when every wave waited for its own next-step weight loads
+// behind them.  Same products in the same order: bit-identical to WL = false.
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void lds_barrier() {  // a barrier that leaves LDS-DMA pieces in flight (no vmcnt(0))
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP, bool SB = false,
+          bool WL = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
     static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
+    static_assert(!WL || (NP == 4 && !DB && !SB), "the weight ring: single-buffered h2 only");
     constexpr uint32_t EB = SB ? 2u : 4u;  // bytes per element
     constexpr int NT = 64 * WAVES_M * WAVES_N;
     constexpr int WPX = TM * 16, WCH = TN * 16;
@@ -74,7 +96,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     constexpr bool H2 = NP == 2 || NP == 4;  // 4: h2 with the activations' low term pre-scaled (x3_common.h)
     constexpr int XP = NP == 1 ? 1 : H2 ? 2 : 3;               // activation planes (LDS)
     constexpr int WP = NP == 1 ? 1 : (NP == 5 || H2) ? 2 : 3;  // weight planes (registers)
-    __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * XP * PA > RED ? NBUF * XP * PA : RED];
+    constexpr int NBB = BN / 32;                               // 32-channel weight blocks of the tile
+    constexpr int WSLOT = WL ? WP * NBB * 2048 : 0;            // WL: bytes of one k-step's weights (one ring slot)
+    constexpr int WG = WSLOT / (1024 * WAVES_M * WAVES_N);     // WL: 1 KB DMA pieces per wave per step
+    static_assert(!WL || WG * 1024 * WAVES_M * WAVES_N == WSLOT, "ring slot splits evenly over the waves");
+    constexpr int HALO_B = NBUF * XP * PA;
+    constexpr int SMEM = HALO_B + 3 * WSLOT > RED ? HALO_B + 3 * WSLOT : RED;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
     float xs = 1.f, xs_inv = 1.f;  // h2: power-of-two scale of the staged activations and its inverse
     if constexpr (H2) h2_scale(*a.src_bound, xs, xs_inv);
 
@@ -143,14 +171,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             const int ch = (img / a.in_seg_imgs) * a.c + cc * 32 + (tid & 7) * 4;
             in_sc = gload4(a.in_scale + ch);
             in_sh = gload4(a.in_shift + ch);
-            if constexpr (H2) {  // fma(y, sc * s, sh * s) == s * fma(y, sc, sh) exactly (s a power of two)
-                in_sc *= xs;
-                in_sh *= xs;
-            }
         }
     };
     auto store_A = [&](int buf) {
         unsigned char *const sb = smem + buf * (XP * PA);
+        // h2: fma(y, sc * s, sh * s) == s * fma(y, sc, sh) exactly (s a power of two).  Scaled here, where the halo
+        // is consumed, not where its coefficients are loaded: a use right behind the loads made the compiler wait for
+        // them there, and vmcnt retires in order, so that wait drained the whole halo prefetch at issue.
+        const f32x4 sc = H2 ? in_sc * xs : in_sc, sh = H2 ? in_sh * xs : in_sh;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i)
             if ((A_CH % NT == 0) || a_off[i] >= 0) {
@@ -159,7 +187,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                 if constexpr (IN_BN) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        x[q] = a_boff[i] == kOOB ? 0.f : fmaxf(fmaf(x[q], in_sc[q], in_sh[q]), 0.f);
+                        x[q] = a_boff[i] == kOOB ? 0.f : fmaxf(fmaf(x[q], sc[q], sh[q]), 0.f);
                 }
                 if constexpr (H2) {
                     if constexpr (!IN_BN) x *= xs;
@@ -192,6 +220,32 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             for (int j = 0; j < TN; ++j)
                 wq[p][j] = bload4u(rs_w, w_base[j] == kOOB ? kOOB : w_base[j] + ko + uint32_t(p) * wplane_b);
     };
+    // WL: step s2's weights -> ring slot s2 % 3.  Piece q (1 KB) = plane q / (2 NBB), 32-channel block (q / 2) % NBB,
+    // 16-deep half q % 2: the slot holds [plane][block][2 KB] in the global fragment order, so a lane reads its fragment
+    // at the same offset within the block's 2 KB as the register path's w_base.
+    const int wave_u = __builtin_amdgcn_readfirstlane(wid);
+    auto issue_W = [&](int s2) {
+        const int c2 = s2 / a.ntaps, t2 = s2 - c2 * a.ntaps;
+        const uint32_t ko = uint32_t(t2 * cpk + c2) * 2048u;
+        unsigned char *const slot = smem + HALO_B + (s2 % 3) * WSLOT;
+#pragma unroll
+        for (int u = 0; u < WG; ++u) {
+            const int q = wave_u * WG + u;
+            const int p = q / (2 * NBB), r = q - p * (2 * NBB);
+            const uint32_t goff = uint32_t(p) * wplane_b + uint32_t(((n0 >> 5) + (r >> 1)) * KS16) * 1024u + ko +
+                                  uint32_t(r & 1) * 1024u + uint32_t(lane) * 16u;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(reinterpret_cast<const unsigned char *>(a.wsplit) + goff),
+                (__attribute__((address_space(3))) void *)(slot + q * 1024), 16, 0, 0);
+        }
+        asm volatile("" ::: "memory");  // the DMA pieces stay older than the halo loads issued after them
+    };
+    int w_lds[TN];  // WL: this lane's fragment offset within a ring slot (plane 0)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int cb = (n0 >> 4) + wn * TN + j;
+        w_lds[j] = ((cb >> 1) - (n0 >> 5)) * 2048 + (g >> 1) * 1024 + (16 * (cb & 1) + l16 + 32 * (g & 1)) * 16;
+    }
 
     f32x4 acc[TN][TM];
 #pragma unroll
@@ -210,10 +264,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     constexpr int T_STORE = 4;  // DB: tap at which the prefetched halo is written to the other buffer
     // single buffer: the tap at which the next chunk's halo loads are issued into registers (stored at the chunk end),
     // 4 taps ahead so HBM latency hides behind 4 taps of MFMAs; SCD_TUNE_HALO16_LATE_LOAD: the last tap (A/B)
-    const int t_load = (a.tune & SCD_TUNE_HALO16_LATE_LOAD) || a.ntaps < 5 ? a.ntaps - 1 : a.ntaps - 5;
+    // (WL: always 4 taps ahead; the launcher takes WL for 9-tap convs only)
+    const int t_load = !WL && ((a.tune & SCD_TUNE_HALO16_LATE_LOAD) || a.ntaps < 5) ? a.ntaps - 1 : a.ntaps - 5;
     u32x4 wq[WP][TN];
+    if constexpr (WL) {
+        issue_W(0);
+        if (nsteps > 1) issue_W(1);
+    }
     load_A(0);
-    load_W(0, 0, wq);
+    if constexpr (!WL) load_W(0, 0, wq);
     store_A(0);
     __syncthreads();
     int cc = 0, t = 0;
@@ -224,10 +283,23 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             cc1 = cc + 1;
         }
         const bool more = s + 1 < nsteps;
-        if constexpr (DB) {
-            if (t == 0 && cc + 1 < cpk) load_A(cc + 1);
-        } else {
+        if constexpr (WL) {
+            // Retire this wave's DMA pieces of step s: younger than them are step s+1's pieces (WG) and, at the step after
+            // the next chunk's halo loads were issued (ahead of step t_load+2's pieces), those loads (HL); then every
+            // wave's pieces.  The halo loads go first at step t_load: the compiler drains vmcnt before reissuing into
+            // their registers, and what is in flight then is only step t_load+1's pieces, issued a step earlier.
+            constexpr int HL = A_PER + (IN_BN ? 2 : 0);
+            if (!more)
+                wait_vm_barrier<0>();
+            else if (cc + 1 < cpk && t == t_load + 1)
+                wait_vm_barrier<WG + HL>();
+            else
+                wait_vm_barrier<WG>();
             if (t == t_load && cc + 1 < cpk) load_A(cc + 1);
+            asm volatile("" ::: "memory");
+            if (s + 2 < nsteps) issue_W(s + 2);  // into the slot of step s-1, which every wave has left
+        } else if constexpr (DB) {
+            if (t == 0 && cc + 1 < cpk) load_A(cc + 1);
         }
         const unsigned char *const sbuf = smem + (DB ? (cc & 1) * (XP * PA) : 0);
         const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
@@ -240,10 +312,20 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             for (int p = 0; p < XP; ++p)
                 xv[p][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(sbuf + p * PA + ad));
         }
+        if constexpr (WL) {
+            const unsigned char *const wslot = smem + HALO_B + (s % 3) * WSLOT;
 #pragma unroll
-        for (int p = 0; p < WP; ++p)
+            for (int p = 0; p < WP; ++p)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) wv[p][j] = __builtin_bit_cast(bf16x8, wq[p][j]);
+                for (int j = 0; j < TN; ++j)
+                    wv[p][j] = __builtin_bit_cast(
+                        bf16x8, *reinterpret_cast<const u32x4 *>(wslot + p * (NBB * 2048) + w_lds[j]));
+        } else {
+#pragma unroll
+            for (int p = 0; p < WP; ++p)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) wv[p][j] = __builtin_bit_cast(bf16x8, wq[p][j]);
+        }
         if constexpr (H2) {
             // h2: w_h x_m (NP 4: (w_h 2^-11) x_m', x_m' pre-scaled by 2^11), w_m x_h, w_h x_h on the fp16 planes
 #pragma unroll
@@ -272,11 +354,27 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv[QW[q]][j], xv[QX[q]][i], acc[j][i],
                                                                                 0, 0, 0);
         }
-        if (more) load_W(cc1, t1, wq);
+        if constexpr (!WL) {
+            if (more) load_W(cc1, t1, wq);
+            // single buffer: the next chunk's halo loads go out BEHIND the next step's weight loads.  vmcnt retires in
+            // order, so halo loads issued ahead of them (at the top of the step, as before round 4) were drained by the
+            // very next weight wait: the prefetch ran synchronously.  Behind them, the first wait that drains the halo
+            // is the weight wait one step later.
+            if constexpr (!DB) {
+                asm volatile("" ::: "memory");
+                if (t == t_load && cc + 1 < cpk) load_A(cc + 1);
+            }
+        }
         if constexpr (DB) {
             // the other buffer was last read in the previous chunk, which every wave has left (barrier below)
             if (t == T_STORE && cc + 1 < cpk) store_A((cc + 1) & 1);
             if (more && t1 == 0) __syncthreads();  // chunk end: the next halo is complete
+        } else if constexpr (WL) {
+            if (more && t1 == 0) {  // as below, with barriers that leave the next two steps' DMA pieces in flight
+                lds_barrier();
+                store_A(0);
+                lds_barrier();
+            }
         } else {
             if (more && t1 == 0) {  // chunk end: every wave is done with this halo; overwrite it with the next one
                 __syncthreads();
@@ -783,10 +881,12 @@ struct H16Cfg {
 // (SCD_TUNE_HALO16_* bits of the launch).
 int halo16_mode(uint32_t tune) {
     const uint32_t v = tune & SCD_TUNE_HALO16_MASK;
-    return v == SCD_TUNE_HALO16_OFF ? 0 : v == 0 ? 1 : int(v) + 1;
+    return v == SCD_TUNE_HALO16_OFF ? 0 : (v == 0 || v == SCD_TUNE_HALO16_WRING) ? 1 : int(v) + 1;
 }
+// SCD_TUNE_HALO16_WRING: automatic tiles, h2 weights through the LDS ring (igemm_halo16_x3's WL).
+bool halo16_wring(uint32_t tune) { return (tune & SCD_TUNE_HALO16_MASK) == SCD_TUNE_HALO16_WRING; }
 
-template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN, bool DB, int NP, bool SB = false>
+template <int WM, int WN, int TM, int TN, int OCC, bool IN_BN, bool DB, int NP, bool SB = false, bool WL = false>
 void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     IgemmArgs b = a;
@@ -794,12 +894,13 @@ void launch16b(const IgemmArgs &a, int tw, hipStream_t s) {
     b.grid_n = (a.n_out + BN - 1) / BN;
     b.remap = halo_remap(a.tune);
     const dim3 grid(b.grid_m * b.grid_n), block(64 * WM * WN);
-    if (tw == 64)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN, DB, NP, SB>), grid, block, 0, s, b);
-    else if (tw == 32)
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN, DB, NP, SB>), grid, block, 0, s, b);
+    if (tw == 64) {
+        if constexpr (!WL)  // (the launcher keeps the weight ring off 64-wide tiles)
+            hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 64, OCC, IN_BN, DB, NP, SB>), grid, block, 0, s, b);
+    } else if (tw == 32)
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 32, OCC, IN_BN, DB, NP, SB, WL>), grid, block, 0, s, b);
     else
-        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN, DB, NP, SB>), grid, block, 0, s, b);
+        hipLaunchKernelGGL((igemm_halo16_x3<WM, WN, TM, TN, 16, OCC, IN_BN, DB, NP, SB, WL>), grid, block, 0, s, b);
 }
 
 // h2: the activation / gradient operand's low term pre-scaled by 2^11 (x3_common.h; floor 2^-36 instead of 2^-25
@@ -820,7 +921,7 @@ int halo16_db(uint32_t tune, bool h2) {
     return h2 ? 0 : 1;
 }
 
-template <int WM, int WN, int TM, int TN, int OCC, bool DB, int NP>
+template <int WM, int WN, int TM, int TN, int OCC, bool DB, int NP, bool WL = false>
 void launch16c(const IgemmArgs &a, int tw, hipStream_t s) {
     if constexpr (NP == 1) {  // the bf16 arithmetic: fp32 or bf16 storage
         if (a.sb) {
@@ -832,9 +933,9 @@ void launch16c(const IgemmArgs &a, int tw, hipStream_t s) {
         }
     }
     if (a.in_scale)
-        launch16b<WM, WN, TM, TN, OCC, true, DB, NP>(a, tw, s);
+        launch16b<WM, WN, TM, TN, OCC, true, DB, NP, false, WL>(a, tw, s);
     else
-        launch16b<WM, WN, TM, TN, OCC, false, DB, NP>(a, tw, s);
+        launch16b<WM, WN, TM, TN, OCC, false, DB, NP, false, WL>(a, tw, s);
 }
 
 template <int WM, int WN, int TM, int TN, int OCC>
@@ -899,6 +1000,9 @@ void launch16_1xn(const IgemmArgs &a, int tw, hipStream_t s) {
     const bool db2 = tw != 64 && halo16_db(a.tune, true) && OCC * 2 * 2 * hr * 64 <= 160 * 1024;
     if (db2)
         launch16c<WM, WN, TM, TN, OCC, true, 4>(a, tw, s);
+    else if (halo16_wring(a.tune) && a.ntaps == 9 && tw != 64 && a.n_out % (WN * TN * 16) == 0)  // pieces in the split;
+        // 64-wide tiles: halo + ring would leave one block per CU
+        launch16c<WM, WN, TM, TN, OCC, false, 4, true>(a, tw, s);
     else
         launch16c<WM, WN, TM, TN, OCC, false, 4>(a, tw, s);
 }
@@ -1562,8 +1666,8 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
         const int img = pi / pimg, pr = pi - img * pimg;
         if (a.src_scale) {
             const int ch = (img / a.src_seg_imgs) * a.C + c0 + (tid & 15) * 4;
-            x_sc = gload4(a.src_scale + ch) * xs;  // h2: the scale folds into the transform exactly
-            x_sh = gload4(a.src_shift + ch) * xs;
+            x_sc = gload4(a.src_scale + ch);  // h2: times xs where consumed (store_patch)
+            x_sh = gload4(a.src_shift + ch);
         }
         x_valid = 0;
         const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
@@ -1586,6 +1690,9 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
     };
     auto store_patch = [&](int buf) {
         unsigned char *const smem_b = smem + buf * STAGE;
+        // h2: the scale folds into the transform exactly; applied here, not behind the coefficient loads, where the
+        // compiler waited for them (vmcnt in order: the wave stalled at issue)
+        const f32x4 sc = H2 ? x_sc * xs : x_sc, sh = H2 ? x_sh * xs : x_sh;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * NT;
@@ -1615,7 +1722,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
                         const bool v = (x_valid >> i) & 1u;
                         f32x4 x = unpk_bf16x4(rb[i]);
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) x[q] = v ? fmaxf(fmaf(x[q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                        for (int q = 0; q < 4; ++q) x[q] = v ? fmaxf(fmaf(x[q], sc[q], sh[q]), 0.f) : 0.f;
                         h = pk_bf16x4(x);
                     }
                     const int e = tid + i * NT;
@@ -1626,7 +1733,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
                 if (a.src_scale) {
                     const bool v = (x_valid >> i) & 1u;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                    for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], sc[q], sh[q]), 0.f) : 0.f;
                 } else if constexpr (H2) {
                     rb[i] *= xs;
                 }
@@ -1837,8 +1944,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
         const int img = pi / pimg, pr = pi - img * pimg;
         if (a.src_scale) {
             const int ch = (img / a.src_seg_imgs) * a.C + (tid & 3) * 4;
-            x_sc = gload4(a.src_scale + ch) * xs;  // h2: the scale folds into the transform exactly
-            x_sh = gload4(a.src_shift + ch) * xs;
+            x_sc = gload4(a.src_scale + ch);  // h2: times xs where consumed (store_patch)
+            x_sh = gload4(a.src_shift + ch);
         }
         if constexpr (RBN) {
             const int c = r0 + (tid & 15) * 4, o = (img / a.rows_seg_imgs) * a.R + c;
@@ -1872,6 +1979,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
         }
     };
     auto store_patch = [&]() {
+        const f32x4 sc = H2 ? x_sc * xs : x_sc, sh = H2 ? x_sh * xs : x_sh;  // as in wgrad_halo16_x3
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * 256;
@@ -1909,7 +2017,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
                         const bool v = (x_valid >> i) & 1u;
                         f32x4 x = unpk_bf16x4(rb[i]);
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) x[q] = v ? fmaxf(fmaf(x[q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                        for (int q = 0; q < 4; ++q) x[q] = v ? fmaxf(fmaf(x[q], sc[q], sh[q]), 0.f) : 0.f;
                         h = pk_bf16x4(x);
                     }
                     const int e = tid + i * 256;
@@ -1920,7 +2028,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
                 if (a.src_scale) {
                     const bool v = (x_valid >> i) & 1u;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], x_sc[q], x_sh[q]), 0.f) : 0.f;
+                    for (int q = 0; q < 4; ++q) rb[i][q] = v ? fmaxf(fmaf(rb[i][q], sc[q], sh[q]), 0.f) : 0.f;
                 } else if constexpr (H2) {
                     rb[i] *= xs;
                 }

@@ -421,6 +421,7 @@ _MATH_BY_ID = {v: k for k, v in _MATH_NAMES.items()}
 
 # SCD_TUNE_* kernel-variant bits (include/scd.h): 0 = the library's measured defaults.
 TUNE_HALO16_OFF = 0xF
+TUNE_HALO16_WRING = 0x8  # automatic tiles, the h2 1 x N tiles' weight fragments through an LDS ring (A/B)
 TUNE_H2_TILE_2X2 = 1 << 4
 TUNE_H2_TILE64_2X2 = 1 << 5
 TUNE_H2_NO_PRESCALE = 1 << 6
@@ -524,7 +525,7 @@ def set_halo16(mode: int) -> int:
     kernel), 1 = automatic, 2 + id = force tile id.  Returns the previous mode."""
     t = _DEFAULT['tune']
     v = t & 0xF
-    prev = 0 if v == TUNE_HALO16_OFF else 1 if v == 0 else v + 1
+    prev = 0 if v == TUNE_HALO16_OFF else 1 if v in (0, TUNE_HALO16_WRING) else v + 1
     new = TUNE_HALO16_OFF if mode == 0 else 0 if mode == 1 else tune_halo16_cfg(int(mode) - 2)
     _DEFAULT['tune'] = (t & ~0xF) | new
     return prev

@@ -589,10 +589,51 @@ def test_h2_tile64_256_matches_128(dev, h2, ci, mode):
         assert ((a - b).abs().max() / b.abs().max()).item() < 1e-5
 
 
-@pytest.mark.parametrize('variant,base', [('TUNE_HALO16_WS', 'TUNE_H2_TILE64_128')])
+@pytest.mark.parametrize('ci,co,mode', [(64, 64, 'stats'), (64, 64, 'in_bn'), (128, 64, 'bn_bwd'), (256, 64, 'in_bn'),
+                                        (128, 128, 'stats'), (64, 256, 'in_bn'), (256, 128, 'bn_bwd'), (64, 96, 'plain')])
+def test_halo16_weight_ring_bit_identical(dev, h2, ci, co, mode):
+    """SCD_TUNE_HALO16_WRING: the h2 1 x N tiles with their weight fragments copied through a 3-slot LDS ring by LDS-DMA
+    (igemm_halo16_x3's WL; counted vmcnt waits, one barrier per k-step) run the same products in the same order as the
+    register path: outputs and epilogue records bit-identical, on the 256 x 64, 128 x 64 and 128 x 128 tiles, one to eight
+    32-channel chunks (96 outputs: not a multiple of the tile, the register path runs)."""
+    from multimodal_siamese_cd_amd import hip
+    from multimodal_siamese_cd_amd.hip import TAPS_3X3, nhwc
+    n, h, w, nseg = 4, 32, 48, 2
+    g = torch.Generator(device=dev).manual_seed(ci * 3 + co)
+    x = torch.randn(n, h, w, ci, device=dev, generator=g)
+    wpk = hip.pack_conv3x3(torch.randn(co, ci, 3, 3, device=dev, generator=g) / (3 * ci ** 0.5), 0)
+    sc = torch.rand(nseg * ci, device=dev, generator=g) + 0.5
+    sh = torch.randn(nseg * ci, device=dev, generator=g) * 0.1
+    bound = x.abs().max().reshape(1) * (2.0 if mode == 'in_bn' else 1.0)
+    yb = torch.randn(n, h, w, co, device=dev, generator=g)
+    mu, iv = torch.randn(nseg * co, device=dev, generator=g) * 0.1, torch.rand(nseg * co, device=dev, generator=g) + .5
+    bsc, bsh = torch.rand(nseg * co, device=dev, generator=g) + 0.5, torch.randn(nseg * co, device=dev, generator=g)
+    outs = []
+    for tune in (0, hip.TUNE_HALO16_WRING):
+        with hip.conv_scope(tune=tune):
+            y = torch.full((n, h, w, co), 7.0, device=dev)
+            extra, rec = {}, None
+            if mode == 'in_bn':
+                extra['in_bn'] = (sc, sh, nseg)
+            elif mode == 'stats':
+                nt, _ = hip.igemm_stat_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), src_bound=bound)
+                rec = extra['stat_rec'] = torch.full((nt * co * 2,), 9.0, device=dev)
+            elif mode == 'bn_bwd':
+                nt, _ = hip.igemm_bn_bwd_tiles(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), bound)
+                rec = torch.full((co * nt * 2,), 9.0, device=dev)
+                extra['bn_bwd'] = (yb, nseg, mu, iv, bsc, bsh, rec)
+            assert hip.igemm_arith(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, nhwc(y), src_bound=bound) == 'h2'
+            hip.conv_igemm(nhwc(x), h, w, 1, TAPS_3X3, wpk, co, None, nhwc(y), src_bound=bound, **extra)
+            outs.append((y.cpu(), None if rec is None else rec.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize('variant,base', [('TUNE_HALO16_WS', 'TUNE_H2_TILE64_128'), ('TUNE_HALO16_WRING', None)])
 def test_halo16_variant_training_step_bit_identical(dev, h2, variant, base):
     """The warp-specialized h2 halo kernel (SCD_TUNE_HALO16_WS: a producer wave stages the halo; both runs on
-    128-pixel tiles, the only ones it has) inside a whole training step of SiameseUNet [64, 128, 256] at 64x64: logits, loss and every gradient bit-identical to the
+    128-pixel tiles, the only ones it has) and the weight ring (SCD_TUNE_HALO16_WRING) inside a whole training step of SiameseUNet [64, 128, 256] at 64x64: logits, loss and every gradient bit-identical to the
     default kernels."""
     from multimodal_siamese_cd_amd import hip, trainers
     from multimodal_siamese_cd_amd.utils import datasets, experiment_manager as em, networks
