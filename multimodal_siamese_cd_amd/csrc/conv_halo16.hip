@@ -81,8 +81,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     constexpr int BM = WAVES_M * WPX, BN = WAVES_N * WCH;
     constexpr int TR = BM / TW;
     constexpr int HWD = TW + 2;
-    constexpr int HR = (TR + 2) * HWD;
-    constexpr int A_CH = HR * 8;  // 16-byte (4-channel) pieces of one 32-channel chunk
+    // LDS row pitch of the halo.  16-wide tiles on one buffer: 24 rows per halo row instead of 18, so the 16-pixel
+    // groups of a wave (one halo row apart) sit 24 rows apart, and 24 / 2 = 12 = 0 mod 4 leaves the row swizzle
+    // unchanged between them: one swizzled address per k-step, the groups at immediate offsets (8 VALU per step
+    // instead of ~50).  The 6 pad rows per halo row are never staged or read.
+    constexpr bool PADP = TW == 16 && !DB && !WL;
+    constexpr int HWP = PADP ? 24 : HWD;
+    constexpr int HR = (TR + 2) * HWP;           // LDS rows of one plane
+    constexpr int A_CH = (TR + 2) * HWD * 8;     // 16-byte (4-channel) pieces of one 32-channel chunk
     constexpr int A_PER = (A_CH + NT - 1) / NT;
     constexpr int PA = HR * 64;
     // Epilogue reductions run over groups of 4 pixel tiles (64 pixels) per wave, so a 1 x N wave layout (TM = 8) sums
@@ -145,7 +151,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
         const bool ok = in && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
         a_boff[i] = ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * EB : kOOB;
-        a_off[i] = in ? soff(hp, col) : -1;
+        a_off[i] = in ? soff(hy * HWP + hx, col) : -1;
     }
     // Weight fragments from the 32-row fragment-major split (scd_split_bf16x3_frag): the 16 rows x 8 k of
     // one 16-lane group are 256 contiguous bytes of a 1 KB 32x16 fragment.
@@ -257,7 +263,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int p = wm * WPX + i * 16 + l16;
-        a_hr[i] = (p / TW + 1) * HWD + (p % TW) + 1;
+        a_hr[i] = (p / TW + 1) * HWP + (p % TW) + 1;
     }
 
     const int nsteps = cpk * a.ntaps;
@@ -302,15 +308,26 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             if (t == 0 && cc + 1 < cpk) load_A(cc + 1);
         }
         const unsigned char *const sbuf = smem + (DB ? (cc & 1) * (XP * PA) : 0);
-        const int toff = tap_at(a.tdy, t) * HWD + tap_at(a.tdx, t);
+        const int toff = tap_at(a.tdy, t) * HWP + tap_at(a.tdx, t);
         bf16x8 xv[XP][TM], wv[WP][TN];
+        if constexpr (PADP) {  // a_hr[i] = a_hr[0] + 24 i: same swizzle, rows 24 i further
+            const int hr = a_hr[0] + toff;
+            const unsigned char *const sb0 = sbuf + hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int hr = a_hr[i] + toff;
-            const int ad = hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int p = 0; p < XP; ++p)
-                xv[p][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(sbuf + p * PA + ad));
+                for (int p = 0; p < XP; ++p)
+                    xv[p][i] = __builtin_bit_cast(bf16x8,
+                                                  *reinterpret_cast<const u32x4 *>(sb0 + p * PA + i * (HWP * 64)));
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int hr = a_hr[i] + toff;
+                const int ad = hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
+#pragma unroll
+                for (int p = 0; p < XP; ++p)
+                    xv[p][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(sbuf + p * PA + ad));
+            }
         }
         if constexpr (WL) {
             const unsigned char *const wslot = smem + HALO_B + (s % 3) * WSLOT;
