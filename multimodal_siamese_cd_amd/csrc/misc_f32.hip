@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const T *__restrict__ 
                                                           const float *__restrict__ b, int n_out, int G,
                                                           const float *__restrict__ scale,
                                                           const float *__restrict__ shift, int64_t pseg,
-                                                          float *__restrict__ out) {
+                                                          FastDiv fseg, FastDiv fhw, float *__restrict__ out) {
     const int lane = threadIdx.x & 63;
     const int q = lane % G, pp = lane / G, ppw = 64 / G;
     const int cq = C / 4;
@@ -341,12 +341,21 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const T *__restrict__ 
                 v[u] = p < npix ? ld4(x + p * ldx + 4 * qq) : bnf4{0.f, 0.f, 0.f, 0.f};
             }
             if (scale) {
+                // segment of a pixel: a multiply-shift below 2^31 pixels.  The U pixels of a lane nearly always share
+                // one segment: then one coefficient load serves them (per-pixel coefficient loads were 4x the bytes
+                // of the activations they transform)
+                auto seg_of = [&](int64_t p) -> int64_t {
+                    return p < npix ? (npix < (int64_t(1) << 31) ? int64_t(fdiv(uint32_t(p), fseg)) : p / pseg) : 0;
+                };
+                const int64_t s0 = seg_of(p0 + pp), s1 = seg_of(p0 + (U - 1) * ppw + pp);
+                bnf4 sc = ld4(scale + s0 * C + 4 * qq), sf = ld4(shift + s0 * C + 4 * qq);
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const int64_t p = p0 + u * ppw + pp;
-                    const int64_t so = (p < npix ? p / pseg : 0) * C + 4 * qq;
-                    const bnf4 sc = ld4(scale + so);
-                    const bnf4 sf = ld4(shift + so);
+                    if (s1 != s0) {
+                        const int64_t so = seg_of(p0 + u * ppw + pp) * C + 4 * qq;
+                        sc = ld4(scale + so);
+                        sf = ld4(shift + so);
+                    }
                     v[u] = bnf4{fmaxf(fmaf(v[u].x, sc.x, sf.x), 0.f), fmaxf(fmaf(v[u].y, sc.y, sf.y), 0.f),
                                 fmaxf(fmaf(v[u].z, sc.z, sf.z), 0.f), fmaxf(fmaf(v[u].w, sc.w, sf.w), 0.f)};
                 }
@@ -372,7 +381,8 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const T *__restrict__ 
             for (int u = 0; u < U; ++u) {
                 const int64_t p = p0 + u * ppw + pp;
                 if (p < npix) {
-                    const int64_t img = p / hw, pix = p - img * hw;
+                    const int64_t img = npix < (int64_t(1) << 31) ? int64_t(fdiv(uint32_t(p), fhw)) : p / hw;
+                    const int64_t pix = p - img * hw;
 #pragma unroll
                     for (int o = 0; o < 4; ++o)
                         if (o < n_out) out[(img * n_out + o) * hw + pix] = s[u][o] + (b ? b[o] : 0.f);
@@ -384,12 +394,27 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const T *__restrict__ 
 
 template <class T>
 __global__ void conv1x1_bwd_dx_kernel(const float *__restrict__ gout, int n_out, int hw, const float *__restrict__ w,
-                                      T *__restrict__ gx, int ldgx, int C, int accumulate, int64_t total) {
+                                      T *__restrict__ gx, int ldgx, int C, int accumulate, int64_t total, FastDiv fcq,
+                                      FastDiv fhw) {
     const int cq = C / 4;
+    // below 2^31 elements the (pixel, quad) and (image, pixel) splits are multiply-shifts: four int64 divisions per
+    // element made this pass VALU-bound (~1.5 TB/s)
+    const bool small = total < (int64_t(1) << 31);
     for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < total; e += int64_t(gridDim.x) * blockDim.x) {
-        const int c = int(e % cq) * 4;
-        const int64_t p = e / cq;
-        const int64_t img = p / hw, pix = p % hw;
+        int c;
+        int64_t p, img, pix;
+        if (small) {
+            const uint32_t pe = fdiv(uint32_t(e), fcq), ie = fdiv(pe, fhw);
+            c = int(uint32_t(e) - pe * uint32_t(cq)) * 4;
+            p = pe;
+            img = ie;
+            pix = int64_t(pe - ie * uint32_t(hw));
+        } else {
+            c = int(e % cq) * 4;
+            p = e / cq;
+            img = p / hw;
+            pix = p % hw;
+        }
         bnf4 r = {0.f, 0.f, 0.f, 0.f};
         for (int o = 0; o < n_out; ++o) {
             const float g = gout[(img * n_out + o) * hw + pix];
@@ -717,7 +742,9 @@ static int conv1x1_fwd_run(const scd_nhwc_t &x, const float *scale, const float 
     if (blocks > 4096) blocks = 4096;
     SCD_WITH_T(x.dtype, T,
                hipLaunchKernelGGL((conv1x1_fwd_kernel<U, T>), dim3(blocks), dim3(256), 0, s, view_ptr<const T>(x),
-                                  x.ldc, x.c, x.h * x.w, npix, w, b, n_out, G, scale, shift, npix / nseg, out));
+                                  x.ldc, x.c, x.h * x.w, npix, w, b, n_out, G, scale, shift, npix / nseg,
+                                  make_fastdiv(uint32_t(npix / nseg > 0 ? npix / nseg : 1)),
+                                  make_fastdiv(uint32_t(x.h * x.w > 0 ? x.h * x.w : 1)), out));
     return launch_status("scd_conv1x1_fwd");
 }
 }  // namespace scd
@@ -775,7 +802,8 @@ extern "C" int scd_conv1x1_bwd(scd_nhwc_t x, const float *w, const float *gout, 
         const int64_t total = npix * (x.c / 4);
         SCD_WITH_T(gx.dtype, T,
                    hipLaunchKernelGGL(conv1x1_bwd_dx_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, gout, n_out,
-                                      hw, w, view_ptr<T>(gx), gx.ldc, x.c, accumulate, total));
+                                      hw, w, view_ptr<T>(gx), gx.ldc, x.c, accumulate, total,
+                                      make_fastdiv(uint32_t(x.c / 4 > 0 ? x.c / 4 : 1)), make_fastdiv(uint32_t(hw > 0 ? hw : 1))));
     }
     float *rec = static_cast<float *>(ws);
     const size_t wbytes = weighted_channel_sum_bytes(x);

@@ -830,6 +830,27 @@ def test_siamese_diff(dev):
     assert torch.equal(d.cpu(), a[3:] - a[:3])
 
 
+@pytest.mark.parametrize('n,nseg,c,n_out,h,w', [(4, 2, 64, 1, 16, 24), (6, 3, 32, 2, 7, 9), (2, 1, 128, 1, 5, 13),
+                                                 (6, 2, 16, 4, 11, 3)])
+def test_head_conv1x1_fused_bn_segments(dev, n, nseg, c, n_out, h, w):
+    """The head read through its BatchNorm + ReLU (scd_conv1x1_fwd_bn): each of the nseg image segments takes its own
+    coefficients (the segment of a pixel is found with a multiply-shift, not an int64 division)."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(n * c + nseg)
+    y = torch.randn(n, h, w, c, generator=g)
+    sc = torch.rand(nseg, c, generator=g) + 0.5
+    sh = torch.randn(nseg, c, generator=g) * 0.2
+    wt = torch.randn(n_out, c, generator=g)
+    b = torch.randn(n_out, generator=g)
+    seg = torch.arange(n) // (n // nseg)
+    a = torch.relu(y.double() * sc.double()[seg][:, None, None, :] + sh.double()[seg][:, None, None, :])
+    ref = torch.einsum('nhwc,oc->nohw', a, wt.double()) + b.double()[None, :, None, None]
+    o = torch.empty(n, n_out, h, w, device=dev)
+    hip.conv1x1_fwd_bn(hip.nhwc(y.to(dev)), sc.reshape(-1).to(dev), sh.reshape(-1).to(dev), nseg, wt.to(dev),
+                       b.to(dev), n_out, o)
+    assert rel(o, ref) < TOL
+
+
 @pytest.mark.parametrize('c,n_out,h,w', [(64, 1, 16, 24), (8, 1, 16, 24), (128, 1, 16, 24), (16, 3, 16, 24),
                                          (64, 1, 7, 9), (32, 4, 5, 13)])  # odd sizes: ragged last pixel group
 def test_head_conv1x1(dev, c, n_out, h, w):

@@ -73,10 +73,13 @@ def main():
     ap.add_argument('--steps', type=int, default=8)
     ap.add_argument('--config', default='baseline_siamese')
     ap.add_argument('--batch', type=int, default=None)
+    ap.add_argument('--math', default=None, help='cfg.MODEL.CONV_MATH (as bench.py --math; bf16 brings bf16 storage)')
     args = ap.parse_args()
     hip.load_library()
     dev = torch.device('cuda:0')
     cfg = experiment_manager.load_cfg(args.config)
+    if args.math:
+        cfg.MODEL.CONV_MATH = args.math
     batch = args.batch or int(cfg.TRAINER.BATCH_SIZE)
     torch.manual_seed(cfg.SEED)
     net = networks.create_network(cfg).to(dev).train()
