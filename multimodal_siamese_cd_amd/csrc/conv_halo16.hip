@@ -85,7 +85,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     // groups of a wave (one halo row apart) sit 24 rows apart, and 24 / 2 = 12 = 0 mod 4 leaves the row swizzle
     // unchanged between them: one swizzled address per k-step, the groups at immediate offsets (8 VALU per step
     // instead of ~50).  The 6 pad rows per halo row are never staged or read.
-    constexpr bool PADP = TW == 16 && !DB && !WL;
+    // (double-buffered tiles too where both padded buffers of every resident block fit the CU's LDS: the bf16 tiles)
+    constexpr bool PADP = TW == 16 && !WL &&
+                          (!DB || OCC * 2 * (NP == 1 ? 1 : (NP == 2 || NP == 4) ? 2 : 3) * (TR + 2) * 24 * 64 <= 160 * 1024);
     constexpr int HWP = PADP ? 24 : HWD;
     constexpr int HR = (TR + 2) * HWP;           // LDS rows of one plane
     constexpr int A_CH = (TR + 2) * HWD * 8;     // 16-byte (4-channel) pieces of one 32-channel chunk
