@@ -219,21 +219,37 @@ def storage_scope(dtype):
 
 def act_storage_for(cfg, math: str | None = None):
     """torch dtype of a model's activations and gradients in HBM: bf16 for the bf16 arithmetic when every conv of the
-    model has a bf16-storage kernel (TOPOLOGY channel counts multiples of 64, input bands <= 16: the bf16 halo16, c16,
-    gather16 and ConvTranspose weight-grad kernels), else fp32.  MODEL.ACT_STORAGE ('fp32' / 'bf16') overrides."""
+    model has a bf16-storage kernel (TOPOLOGY channel counts multiples of 64, padded input widths 16 or a multiple of
+    64 (input_widths): the bf16 halo16, c16, gather16 and ConvTranspose weight-grad kernels), else fp32.  MODEL.ACT_STORAGE ('fp32' / 'bf16') overrides."""
     math = math or conv_math_for(cfg)
     want = str(cfg.MODEL.get('ACT_STORAGE', '') or '').lower()
     if want in ('fp32', 'f32', 'float32'):
         return _F32
-    ok = math == 'bf16' and all(int(c) % 64 == 0 for c in cfg.MODEL.TOPOLOGY)
+    ok = (math == 'bf16' and all(int(c) % 64 == 0 for c in cfg.MODEL.TOPOLOGY)
+          and all(w == 16 or w % 64 == 0 for w in input_widths(cfg)))
     if want in ('bf16', 'bfloat16'):
         if not ok:
-            raise ValueError("MODEL.ACT_STORAGE bf16 needs MODEL.PRECISION bf16 and TOPOLOGY channels in multiples "
-                             "of 64")
+            raise ValueError("MODEL.ACT_STORAGE bf16 needs MODEL.PRECISION bf16, TOPOLOGY channels in multiples of 64 "
+                             f"and padded input widths of 16 or multiples of 64 (got {input_widths(cfg)})")
         return torch.bfloat16
     if want:
         raise ValueError(f"MODEL.ACT_STORAGE {want!r}: expected 'fp32' or 'bf16'")
     return torch.bfloat16 if ok else _F32
+
+
+def input_widths(cfg) -> list:
+    """The channel widths a model's input layers see under the bf16 arithmetic (bands padded to the 16-channel
+    granule, pad_in): pack_pair of IN_CHANNELS (Siamese, dual-task), pack_stream of both dates' bands (UNet,
+    DualStream, WhateverNet2), pack_pair per modality (WhateverNet)."""
+    def p16(c):
+        return (int(c) + 15) // 16 * 16
+    t = str(cfg.MODEL.TYPE)
+    if t in ('dualstreamunet', 'whatevernet', 'whatevernet2'):
+        n1, n2 = len(cfg.DATALOADER.S1_BANDS), len(cfg.DATALOADER.S2_BANDS)
+        k = 1 if t == 'whatevernet' else 2
+        return [p16(k * n1), p16(k * n2)]
+    c = int(cfg.MODEL.IN_CHANNELS)
+    return [p16(2 * c if t == 'unet' else c)]
 
 
 def storage_for_input(dtype, h: int, w: int, levels: int):

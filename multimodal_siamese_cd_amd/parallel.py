@@ -142,8 +142,12 @@ def loss_scope(net):
 def allreduce_max(value: float, device) -> float:
     if not is_distributed():
         return value
-    on_dev = device is not None and dist.get_backend() == 'nccl'
-    t = torch.tensor([value], dtype=torch.float64, device=device if on_dev else 'cpu')
+    if dist.get_backend() == 'nccl':
+        if device is None or getattr(device, 'type', 'cpu') != 'cuda':
+            device = torch.device('cuda', torch.cuda.current_device())
+    else:
+        device = 'cpu'
+    t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -160,8 +164,12 @@ def gather_floats(value: float, device=None) -> list:
     """Every rank's `value`, in rank order (one SUM all-reduce of a one-hot vector)."""
     if not is_distributed():
         return [float(value)]
-    on_dev = device is not None and getattr(device, 'type', 'cpu') == 'cuda' and dist.get_backend() == 'nccl'
-    t = torch.zeros(dist.get_world_size(), dtype=torch.float64, device=device if on_dev else 'cpu')
+    if dist.get_backend() == 'nccl':  # RCCL reduces device tensors only
+        if device is None or getattr(device, 'type', 'cpu') != 'cuda':
+            device = torch.device('cuda', torch.cuda.current_device())
+    else:
+        device = 'cpu'
+    t = torch.zeros(dist.get_world_size(), dtype=torch.float64, device=device)
     t[dist.get_rank()] = float(value)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(v) for v in t.tolist()]

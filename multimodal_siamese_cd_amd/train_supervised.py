@@ -110,6 +110,11 @@ def run_training(cfg, device, max_steps: int | None = None):
                 _evaluate(net, cfg, device, ('training', 'validation'), epoch_float, global_step, rank)
             if max_steps is not None and global_step >= max_steps:
                 break
+        # every rank checks the steps since the last log-step check (the epoch's tail when steps_per_epoch is not a
+        # multiple of LOG_FREQ, a DEBUG or max_steps break) before rank 0 reports the epoch: a non-finite loss there
+        # stops every rank together instead of rank 0 alone while the others enter the next collective
+        _check_finite(bad, cfg, global_step, device)
+        bad = None
         if not cfg.DEBUG:  # evaluation at the end of an epoch (train_supervised.py:107-110)
             _evaluate(net, cfg, device, ('training', 'validation', 'test'), global_step / steps_per_epoch,
                       global_step, rank)

@@ -187,3 +187,26 @@ def test_bf16_storage_needs_every_level_tiled():
     assert engine.storage_for_input(f32, 256, 256, 5) == f32
     src = Path(__file__).resolve().parents[1] / 'multimodal_siamese_cd_amd' / 'utils' / 'networks.py'
     assert 'len(self.cfg.MODEL.TOPOLOGY) + 1' in src.read_text()
+
+
+def test_bf16_storage_needs_a_tiled_input_width():
+    """bf16 storage also needs every input layer's padded width (16 or a multiple of 64: the bf16 c16 and
+    halo16 kernels); a bf16 config whose padded input has 17-63 channels (e.g. dualstream with 10 S2 bands -> 20 -> 32)
+    stores fp32 instead of failing in the input layer's kernels, and an explicit ACT_STORAGE bf16 is refused."""
+    from multimodal_siamese_cd_amd import engine
+    cfg = em.load_cfg('baseline_dualstream')
+    assert engine.input_widths(cfg) == [16, 16]
+    assert engine.act_storage_for(cfg) == torch.bfloat16
+    cfg.DATALOADER.S2_BANDS = list(range(10))
+    assert engine.input_widths(cfg) == [16, 32]
+    assert engine.act_storage_for(cfg) == torch.float32
+    cfg.MODEL.ACT_STORAGE = 'bf16'
+    with pytest.raises(ValueError, match='input widths'):
+        engine.act_storage_for(cfg)
+    cfg = em.load_cfg('baseline_siamese')
+    cfg.MODEL.PRECISION = 'bf16'
+    assert engine.input_widths(cfg) == [16] and engine.act_storage_for(cfg) == torch.bfloat16
+    cfg.MODEL.IN_CHANNELS = 40  # padded to 48
+    assert engine.act_storage_for(cfg) == torch.float32
+    cfg.MODEL.IN_CHANNELS = 64
+    assert engine.act_storage_for(cfg) == torch.bfloat16

@@ -383,3 +383,64 @@ def test_nonfinite_loss_stops_every_rank_world2():
         mp.spawn(_worker_nonfinite, args=(world, _free_port(), d), nprocs=world, join=True)
         res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
     assert all(r['raised'] for r in res)
+
+
+class _TinyNet(torch.nn.Module):
+    """A CPU stand-in for the HIP model (run_training's loop, not the kernels, is under test)."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = torch.nn.Conv2d(5, 1, 1)
+
+    def forward(self, x_t1, x_t2):
+        return self.conv(x_t2 - x_t1)
+
+
+def _worker_nonfinite_tail(rank, world, port, out_dir):
+    import datetime
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    # a short collective timeout: if one rank stopped alone the other would fail here instead of hanging the test
+    torch.distributed.init_process_group('gloo', timeout=datetime.timedelta(seconds=60))
+    from multimodal_siamese_cd_amd import train_supervised, trainers
+    from multimodal_siamese_cd_amd.utils import experiment_manager as em, networks
+    cfg = em.load_cfg('debug')
+    cfg.DEBUG, cfg.EVALUATE, cfg.LOG_FREQ, cfg.SAVE_CHECKPOINTS = False, False, 3, []
+    cfg.TRAINER.EPOCHS, cfg.TRAINER.STEPS_PER_EPOCH, cfg.TRAINER.BATCH_SIZE = 2, 5, 2
+    cfg.AUGMENTATION.CROP_SIZE = 8
+    calls = {'n': 0}
+
+    def loss_fn(_cfg, out, batch, _net):
+        calls['n'] += 1
+        loss = (out - batch['y_change']).pow(2).mean()
+        if rank == 0 and calls['n'] == 5:  # step 5: after the step-3 log check, inside the epoch's tail
+            loss = loss * float('nan')
+        return loss
+
+    orig_net, orig_loss = networks.create_network, trainers.step_loss
+    networks.create_network = lambda _cfg: networks.ModelWrapper(_TinyNet())
+    trainers.step_loss = loss_fn
+    err = None
+    try:
+        train_supervised.run_training(cfg, torch.device('cpu'))
+    except FloatingPointError as e:
+        err = str(e)
+    finally:
+        networks.create_network, trainers.step_loss = orig_net, orig_loss
+    torch.save({'err': err, 'steps': calls['n']}, os.path.join(out_dir, f'rank{rank}.pt'))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_nonfinite_loss_in_epoch_tail_stops_every_rank_world2():
+    """a NaN loss on rank 0 after the last log-step check of an epoch (steps 4-5 of 5 with LOG_FREQ 3)
+    is caught by the epoch-end check on every rank, before rank 0's epoch report: both ranks raise at step 5 and
+    neither enters the next epoch's collectives alone."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_nonfinite_tail, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+    for r in res:
+        assert r['err'] is not None and 'up to step 5' in r['err']
+        assert r['steps'] == 5
