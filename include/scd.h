@@ -147,8 +147,10 @@ enum scd_conv_math {
  *   4: scd_pack_nchw takes a nullable `bound` (the input layer's h2 operand bound).
  *   5: scd_bn_relu_backward_coef takes `da_bound` / `dy_bound` (the h2 bound of the dy a weight grad forms itself);
  *      the 16-channel-source weight grad runs h2 when both scd_wgrad_t bounds are set.
- *   6: scd_nhwc_t.dtype: bf16 activation / gradient storage (the bf16 configs), every NHWC kernel. */
-#define SCD_ABI_VERSION 6
+ *   6: scd_nhwc_t.dtype: bf16 activation / gradient storage (the bf16 configs), every NHWC kernel.
+ *   7: scd_bn_relu_pool_out (plain and dual-task encoder levels written into the decoders' concat buffers),
+ *      scd_bn_relu_backward_pooled2 (a second, swapped skip gradient), scd_conv1x1_fwd_bn2 (two-source heads). */
+#define SCD_ABI_VERSION 7
 int scd_abi_version(void);
 /* The arithmetic scd_conv_igemm / scd_conv_wgrad will use for a descriptor (its `math`, or SCD_MATH_X3 / F32 where
  * the shape or the missing operand bounds keep the conv off the requested kernels); negative = invalid descriptor.
@@ -421,6 +423,18 @@ int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx,
                                 const float *gamma, const float *scale, const float *shift, float *dgamma,
                                 float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws,
                                 size_t ws_bytes, scd_stream_t stream);
+/* scd_bn_relu_backward_pooled with a second skip gradient (the dual-task encoder, networks.py:176-197, whose level
+ * activations feed both the difference of decoder_change and, as [a_t2; a_t1], the 2B-image skip batch of
+ * decoder_sem):  skip_mode 2 (y.n = 2 * gskip.n, nseg 2):
+ *   da[img] = maxpool_bwd(gy, idx)[img] + (sgn(img) * gskip[img % gskip.n] + gskip2[img < n ? img + n : img - n])
+ * with sgn as skip_mode 1 and n = gskip.n: bit-identical to the autograd sum of the difference gradient and the two
+ * semantic skip slices fed to scd_bn_relu_backward_pooled as one plain skip.  skip_mode 0 / 1 with gskip2 null are
+ * scd_bn_relu_backward_pooled. */
+int scd_bn_relu_backward_pooled2(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip,
+                                 int32_t skip_mode, scd_nhwc_t gskip2, int32_t nseg, const float *save_mean,
+                                 const float *save_invstd, const float *gamma, const float *scale, const float *shift,
+                                 float *dgamma, float *dbeta, float *dbias_prev, scd_nhwc_t dy, float *dy_bound,
+                                 void *ws, size_t ws_bytes, scd_stream_t stream);
 /* scd_bn_relu_backward whose incoming gradient is the 1x1 head's input gradient, formed on the fly:
  *   da[p][c] = sum_o gout[img][o][pix] * w_head[o][c]   (gout NCHW [n][n_out][h][w], n_out <= 4)
  * -- what scd_conv1x1_bwd would write into gx (same fma chain, bit-identical results); y.n * y.h * y.w < 2^31.
@@ -491,6 +505,17 @@ int scd_bn_relu_siamese_diff(scd_nhwc_t a, const float *scale, const float *shif
  * Bit-identical to the two calls. */
 int scd_bn_relu_pool_diff(scd_nhwc_t a, const float *scale, const float *shift, scd_nhwc_t d, scd_nhwc_t y,
                           uint8_t *idx, scd_stream_t stream);
+/* An encoder level's consumers of relu(BN1(a)) in one pass over 2x2 cells (even h, w), coefficients [nseg][c]:
+ *   mode 0 (Siamese, nseg 2): scd_bn_relu_pool_diff (o unused);
+ *   mode 1 (plain encoder, networks.py:334-343, 449): o = relu(bn(a)) (n images; o may be the skip slice of the
+ *          decoder's concat buffer: zero-copy cat), images in nseg segments of n / nseg;
+ *   mode 2 (dual-task Siamese, nseg 2, networks.py:176-197): d (n/2 images) as mode 0 and o (n images) =
+ *          [relu(bn_t2(a_t2)); relu(bn_t1(a_t1))], the semantic decoder's skip batch (t2 first);
+ * plus, when y.data != NULL, y / idx = MaxPool2d(2) of every image of a (networks.py:420).  Modes 1 and 2 derive every
+ * output from the stored activation (rounded to the view's type), so they are bit-identical to scd_bn_relu_apply
+ * followed by scd_maxpool2_fwd / scd_siamese_diff / copies of the materialised activation. */
+int scd_bn_relu_pool_out(scd_nhwc_t a, int32_t nseg, const float *scale, const float *shift, int32_t mode,
+                         scd_nhwc_t d, scd_nhwc_t o, scd_nhwc_t y, uint8_t *idx, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * OutConv 1x1 head (networks.py:454-461): out NCHW [n][n_out][h][w] = b + x . w   (n_out <= 4)
@@ -511,6 +536,13 @@ int scd_conv1x1_fwd_bn(scd_nhwc_t y, const float *scale, const float *shift, int
 int scd_conv1x1_bwd_bn(scd_nhwc_t y, const float *scale, const float *shift, int32_t nseg, const float *w,
                        const float *gout, int32_t n_out, float *gw, float *gb, void *ws, size_t ws_bytes,
                        scd_stream_t stream);
+/* The heads over two decoder outputs (the fusion heads, networks.py:119, 258, and WhateverNet's per-stream heads in
+ * the same launch): out = b + cat([xa, xb], channel) . w, w [n_out][ya.c + yb.c] (zeros where a head does not read a
+ * source), each source read through its own coefficients (both given, or neither: plain activations).  yb.data NULL:
+ * scd_conv1x1_fwd_bn.  Bit-identical to the single-source call on the concatenated activation. */
+int scd_conv1x1_fwd_bn2(scd_nhwc_t ya, const float *scale_a, const float *shift_a, scd_nhwc_t yb,
+                        const float *scale_b, const float *shift_b, int32_t nseg, const float *w, const float *b,
+                        int32_t n_out, float *out, scd_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * power_jaccard_loss (utils/loss_functions.py:141-150): p = sigmoid(logit); I = sum p*t;

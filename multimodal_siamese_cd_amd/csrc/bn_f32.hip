@@ -329,6 +329,9 @@ struct DaPlain {  // a materialised tensor
 // The encoder level's gradient, formed on the fly with the expressions of feature_grad_kernel (misc_f32.hip):
 // MaxPool2d backward of the next level's input gradient gy through the argmax bytes, plus -/+ the gradient of
 // the Siamese feature difference (skip_mode 1: t1 images subtract) or a plain skip gradient (skip_mode 0).
+// skip_mode 2 (the dual-task encoder): also the semantic decoder's skip gradient gs2, a [t2; t1] batch of 2 gsn images
+// (image img of the [t1; t2] level reads gs2 image img + gsn for t1, img - gsn for t2), added to the difference term
+// first: (sg * gs + gs2) is the one rounding autograd's sum of the two skip gradients makes.
 template <class T>
 struct DaPooled {
     const T *gy;  // (n, h/2, w/2, C) or null
@@ -336,6 +339,8 @@ struct DaPooled {
     int hy, wy, ldgy;
     const T *gs;  // (gsn, h, w, C) or null
     int gsn, ldgs, skip_mode;
+    const T *gs2;  // skip_mode 2: (2 gsn, h, w, C), else null
+    int ldgs2;
     int hx, wx, C;
     FastDiv div_hw, div_w, div_gsn;
     __device__ __forceinline__ f4 operator()(int64_t p, int c) const {
@@ -358,12 +363,21 @@ struct DaPooled {
         }
         if (gs) {
             const int simg = int(img - fdiv(img, div_gsn) * uint32_t(gsn));
-            const float sg = (skip_mode == 1 && int(img) < gsn) ? -1.f : 1.f;
+            const float sg = (skip_mode != 0 && int(img) < gsn) ? -1.f : 1.f;
             const f4 sv = ld4(gs + ((int64_t(simg) * hx + yy) * wx + x) * ldgs + c);
-            r.x += sg * sv.x;
-            r.y += sg * sv.y;
-            r.z += sg * sv.z;
-            r.w += sg * sv.w;
+            if (gs2) {
+                const int img2 = int(img) < gsn ? int(img) + gsn : int(img) - gsn;
+                const f4 s2 = ld4(gs2 + ((int64_t(img2) * hx + yy) * wx + x) * ldgs2 + c);
+                r.x += sg * sv.x + s2.x;
+                r.y += sg * sv.y + s2.y;
+                r.z += sg * sv.z + s2.z;
+                r.w += sg * sv.w + s2.w;
+            } else {
+                r.x += sg * sv.x;
+                r.y += sg * sv.y;
+                r.z += sg * sv.z;
+                r.w += sg * sv.w;
+            }
         }
         return r;
     }
@@ -404,7 +418,8 @@ struct PooledCells {
 };
 
 // dL/da of the four pixels of `cell` (flat cell index over images) at channel quad c; ok[k]: pixel k exists.
-template <class T>
+// S2: the dual-task second skip gradient (DaPooled.gs2, with gs present).
+template <class T, bool S2>
 __device__ __forceinline__ void cell_grads(const PooledCells<T> &P, uint32_t cell, int c, f4 (&g)[4], int64_t (&pix)[4],
                                            bool (&ok)[4], const T *fallback) {
     const DaPooled<T> &d = P.da;
@@ -422,12 +437,16 @@ __device__ __forceinline__ void cell_grads(const PooledCells<T> &P, uint32_t cel
         (has_gy ? d.idx : reinterpret_cast<const uint8_t *>(fallback)) + q * d.C + c);
     f4 gp = ld4((has_gy ? d.gy : fallback) + q * d.ldgy + c);
     const int simg = d.gs ? int(img - fdiv(img, d.div_gsn) * uint32_t(d.gsn)) : 0;
-    const float sg = (d.gs && d.skip_mode == 1 && int(img) < d.gsn) ? -1.f : 1.f;
-    f4 sv[4];
+    const float sg = (d.gs && d.skip_mode != 0 && int(img) < d.gsn) ? -1.f : 1.f;
+    f4 sv[4], s2v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int yy = min(2 * cy + (k >> 1), d.hx - 1), xx = min(2 * cx + (k & 1), d.wx - 1);
         sv[k] = ld4((d.gs ? d.gs : fallback) + (d.gs ? ((int64_t(simg) * d.hx + yy) * d.wx + xx) * d.ldgs : 0) + c);
+        if constexpr (S2) {
+            const int img2 = int(img) < d.gsn ? int(img) + d.gsn : int(img) - d.gsn;
+            s2v[k] = ld4(d.gs2 + ((int64_t(img2) * d.hx + yy) * d.wx + xx) * d.ldgs2 + c);
+        }
     }
     if (!in) {  // no pooled gradient: no byte matches a sub-pixel
         pk = 0xffffffffu;
@@ -443,8 +462,14 @@ __device__ __forceinline__ void cell_grads(const PooledCells<T> &P, uint32_t cel
                 ((pk >> 16) & 0xff) == want ? gp.z : 0.f, ((pk >> 24) & 0xff) == want ? gp.w : 0.f};
         // the skip term of a missing pixel (ok[k] false) reads a clamped neighbour: its g is never used; a select,
         // not a branch, so the caller's loads can be scheduled above
-        const f4 t = {v.x + sg * sv[k].x, v.y + sg * sv[k].y, v.z + sg * sv[k].z, v.w + sg * sv[k].w};
-        g[k] = d.gs ? t : v;
+        if constexpr (S2) {
+            const f4 u = {sg * sv[k].x + s2v[k].x, sg * sv[k].y + s2v[k].y, sg * sv[k].z + s2v[k].z,
+                          sg * sv[k].w + s2v[k].w};
+            g[k] = v + u;
+        } else {
+            const f4 t = {v.x + sg * sv[k].x, v.y + sg * sv[k].y, v.z + sg * sv[k].z, v.w + sg * sv[k].w};
+            g[k] = d.gs ? t : v;
+        }
     }
 }
 
@@ -457,7 +482,7 @@ __device__ __forceinline__ int64_t cell_load_pix(const int64_t (&pix)[4], const 
 // cell_grads for a Siamese pair (skip_mode 1, two segments of gsn images): `cell` lies in a t1 image, its partner
 // cell (same place) in image img + gsn.  The difference gradient is read once for both (t1 subtracts it, t2 adds
 // it, with cell_grads' expressions: bit-identical).  pix[k] is the t1 pixel; its t2 partner is pix[k] + gsn*hx*wx.
-template <class T>
+template <class T, bool S2>
 __device__ __forceinline__ void cell_grads_pair(const PooledCells<T> &P, uint32_t cell, int c, f4 (&g0)[4], f4 (&g1)[4],
                                                 int64_t (&pix)[4], bool (&ok)[4]) {
     const DaPooled<T> &d = P.da;
@@ -475,11 +500,15 @@ __device__ __forceinline__ void cell_grads_pair(const PooledCells<T> &P, uint32_
     uint32_t pk0 = *reinterpret_cast<const uint32_t *>(ib + q0 * d.C + c);
     uint32_t pk1 = *reinterpret_cast<const uint32_t *>(ib + q1 * d.C + c);
     f4 gp0 = ld4(gb + q0 * d.ldgy + c), gp1 = ld4(gb + q1 * d.ldgy + c);
-    f4 svs[4];
+    f4 svs[4], s2a[4], s2b[4];  // S2: the semantic skip gradient of the t1 (image img + gsn) and t2 (img) pixel
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int yy = min(2 * cy + (k >> 1), d.hx - 1), xx = min(2 * cx + (k & 1), d.wx - 1);
         svs[k] = ld4(d.gs + ((int64_t(img) * d.hx + yy) * d.wx + xx) * d.ldgs + c);
+        if constexpr (S2) {
+            s2a[k] = ld4(d.gs2 + ((int64_t(img + d.gsn) * d.hx + yy) * d.wx + xx) * d.ldgs2 + c);
+            s2b[k] = ld4(d.gs2 + ((int64_t(img) * d.hx + yy) * d.wx + xx) * d.ldgs2 + c);
+        }
     }
     if (!in) {
         pk0 = pk1 = 0xffffffffu;
@@ -495,7 +524,12 @@ __device__ __forceinline__ void cell_grads_pair(const PooledCells<T> &P, uint32_
                  ((pk0 >> 16) & 0xff) == want ? gp0.z : 0.f, ((pk0 >> 24) & 0xff) == want ? gp0.w : 0.f};
         f4 v1 = {((pk1 >> 0) & 0xff) == want ? gp1.x : 0.f, ((pk1 >> 8) & 0xff) == want ? gp1.y : 0.f,
                  ((pk1 >> 16) & 0xff) == want ? gp1.z : 0.f, ((pk1 >> 24) & 0xff) == want ? gp1.w : 0.f};
-        {  // unconditional: a missing pixel's (ok[k] false) gradient is never used (see cell_grads)
+        if constexpr (S2) {  // (sg * gs + gs2) first: see DaPooled
+            const f4 sv = svs[k];
+            const float m = -1.f, p1 = 1.f;
+            v0 += f4{m * sv.x + s2a[k].x, m * sv.y + s2a[k].y, m * sv.z + s2a[k].z, m * sv.w + s2a[k].w};
+            v1 += f4{p1 * sv.x + s2b[k].x, p1 * sv.y + s2b[k].y, p1 * sv.z + s2b[k].z, p1 * sv.w + s2b[k].w};
+        } else {  // unconditional: a missing pixel's (ok[k] false) gradient is never used (see cell_grads)
             const f4 sv = svs[k];
             const float m = -1.f, p1 = 1.f;
             v0.x += m * sv.x;
@@ -541,7 +575,7 @@ __device__ __forceinline__ void pooled_rec2(f4 (&sh1)[BN_THREADS], f4 (&sh2)[BN_
 
 // bn_bwd_pooled_partial for a Siamese pair: block k covers chunk k of the t1 segment and chunk k of the t2 segment
 // (same cells), reading the shared difference gradient once; same per-chunk records, bit-identical.
-template <class T>
+template <class T, bool S2>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial_pair(const T *__restrict__ y, int ldy,
                                                                          PooledCells<T> P, int C, int64_t cseg, int ncps,
                                                                          int chunk, int nrec, int qpb,
@@ -562,7 +596,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial_pair(const T
             f4 g0[4], g1[4];
             int64_t pix[4];
             bool ok[4];
-            cell_grads_pair(P, uint32_t(cell), c, g0, g1, pix, ok);
+            cell_grads_pair<T, S2>(P, uint32_t(cell), c, g0, g1, pix, ok);
             f4 y0[4], y1[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {  // unconditional (a missing pixel reads the cell's first; not used)
@@ -586,7 +620,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial_pair(const T
 }
 
 // bn_bwd_partial over cells: rec[c][chunk][2] = {sum dz, sum dz*xhat} of the chunk's cells' pixels.
-template <class T>
+template <class T, bool S2>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const T *__restrict__ y, int ldy, PooledCells<T> P,
                                                                     int C, int64_t cseg, int ncps, int chunk, int nrec,
                                                                     int qpb, const float *smean, const float *sinv,
@@ -605,7 +639,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const T *__r
             f4 g[4];
             int64_t pix[4];
             bool ok[4];
-            cell_grads(P, uint32_t(cell), c, g, pix, ok, y);
+            cell_grads<T, S2>(P, uint32_t(cell), c, g, pix, ok, y);
             f4 yv[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) yv[k] = ld4(y + cell_load_pix(pix, ok, k) * ldy + c);  // see above
@@ -641,7 +675,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_partial(const T *__r
 }
 
 // bn_bwd_apply over cells (see bn_bwd_pooled_partial); brec[c][chunk] (conv bias grad) and dy_bound optional.
-template <class T>
+template <class T, bool S2>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const T *__restrict__ y, int ldy, PooledCells<T> P,
                                                                   T *__restrict__ dy, int lddy, int C, int64_t cseg,
                                                                   int ncps, int chunk, int nrec, int qpb,
@@ -668,7 +702,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const T *__res
             f4 g[4];
             int64_t pix[4];
             bool ok[4];
-            cell_grads(P, uint32_t(cell), c, g, pix, ok, y);
+            cell_grads<T, S2>(P, uint32_t(cell), c, g, pix, ok, y);
             f4 yv[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) yv[k] = ld4(y + cell_load_pix(pix, ok, k) * ldy + c);  // see above
@@ -700,7 +734,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply(const T *__res
 
 // bn_bwd_pooled_apply for a Siamese pair (see bn_bwd_pooled_partial_pair): both segments' dy per cell, the conv-bias
 // records of chunk k of each segment, bit-identical.
-template <class T>
+template <class T, bool S2>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply_pair(
     const T *__restrict__ y, int ldy, PooledCells<T> P, T *__restrict__ dy, int lddy, int C, int64_t cseg, int ncps,
     int chunk, int nrec, int qpb, const float *smean, const float *sinv, const float *gamma, const float *scale,
@@ -725,7 +759,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_pooled_apply_pair(
             f4 g0[4], g1[4];
             int64_t pix[4];
             bool ok[4];
-            cell_grads_pair(P, uint32_t(cell), c, g0, g1, pix, ok);
+            cell_grads_pair<T, S2>(P, uint32_t(cell), c, g0, g1, pix, ok);
             f4 y0[4], y1[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {  // unconditional (a missing pixel reads the cell's first; not used)
@@ -1376,6 +1410,13 @@ static void bn_backward_run_head(const scd_nhwc_t &y, const DaHead &da, int nseg
 #ifndef SCD_BN_POOLED_PAIR
 #define SCD_BN_POOLED_PAIR 1
 #endif
+template <class T, bool S2>
+static void bn_backward_pooled_cells(const scd_nhwc_t &y, const PooledCells<T> &P, int nseg, const BnGeom &g,
+                                     int64_t cseg, int chunk, int ncps, int nrec, const float *save_mean,
+                                     const float *save_invstd, const float *gamma, const float *scale,
+                                     const float *shift, float *dgamma, float *dbeta, float *dbias_prev,
+                                     const scd_nhwc_t &dy, float *dy_bound, float *rec, float *brec, float *coef,
+                                     hipStream_t s);
 template <class T>
 static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled<T> &da, int nseg, const float *save_mean,
                                    const float *save_invstd, const float *gamma, const float *scale, const float *shift,
@@ -1402,25 +1443,42 @@ static void bn_backward_run_pooled(const scd_nhwc_t &y, const DaPooled<T> &da, i
     float *coef = brec + size_t(g.nrec) * y.c;
     // Siamese pairs (-DSCD_BN_POOLED_PAIR=0: one image per cell walk): the t1 and t2 cells at one place in one block,
     // the shared difference gradient read once instead of once per branch
-    if (SCD_BN_POOLED_PAIR && nseg == 2 && da.gs && da.skip_mode == 1 && 2 * da.gsn == y.n) {
-        hipLaunchKernelGGL(bn_bwd_pooled_partial_pair<T>, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
+    if (da.gs2) {
+        bn_backward_pooled_cells<T, true>(y, P, nseg, g, cseg, chunk, ncps, nrec, save_mean, save_invstd, gamma, scale,
+                                          shift, dgamma, dbeta, dbias_prev, dy, dy_bound, rec, brec, coef, s);
+    } else {
+        bn_backward_pooled_cells<T, false>(y, P, nseg, g, cseg, chunk, ncps, nrec, save_mean, save_invstd, gamma, scale,
+                                           shift, dgamma, dbeta, dbias_prev, dy, dy_bound, rec, brec, coef, s);
+    }
+}
+
+template <class T, bool S2>
+static void bn_backward_pooled_cells(const scd_nhwc_t &y, const PooledCells<T> &P, int nseg, const BnGeom &g,
+                                     int64_t cseg, int chunk, int ncps, int nrec, const float *save_mean,
+                                     const float *save_invstd, const float *gamma, const float *scale,
+                                     const float *shift, float *dgamma, float *dbeta, float *dbias_prev,
+                                     const scd_nhwc_t &dy, float *dy_bound, float *rec, float *brec, float *coef,
+                                     hipStream_t s) {
+    const DaPooled<T> &da = P.da;
+    if (SCD_BN_POOLED_PAIR && nseg == 2 && da.gs && (da.skip_mode == 1 || da.skip_mode == 2) && 2 * da.gsn == y.n) {
+        hipLaunchKernelGGL((bn_bwd_pooled_partial_pair<T, S2>), dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
                            view_ptr<const T>(y), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
                            save_invstd, scale, shift, rec);
         hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, ncps, nrec, g.pseg,
                            coef, dgamma, dbeta);
-        hipLaunchKernelGGL(bn_bwd_pooled_apply_pair<T>, dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
+        hipLaunchKernelGGL((bn_bwd_pooled_apply_pair<T, S2>), dim3(ncps, g.cgroups), dim3(BN_THREADS), 0, s,
                            view_ptr<const T>(y), y.ldc, P, view_ptr<T>(dy), dy.ldc, y.c,
                            cseg, ncps, chunk, nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
                            dbias_prev ? brec : nullptr, dy_bound);
         if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, nrec, dbias_prev);
         return;
     }
-    hipLaunchKernelGGL(bn_bwd_pooled_partial<T>, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+    hipLaunchKernelGGL((bn_bwd_pooled_partial<T, S2>), dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        view_ptr<const T>(y), y.ldc, P, y.c, cseg, ncps, chunk, nrec, g.qpb, save_mean,
                        save_invstd, scale, shift, rec);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, ncps, nrec, g.pseg, coef,
                        dgamma, dbeta);
-    hipLaunchKernelGGL(bn_bwd_pooled_apply<T>, dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+    hipLaunchKernelGGL((bn_bwd_pooled_apply<T, S2>), dim3(nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        view_ptr<const T>(y), y.ldc, P, view_ptr<T>(dy), dy.ldc, y.c, cseg,
                        ncps, chunk, nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
                        dbias_prev ? brec : nullptr, dy_bound);
@@ -1500,10 +1558,26 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
                                            const float *save_invstd, const float *gamma, const float *scale,
                                            const float *shift, float *dgamma, float *dbeta, float *dbias_prev,
                                            scd_nhwc_t dy, float *dy_bound, void *ws, size_t ws_bytes, scd_stream_t stream) {
+    if (skip_mode == 2) {
+        clear_error();
+        set_error("bn_relu_backward_pooled: skip_mode 2 takes a second skip gradient (scd_bn_relu_backward_pooled2)");
+        return SCD_ERR_ARG;
+    }
+    return scd_bn_relu_backward_pooled2(y, gy, idx, gskip, skip_mode, scd_nhwc_t{}, nseg, save_mean, save_invstd, gamma,
+                                        scale, shift, dgamma, dbeta, dbias_prev, dy, dy_bound, ws, ws_bytes, stream);
+}
+
+extern "C" int scd_bn_relu_backward_pooled2(scd_nhwc_t y, scd_nhwc_t gy, const uint8_t *idx, scd_nhwc_t gskip,
+                                            int32_t skip_mode, scd_nhwc_t gskip2, int32_t nseg,
+                                            const float *save_mean, const float *save_invstd, const float *gamma,
+                                            const float *scale, const float *shift, float *dgamma, float *dbeta,
+                                            float *dbias_prev, scd_nhwc_t dy, float *dy_bound, void *ws,
+                                            size_t ws_bytes, scd_stream_t stream) {
     clear_error();
     SCD_TRY(bn_check(y, nseg));
     SCD_TRY(check_view(gy, "bn_bwd_pooled.gy", true));
     SCD_TRY(check_view(gskip, "bn_bwd_pooled.gskip", true));
+    SCD_TRY(check_view(gskip2, "bn_bwd_pooled.gskip2", true));
     SCD_TRY(check_view(dy, "bn_bwd_pooled.dy"));
     if (dy.n != y.n || dy.h != y.h || dy.w != y.w || dy.c != y.c || !save_mean || !save_invstd || !scale || !shift ||
         (!gy.data && !gskip.data) || pixels(y) >= (int64_t(1) << 31)) {
@@ -1516,15 +1590,22 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
         return SCD_ERR_ARG;
     }
     if (gskip.data && (gskip.c != y.c || gskip.h != y.h || gskip.w != y.w || y.n % gskip.n ||
-                       (skip_mode == 1 && y.n != 2 * gskip.n) || (skip_mode != 0 && skip_mode != 1))) {
+                       (skip_mode != 0 && y.n != 2 * gskip.n) || skip_mode < 0 || skip_mode > 2)) {
         set_error("bn_relu_backward_pooled: gskip shape/mode mismatch");
+        return SCD_ERR_ARG;
+    }
+    if ((skip_mode == 2) != (gskip2.data != nullptr) ||
+        (gskip2.data && (!gskip.data || nseg != 2 || gskip2.n != y.n || gskip2.h != y.h || gskip2.w != y.w ||
+                         gskip2.c != y.c))) {
+        set_error("bn_relu_backward_pooled: skip_mode 2 needs gskip (n/2 images), gskip2 (n images) and nseg 2; "
+                  "gskip2 only with skip_mode 2");
         return SCD_ERR_ARG;
     }
     if (!ws || ws_bytes < scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg)) {
         set_error("bn_relu_backward_pooled: workspace too small");
         return SCD_ERR_WORKSPACE;
     }
-    const int dt = common_dtype("bn_relu_backward_pooled", {&y, &gy, &gskip, &dy});
+    const int dt = common_dtype("bn_relu_backward_pooled", {&y, &gy, &gskip, &gskip2, &dy});
     if (dt < 0) return SCD_ERR_ARG;
     SCD_WITH_T(dt, T, {
         DaPooled<T> da;
@@ -1537,6 +1618,8 @@ extern "C" int scd_bn_relu_backward_pooled(scd_nhwc_t y, scd_nhwc_t gy, const ui
         da.gsn = gskip.n > 0 ? gskip.n : 1;
         da.ldgs = gskip.ldc;
         da.skip_mode = skip_mode;
+        da.gs2 = view_ptr<const T>(gskip2);
+        da.ldgs2 = gskip2.ldc;
         da.hx = y.h;
         da.wx = y.w;
         da.C = y.c;

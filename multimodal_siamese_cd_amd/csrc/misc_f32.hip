@@ -253,26 +253,41 @@ __global__ void siamese_diff_kernel(const T *__restrict__ a, int lda, T *__restr
     }
 }
 
-// One encoder level's two consumers of relu(BN1(y1)) in one read of y1 (even h, w): the feature difference
-// d[b] = a_t2 - a_t1 at full resolution and MaxPool2d(2) of both branches for the next level.  Same per-element
-// expressions as siamese_diff_kernel<true> and maxpool2_fwd_kernel<true>, so results are bit-identical to the
-// two-kernel path.  One thread = one pooled pixel quad of pair b, both branches; rows = pairs * hy.
-template <class T>
-__global__ void bn_relu_pool_diff_kernel(const T *__restrict__ x, int hx, int wx, int ldx, T *__restrict__ y,
-                                         int hy, int wy, int ldy, uint8_t *__restrict__ idx, T *__restrict__ d,
-                                         int ldd, int C, int pairs, int rows, FastDiv div_cq,
-                                         const float *__restrict__ bsc, const float *__restrict__ bsh) {
+// One encoder level's consumers of relu(BN1(y1)) in one read of y1 (even h, w), per 2x2 cell of the map:
+//  MODE 0 (Siamese pairs): the feature difference d[b] = a_t2 - a_t1 at full resolution (into the decoder's concat
+//          buffer) -- the expressions of siamese_diff_kernel<true> and maxpool2_fwd_kernel<true>, bit-identical to the
+//          two-kernel path;
+//  MODE 1 (plain images, `nseg` coefficient segments of seg_imgs images): the activation itself written into o (the
+//          decoder's concat buffer slice: the skip of a plain encoder, zero-copy cat);
+//  MODE 2 (Siamese pairs, dual-task): d as MODE 0 and o = [a_t2; a_t1] (the semantic decoder's 2B-image skip batch,
+//          t2 first as the reference calls decoder_sem(features_t2) first).
+// MODEs 1 and 2 form every output from the STORED activation (bf16-rounded under bf16 storage; identity in fp32), so
+// they are bit-identical to materialising a with bn_relu_apply and running maxpool2_fwd / siamese_diff / copies on it.
+// y / idx null: no pooling (the deepest level).  One thread = one cell quad of one unit (pair or image); rows = units * hy.
+template <int MODE, class T>
+__global__ void bn_relu_pool_out_kernel(const T *__restrict__ x, int hx, int wx, int ldx, T *__restrict__ y, int hy,
+                                        int wy, int ldy, uint8_t *__restrict__ idx, T *__restrict__ d, int ldd,
+                                        T *__restrict__ o, int ldo, int C, int units, int seg_imgs, int rows,
+                                        FastDiv div_cq, const float *__restrict__ bsc, const float *__restrict__ bsh) {
+    constexpr bool PAIR = MODE != 1;
     const int cq = C / 4;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= wy * cq) return;
     const int ox = int(fdiv(uint32_t(e), div_cq));
     const int c = (e - ox * cq) * 4;
-    const bnf4 sc1 = ld4(bsc + c), sh1 = ld4(bsh + c);
-    const bnf4 sc2 = ld4(bsc + C + c);
-    const bnf4 sh2 = ld4(bsh + C + c);
-    const int64_t half = int64_t(pairs) * hx * wx;  // pixels of one branch
+    bnf4 sc1 = ld4(bsc + c), sh1 = ld4(bsh + c), sc2 = sc1, sh2 = sh1;
+    if constexpr (PAIR) {
+        sc2 = ld4(bsc + C + c);
+        sh2 = ld4(bsh + C + c);
+    }
+    const int64_t half = int64_t(units) * hx * wx;  // pixels of one branch (pairs)
     for (int row = blockIdx.y; row < rows; row += gridDim.y) {
         const int b = row / hy, oy = row - b * hy;
+        if constexpr (!PAIR) {
+            const int so = (b / seg_imgs) * C + c;
+            sc1 = ld4(bsc + so);
+            sh1 = ld4(bsh + so);
+        }
         const int64_t q[4] = {(int64_t(b) * hx + 2 * oy) * wx + 2 * ox, (int64_t(b) * hx + 2 * oy) * wx + 2 * ox + 1,
                               (int64_t(b) * hx + 2 * oy + 1) * wx + 2 * ox,
                               (int64_t(b) * hx + 2 * oy + 1) * wx + 2 * ox + 1};
@@ -280,16 +295,34 @@ __global__ void bn_relu_pool_diff_kernel(const T *__restrict__ x, int hx, int wx
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             v1[k] = bn_relu_f4(ld4(x + q[k] * ldx + c), sc1, sh1);
-            v2[k] = bn_relu_f4(ld4(x + (q[k] + half) * ldx + c), sc2, sh2);
+            if constexpr (MODE != 0) v1[k] = stored4(o, v1[k]);
+            if constexpr (PAIR) {
+                v2[k] = bn_relu_f4(ld4(x + (q[k] + half) * ldx + c), sc2, sh2);
+                if constexpr (MODE != 0) v2[k] = stored4(o, v2[k]);
+            }
         }
+        if constexpr (PAIR) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) st4(d + q[k] * ldd + c, v2[k] - v1[k]);
+            for (int k = 0; k < 4; ++k) st4(d + q[k] * ldd + c, v2[k] - v1[k]);
+        }
+        if constexpr (MODE == 1) {
 #pragma unroll
-        for (int br = 0; br < 2; ++br) {
+            for (int k = 0; k < 4; ++k) st4(o + q[k] * ldo + c, v1[k]);
+        }
+        if constexpr (MODE == 2) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                st4(o + q[k] * ldo + c, v2[k]);
+                st4(o + (q[k] + half) * ldo + c, v1[k]);
+            }
+        }
+        if (!y) continue;  // uniform
+#pragma unroll
+        for (int br = 0; br < (PAIR ? 2 : 1); ++br) {
             const bnf4 *v = br ? v2 : v1;
             const float a0[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, a1[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
             const float a2[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, a3[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
-            float o[4];
+            float om[4];
             uint32_t packed = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -299,74 +332,125 @@ __global__ void bn_relu_pool_diff_kernel(const T *__restrict__ x, int hx, int wx
                 pool_pick(a1[k], 1, mx, id);
                 pool_pick(a2[k], 2, mx, id);
                 pool_pick(a3[k], 3, mx, id);
-                o[k] = mx;
+                om[k] = mx;
                 packed |= uint32_t(id) << (8 * k);
             }
-            const int64_t p = (int64_t(b + br * pairs) * hy + oy) * wy + ox;
-            st4(y + p * ldy + c, bnf4{o[0], o[1], o[2], o[3]});
+            const int64_t p = (int64_t(b + br * units) * hy + oy) * wy + ox;
+            st4(y + p * ldy + c, bnf4{om[0], om[1], om[2], om[3]});
             *reinterpret_cast<uint32_t *>(idx + p * C + c) = packed;
         }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// Wave-cooperative 1x1 conv: G = pow2 >= C/4 lanes share a pixel (each a channel quad, coalesced 16-byte
-// loads), partial dots are combined with a fixed xor-shuffle tree.  grid-stride over groups of U pixel sets per
-// wave, whose loads are all issued before the arithmetic (U x the bytes in flight of one set per iteration).
-// scale / shift (optional): the input is read through the producing BatchNorm + ReLU, relu(fma(x, scale, shift))
-// per segment of pseg pixels (bn_relu_apply_kernel's expression), so that activation never has to be written.
-template <int U, class T>
-__global__ __launch_bounds__(256) void conv1x1_fwd_kernel(const T *__restrict__ x, int ldx, int C, int hw,
+// Wave-cooperative 1x1 conv (the OutConv heads): G = pow2 >= P lanes share a pixel, each a 16-byte piece of CP
+// channels (CP = 4 fp32 / 8 bf16 channels: a bf16 lane loads 16 bytes, not 8), partial dots combined with a fixed
+// xor-shuffle tree.  Grid-stride over groups of U pixel sets per wave, whose loads are all issued before the arithmetic.
+// Two sources (a: pieces [0, pa), b: pieces [pa, P)) read as ONE concatenated input: the fusion heads' cat([x_a, x_b])
+// (networks.py:119, 258) without the cat, each source through its own BatchNorm + ReLU coefficients.  The piece order,
+// per-lane chains and tree are those of the single-source kernel over the concatenated tensor, so the two-source launch
+// is bit-identical to cat + conv.  Several heads over the same sources are one launch: the n_out <= 4 rows of w
+// ([n_out][C], zeros where a head does not read a source) -- each source is read once for all heads.
+// scale / shift (optional, per source): relu(fma(x, scale, shift)) per segment of pseg pixels
+// (bn_relu_apply_kernel's expression), so the decoders' last activations are never written.
+template <class T, int CP>
+struct HeadPiece;
+template <class T>
+struct HeadPiece<T, 4> {
+    bnf4 v[1];
+    __device__ __forceinline__ void load(const T *p) { v[0] = ld4(p); }
+};
+template <>
+struct HeadPiece<bf16_t, 8> {
+    bnf4 v[2];
+    __device__ __forceinline__ void load(const bf16_t *p) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 r = *reinterpret_cast<const u32x4 *>(p);
+        v[0] = unpk_bf16x4(scd_u32x2{r[0], r[1]});
+        v[1] = unpk_bf16x4(scd_u32x2{r[2], r[3]});
+    }
+};
+
+struct HeadSrc {
+    const void *x;
+    int ld, C;  // row stride and channels of the source
+    const float *scale, *shift;
+};
+
+template <int U, class T, int CP>
+__global__ __launch_bounds__(256) void conv1x1_fwd_kernel(HeadSrc sa, HeadSrc sb, int pa, int P, int C, int hw,
                                                           int64_t npix, const float *__restrict__ w,
                                                           const float *__restrict__ b, int n_out, int G,
-                                                          const float *__restrict__ scale,
-                                                          const float *__restrict__ shift, int64_t pseg,
-                                                          FastDiv fseg, FastDiv fhw, float *__restrict__ out) {
+                                                          int64_t pseg, FastDiv fseg, FastDiv fhw,
+                                                          float *__restrict__ out) {
+    constexpr int NQ = CP / 4;  // channel quads per piece
     const int lane = threadIdx.x & 63;
     const int q = lane % G, pp = lane / G, ppw = 64 / G;
-    const int cq = C / 4;
     const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+    const bool bn = sa.scale != nullptr;  // uniform: both sources or neither
     for (int64_t p0 = wave * ppw * U; p0 < npix; p0 += nwaves * ppw * U) {
         float s[U][4];
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int o = 0; o < 4; ++o) s[u][o] = 0.f;
-        for (int qq = q; qq < cq; qq += G) {
-            bnf4 v[U];
+        for (int qq = q; qq < P; qq += G) {
+            const bool in_a = qq < pa;  // a select, not a branch: lanes of one pixel may read different sources
+            const T *xs = static_cast<const T *>(in_a ? sa.x : sb.x);
+            const int ld = in_a ? sa.ld : sb.ld, cs = in_a ? sa.C : sb.C;
+            const int ch = (in_a ? qq : qq - pa) * CP;
+            HeadPiece<T, CP> v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t p = p0 + u * ppw + pp;
-                v[u] = p < npix ? ld4(x + p * ldx + 4 * qq) : bnf4{0.f, 0.f, 0.f, 0.f};
+                if (p < npix) {
+                    v[u].load(xs + p * ld + ch);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < NQ; ++k) v[u].v[k] = bnf4{0.f, 0.f, 0.f, 0.f};
+                }
             }
-            if (scale) {
+            if (bn) {
+                const float *scl = in_a ? sa.scale : sb.scale, *shf = in_a ? sa.shift : sb.shift;
                 // segment of a pixel: a multiply-shift below 2^31 pixels.  The U pixels of a lane nearly always share
-                // one segment: then one coefficient load serves them (per-pixel coefficient loads were 4x the bytes
-                // of the activations they transform)
+                // one segment: then one coefficient load serves them
                 auto seg_of = [&](int64_t p) -> int64_t {
                     return p < npix ? (npix < (int64_t(1) << 31) ? int64_t(fdiv(uint32_t(p), fseg)) : p / pseg) : 0;
                 };
                 const int64_t s0 = seg_of(p0 + pp), s1 = seg_of(p0 + (U - 1) * ppw + pp);
-                bnf4 sc = ld4(scale + s0 * C + 4 * qq), sf = ld4(shift + s0 * C + 4 * qq);
+                bnf4 sc[NQ], sf[NQ];
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) {
+                    sc[k] = ld4(scl + s0 * cs + ch + 4 * k);
+                    sf[k] = ld4(shf + s0 * cs + ch + 4 * k);
+                }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     if (s1 != s0) {
-                        const int64_t so = seg_of(p0 + u * ppw + pp) * C + 4 * qq;
-                        sc = ld4(scale + so);
-                        sf = ld4(shift + so);
+                        const int64_t so = seg_of(p0 + u * ppw + pp) * cs + ch;
+#pragma unroll
+                        for (int k = 0; k < NQ; ++k) {
+                            sc[k] = ld4(scl + so + 4 * k);
+                            sf[k] = ld4(shf + so + 4 * k);
+                        }
                     }
-                    v[u] = bnf4{fmaxf(fmaf(v[u].x, sc.x, sf.x), 0.f), fmaxf(fmaf(v[u].y, sc.y, sf.y), 0.f),
-                                fmaxf(fmaf(v[u].z, sc.z, sf.z), 0.f), fmaxf(fmaf(v[u].w, sc.w, sf.w), 0.f)};
+#pragma unroll
+                    for (int k = 0; k < NQ; ++k) v[u].v[k] = bn_relu_f4(v[u].v[k], sc[k], sf[k]);
                 }
             }
 #pragma unroll
             for (int o = 0; o < 4; ++o) {
                 if (o < n_out) {
-                    const bnf4 wv = ld4(w + int64_t(o) * C + 4 * qq);
 #pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        s[u][o] = fmaf(v[u].x, wv.x, fmaf(v[u].y, wv.y, fmaf(v[u].z, wv.z, fmaf(v[u].w, wv.w, s[u][o]))));
+                    for (int k = 0; k < NQ; ++k) {
+                        const bnf4 wv = ld4(w + int64_t(o) * C + qq * CP + 4 * k);
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const bnf4 x4 = v[u].v[k];
+                            s[u][o] = fmaf(x4.x, wv.x, fmaf(x4.y, wv.y, fmaf(x4.z, wv.z, fmaf(x4.w, wv.w, s[u][o]))));
+                        }
+                    }
                 }
             }
         }
@@ -543,7 +627,7 @@ __global__ void pjaccard_bwd_kernel(const float *__restrict__ logits, const floa
 using namespace scd;
 
 // ------------------------------------------------------------------------------------------------
-extern "C" const char *scd_version(void) { return "libscd 0.6.0 (gfx950, ABI 6: bf16 activation storage, per-descriptor conv arithmetic)"; }
+extern "C" const char *scd_version(void) { return "libscd 0.7.0 (gfx950, ABI 7: fused plain / dual-task encoder levels and multi-source heads)"; }
 extern "C" const char *scd_last_error(void) { return g_err.c_str(); }
 
 extern "C" int scd_device_check(int device) {
@@ -731,21 +815,52 @@ extern "C" int scd_bn_relu_siamese_diff(scd_nhwc_t a, const float *scale, const 
 }
 
 namespace scd {
-static int conv1x1_fwd_run(const scd_nhwc_t &x, const float *scale, const float *shift, int nseg, const float *w,
-                           const float *b, int n_out, float *out, hipStream_t s) {
-    const int64_t npix = pixels(x);
+// One launch of the head kernel over one or two sources (b.data null: one).  16-byte bf16 pieces when every source
+// allows them (channels and row stride multiples of 8, 16-byte aligned data), else channel quads.
+static int conv1x1_fwd_run(const scd_nhwc_t &a, const float *sca, const float *sha, const scd_nhwc_t &b,
+                           const float *scb, const float *shb, int nseg, const float *w, const float *bias, int n_out,
+                           float *out, hipStream_t s) {
+    const int64_t npix = pixels(a);
+    const bool two = b.data != nullptr;
+    const int C = a.c + (two ? b.c : 0);
+    auto wide_ok = [](const scd_nhwc_t &v) { return is_bf16(v) && v.c % 8 == 0 && v.ldc % 8 == 0 && aligned16(v.data); };
+    const bool wide = wide_ok(a) && (!two || wide_ok(b));
+    const int CP = wide ? 8 : 4;
+    const int P = C / CP, pa = a.c / CP;
     int G = 1;
-    while (G < x.c / 4 && G < 64) G *= 2;
+    while (G < P && G < 64) G *= 2;
     constexpr int U = 4;
     const int64_t waves = (npix + (64 / G) * U - 1) / ((64 / G) * U);
     int blocks = int((waves + 3) / 4);
     if (blocks > 4096) blocks = 4096;
-    SCD_WITH_T(x.dtype, T,
-               hipLaunchKernelGGL((conv1x1_fwd_kernel<U, T>), dim3(blocks), dim3(256), 0, s, view_ptr<const T>(x),
-                                  x.ldc, x.c, x.h * x.w, npix, w, b, n_out, G, scale, shift, npix / nseg,
-                                  make_fastdiv(uint32_t(npix / nseg > 0 ? npix / nseg : 1)),
-                                  make_fastdiv(uint32_t(x.h * x.w > 0 ? x.h * x.w : 1)), out));
+    if (blocks < 1) blocks = 1;
+    const HeadSrc A{a.data, a.ldc, a.c, sca, sha};
+    const HeadSrc B{two ? b.data : a.data, two ? b.ldc : a.ldc, two ? b.c : a.c, two ? scb : sca, two ? shb : sha};
+    const FastDiv fseg = make_fastdiv(uint32_t(npix / nseg > 0 ? npix / nseg : 1));
+    const FastDiv fhw = make_fastdiv(uint32_t(a.h * a.w > 0 ? a.h * a.w : 1));
+    if (wide) {
+        hipLaunchKernelGGL((conv1x1_fwd_kernel<U, bf16_t, 8>), dim3(blocks), dim3(256), 0, s, A, B, pa, P, C, a.h * a.w,
+                           npix, w, bias, n_out, G, npix / nseg, fseg, fhw, out);
+    } else {
+        SCD_WITH_T(a.dtype, T,
+                   hipLaunchKernelGGL((conv1x1_fwd_kernel<U, T, 4>), dim3(blocks), dim3(256), 0, s, A, B, pa, P, C,
+                                      a.h * a.w, npix, w, bias, n_out, G, npix / nseg, fseg, fhw, out));
+    }
     return launch_status("scd_conv1x1_fwd");
+}
+
+template <int MODE>
+static int pool_out_run(const scd_nhwc_t &a, const float *scale, const float *shift, int nseg, const scd_nhwc_t &d,
+                        const scd_nhwc_t &o, const scd_nhwc_t &y, uint8_t *idx, int dt, hipStream_t s) {
+    const int units = MODE == 1 ? a.n : a.n / 2;
+    const int hy = a.h / 2, wy = a.w / 2;
+    const int64_t rows = int64_t(units) * hy;
+    SCD_WITH_T(dt, T,
+               hipLaunchKernelGGL((bn_relu_pool_out_kernel<MODE, T>), row_grid(wy * (a.c / 4), rows), dim3(256), 0, s,
+                                  view_ptr<const T>(a), a.h, a.w, a.ldc, view_ptr<T>(y), hy, wy, y.ldc, idx,
+                                  view_ptr<T>(d), d.ldc, view_ptr<T>(o), o.ldc, a.c, units, a.n / nseg, int(rows),
+                                  make_fastdiv(uint32_t(a.c / 4)), scale, shift));
+    return launch_status("scd_bn_relu_pool_out");
 }
 }  // namespace scd
 
@@ -757,7 +872,8 @@ extern "C" int scd_conv1x1_fwd(scd_nhwc_t x, const float *w, const float *b, int
         set_error("conv1x1_fwd: bad arguments (n_out in [1,4])");
         return SCD_ERR_ARG;
     }
-    return conv1x1_fwd_run(x, nullptr, nullptr, 1, w, b, n_out, out, as_stream(stream));
+    return conv1x1_fwd_run(x, nullptr, nullptr, scd_nhwc_t{}, nullptr, nullptr, 1, w, b, n_out, out,
+                           as_stream(stream));
 }
 
 extern "C" int scd_conv1x1_fwd_bn(scd_nhwc_t y, const float *scale, const float *shift, int32_t nseg, const float *w,
@@ -769,7 +885,27 @@ extern "C" int scd_conv1x1_fwd_bn(scd_nhwc_t y, const float *scale, const float 
         set_error("conv1x1_fwd_bn: bad arguments (n_out in [1,4], 16-byte aligned scale/shift, nseg | n)");
         return SCD_ERR_ARG;
     }
-    return conv1x1_fwd_run(y, scale, shift, nseg, w, b, n_out, out, as_stream(stream));
+    return conv1x1_fwd_run(y, scale, shift, scd_nhwc_t{}, nullptr, nullptr, nseg, w, b, n_out, out,
+                           as_stream(stream));
+}
+
+extern "C" int scd_conv1x1_fwd_bn2(scd_nhwc_t ya, const float *scale_a, const float *shift_a, scd_nhwc_t yb,
+                                   const float *scale_b, const float *shift_b, int32_t nseg, const float *w,
+                                   const float *b, int32_t n_out, float *out, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(ya, "conv1x1_bn2.ya"));
+    SCD_TRY(check_view(yb, "conv1x1_bn2.yb", true));
+    const bool bn = scale_a != nullptr;
+    if (!w || !out || n_out < 1 || n_out > 4 || nseg < 1 || ya.n % nseg ||
+        (bn && (!shift_a || !aligned16(scale_a) || !aligned16(shift_a))) ||
+        (yb.data && (yb.n != ya.n || yb.h != ya.h || yb.w != ya.w ||
+                     (bn != (scale_b != nullptr)) || (bn && (!shift_b || !aligned16(scale_b) || !aligned16(shift_b)))))) {
+        set_error("conv1x1_fwd_bn2: bad arguments (n_out in [1,4]; ya, yb of one (n, h, w); coefficients for both "
+                  "sources or neither, 16-byte aligned; nseg | n)");
+        return SCD_ERR_ARG;
+    }
+    if (common_dtype("conv1x1_fwd_bn2", {&ya, &yb}) < 0) return SCD_ERR_ARG;
+    return conv1x1_fwd_run(ya, scale_a, shift_a, yb, scale_b, shift_b, nseg, w, b, n_out, out, as_stream(stream));
 }
 
 extern "C" size_t scd_conv1x1_workspace_bytes(scd_nhwc_t x, int32_t n_out) {
@@ -890,23 +1026,35 @@ extern "C" int scd_pjaccard_bwd(const float *logits, const float *target, int64_
 extern "C" int scd_bn_relu_pool_diff(scd_nhwc_t a, const float *scale, const float *shift, scd_nhwc_t d,
                                      scd_nhwc_t y, uint8_t *idx, scd_stream_t stream) {
     clear_error();
-    SCD_TRY(check_view(a, "pool_diff.a"));
-    SCD_TRY(check_view(d, "pool_diff.d"));
     SCD_TRY(check_view(y, "pool_diff.y"));
-    if (a.n != 2 * d.n || a.h != d.h || a.w != d.w || a.c != d.c || (a.h & 1) || (a.w & 1) || a.h < 2 || a.w < 2 ||
-        y.n != a.n || y.c != a.c || y.h != a.h / 2 || y.w != a.w / 2 || !idx || (reinterpret_cast<uintptr_t>(idx) & 3) ||
-        !scale || !shift || !aligned16(scale) || !aligned16(shift)) {
-        set_error("bn_relu_pool_diff: a (2n, h, w, c) with even h, w; d (n, h, w, c); y (2n, h/2, w/2, c) with idx; "
-                  "aligned coefficients [2][c]");
+    return scd_bn_relu_pool_out(a, 2, scale, shift, 0, d, scd_nhwc_t{}, y, idx, stream);
+}
+
+extern "C" int scd_bn_relu_pool_out(scd_nhwc_t a, int32_t nseg, const float *scale, const float *shift, int32_t mode,
+                                    scd_nhwc_t d, scd_nhwc_t o, scd_nhwc_t y, uint8_t *idx, scd_stream_t stream) {
+    clear_error();
+    SCD_TRY(check_view(a, "pool_out.a"));
+    SCD_TRY(check_view(d, "pool_out.d", mode == 1));
+    SCD_TRY(check_view(o, "pool_out.o", mode == 0));
+    SCD_TRY(check_view(y, "pool_out.y", true));
+    const bool pair = mode != 1;
+    const int units = pair ? a.n / 2 : a.n;
+    bool ok = mode >= 0 && mode <= 2 && (a.h & 1) == 0 && (a.w & 1) == 0 && a.h >= 2 && a.w >= 2 && scale && shift &&
+              aligned16(scale) && aligned16(shift) && nseg >= 1 && a.n % nseg == 0 && (!pair || (nseg == 2 && a.n % 2 == 0));
+    if (ok && pair) ok = d.n == units && d.h == a.h && d.w == a.w && d.c == a.c;
+    if (ok && mode != 0) ok = o.n == a.n && o.h == a.h && o.w == a.w && o.c == a.c;
+    if (ok && y.data)
+        ok = y.n == a.n && y.c == a.c && y.h == a.h / 2 && y.w == a.w / 2 && idx && !(reinterpret_cast<uintptr_t>(idx) & 3);
+    if (!ok) {
+        set_error("bn_relu_pool_out: mode %d: a (n, h, w, c) with even h, w (pairs: 2 segments of n/2 images); d "
+                  "(n/2, h, w, c) for modes 0, 2; o (n, h, w, c) for modes 1, 2; y (n, h/2, w/2, c) with 4-byte aligned "
+                  "idx or null; aligned coefficients [nseg][c]", mode);
         return SCD_ERR_ARG;
     }
-    const int64_t rows = int64_t(d.n) * y.h;
-    const int dt = common_dtype("bn_relu_pool_diff", {&a, &d, &y});
+    const int dt = common_dtype("bn_relu_pool_out", {&a, &d, &o, &y});
     if (dt < 0) return SCD_ERR_ARG;
-    SCD_WITH_T(dt, T,
-               hipLaunchKernelGGL(bn_relu_pool_diff_kernel<T>, row_grid(y.w * (y.c / 4), rows), dim3(256), 0,
-                                  as_stream(stream), view_ptr<const T>(a), a.h, a.w, a.ldc, view_ptr<T>(y), y.h, y.w,
-                                  y.ldc, idx, view_ptr<T>(d), d.ldc, d.c, d.n, int(rows),
-                                  make_fastdiv(uint32_t(y.c / 4)), scale, shift));
-    return launch_status("scd_bn_relu_pool_diff");
+    hipStream_t s = as_stream(stream);
+    if (mode == 0) return pool_out_run<0>(a, scale, shift, nseg, d, o, y, idx, dt, s);
+    if (mode == 1) return pool_out_run<1>(a, scale, shift, nseg, d, o, y, idx, dt, s);
+    return pool_out_run<2>(a, scale, shift, nseg, d, o, y, idx, dt, s);
 }

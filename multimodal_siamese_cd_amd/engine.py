@@ -33,7 +33,8 @@ _F32 = torch.float32
 # Fusion switches (tools/ab_step.py flips them for in-process A/B; results are identical either way).
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
          'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True, 'defer_bn_bwd': True, 'fuse_head': True,
-         'convT_bias_in_wgrad': True, 'head_wgrad_in_bn_bwd': True}
+         'convT_bias_in_wgrad': True, 'head_wgrad_in_bn_bwd': True, 'fuse_plain_encoder': True,
+         'fuse_dualtask': True, 'dt_sem_batched': True, 'fuse_heads': True}
 
 
 def conv_math_for(cfg) -> str:
@@ -65,7 +66,16 @@ def set_options(**kw) -> dict:
     defer_bn_bwd: the input layer's BatchNorm backward stops at its statistics and the weight grad (its only
     reader) forms dy while staging, so that gradient is never written.
     fuse_head: a 1x1 head that is a decoder output's only reader runs inside the decoder stage (run_decoder head=),
-    reading the last BatchNorm + ReLU through its coefficients.  Returns the previous options."""
+    reading the last BatchNorm + ReLU through its coefficients.
+    fuse_plain_encoder: a plain (non-Siamese) encoder level writes its activation straight into the decoder's concat
+    buffer and pools it in the same pass (scd_bn_relu_pool_out mode 1): no bn_relu_apply, no skip copy.
+    fuse_dualtask: DualTaskSiameseUNet's encoder levels write the difference (decoder_change) and the [t2; t1] skip
+    batch (decoder_sem) in one pass (mode 2), the encoder backward forms both skip gradients on the fly.
+    dt_sem_batched: decoder_sem runs both dates as ONE 2B-image batch with per-date BatchNorm segments (t2 first)
+    instead of two calls (same per-call statistics and running-stat order; weight grads summed in another order).
+    fuse_heads: the two-decoder models' heads (DualStream's outc, WhateverNet(2)'s outc_stream1/2 + outc_fusion) run as
+    one launch over both decoders' last BatchNorm + ReLU (no cat, no materialised decoder outputs).
+    Returns the previous options."""
     prev = dict(_OPTS)
     for k, v in kw.items():
         if k not in _OPTS:
@@ -521,6 +531,7 @@ class _PooledGrad:
     idx: torch.Tensor | None
     gskip: torch.Tensor | None
     skip_mode: int
+    gskip2: torch.Tensor | None = None  # skip_mode 2: the dual-task semantic skip gradient, [t2; t1]
 
 
 @dataclass
@@ -549,6 +560,10 @@ def _bn_backward(y, g, st: _BNSaved, bn, conv_bias_grad: bool, tiles=None, dy_bo
             ws = _ws(hip.bn_head_workspace_bytes(n, h, w, c, st.nseg, g.n_out), y)
         hip.bn_relu_backward_head(nhwc(y), g.g, g.w2, g.n_out, st.nseg, st.smean, st.sinv, bn.weight, st.scale,
                                   st.shift, dgamma, dbeta, dbias, nhwc(dy), ws, dy_bound, g.w_grad)
+    elif isinstance(g, _PooledGrad) and g.gskip2 is not None:
+        hip.bn_relu_backward_pooled2(nhwc(y), nhwc(g.gy) if g.gy is not None else hip._NULL, g.idx, nhwc(g.gskip),
+                                     g.skip_mode, nhwc(g.gskip2), st.nseg, st.smean, st.sinv, bn.weight, st.scale,
+                                     st.shift, dgamma, dbeta, dbias, nhwc(dy), ws, dy_bound)
     elif isinstance(g, _PooledGrad):
         hip.bn_relu_backward_pooled(nhwc(y), nhwc(g.gy) if g.gy is not None else hip._NULL, g.idx,
                                     nhwc(g.gskip) if g.gskip is not None else hip._NULL, g.skip_mode, st.nseg,
@@ -601,17 +616,23 @@ def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Te
     return ga0, None, gb
 
 
-def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None):
+def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None, dy1_given: bool = False):
     """g_out: gradient of the block output (a tensor, or a _PooledGrad formed inside the BatchNorm backward).
     Returns (grad wrt DoubleConv input or None, [8 param grads in dc_params order]).  `pool` (h2): bounds of the
-    two BatchNorm-backward outputs, the operands of the data-grad and weight-grad convs."""
+    two BatchNorm-backward outputs, the operands of the data-grad and weight-grad convs.
+    dy1_given: g_out is already the gradient of the second conv's output y1 (its BatchNorm backward ran in the heads'
+    backward, HeadsFn); that BatchNorm's and conv bias's gradients are then None here."""
     x, y0, a0, st0, y1, st1, x_bound, b0 = saved
     s = dc.conv
     conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
     if st1.smean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported (call net.train())")
-    d1 = _take(pool)
-    dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None, dy_bound=d1)
+    if dy1_given:
+        dy1, dg1, db1, dbias1 = g_out, None, None, None
+        d1 = _bound_of(dy1, pool)
+    else:
+        d1 = _take(pool)
+        dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None, dy_bound=d1)
     if a0 is None:  # fused forward: the weight grad reads y0 through BN0 + ReLU as well
         gw1 = _wgrad3x3(dy1, y0, conv1.weight, (st0.scale, st0.shift, st0.nseg), d1, b0)
     else:
@@ -734,25 +755,55 @@ def _level_grad(g_pool, idx, g_skip, skip_mode: int, like: torch.Tensor):
     return ga
 
 
+def _even(h: int, w: int) -> bool:
+    return h % 2 == 0 and w % 2 == 0 and h >= 2 and w >= 2
+
+
+def _plain_level_out(y1, st1: _BNSaved, a, nxt, idx):
+    """a = relu(BN1(y1)) (a may be the skip slice of a decoder concat buffer) and, if nxt is given, MaxPool2d(a) into
+    nxt / idx: one pass over y1 for even maps (scd_bn_relu_pool_out mode 1), else apply + pool (bit-identical)."""
+    _, h, w, _ = y1.shape
+    if _even(h, w):
+        hip.bn_relu_pool_out(nhwc(y1), st1.nseg, st1.scale, st1.shift, hip.POOL_COPY, hip._NULL, nhwc(a),
+                             nhwc(nxt) if nxt is not None else hip._NULL, idx)
+        return
+    hip.bn_relu_apply(nhwc(y1), st1.nseg, st1.scale, st1.shift, nhwc(a))
+    if nxt is not None:
+        hip.maxpool2_fwd(nhwc(a), nhwc(nxt), idx)
+
+
 class EncoderLevelFn(torch.autograd.Function):
     """One level of InConv + Encoder (networks.py:313-343, 405-426) on one BatchNorm-segmented batch: the level's
-    DoubleConv output activation a (materialised: it is a decoder skip) and, below the deepest level, the next level's
-    input MaxPool2d(a) with its argmax bytes.  meta.x_bound (h2) bounds the input; meta.out_bound receives a's."""
+    DoubleConv output activation a (a decoder skip) and, below the deepest level, the next level's input MaxPool2d(a)
+    with its argmax bytes.  meta.x_bound (h2) bounds the input; meta.out_bound receives a's.
+    With the engine option fuse_plain_encoder, a is written by one pass over the conv output that also pools it, into
+    channels [0, C) of the decoder's concat buffer when meta.extra names the Up's ConvT channels (zero-copy cat,
+    networks.py:449; meta.buf is then that buffer)."""
 
     @staticmethod
     def forward(ctx, x, meta, *params):
         ctx.set_materialize_grads(False)
         meta.scope = (hip.conv_math(), hip.conv_tune())
-        a, sv, _, _, bound = _dc_forward(x, meta.dc, meta.nseg, meta.training, meta.save, pool=meta.pool,
-                                         x_bound=meta.x_bound)
+        fused = _OPTS['fuse_plain_encoder']
+        a, sv, y1, st1, bound = _dc_forward(x, meta.dc, meta.nseg, meta.training, meta.save, materialize=not fused,
+                                            pool=meta.pool, x_bound=meta.x_bound)
         meta.out_bound = bound
-        outs, idx = (a,), None
+        meta.buf = None
+        n, h, w, c = y1.shape
+        extra = getattr(meta, 'extra', 0)
+        idx = nxt = None
         if not meta.last:
-            n, h, w, c = a.shape
-            nxt = _act((n, h // 2, w // 2, c), a)
-            idx = _empty((n, h // 2, w // 2, c), a, dtype=torch.uint8)
-            hip.maxpool2_fwd(nhwc(a), nhwc(nxt), idx)  # the pooled map keeps the level's bound
-            outs = (a, nxt)
+            nxt = _act((n, h // 2, w // 2, c), y1)
+            idx = _empty((n, h // 2, w // 2, c), y1, dtype=torch.uint8)
+        if fused:
+            buf = _act((n, h, w, c + extra), y1)
+            a = buf[..., :c] if extra else buf
+            _plain_level_out(y1, st1, a, nxt, idx)  # the pooled map keeps the level's bound
+            _set_bound(a, bound)
+            meta.buf = buf if extra else None
+        elif nxt is not None:
+            hip.maxpool2_fwd(nhwc(a), nhwc(nxt), idx)
+        outs = (a,) if nxt is None else (a, nxt)
         if meta.save:
             ctx.meta, ctx.saved = meta, (sv, idx)
         return outs
@@ -768,25 +819,121 @@ class EncoderLevelFn(torch.autograd.Function):
         return (gx, None, *pg)
 
 
-def run_encoder(inc, encoder, x: torch.Tensor, nseg: int, training: bool) -> list:
-    """InConv + Encoder: the level activations, level 0 first (Encoder.forward returns them reversed)."""
+def run_encoder(inc, encoder, x: torch.Tensor, nseg: int, training: bool, extra: dict | None = None,
+                with_buffers: bool = False):
+    """InConv + Encoder: the level activations, level 0 first (Encoder.forward returns them reversed).
+    `extra` {level: ConvT channels} (decoder_cat_channels, engine option fuse_plain_encoder): each such level writes its
+    activation into a decoder concat buffer; with_buffers=True returns (activations, buffers or None per level)."""
     blocks = encoder_blocks(inc, encoder)
+    extra = extra if _OPTS['fuse_plain_encoder'] else None
+    extra = extra or {}
     pool, bound = _bounds(x), None
-    feats, cur = [], x
+    feats, bufs, cur = [], [], x
     try:
         for level, dc in enumerate(blocks):
             params = dc_params(dc)
             save = torch.is_grad_enabled() and (cur.requires_grad or any(p.requires_grad for p in params))
             meta = _Meta(dc=dc, nseg=nseg, training=training, save=save, last=level == len(blocks) - 1, pool=pool,
-                         x_bound=bound)
+                         x_bound=bound, extra=extra.get(level, 0))
             outs = EncoderLevelFn.apply(cur, meta, *params)
             feats.append(outs[0])
+            bufs.append(meta.buf)
             bound = meta.out_bound
             if not meta.last:
                 cur = outs[1]
     finally:
         flush_bn_counters()
-    return feats
+    return (feats, bufs) if with_buffers else feats
+
+
+# ------------------------------------------------------------------------------------------------
+# Dual-task Siamese encoder (DualTaskSiameseUNet, networks.py:176-197): every level activation of both dates feeds the
+# difference (decoder_change) and, as itself, decoder_sem; both are written by one pass into the two decoders' concat
+# buffers, and the backward forms maxpool_bwd(g_pool) -/+ g_diff + g_sem inside the level's BatchNorm backward.
+# ------------------------------------------------------------------------------------------------
+class DualTaskLevelFn(torch.autograd.Function):
+    """One encoder level of DualTaskSiameseUNet on the [t1; t2] pair batch: the difference d = a_t2 - a_t1 (B images,
+    decoder_change's skip or deepest input), the semantic batch o = [a_t2; a_t1] (2B images, decoder_sem's: t2 first,
+    as the reference calls decoder_sem(features_t2) first) and, below the deepest level, the next level's pooled input.
+    The activation itself is never written outside those (scd_bn_relu_pool_out mode 2).  meta.extra_c / extra_s: the
+    ConvT channels of the two decoders' Ups taking this level (zero-copy cat; meta.bufc / bufs the buffers)."""
+
+    @staticmethod
+    def forward(ctx, x, meta, *params):
+        ctx.set_materialize_grads(False)
+        meta.scope = (hip.conv_math(), hip.conv_tune())
+        _, sv, y1, st1, bound = _dc_forward(x, meta.dc, 2, meta.training, meta.save, materialize=False,
+                                            pool=meta.pool, x_bound=meta.x_bound)
+        meta.out_bound = bound
+        n2, h, w, c = y1.shape
+        b = n2 // 2
+        bufc = _act((b, h, w, c + meta.extra_c), y1)
+        bufs = _act((n2, h, w, c + meta.extra_s), y1)
+        d = bufc[..., :c] if meta.extra_c else bufc
+        o = bufs[..., :c] if meta.extra_s else bufs
+        sc, sh = _two_seg(st1)
+        idx = nxt = None
+        if not meta.last:
+            nxt = _act((n2, h // 2, w // 2, c), y1)
+            idx = _empty((n2, h // 2, w // 2, c), y1, dtype=torch.uint8)
+        if _even(h, w):
+            hip.bn_relu_pool_out(nhwc(y1), 2, sc, sh, hip.POOL_DIFF_COPY, nhwc(d), nhwc(o),
+                                 nhwc(nxt) if nxt is not None else hip._NULL, idx)
+        else:  # odd maps (e.g. evaluation on odd tiles): materialise, then the difference, the copies and the pooling
+            a = _act(tuple(y1.shape), y1)
+            hip.bn_relu_apply(nhwc(y1), 2, sc, sh, nhwc(a))
+            hip.siamese_diff(nhwc(a), nhwc(d))
+            hip.feature_grad(hip._NULL, None, nhwc(a[b:]), 0, nhwc(o[:b]))
+            hip.feature_grad(hip._NULL, None, nhwc(a[:b]), 0, nhwc(o[b:]))
+            if nxt is not None:
+                hip.maxpool2_fwd(nhwc(a), nhwc(nxt), idx)
+        _set_bound(d, bound)  # |a_t2 - a_t1| <= max(a_t1, a_t2) for ReLU outputs
+        _set_bound(o, bound)
+        meta.bufc = bufc if meta.extra_c else None
+        meta.bufs = bufs if meta.extra_s else None
+        if meta.save:
+            ctx.meta, ctx.saved = meta, (sv, idx, b)
+        return (d, o) if nxt is None else (d, o, nxt)
+
+    @staticmethod
+    def backward(ctx, g_d, g_o, g_next=None):
+        meta = ctx.meta
+        with hip.conv_scope(*meta.scope):
+            sv, idx, b = ctx.saved
+            y1 = sv[4]
+            if g_o is None:  # the semantic branch took no gradient: the Siamese level's backward
+                ga = _level_grad(g_next, idx, g_d, 1, y1)
+            else:
+                if g_d is None:
+                    g_d = torch.zeros((b,) + tuple(y1.shape[1:]), device=y1.device, dtype=y1.dtype)
+                ga = _PooledGrad(g_next, idx if g_next is not None else None, g_d, 2, g_o)
+            gx, pg = _dc_backward(ga, sv, meta.dc, need_dx=ctx.needs_input_grad[0], pool=_bounds(y1))
+        ctx.saved = None
+        return (gx, None, *pg)
+
+
+def run_dualtask_encoder(inc, encoder, x: torch.Tensor, training: bool, extra_c: dict, extra_s: dict):
+    """Per level (level 0 first): (difference, semantic [t2; t1] batch, decoder_change buffer, decoder_sem buffer)."""
+    blocks = encoder_blocks(inc, encoder)
+    pool, bound = _bounds(x), None
+    diffs, sems, bufc, bufs, cur = [], [], [], [], x
+    try:
+        for level, dc in enumerate(blocks):
+            params = dc_params(dc)
+            save = torch.is_grad_enabled() and (cur.requires_grad or any(p.requires_grad for p in params))
+            meta = _Meta(dc=dc, training=training, save=save, last=level == len(blocks) - 1, pool=pool,
+                         x_bound=bound, extra_c=extra_c.get(level, 0), extra_s=extra_s.get(level, 0))
+            outs = DualTaskLevelFn.apply(cur, meta, *params)
+            diffs.append(outs[0])
+            sems.append(outs[1])
+            bufc.append(meta.bufc)
+            bufs.append(meta.bufs)
+            bound = meta.out_bound
+            if not meta.last:
+                cur = outs[2]
+    finally:
+        flush_bn_counters()
+    return diffs, sems, bufc, bufs
 
 
 # ------------------------------------------------------------------------------------------------
@@ -949,10 +1096,16 @@ class DecoderFn(torch.autograd.Function):
                                store_mode=1, src_bound=cur_bound, dst_bound=epi_bound)
             if cat_bound is not None and epi_bound is None:
                 hip.absmax_bound(nhwc(cat, cs, cto), cat_bound)
-            a, sv, y1, st1, _ = _dc_forward(cat, up.conv, 1, meta.training, meta.save, materialize=not last_into_head,
-                                            pool=pool, x_bound=cat_bound)
+            last_raw = meta.raw and k == len(ups) - 1
+            a, sv, y1, st1, _ = _dc_forward(cat, up.conv, meta.nseg, meta.training, meta.save,
+                                            materialize=not (last_into_head or last_raw), pool=pool, x_bound=cat_bound)
             saved.append((cur, cat, cs, sv, cur_bound))
             cur = a
+            if last_raw:
+                # the decoder's last conv output y1 itself: its BatchNorm + ReLU are read by the heads (HeadsFn), which
+                # also run that BatchNorm's backward; meta.raw_state carries the coefficients to them
+                cur = y1
+                meta.raw_state = (st1, up.conv)
             if last_into_head:
                 # OutConv (networks.py:457) reading relu(BN1(y1)) through the coefficients: the decoder's output
                 # activation is never written
@@ -1003,7 +1156,7 @@ class DecoderFn(torch.autograd.Function):
         for k in range(n - 1, -1, -1):
             up = ups[k]
             cur, cat, cs, sv, cur_bound = saved[k]
-            g_cat, pg = _dc_backward(g, sv, up.conv, need_dx=True, pool=pool)
+            g_cat, pg = _dc_backward(g, sv, up.conv, need_dx=True, pool=pool, dy1_given=meta.raw and k == n - 1)
             g_skips[k] = g_cat[..., :cs]
             convT = up.up
             cto = convT.out_channels
@@ -1051,32 +1204,161 @@ def decoder_cat_channels(decoder, n_levels: int) -> dict:
     return {n_levels - 2 - k: up.up.out_channels for k, up in enumerate(ups)}
 
 
-def run_decoder(decoder, features: list, training: bool, cat_buffers: list | None = None, head=None) -> torch.Tensor:
+def run_decoder(decoder, features: list, training: bool, cat_buffers: list | None = None, head=None, nseg: int = 1):
     """`features` in the reference's order: [deepest, ..., level 0] (Encoder.forward's reversed list).
     `cat_buffers`: per Up (same order as decoder.up_seq), the concat buffer its skip already lives in, or None.
     `head` (an OutConv that is the decoder output's only reader): returns the head's logits (NCHW) instead, with
     the head reading the last BatchNorm + ReLU through its coefficients (scd_conv1x1_fwd_bn) and its backward
     feeding that BatchNorm's backward directly (scd_bn_relu_backward_head); results are bit-identical to
-    run_head(head, run_decoder(...))."""
-    return run_ups(list(decoder.up_seq.values()), features, training, cat_buffers, head)
+    run_head(head, run_decoder(...)).  head='raw': returns a RawDecoderOut for run_heads (several heads, or a head over
+    two decoders).  nseg: BatchNorm segments of the batch (decoder_sem's [t2; t1] batch: 2)."""
+    return run_ups(list(decoder.up_seq.values()), features, training, cat_buffers, head, nseg)
 
 
-def run_ups(ups: list, features: list, training: bool, cat_buffers: list | None = None, head=None) -> torch.Tensor:
+@dataclass
+class RawDecoderOut:
+    """A decoder's output left unmaterialised for run_heads: its last conv output y (NHWC, the autograd output of the
+    decoder stage), the BatchNorm coefficients / statistics the heads read it through, and that DoubleConv."""
+    y: torch.Tensor
+    st: '_BNSaved'
+    dc: object
+
+
+def run_ups(ups: list, features: list, training: bool, cat_buffers: list | None = None, head=None, nseg: int = 1):
     """Up blocks in sequence (Decoder.forward, networks.py:375-382): features[0] is the deepest map, features[1 + k]
     the skip of ups[k]."""
+    raw = isinstance(head, str) and head == 'raw'
+    if raw:
+        head = None
     if head is not None and (not _OPTS['fuse_head'] or head.conv.out_channels > 4):
-        return run_head(head, run_ups(ups, features, training, cat_buffers))
+        return run_head(head, run_ups(ups, features, training, cat_buffers, nseg=nseg))
     params = [p for up in ups for p in up_params(up)]
     if head is not None:
         params += [head.conv.weight, head.conv.bias]
         if head.conv.bias is None:
             raise ValueError("run_decoder: the fused head expects OutConv's bias (networks.py:457)")
     save = torch.is_grad_enabled() and (any(p.requires_grad for p in params) or any(f.requires_grad for f in features))
-    meta = _Meta(ups=ups, training=training, save=save, cat_buffers=cat_buffers, head=head)
+    meta = _Meta(ups=ups, training=training, save=save, cat_buffers=cat_buffers, head=head, raw=raw, nseg=nseg,
+                 raw_state=None)
     try:
-        return DecoderFn.apply(meta, features[0], *features[1:1 + len(ups)], *params)
+        out = DecoderFn.apply(meta, features[0], *features[1:1 + len(ups)], *params)
     finally:
         flush_bn_counters()
+    if raw:
+        st, dc = meta.raw_state
+        return RawDecoderOut(out, st, dc)
+    return out
+
+
+class HeadsFn(torch.autograd.Function):
+    """OutConv heads (networks.py:454-461) over one or two decoder outputs, each read through its last BatchNorm + ReLU
+    (networks.py:380-381): DualStreamUNet's outc over cat(x_stream1, x_stream2) (networks.py:117-120) and WhateverNet /
+    WhateverNet2's outc_stream1, outc_stream2 and outc_fusion (networks.py:241-263, 288-310) in ONE launch
+    (scd_conv1x1_fwd_bn2): each decoder output is read once for all heads, and neither it nor the cat is written.
+    Output: [n, K, h, w], the heads' logits stacked along channels (K = their output channels, <= 4).
+    Backward: per source, that BatchNorm's backward with dL/da = sum_k g_k w_k[source] formed on the fly and the heads'
+    weight grads from the same pass (scd_bn_relu_backward_head over the stacked [K][C_s] weights); it returns dL/dy
+    of the source to its decoder stage (DecoderFn raw mode) plus the BatchNorm's and conv bias's gradients."""
+
+    @staticmethod
+    def forward(ctx, meta, *args):
+        srcs, heads = meta.srcs, meta.heads
+        ns = len(srcs)
+        ys = args[:ns]
+        hp = args[4 * ns:]
+        y0 = ys[0]
+        n, h, w, _ = y0.shape
+        cs = [y.shape[3] for y in ys]
+        offs = [sum(cs[:i]) for i in range(ns)]
+        ctot = sum(cs)
+        K = sum(hp[2 * j].shape[0] for j in range(len(heads)))
+        wall = torch.zeros((K, ctot), device=y0.device, dtype=_F32)
+        ball = torch.zeros((K,), device=y0.device, dtype=_F32)
+        rows, k0 = [], 0
+        with torch.no_grad():
+            for j, sel in enumerate(heads):
+                wt, bt = hp[2 * j], hp[2 * j + 1]
+                no = wt.shape[0]
+                w2 = wt.detach().reshape(no, -1)
+                col = 0
+                for si in sel:  # the head's input channels: its sources concatenated in the listed order
+                    wall[k0:k0 + no, offs[si]:offs[si] + cs[si]] = w2[:, col:col + cs[si]]
+                    col += cs[si]
+                if col != w2.shape[1]:
+                    raise ValueError(f"head {j}: weight takes {w2.shape[1]} channels, its sources give {col}")
+                if bt is not None:
+                    ball[k0:k0 + no] = bt.detach()
+                rows.append((k0, no, tuple(sel), tuple(wt.shape), bt is not None))
+                k0 += no
+        out = _empty((n, K, h, w), y0)
+        sa, sb = srcs[0].st, srcs[1].st if ns > 1 else None
+        hip.conv1x1_fwd_bn2(nhwc(ys[0]), sa.scale, sa.shift, nhwc(ys[1]) if ns > 1 else hip._NULL,
+                            sb.scale if sb else None, sb.shift if sb else None, sa.nseg, wall, ball, K, out)
+        ctx.meta = meta
+        ctx.state = (ys, wall, rows, offs, cs, K)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        meta = ctx.meta
+        ys, wall, rows, offs, cs, K = ctx.state
+        ctx.state = None
+        ns = len(meta.srcs)
+        if g is None:
+            return (None,) * (1 + 4 * ns + 2 * len(rows))
+        g = g.contiguous()
+        pool = _bounds(ys[0])
+        dys, bn_grads, wgs = [], [], []
+        for i, (y, src) in enumerate(zip(ys, meta.srcs)):
+            st, dc = src.st, src.dc
+            if st.smean is None:
+                raise RuntimeError("backward through an eval-mode BatchNorm is not supported (call net.train())")
+            bn, conv = dc.conv[4], dc.conv[3]
+            n, h, w, c = y.shape
+            ws_ = wall[:, offs[i]:offs[i] + cs[i]].contiguous()
+            dy = torch.empty_like(y)
+            dgamma, dbeta = _empty((c,), y), _empty((c,), y)
+            dbias = _empty((c,), y) if conv.bias is not None else None
+            wg = _empty((K, c), y)
+            db = _take(pool)
+            ws = _ws(hip.bn_head_workspace_bytes(n, h, w, c, st.nseg, K), y)
+            hip.bn_relu_backward_head(nhwc(y), g, ws_, K, st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift,
+                                      dgamma, dbeta, dbias, nhwc(dy), ws, db, wg)
+            dys.append(_set_bound(dy, db))
+            bn_grads += [dgamma, dbeta, dbias]
+            wgs.append(wg)
+        y0, st0 = ys[0], meta.srcs[0].st
+        gb = _empty((K,), y0)
+        ws = _ws(hip.conv1x1_workspace_bytes(nhwc(y0), K), y0)
+        hip.conv1x1_bwd_bn(nhwc(y0), st0.scale, st0.shift, st0.nseg, wall[:, :cs[0]].contiguous(), g, K, None, gb, ws)
+        head_grads = []
+        for k0, no, sel, wshape, has_b in rows:
+            gw = torch.cat([wgs[si][k0:k0 + no] for si in sel], dim=1).reshape(wshape)
+            head_grads += [gw, gb[k0:k0 + no].clone() if has_b else None]
+        return (None, *dys, *bn_grads, *head_grads)
+
+
+def run_heads(sources: list, heads: list) -> list:
+    """heads: [(OutConv, (source indices in its input's channel order))] over `sources` (RawDecoderOut of run_decoder
+    head='raw'); returns each head's NCHW logits (channel slices of one stacked output).  Takes <= 2 sources of one
+    (n, h, w) and BatchNorm segment count and <= 4 output channels over all heads, each with its bias (OutConv's)."""
+    y0 = sources[0].y
+    if not 1 <= len(sources) <= 2 or any(s.y.shape[:3] != y0.shape[:3] or s.st.nseg != sources[0].st.nseg
+                                         or s.y.shape[3] % 4 for s in sources):
+        raise ValueError("run_heads: 1-2 decoder outputs of one (n, h, w) and segment count, channels in multiples of 4")
+    if sum(o.conv.out_channels for o, _ in heads) > 4 or any(o.conv.bias is None for o, _ in heads):
+        raise ValueError("run_heads: at most 4 output channels over all heads, each head with a bias")
+    params = [p for s in sources for p in (s.dc.conv[4].weight, s.dc.conv[4].bias, s.dc.conv[3].bias)]
+    for outc, _ in heads:
+        params += [outc.conv.weight, outc.conv.bias]
+    meta = _Meta(srcs=sources, heads=[tuple(sel) for _, sel in heads])
+    out = HeadsFn.apply(meta, *[s.y for s in sources], *params)
+    res, k0 = [], 0
+    for outc, _ in heads:
+        no = outc.conv.out_channels
+        res.append(out[:, k0:k0 + no])
+        k0 += no
+    return res
 
 
 # ------------------------------------------------------------------------------------------------

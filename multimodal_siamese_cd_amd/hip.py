@@ -151,6 +151,9 @@ _SIGS = {
     "scd_bn_relu_backward_pooled": ([NHWC, NHWC, c_void_p, NHWC, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p,
                                      c_size_t, c_void_p], c_int),
+    "scd_bn_relu_backward_pooled2": ([NHWC, NHWC, c_void_p, NHWC, c_int32, NHWC, c_int32, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p,
+                                      c_size_t, c_void_p], c_int),
     "scd_bn_head_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32, c_int32], c_size_t),
     "scd_bn_relu_backward_head": ([NHWC, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_void_p,
@@ -170,10 +173,13 @@ _SIGS = {
     "scd_bn_relu_maxpool2_fwd": ([NHWC, c_int32, c_void_p, c_void_p, NHWC, c_void_p, c_void_p], c_int),
     "scd_bn_relu_siamese_diff": ([NHWC, c_void_p, c_void_p, NHWC, c_void_p], c_int),
     "scd_bn_relu_pool_diff": ([NHWC, c_void_p, c_void_p, NHWC, NHWC, c_void_p, c_void_p], c_int),
+    "scd_bn_relu_pool_out": ([NHWC, c_int32, c_void_p, c_void_p, c_int32, NHWC, NHWC, NHWC, c_void_p, c_void_p], c_int),
     "scd_feature_grad": ([NHWC, c_void_p, NHWC, c_int32, NHWC, c_int32, c_void_p], c_int),
     "scd_siamese_diff": ([NHWC, NHWC, c_void_p], c_int),
     "scd_conv1x1_fwd": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p], c_int),
     "scd_conv1x1_fwd_bn": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p], c_int),
+    "scd_conv1x1_fwd_bn2": ([NHWC, c_void_p, c_void_p, NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32,
+                             c_void_p, c_void_p], c_int),
     "scd_conv1x1_bwd_bn": ([NHWC, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
                             c_void_p, c_size_t, c_void_p], c_int),
     "scd_conv1x1_workspace_bytes": ([NHWC, c_int32], c_size_t),
@@ -200,7 +206,7 @@ _SIGS = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
-ABI_VERSION = 6  # SCD_ABI_VERSION of include/scd.h
+ABI_VERSION = 7  # SCD_ABI_VERSION of include/scd.h
 
 
 def load_library(path: str = LIB_PATH):
@@ -739,6 +745,18 @@ def bn_relu_backward_pooled(y: NHWC, gy: NHWC, idx, gskip: NHWC, skip_mode: int,
         "scd_bn_relu_backward_pooled")
 
 
+def bn_relu_backward_pooled2(y: NHWC, gy: NHWC, idx, gskip: NHWC, skip_mode: int, gskip2: NHWC, nseg, smean, sinv,
+                             gamma, scale, shift, dgamma, dbeta, dbias, dy: NHWC, ws, dy_bound=None):
+    """bn_relu_backward_pooled with the dual-task second skip gradient (skip_mode 2: gskip2 = the semantic decoder's
+    [t2; t1] skip gradient, added to the -/+ difference gradient before the pooled term)."""
+    _check(
+        lib().scd_bn_relu_backward_pooled2(y, gy, _ptr(idx), gskip, skip_mode, gskip2, nseg, smean.data_ptr(),
+                                           sinv.data_ptr(), _ptr(gamma), scale.data_ptr(), shift.data_ptr(),
+                                           _ptr(dgamma), _ptr(dbeta), _ptr(dbias), dy, _ptr(dy_bound), ws.data_ptr(),
+                                           ws.numel(), _stream()),
+        "scd_bn_relu_backward_pooled2")
+
+
 def bn_head_workspace_bytes(n, h, w, c, nseg, n_out) -> int:
     return lib().scd_bn_head_workspace_bytes(n, h, w, c, nseg, n_out)
 
@@ -806,6 +824,16 @@ def bn_relu_pool_diff(a: NHWC, scale, shift, d: NHWC, y: NHWC, idx: torch.Tensor
            "scd_bn_relu_pool_diff")
 
 
+POOL_DIFF, POOL_COPY, POOL_DIFF_COPY = 0, 1, 2  # scd_bn_relu_pool_out modes
+
+
+def bn_relu_pool_out(a: NHWC, nseg: int, scale, shift, mode: int, d: NHWC, o: NHWC, y: NHWC, idx):
+    """One pass over an encoder level's conv output a (even h, w): mode 0 the Siamese difference d, 1 the activation
+    into o (a concat-buffer slice), 2 both with o = [a_t2; a_t1]; plus MaxPool2d(2) into y / idx unless y is _NULL."""
+    _check(lib().scd_bn_relu_pool_out(a, nseg, scale.data_ptr(), shift.data_ptr(), mode, d, o, y, _ptr(idx),
+                                      _stream()), "scd_bn_relu_pool_out")
+
+
 def feature_grad(gy: NHWC, idx, gskip: NHWC, skip_mode: int, gx: NHWC, accumulate: bool = False):
     _check(lib().scd_feature_grad(gy, _ptr(idx), gskip, skip_mode, gx, int(accumulate), _stream()), "scd_feature_grad")
 
@@ -822,6 +850,13 @@ def conv1x1_fwd_bn(y: NHWC, scale, shift, nseg, w, b, n_out, out: torch.Tensor):
     """conv1x1_fwd of relu(fma(y, scale, shift)) (the head reading its input through the last BatchNorm + ReLU)."""
     _check(lib().scd_conv1x1_fwd_bn(y, scale.data_ptr(), shift.data_ptr(), nseg, w.data_ptr(), _ptr(b), n_out,
                                     out.data_ptr(), _stream()), "scd_conv1x1_fwd_bn")
+
+
+def conv1x1_fwd_bn2(ya: NHWC, sa, ha, yb: NHWC, sb, hb, nseg, w, b, n_out, out: torch.Tensor):
+    """The heads over cat([relu(bn_a(ya)), relu(bn_b(yb))]) without the cat (w [n_out][ya.c + yb.c]); coefficients for
+    both sources or for neither (sa = None: the sources are plain activations)."""
+    _check(lib().scd_conv1x1_fwd_bn2(ya, _ptr(sa), _ptr(ha), yb, _ptr(sb), _ptr(hb), nseg, w.data_ptr(), _ptr(b), n_out,
+                                     out.data_ptr(), _stream()), "scd_conv1x1_fwd_bn2")
 
 
 def conv1x1_bwd_bn(y: NHWC, scale, shift, nseg, w, gout, n_out, gw, gb, ws):

@@ -231,21 +231,38 @@ class _HipNet(nn.Module):
         return tw, self._twin_maps
 
 
+def _ups_buffers(bufs, decoder, n_levels):
+    """Per Up of `decoder` (up_seq order), the concat buffer the encoder wrote its skip into (or None)."""
+    return [bufs[n_levels - 2 - k] for k in range(len(decoder.up_seq))]
+
+
 def _stream(inc, encoder, decoder, x, nseg, training, siamese, head=None):
     """inc + encoder (+ Siamese diff) + decoder of one stream; returns (decoder output, features).  With `head` (the
-    OutConv that is the decoder output's only reader) the first item is the head's logits (engine.run_decoder)."""
+    OutConv that is the decoder output's only reader) the first item is the head's logits (engine.run_decoder); with
+    head='raw' it is the decoder's unmaterialised output for engine.run_heads."""
+    n_levels = len(encoder.down_seq) + 1
     if siamese and engine.option('fuse_siamese_encoder'):  # networks.py:141-150, fused (engine.SiameseLevelFn)
-        n_levels = len(encoder.down_seq) + 1
         diffs, bufs = engine.run_siamese_encoder(inc, encoder, x, training,
                                                  engine.decoder_cat_channels(decoder, n_levels))
         feats = diffs[::-1]  # Encoder.forward returns the reversed list (networks.py:342)
-        ups_bufs = [bufs[n_levels - 2 - k] for k in range(len(decoder.up_seq))]
-        return engine.run_decoder(decoder, feats, training, ups_bufs, head=head), feats
+        return engine.run_decoder(decoder, feats, training, _ups_buffers(bufs, decoder, n_levels), head=head), feats
+    if not siamese and engine.option('fuse_plain_encoder'):  # each level's skip written into its concat buffer
+        feats, bufs = engine.run_encoder(inc, encoder, x, nseg, training,
+                                         engine.decoder_cat_channels(decoder, n_levels), with_buffers=True)
+        feats = feats[::-1]
+        return engine.run_decoder(decoder, feats, training, _ups_buffers(bufs, decoder, n_levels), head=head), feats
     feats = engine.run_encoder(inc, encoder, x, nseg, training)
     if siamese:
         feats = [engine.siamese_diff(f) for f in feats]
     feats = feats[::-1]
     return engine.run_decoder(decoder, feats, training, head=head), feats
+
+
+def _fused_heads(cfg, heads) -> bool:
+    """Whether a two-decoder model runs its heads as one engine.run_heads launch (engine option fuse_heads; at most 4
+    output channels over all its heads, e.g. OUT_CHANNELS 1 for WhateverNet's three heads)."""
+    return (engine.option('fuse_heads') and sum(o.conv.out_channels for o in heads) <= 4
+            and all(o.conv.bias is not None for o in heads))
 
 
 class UNet(_HipNet):
@@ -279,10 +296,16 @@ class DualStreamUNet(_HipNet):
     def _forward(self, x_t1, x_t2):
         n1, _ = _band_counts(self.cfg)
         c = x_t1.shape[1]
+        fused = _fused_heads(self.cfg, [self.outc])
+        head = 'raw' if fused else None
         x1 = engine.pack_stream(x_t1, x_t2, 0, n1)
-        d1, _ = _stream(self.inc_stream1, self.encoder_stream1, self.decoder_stream1, x1, 1, self.training, False)
+        d1, _ = _stream(self.inc_stream1, self.encoder_stream1, self.decoder_stream1, x1, 1, self.training, False, head)
         x2 = engine.pack_stream(x_t1, x_t2, n1, c - n1)
-        d2, _ = _stream(self.inc_stream2, self.encoder_stream2, self.decoder_stream2, x2, 1, self.training, False)
+        d2, _ = _stream(self.inc_stream2, self.encoder_stream2, self.decoder_stream2, x2, 1, self.training, False, head)
+        if fused:
+            # self.outc(cat(x_stream1, x_stream2)) (networks.py:117-120): one launch over both decoders' last BatchNorm
+            # + ReLU, no cat and no materialised decoder outputs
+            return engine.run_heads([d1, d2], [(self.outc, (0, 1))])[0]
         return engine.run_head(self.outc, engine.cat_channels(d1, d2))
 
 
@@ -321,6 +344,8 @@ class DualTaskSiameseUNet(_HipNet):
     def _forward(self, x_t1, x_t2):
         b = x_t1.shape[0]
         x = engine.pack_pair(x_t1, x_t2)
+        if engine.option('fuse_dualtask') and engine.option('pooled_bn_bwd'):
+            return self._forward_fused(x, b)
         feats = engine.run_encoder(self.inc, self.encoder, x, 2, self.training)
         diffs = [engine.siamese_diff(f) for f in feats][::-1]
         # each decoder output feeds one head (networks.py:187-195): the heads run fused into the decoder stages
@@ -330,6 +355,49 @@ class DualTaskSiameseUNet(_HipNet):
         f_t1 = [f[:b] for f in feats][::-1]
         out_sem_t1 = engine.run_decoder(self.decoder_sem, f_t1, self.training, head=self.outc_sem)
         return out_change, out_sem_t1, out_sem_t2
+
+    def _forward_fused(self, x, b):
+        """One pass per encoder level writes the difference into decoder_change's concat buffers and [f_t2; f_t1] into
+        decoder_sem's (engine.DualTaskLevelFn); decoder_sem then runs both dates as one 2B batch whose BatchNorm
+        segments are the two reference calls, t2 first (networks.py:190-195), or (engine option dt_sem_batched off) as
+        two calls on the halves of the same buffers."""
+        n_levels = len(self.encoder.down_seq) + 1
+        diffs, sems, bufc, bufs = engine.run_dualtask_encoder(
+            self.inc, self.encoder, x, self.training, engine.decoder_cat_channels(self.decoder_change, n_levels),
+            engine.decoder_cat_channels(self.decoder_sem, n_levels))
+        out_change = engine.run_decoder(self.decoder_change, diffs[::-1], self.training,
+                                        _ups_buffers(bufc, self.decoder_change, n_levels), head=self.outc_change)
+        sem_bufs = _ups_buffers(bufs, self.decoder_sem, n_levels)
+        if engine.option('dt_sem_batched'):
+            sem = engine.run_decoder(self.decoder_sem, sems[::-1], self.training, sem_bufs, head=self.outc_sem, nseg=2)
+            return out_change, sem[b:], sem[:b]
+        outs = []
+        for lo in (0, b):  # t2 (images [0, b) of the semantic batch) first, then t1
+            outs.append(engine.run_decoder(self.decoder_sem, [f[lo:lo + b] for f in sems[::-1]], self.training,
+                                           [None if t is None else t[lo:lo + b] for t in sem_bufs],
+                                           head=self.outc_sem))
+        return out_change, outs[1], outs[0]
+
+
+def _two_stream_heads(net, x1, x2, nseg: int, siamese: bool):
+    """WhateverNet / WhateverNet2 (networks.py:226-263, 282-310): both streams, then outc_stream1(x_stream1),
+    outc_stream2(x_stream2) and outc_fusion(cat(x_stream1, x_stream2)).  Fused (engine option fuse_heads): the three
+    heads are one launch over both decoders' last BatchNorm + ReLU (engine.run_heads); else materialised outputs, a cat
+    and three head launches."""
+    heads = [(net.outc_fusion, (0, 1)), (net.outc_stream1, (0,)), (net.outc_stream2, (1,))]
+    fused = _fused_heads(net.cfg, [h for h, _ in heads])
+    head = 'raw' if fused else None
+    d1, _ = _stream(net.inc_stream1, net.encoder_stream1, net.decoder_stream1, x1, nseg, net.training, siamese, head)
+    d2, _ = _stream(net.inc_stream2, net.encoder_stream2, net.decoder_stream2, x2, nseg, net.training, siamese, head)
+    if fused:
+        out_fusion, out_stream1, out_stream2 = engine.run_heads([d1, d2], heads)
+    else:
+        out_stream1 = engine.run_head(net.outc_stream1, d1)
+        out_stream2 = engine.run_head(net.outc_stream2, d2)
+        out_fusion = engine.run_head(net.outc_fusion, engine.cat_channels(d1, d2))
+    if net.training:
+        return out_fusion, out_stream1, out_stream2
+    return out_fusion
 
 
 class WhateverNet(_HipNet):
@@ -352,15 +420,8 @@ class WhateverNet(_HipNet):
         n1, _ = _band_counts(self.cfg)
         c = x_t1.shape[1]
         x1 = engine.pack_pair(x_t1, x_t2, 0, n1)
-        d1, _ = _stream(self.inc_stream1, self.encoder_stream1, self.decoder_stream1, x1, 2, self.training, True)
-        out_stream1 = engine.run_head(self.outc_stream1, d1)
         x2 = engine.pack_pair(x_t1, x_t2, n1, c - n1)
-        d2, _ = _stream(self.inc_stream2, self.encoder_stream2, self.decoder_stream2, x2, 2, self.training, True)
-        out_stream2 = engine.run_head(self.outc_stream2, d2)
-        out_fusion = engine.run_head(self.outc_fusion, engine.cat_channels(d1, d2))
-        if self.training:
-            return out_fusion, out_stream1, out_stream2
-        return out_fusion
+        return _two_stream_heads(self, x1, x2, 2, True)
 
 
 class WhateverNet2(_HipNet):
@@ -383,15 +444,8 @@ class WhateverNet2(_HipNet):
         n1, _ = _band_counts(self.cfg)
         c = x_t1.shape[1]
         x1 = engine.pack_stream(x_t1, x_t2, 0, n1)
-        d1, _ = _stream(self.inc_stream1, self.encoder_stream1, self.decoder_stream1, x1, 1, self.training, False)
-        out_stream1 = engine.run_head(self.outc_stream1, d1)
         x2 = engine.pack_stream(x_t1, x_t2, n1, c - n1)
-        d2, _ = _stream(self.inc_stream2, self.encoder_stream2, self.decoder_stream2, x2, 1, self.training, False)
-        out_stream2 = engine.run_head(self.outc_stream2, d2)
-        out_fusion = engine.run_head(self.outc_fusion, engine.cat_channels(d1, d2))
-        if self.training:
-            return out_fusion, out_stream1, out_stream2
-        return out_fusion
+        return _two_stream_heads(self, x1, x2, 1, False)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -26,8 +26,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from multimodal_siamese_cd_amd import engine, hip  # noqa: E402
-from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, loss_functions, networks  # noqa: E402
+from multimodal_siamese_cd_amd import engine, hip, trainers  # noqa: E402
+from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, networks  # noqa: E402
 
 
 _DEFAULT_OPTS = dict(engine._OPTS)
@@ -84,13 +84,12 @@ def main():
     torch.manual_seed(cfg.SEED)
     net = networks.create_network(cfg).to(dev).train()
     opt = torch.optim.AdamW(net.parameters(), lr=float(cfg.TRAINER.LR), weight_decay=0.01, fused=True)
-    crit = loss_functions.get_criterion(cfg.MODEL.LOSS_TYPE)
     gen = torch.Generator(device=dev).manual_seed(7)
     b = datasets.synthetic_batch(cfg, batch, dev, gen)
 
-    def step():
+    def step():  # the config's trainer loss (single-task, dual-task, MMCR: trainers.step_loss)
         opt.zero_grad(set_to_none=True)
-        loss = crit(net(b['x_t1'], b['x_t2']), b['y_change'])
+        loss = trainers.step_loss(cfg, net(b['x_t1'], b['x_t2']), b)
         loss.backward()
         opt.step()
 
