@@ -28,14 +28,17 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in deps())
 
 
-def build_lib(force: bool = False, verbose: bool = True, jobs: int | None = None) -> str:
-    """One object per translation unit, compiled in parallel (the units share no device code), then linked."""
-    if not force and up_to_date():
+def build_lib(force: bool = False, verbose: bool = True, jobs: int | None = None, out: str | None = None,
+              defines: tuple = ()) -> str:
+    """One object per translation unit, compiled in parallel (the units share no device code), then linked.
+    `out` / `defines` (e.g. ('SCD_WGRAD_ROW_WALK=1',)): an A/B variant library elsewhere (SCD_LIB selects it)."""
+    OUT_ = out or OUT
+    if out is None and not force and up_to_date():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    objdir = os.path.join(os.path.dirname(OUT), 'obj')
+    os.makedirs(os.path.dirname(OUT_), exist_ok=True)
+    objdir = os.path.join(os.path.dirname(OUT_), 'obj')
     os.makedirs(objdir, exist_ok=True)
-    cflags = [f for f in FLAGS if f != '-shared']
+    cflags = [f for f in FLAGS if f != '-shared'] + [f'-D{d}' for d in defines]
     procs, objs = [], []
     jobs = jobs or min(8, os.cpu_count() or 1)
     for src in sources():
@@ -49,11 +52,15 @@ def build_lib(force: bool = False, verbose: bool = True, jobs: int | None = None
             procs[[p.poll() is None for p in procs].index(True)].wait()
     if any(p.wait() != 0 for p in procs):
         raise RuntimeError('hipcc failed (see the compiler output above)')
-    tmp = OUT + '.tmp'
+    tmp = OUT_ + '.tmp'
     subprocess.run([HIPCC, *FLAGS, '-o', tmp, *objs], check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, OUT_)
+    return OUT_
 
 
 if __name__ == '__main__':
-    build_lib(force=True)
+    import sys
+    if len(sys.argv) > 1:  # python -m multimodal_siamese_cd_amd.build <out.so> [DEFINE=VALUE ...]
+        build_lib(out=os.path.abspath(sys.argv[1]), defines=tuple(sys.argv[2:]))
+    else:
+        build_lib(force=True)

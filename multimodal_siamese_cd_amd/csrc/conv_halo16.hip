@@ -1511,6 +1511,21 @@ void launch_halo16_c16(const IgemmArgs &a, int tw, hipStream_t s) {
 namespace {
 constexpr int kW16RS = 160;
 
+// Patch walk of a split (a contiguous range of patch indices): DOWN each 16-pixel column strip of an image, so two
+// consecutive patches share two of their four halo rows -- a re-read the L2 still holds one patch later.  The row walk
+// (-DSCD_WGRAD_ROW_WALK=1, the round-4 order) re-read those rows a whole strip row (w / 16 patches) later, past the L2
+// with ~64 blocks per XCD streaming: the 256^2 weight grads fetched 1.5-1.7x their algorithmic bytes
+// (profiles/r05_traffic_table.txt).  Same patches per split, so only the order of the split's accumulation changes.
+#ifndef SCD_WGRAD_ROW_WALK
+#define SCD_WGRAD_ROW_WALK 0
+#endif
+__device__ __forceinline__ int patch_y0(int pr, int pw_n, int ph_n, int ph) {
+    return SCD_WGRAD_ROW_WALK ? (pr / pw_n) * ph : (pr - (pr / ph_n) * ph_n) * ph;
+}
+__device__ __forceinline__ int patch_x0(int pr, int pw_n, int ph_n, int pw) {
+    return SCD_WGRAD_ROW_WALK ? (pr - (pr / pw_n) * pw_n) * pw : (pr / ph_n) * pw;
+}
+
 // X planes of the weight-grad kernel per arithmetic: x3 3, x5 2 (its l term is the dropped product's), bf16 1,
 // h2 2 (fp16 h, m).  dY planes: x3 / x5 3, bf16 1, h2 2.
 template <int NP>
@@ -1689,7 +1704,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
             x_sh = gload4(a.src_shift + ch);
         }
         x_valid = 0;
-        const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
+        const int y0 = patch_y0(pr, pw_n, ph_n, PH), x0 = patch_x0(pr, pw_n, ph_n, PW);
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * NT, q = e / CQ, cq = e % CQ;
@@ -1978,7 +1993,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_halo16_c16(WgradArgs a) {
             r_mul = (a.rbn_gamma ? gload4(a.rbn_gamma + c) : f32x4{1.f, 1.f, 1.f, 1.f}) * r_iv;
         }
         x_valid = 0;
-        const int y0 = (pr / pw_n) * PH, x0 = (pr - (pr / pw_n) * pw_n) * PW;
+        const int y0 = patch_y0(pr, pw_n, ph_n, PH), x0 = patch_x0(pr, pw_n, ph_n, PW);
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * 256, q = e >> 4, cq = e & 15;

@@ -377,18 +377,135 @@ struct HeadSrc {
     const float *scale, *shift;
 };
 
-template <int U, class T, int CP>
+// Sum over groups of G lanes (G a power of two <= 64, groups aligned), every lane of a group receiving the total:
+// DPP quad permutes and row mirrors inside a row of 16 (VALU ops, no LDS traffic), then cross-row shuffles.  The tree
+// adds the nearest lanes first, so a sum over G lanes whose upper G/2 lanes hold +0 equals the sum over the lower G/2.
+template <int CTRL>
+__device__ __forceinline__ float head_dpp(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float group_sum(float x, int G) {
+    if (G >= 2) x += head_dpp<0xB1>(x);   // quad_perm [1,0,3,2]
+    if (G >= 4) x += head_dpp<0x4E>(x);   // quad_perm [2,3,0,1]
+    if (G >= 8) x += head_dpp<0x141>(x);  // row_half_mirror: i <-> 7 - i within each half row
+    if (G >= 16) x += head_dpp<0x140>(x); // row_mirror: i <-> 15 - i
+    if (G >= 32) x += __shfl_xor(x, 16, 64);
+    if (G >= 64) x += __shfl_xor(x, 32, 64);
+    return x;
+}
+
+// ONE: every piece has its own lane (P <= G): the lane's coefficients and weights are loaded once per kernel, pixel
+// loads are unconditional (clamped to the last pixel; lanes past P read a valid piece and contribute +0).
+template <int U, class T, int CP, bool ONE, int NO>
 __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(HeadSrc sa, HeadSrc sb, int pa, int P, int C, int hw,
                                                           int64_t npix, const float *__restrict__ w,
-                                                          const float *__restrict__ b, int n_out, int G,
+                                                          const float *__restrict__ b, int G,
                                                           int64_t pseg, FastDiv fseg, FastDiv fhw,
                                                           float *__restrict__ out) {
     constexpr int NQ = CP / 4;  // channel quads per piece
+    constexpr int n_out = NO;   // output channels (heads) of the launch
     const int lane = threadIdx.x & 63;
     const int q = lane % G, pp = lane / G, ppw = 64 / G;
     const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
     const bool bn = sa.scale != nullptr;  // uniform: both sources or neither
+    const bool segs = bn && pseg < npix;  // uniform: more than one coefficient segment
+    auto seg_of = [&](int64_t p) -> int64_t {
+        return npix < (int64_t(1) << 31) ? int64_t(fdiv(uint32_t(p), fseg)) : p / pseg;
+    };
+    if constexpr (ONE) {
+        const bool act = q < P;
+        const int qq = act ? q : P - 1;
+        const bool in_a = qq < pa;
+        const T *xs = static_cast<const T *>(in_a ? sa.x : sb.x);
+        const int ld = in_a ? sa.ld : sb.ld, cs = in_a ? sa.C : sb.C;
+        const int ch = (in_a ? qq : qq - pa) * CP;
+        const float *scl = in_a ? sa.scale : sb.scale, *shf = in_a ? sa.shift : sb.shift;
+        bnf4 wv[4][NQ];
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+#pragma unroll
+            for (int k = 0; k < NQ; ++k)
+                wv[o][k] = o < n_out ? ld4(w + int64_t(o) * C + qq * CP + 4 * k) : bnf4{0.f, 0.f, 0.f, 0.f};
+        bnf4 sc[NQ], sf[NQ];
+        int64_t cur = 0;
+        if (bn) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                sc[k] = ld4(scl + ch + 4 * k);
+                sf[k] = ld4(shf + ch + 4 * k);
+            }
+        }
+        for (int64_t p0 = wave * ppw * U; p0 < npix; p0 += nwaves * ppw * U) {
+            HeadPiece<T, CP> v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int64_t p = p0 + u * ppw + pp;
+                p = p < npix ? p : npix - 1;
+                v[u].load(xs + p * ld + ch);
+            }
+            float s[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (bn) {
+                    if (segs) {  // the lane's coefficients follow its pixel's segment (rarely changes within a wave)
+                        int64_t p = p0 + u * ppw + pp;
+                        const int64_t sg = seg_of(p < npix ? p : npix - 1);
+                        if (sg != cur) {
+                            cur = sg;
+#pragma unroll
+                            for (int k = 0; k < NQ; ++k) {
+                                sc[k] = ld4(scl + sg * cs + ch + 4 * k);
+                                sf[k] = ld4(shf + sg * cs + ch + 4 * k);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < NQ; ++k) v[u].v[k] = bn_relu_f4(v[u].v[k], sc[k], sf[k]);
+                }
+                if (!act) {
+#pragma unroll
+                    for (int k = 0; k < NQ; ++k) v[u].v[k] = bnf4{0.f, 0.f, 0.f, 0.f};
+                }
+                // one chain per channel quad, the quads' partial sums added: a 16-byte bf16 piece (two quads) forms
+                // exactly what two fp32 lanes and the first step of their tree form, so bf16 storage of
+                // bf16-representable values gives the fp32 path's bits
+#pragma unroll
+                for (int o = 0; o < 4; ++o) {
+                    float acc = 0.f;
+                    if (o < n_out) {
+#pragma unroll
+                        for (int k = 0; k < NQ; ++k) {
+                            const bnf4 x4 = v[u].v[k], w4 = wv[o][k];
+                            const float c4 = fmaf(x4.x, w4.x, fmaf(x4.y, w4.y, fmaf(x4.z, w4.z, fmaf(x4.w, w4.w, 0.f))));
+                            acc = k == 0 ? c4 : acc + c4;
+                        }
+                    }
+                    s[u][o] = acc;
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < 4; ++o)
+                if (o < n_out)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) s[u][o] = group_sum(s[u][o], G);
+            if (q == 0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int64_t p = p0 + u * ppw + pp;
+                    if (p < npix) {
+                        const int64_t img = npix < (int64_t(1) << 31) ? int64_t(fdiv(uint32_t(p), fhw)) : p / hw;
+                        const int64_t pix = p - img * hw;
+#pragma unroll
+                        for (int o = 0; o < 4; ++o)
+                            if (o < n_out) out[(img * n_out + o) * hw + pix] = s[u][o] + (b ? b[o] : 0.f);
+                    }
+                }
+            }
+        }
+        return;
+    }
+    // P > G: each lane walks pieces q, q + G, ...
     for (int64_t p0 = wave * ppw * U; p0 < npix; p0 += nwaves * ppw * U) {
         float s[U][4];
 #pragma unroll
@@ -403,40 +520,19 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(HeadSrc sa, HeadSrc sb
             HeadPiece<T, CP> v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int64_t p = p0 + u * ppw + pp;
-                if (p < npix) {
-                    v[u].load(xs + p * ld + ch);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < NQ; ++k) v[u].v[k] = bnf4{0.f, 0.f, 0.f, 0.f};
-                }
+                int64_t p = p0 + u * ppw + pp;
+                p = p < npix ? p : npix - 1;
+                v[u].load(xs + p * ld + ch);
             }
             if (bn) {
                 const float *scl = in_a ? sa.scale : sb.scale, *shf = in_a ? sa.shift : sb.shift;
-                // segment of a pixel: a multiply-shift below 2^31 pixels.  The U pixels of a lane nearly always share
-                // one segment: then one coefficient load serves them
-                auto seg_of = [&](int64_t p) -> int64_t {
-                    return p < npix ? (npix < (int64_t(1) << 31) ? int64_t(fdiv(uint32_t(p), fseg)) : p / pseg) : 0;
-                };
-                const int64_t s0 = seg_of(p0 + pp), s1 = seg_of(p0 + (U - 1) * ppw + pp);
-                bnf4 sc[NQ], sf[NQ];
-#pragma unroll
-                for (int k = 0; k < NQ; ++k) {
-                    sc[k] = ld4(scl + s0 * cs + ch + 4 * k);
-                    sf[k] = ld4(shf + s0 * cs + ch + 4 * k);
-                }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (s1 != s0) {
-                        const int64_t so = seg_of(p0 + u * ppw + pp) * cs + ch;
+                    int64_t p = p0 + u * ppw + pp;
+                    const int64_t so = (segs ? seg_of(p < npix ? p : npix - 1) : 0) * cs + ch;
 #pragma unroll
-                        for (int k = 0; k < NQ; ++k) {
-                            sc[k] = ld4(scl + so + 4 * k);
-                            sf[k] = ld4(shf + so + 4 * k);
-                        }
-                    }
-#pragma unroll
-                    for (int k = 0; k < NQ; ++k) v[u].v[k] = bn_relu_f4(v[u].v[k], sc[k], sf[k]);
+                    for (int k = 0; k < NQ; ++k)
+                        v[u].v[k] = bn_relu_f4(v[u].v[k], ld4(scl + so + 4 * k), ld4(shf + so + 4 * k));
                 }
             }
 #pragma unroll
@@ -458,8 +554,7 @@ __global__ __launch_bounds__(256) void conv1x1_fwd_kernel(HeadSrc sa, HeadSrc sb
         for (int o = 0; o < 4; ++o)
             if (o < n_out)
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    for (int off = G / 2; off > 0; off >>= 1) s[u][o] += __shfl_xor(s[u][o], off, 64);
+                for (int u = 0; u < U; ++u) s[u][o] = group_sum(s[u][o], G);
         if (q == 0) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -832,20 +927,40 @@ static int conv1x1_fwd_run(const scd_nhwc_t &a, const float *sca, const float *s
     constexpr int U = 4;
     const int64_t waves = (npix + (64 / G) * U - 1) / ((64 / G) * U);
     int blocks = int((waves + 3) / 4);
-    if (blocks > 4096) blocks = 4096;
+    if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
     const HeadSrc A{a.data, a.ldc, a.c, sca, sha};
     const HeadSrc B{two ? b.data : a.data, two ? b.ldc : a.ldc, two ? b.c : a.c, two ? scb : sca, two ? shb : sha};
     const FastDiv fseg = make_fastdiv(uint32_t(npix / nseg > 0 ? npix / nseg : 1));
     const FastDiv fhw = make_fastdiv(uint32_t(a.h * a.w > 0 ? a.h * a.w : 1));
-    if (wide) {
-        hipLaunchKernelGGL((conv1x1_fwd_kernel<U, bf16_t, 8>), dim3(blocks), dim3(256), 0, s, A, B, pa, P, C, a.h * a.w,
-                           npix, w, bias, n_out, G, npix / nseg, fseg, fhw, out);
-    } else {
-        SCD_WITH_T(a.dtype, T,
-                   hipLaunchKernelGGL((conv1x1_fwd_kernel<U, T, 4>), dim3(blocks), dim3(256), 0, s, A, B, pa, P, C,
-                                      a.h * a.w, npix, w, bias, n_out, G, npix / nseg, fseg, fhw, out));
+    const bool one = P <= G;
+#define SCD_HEAD_LAUNCH(T_, CP_, ONE_, NO_)                                                                              \
+    hipLaunchKernelGGL((conv1x1_fwd_kernel<U, T_, CP_, ONE_, NO_>), dim3(blocks), dim3(256), 0, s, A, B, pa, P, C,       \
+                       a.h * a.w, npix, w, bias, G, npix / nseg, fseg, fhw, out)
+#define SCD_HEAD_NO(T_, CP_, ONE_)                  \
+    switch (n_out) {                                \
+        case 1: SCD_HEAD_LAUNCH(T_, CP_, ONE_, 1); break; \
+        case 2: SCD_HEAD_LAUNCH(T_, CP_, ONE_, 2); break; \
+        case 3: SCD_HEAD_LAUNCH(T_, CP_, ONE_, 3); break; \
+        default: SCD_HEAD_LAUNCH(T_, CP_, ONE_, 4); break; \
     }
+    if (wide) {
+        if (one) {
+            SCD_HEAD_NO(bf16_t, 8, true);
+        } else {
+            SCD_HEAD_NO(bf16_t, 8, false);
+        }
+    } else {
+        SCD_WITH_T(a.dtype, T, {
+            if (one) {
+                SCD_HEAD_NO(T, 4, true);
+            } else {
+                SCD_HEAD_NO(T, 4, false);
+            }
+        });
+    }
+#undef SCD_HEAD_NO
+#undef SCD_HEAD_LAUNCH
     return launch_status("scd_conv1x1_fwd");
 }
 

@@ -1,9 +1,11 @@
-"""HIP-event timing of the OutConv 1x1 head forward on the bench shape ([32, 256, 256, 64] NHWC -> 1 channel).
+"""HIP-event timing of the OutConv 1x1 head forwards (scd_conv1x1_fwd_bn2 / _fwd_bn), on the configs' shapes.
 
     python tools/perf_head.py [--reps 20]
 
-Measured (final code): 103-110 us = 4.9-5.2 TB/s with U = 4 pixel sets per wave iteration; U = 8 and 16 were
-slower (120, 178 us) in a one-off study.
+Cases: the Siamese head (fp32, bs=32, through the last BatchNorm), the dual-task semantic head (fp32, 2 x 64 images,
+two BatchNorm segments), DualStream's fusion head (bf16, bs=64, two decoders) and WhateverNet's three heads in one
+launch (bf16, bs=16 at 512^2, two decoders).  TB/s counts the bytes read (the activations) plus the logits written.
+Round 4 (the bench step, rocprof): Siamese 156 us, DualStream 505 us (2.1 TB/s), WhateverNet 780 us (1.4 TB/s).
 """
 import argparse
 import os
@@ -16,28 +18,43 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from multimodal_siamese_cd_amd import hip  # noqa: E402
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--reps', type=int, default=20)
-    ap.add_argument('--batch', type=int, default=32)
-    args = ap.parse_args()
-    hip.load_library()
-    dev = torch.device('cuda:0')
-    x = torch.randn(args.batch, 256, 256, 64, device=dev)
-    w = torch.randn(1, 64, device=dev)
-    b = torch.randn(1, device=dev)
-    o = torch.empty(args.batch, 1, 256, 256, device=dev)
-    fn = lambda: hip.conv1x1_fwd(hip.nhwc(x), w, b, 1, o)  # noqa: E731
+def bench(fn, reps):
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(args.reps):
+    for _ in range(reps):
         fn()
     e1.record()
     torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / args.reps
-    print(f'head 1x1 fwd: {t * 1e3:.1f} us, {x.numel() * 4 / t / 1e9:.2f} TB/s')
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--reps', type=int, default=20)
+    args = ap.parse_args()
+    hip.load_library()
+    dev = torch.device('cuda:0')
+    cases = [('siamese fp32 bs32', torch.float32, 32, 256, 1, 1, 1),
+             ('dtsiamese sem fp32 2x64', torch.float32, 128, 256, 1, 1, 2),
+             ('dualstream bf16 bs64', torch.bfloat16, 64, 256, 2, 1, 1),
+             ('whatevernet bf16 bs16 512^2 x3 heads', torch.bfloat16, 16, 512, 2, 3, 1)]
+    for name, dt, n, s, nsrc, nout, nseg in cases:
+        ys = [torch.randn(n, s, s, 64, device=dev).to(dt) for _ in range(nsrc)]
+        sc = [torch.rand(nseg * 64, device=dev) + 0.5 for _ in range(nsrc)]
+        sh = [torch.randn(nseg * 64, device=dev) for _ in range(nsrc)]
+        w = torch.randn(nout, 64 * nsrc, device=dev)
+        b = torch.randn(nout, device=dev)
+        o = torch.empty(n, nout, s, s, device=dev)
+        if nsrc == 2:
+            fn = lambda: hip.conv1x1_fwd_bn2(hip.nhwc(ys[0]), sc[0], sh[0], hip.nhwc(ys[1]), sc[1], sh[1], nseg, w, b,  # noqa: E731
+                                             nout, o)
+        else:
+            fn = lambda: hip.conv1x1_fwd_bn(hip.nhwc(ys[0]), sc[0], sh[0], nseg, w, b, nout, o)  # noqa: E731
+        t = bench(fn, args.reps)
+        nbytes = sum(y.numel() * y.element_size() for y in ys) + o.numel() * 4
+        print(f'{name:40s} {t * 1e3:8.1f} us  {nbytes / t / 1e9:5.2f} TB/s', flush=True)
 
 
 if __name__ == '__main__':
