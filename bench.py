@@ -91,6 +91,18 @@ def kernel_class(kind: str, ntaps: int, src_c: int) -> str:
     return f"{kind}_convT"
 
 
+def _eb(v) -> int:
+    return 2 if v.dtype == hip.DT_BF16 else 4
+
+
+def _vbytes(v) -> int:  # an NHWC view's payload
+    return int(v.n) * int(v.h) * int(v.w) * int(v.c) * _eb(v)
+
+
+def _tbytes(t) -> int:
+    return t.numel() * t.element_size()
+
+
 class KernelTimer:
     """HIP-event brackets around every MFMA conv launch (on torch's current stream, where libscd launches)."""
 
@@ -113,7 +125,11 @@ class KernelTimer:
             r = timer._igemm(src, out_h, out_w, stride, taps, wpk, n_out, *a, **k)
             e.record()
             flops = 2.0 * src.n * out_h * out_w * n_out * len(taps[0]) * src.c
-            timer.events.append(('igemm', s, e, flops, arith, kernel_class('igemm', len(taps[0]), src.c)))
+            dst = a[1] if len(a) > 1 else k['dst']
+            planes = {'h2': 2, 'x3': 3, 'x5': 2, 'bf16': 1, 'f32': 2}[arith]
+            alg = (_vbytes(src) + src.n * out_h * out_w * n_out * _eb(dst) + planes * len(taps[0]) * src.c * n_out * 2
+                   + (_tbytes(k['bn_bwd'][0]) if k.get('bn_bwd') is not None else 0))
+            timer.events.append(('igemm', s, e, flops, arith, kernel_class('igemm', len(taps[0]), src.c), alg))
             return r
 
         def wgrad(d, slabs):
@@ -125,7 +141,9 @@ class KernelTimer:
             r = timer._wgrad(d, slabs)
             e.record()
             flops = 2.0 * d.rows.n * d.rows.h * d.rows.w * d.rows.c * d.ntaps * d.src.c
-            timer.events.append(('wgrad', s, e, flops, arith, kernel_class('wgrad', d.ntaps, d.src.c)))
+            alg = (_vbytes(d.rows) + _vbytes(d.src) + slabs.numel() * slabs.element_size()
+                   + (_vbytes(d.rows_y) if d.rows_y.data else 0))
+            timer.events.append(('wgrad', s, e, flops, arith, kernel_class('wgrad', d.ntaps, d.src.c), alg))
             return r
 
         hip.conv_igemm = igemm
@@ -143,7 +161,7 @@ class KernelTimer:
         """Per kernel class (kernel_class): launches, ms, FLOPs per step, TFLOP/s and the fraction of that class's
         flop-weighted arithmetic peak; the class with the most time is the step's dominant kernel."""
         out = {}
-        for _, s, e, fl, arith, cls in self.events:
+        for _, s, e, fl, arith, cls, _alg in self.events:
             c = out.setdefault(cls, {'n': 0, 'ms': 0.0, 'flop': 0.0, 'tpeak': 0.0})
             c['n'] += 1
             c['ms'] += s.elapsed_time(e)
@@ -167,6 +185,11 @@ class KernelTimer:
 
     def launched_flops(self, reps):
         return sum(ev[3] for ev in self.events) / reps
+
+    def alg_bytes(self, reps):
+        """Algorithmic bytes of the conv launches per step: every operand read once, every output written once (src +
+        dst + split weights for igemm, dY + X + slabs for wgrad, + the y a fused BatchNorm transform reads)."""
+        return sum(ev[6] for ev in self.events) / reps
 
 
 def host_cores() -> tuple:
@@ -234,6 +257,65 @@ def cpu_baseline(cfg, batches=(2, 8), min_seconds=(8.0, 6.0), size: int = 256):
                       f"{ncpu}); " + '; '.join(notes)}
 
 
+def _conv_family(name: str):
+    n = name.split('(')[0].replace('void ', '').replace('scd::', '').strip()
+    if n.startswith('igemm'):
+        return 'igemm'
+    if n.startswith(('wgrad_halo', 'wgrad_x3', 'wgrad_f32')):
+        return 'wgrad'
+    return None
+
+
+def live_traffic(args, batch: int, size: int, timeout_s: int = 180):
+    """The conv kernels' HBM-side traffic per step, measured now: two child processes run 3 steps of this workload
+    (1 warm-up + 2) under `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (separate passes, MI355X_MICROARCH.md
+    HBM); FETCH_SIZE is doubled (the gfx950 correction for 16-byte-per-lane streaming reads), both are KiB.  Returns
+    {bytes_per_step, by_family, source} or raises."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which('rocprofv3') or '/opt/rocm/bin/rocprofv3'
+    if not os.path.exists(prof):
+        raise RuntimeError('rocprofv3 not found')
+    child = [sys.executable, os.path.join(ROOT, 'bench.py'), '--steps', '2', '--warmup', '1', '--no-cpu-baseline',
+             '--no-kernel-timing', '--no-traffic', '--config', args.config, '--batch', str(batch), '--size', str(size)]
+    if args.math:
+        child += ['--math', args.math]
+    if args.storage:
+        child += ['--storage', args.storage]
+    steps = 3
+    tot = {}
+    tmp = tempfile.mkdtemp(prefix='scd_pmc_', dir='/tmp')
+    env = dict(os.environ, TMPDIR='/tmp')
+    try:
+        for counter in ('FETCH_SIZE', 'WRITE_SIZE'):
+            d = os.path.join(tmp, counter)
+            subprocess.run([prof, '--pmc', counter, '--output-format', 'csv', '-d', d, '-o', 'run', '--', *child],
+                           cwd='/tmp', env=env, timeout=timeout_s, check=True, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL)
+            found = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs if f.endswith('counter_collection.csv')]
+            if not found:
+                raise RuntimeError(f'{counter}: no counter_collection.csv')
+            fam = {'igemm': 0.0, 'wgrad': 0.0}
+            with open(found[0]) as f:
+                for r in csv.DictReader(f):
+                    k = _conv_family(r['Kernel_Name'])
+                    if r['Counter_Name'] == counter and k:
+                        fam[k] += float(r['Counter_Value'])
+            tot[counter] = fam
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    by = {k: (2.0 * tot['FETCH_SIZE'][k] + tot['WRITE_SIZE'][k]) * 1024.0 / steps for k in ('igemm', 'wgrad')}
+    return {"bytes_per_step": round(sum(by.values())), "by_family": {k: round(v) for k, v in by.items()},
+            "fetch_bytes_per_step": round(2.0 * sum(tot['FETCH_SIZE'].values()) * 1024.0 / steps),
+            "write_bytes_per_step": round(sum(tot['WRITE_SIZE'].values()) * 1024.0 / steps),
+            "source": "measured by this run: two child processes of this workload (3 steps each) under rocprofv3 "
+                      "--pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), FETCH x2 (gfx950 wide-read correction), "
+                      "KiB x 1024 / 3 steps; L2-miss fabric bytes of the igemm / wgrad kernels (Infinity-Cache hits "
+                      "included, MI355X_MICROARCH.md HBM)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -244,6 +326,8 @@ def main():
     ap.add_argument('--size', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--no-traffic', action='store_true',
+                    help='skip the live PMC traffic passes (two rocprofv3 child runs of this workload)')
     ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16', 'h2'],
                     help='conv arithmetic (default: from the config, engine.conv_math_for: MODEL.PRECISION fp32 -> h2)')
     ap.add_argument('--storage', default=None, choices=['fp32', 'bf16'],
@@ -353,18 +437,15 @@ def main():
         flop_step = f3 + fT if cfg.MODEL.TYPE == 'siameseunet' else timer.launched_flops(reps)
         achieved = flop_step / (t_ms * 1e-3) / 1e12
         traffic = None
-        pmc = []  # the latest round's PMC traffic of this workload and arithmetic (profiles/rNN_pmc_traffic.json)
-        for fn in sorted(f for f in os.listdir(os.path.join(ROOT, 'profiles')) if f.endswith('_pmc_traffic.json')):
-            with open(os.path.join(ROOT, 'profiles', fn)) as f:
-                tr = json.load(f)
-            if tr.get('math', 'x3') == math:
-                pmc.append((fn, tr))
-        if pmc and args.config == 'baseline_siamese' and batch == 32 and size == 256:
-            fn, tr = pmc[-1]
-            traffic = {"bytes_per_step": round(tr['per_step_bytes']['total']),
-                       "by_family": {k: round(v) for k, v in tr['per_step_bytes'].items() if k != 'total'},
-                       "source": f"profiles/{fn}: {tr['source']}; L2-miss fabric bytes (Infinity-Cache "
-                                 "hits included, MI355X_MICROARCH.md HBM)"}
+        if world == 1 and not args.no_traffic:
+            try:
+                traffic = live_traffic(args, batch, size)
+            except Exception as e:  # noqa: BLE001 - reported in the line, never fatal to the bench
+                traffic = {"bytes_per_step": None, "source": f"live PMC passes failed: {type(e).__name__}: {e}"}
+            alg = timer.alg_bytes(reps)
+            traffic["algorithmic_bytes_per_step"] = round(alg)
+            if traffic.get("bytes_per_step"):
+                traffic["traffic_over_algorithmic"] = round(traffic["bytes_per_step"] / alg, 3)
         peak, shares = timer.peak()
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",

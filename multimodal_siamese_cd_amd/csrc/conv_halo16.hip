@@ -1030,9 +1030,13 @@ void launch16_1xn(const IgemmArgs &a, int tw, hipStream_t s) {
 bool wide_1xn_ok(const IgemmArgs &a) {
     return a.src_bound && h2_weight_format(a.math, a.ntaps, a.c) && h2_prescale(a.tune);
 }
-// The bf16 arithmetic on the 1 x N tiles (SCD_TUNE_BF16_1XN, A/B): one wave per weight fragment, no fragment loaded by
-// two waves (the 2 x 2 tiles' duplicate L2 weight loads per MFMA bound the one-product bf16 steps).
-bool bf16_1xn(const IgemmArgs &a) { return (a.tune & SCD_TUNE_BF16_1XN) && a.math == SCD_MATH_BF16; }
+// The bf16 arithmetic on the 1 x N tiles: one wave per weight fragment, no fragment loaded by two waves.  The default
+// with bf16 storage (round 5: baseline_dualstream bs=64 42.23 -> 41.77 ms per step, same-process A/B,
+// profiles/r05_bf16_tiles_ab.txt; round 4: +0.45%); the 2 x 2 tiles with fp32 storage (round 3: the 1 x N tiles 1.6%
+// slower there).  SCD_TUNE_BF16_1XN flips the choice (A/B).
+bool bf16_1xn(const IgemmArgs &a) {
+    return a.math == SCD_MATH_BF16 && (bool(a.sb) != bool(a.tune & SCD_TUNE_BF16_1XN));
+}
 
 // The 1 x N tiles in the bf16 arithmetic (fp32 or bf16 storage, double-buffered: one plane always fits).
 template <int WM, int WN, int TM, int TN, int OCC>

@@ -435,7 +435,7 @@ TUNE_NO_XCD_REMAP = 1 << 7
 TUNE_HALO_ORDER_M = 1 << 8
 TUNE_W16_LAYOUT_2X2 = 1 << 9
 TUNE_WGRAD_R64 = 1 << 10
-TUNE_BF16_1XN = 1 << 11
+TUNE_BF16_1XN = 1 << 11  # flips the bf16 tile layout (1 x N with bf16 storage by default, 2 x 2 with fp32)
 TUNE_HALO16_DB_OFF = 1 << 20
 TUNE_HALO16_DB_ON = 1 << 21
 TUNE_NO_GATHER16 = 1 << 22

@@ -456,7 +456,7 @@ def test_bf16_models_store_bf16_activations(dev):
 @pytest.mark.parametrize('ci,co,mode', [(64, 64, 'stats'), (128, 128, 'stats'), (64, 128, 'bn_bwd'), (64, 64, 'in_bn'),
                                         (256, 64, 'plain')])
 def test_bf16_1xn_tiles_bit_identical(dev, st, ci, co, mode):
-    """The bf16 arithmetic on the 1 x N wave tiles (SCD_TUNE_BF16_1XN) against its 2 x 2 tiles, both on 128-pixel tiles
+    """The bf16 arithmetic on the 1 x N wave tiles against its 2 x 2 tiles (SCD_TUNE_BF16_1XN flips the layout), both on 128-pixel tiles
     (SCD_TUNE_H2_TILE64_128): every output accumulates the same products in the same order and the epilogue reduces
     in 64-pixel groups in both, so outputs and statistics / BatchNorm-backward records are bit-identical (bf16 and
     fp32 storage)."""

@@ -58,6 +58,8 @@ def main():
                     help='input-layer channels as stored (default: the model\'s padding of 5 bands, engine.pad_in)')
     ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16', 'h2'],
                     help='conv arithmetic (default: library default; h2 gets absmax operand bounds)')
+    ap.add_argument('--storage', default='fp32', choices=['fp32', 'bf16'],
+                    help='activation / gradient storage of the operands (bf16: the bf16 configs, with --math bf16)')
     ap.add_argument('--variants', default=None,
                     help='comma-separated variants, interleaved per layer; a variant is "+"-joined settings '
                          'h16=<hip.set_halo16 mode> or tune=<SCD_TUNE_* bits, OR-ed>, e.g. h16=1+tune=0x100000,h16=1')
@@ -76,11 +78,12 @@ def main():
     for name, n, s, ci, co in layers(args.batch, cin=cin):
         if args.layer and name != args.layer:
             continue
-        x = torch.randn(n, s, s, ci, device=dev)
-        dy = torch.randn(n, s, s, co, device=dev)
+        sdt = torch.bfloat16 if args.storage == 'bf16' else torch.float32
+        x = torch.randn(n, s, s, ci, device=dev).to(sdt)
+        dy = torch.randn(n, s, s, co, device=dev).to(sdt)
         w = torch.randn(co, ci, 3, 3, device=dev) * 0.05
-        y = torch.empty(n, s, s, co, device=dev)
-        dx = torch.empty(n, s, s, ci, device=dev)
+        y = torch.empty(n, s, s, co, device=dev, dtype=sdt)
+        dx = torch.empty(n, s, s, ci, device=dev, dtype=sdt)
         wf = hip.pack_conv3x3(w, 0)
         wb = hip.pack_conv3x3(w, 1)
         flops = 2.0 * n * s * s * co * 9 * ci
