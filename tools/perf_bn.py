@@ -1,10 +1,11 @@
 """Per-layer timing of the BatchNorm / elementwise kernels of the bench workload (SiameseUNet 256^2, bs=32).
 
-    python tools/perf_bn.py [--batch 32] [--reps 5]
+    python tools/perf_bn.py [--batch 32] [--reps 5] [--storage bf16]
 
 For every conv output of one training step, times scd_bn_train_stats, scd_bn_relu_apply and
 scd_bn_relu_backward with HIP events.  Prints the achieved HBM rate from the algorithmic bytes:
-4, 8 and 20 B/elem respectively (the backward reads y and da twice and writes dy).
+4, 8 and 20 B/elem respectively (the backward reads y and da twice and writes dy); half of that with
+--storage bf16 (bf16 activations and gradients, the bf16 configs' ACT_STORAGE).
 """
 import argparse
 import os
@@ -22,7 +23,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--storage', choices=('f32', 'bf16'), default='f32')
     args = ap.parse_args()
+    dt = torch.bfloat16 if args.storage == 'bf16' else torch.float32
+    eb = 2 if args.storage == 'bf16' else 4
     hip.load_library()
     dev = torch.device('cuda:0')
     # streaming references on the largest map: torch's float4 copy (1 read + 1 write) and add (2 reads + 1 write)
@@ -49,8 +53,8 @@ def main():
           f'{"bwd ms":>8s} {"TB/s":>5s}')
     for name, n, s, _, co in layers(args.batch):
         nseg = 2 if name.startswith('enc') else 1
-        y = torch.randn(n, s, s, co, device=dev)
-        da = torch.randn(n, s, s, co, device=dev)
+        y = torch.randn(n, s, s, co, device=dev, dtype=dt)
+        da = torch.randn(n, s, s, co, device=dev, dtype=dt)
         a = torch.empty_like(y)
         dy = torch.empty_like(y)
         gamma = torch.rand(co, device=dev) + 0.5
@@ -68,7 +72,7 @@ def main():
         t_b = timeit(lambda: hip.bn_relu_backward(Y, DA, nseg, sm, si, gamma, sc, sh, dg, db, dbias, DY, ws),
                      args.reps)
         cells = []
-        for k, t, b in (('stats', t_s, 4), ('apply', t_a, 8), ('bwd', t_b, 20)):
+        for k, t, b in (('stats', t_s, eb), ('apply', t_a, 2 * eb), ('bwd', t_b, 5 * eb)):
             tot[k] += t
             byt[k] += b * el
             cells.append(f'{t:8.3f} {b * el / t / 1e9:5.2f}')
@@ -77,16 +81,16 @@ def main():
         print(f'{k:6s} total {tot[k]:8.2f} ms  {byt[k] / tot[k] / 1e9:5.2f} TB/s')
     # the encoder levels' backward: da = maxpool_bwd(gy, idx) -/+ the Siamese difference gradient, formed on the fly
     # (scd_bn_relu_backward_pooled, the pair kernels); algorithmic bytes per y element: 2 x (y 4 + difference 2 (one
-    # t1/t2 pair reads it once) + pooled gradient 1 + argmax 0.25) + dy 4 = 18.5
+    # t1/t2 pair reads it once) + pooled gradient 1 + argmax 0.25) + dy 4 = 18.5 (fp32; bf16 storage: 9.5)
     print(f'{"level":8s} {"n":>3s} {"hw":>4s} {"c":>5s} | {"pooled bwd ms":>13s} {"TB/s":>5s}')
     tp, bp = 0.0, 0.0
     for name, n, s, _, co in layers(args.batch):
         if not (name.startswith('enc') and name.endswith('b')):
             continue
-        y = torch.randn(n, s, s, co, device=dev)
-        gy = torch.randn(n, s // 2, s // 2, co, device=dev)
+        y = torch.randn(n, s, s, co, device=dev, dtype=dt)
+        gy = torch.randn(n, s // 2, s // 2, co, device=dev, dtype=dt)
         idx = torch.randint(0, 4, (n, s // 2, s // 2, co), device=dev, dtype=torch.uint8)
-        cat = torch.randn(n // 2, s, s, 2 * co, device=dev)
+        cat = torch.randn(n // 2, s, s, 2 * co, device=dev, dtype=dt)
         dy = torch.empty_like(y)
         gamma = torch.rand(co, device=dev) + 0.5
         sm, si = torch.randn(2 * co, device=dev), torch.rand(2 * co, device=dev) + 0.5
@@ -95,7 +99,7 @@ def main():
         ws = torch.empty(hip.bn_workspace_bytes(n, s, s, co, 2), dtype=torch.uint8, device=dev)
         t = timeit(lambda: hip.bn_relu_backward_pooled(hip.nhwc(y), hip.nhwc(gy), idx, hip.nhwc(cat, 0, co), 1, 2, sm,
                                                        si, gamma, sc, sh, dg, db, dbias, hip.nhwc(dy), ws), args.reps)
-        b = 18.5 * y.numel()
+        b = (18.5 if eb == 4 else 9.5) * y.numel()
         tp += t
         bp += b
         print(f'{name:8s} {n:3d} {s:4d} {co:5d} | {t:13.3f} {b / t / 1e9:5.2f}', flush=True)
