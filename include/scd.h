@@ -171,7 +171,8 @@ int scd_abi_version(void);
 #define SCD_TUNE_WGRAD_R64        (1u << 10)  /* halo weight grad: 64-row blocks instead of 128                   */
 #define SCD_TUNE_BF16_1XN         (1u << 11)  /* flips the bf16 arithmetic's 3x3 tile layout: 1 x N wave tiles (as h2;
                                                  the default with bf16 storage) <-> 2 x 2 (the default with fp32)     */
-#define SCD_TUNE_X3_TILE(t)       ((uint32_t)(t) << 12)   /* per-tap x3 igemm tile 1..5 (0 = automatic)          */
+#define SCD_TUNE_X3_TILE(t)       ((uint32_t)(t) << 12)   /* per-tap x3 igemm tile 1..5 (0 = automatic); on the ConvT
+                                                            gather kernel tile 1..3 (128x128, 128x64, 64x128)    */
 #define SCD_TUNE_X3_TILE_MASK     (0xFu << 12)
 #define SCD_TUNE_C16_TILES(k)     ((uint32_t)(k) << 16)   /* input-layer forward: tiles per block (0 = 4; 15 =
                                                              one resident round)                                 */

@@ -345,6 +345,9 @@ int gather16_pick(const IgemmArgs &a) {
         (a.bias && (reinterpret_cast<uintptr_t>(a.bias) & 15)) || (a.store_mode != 0 && a.store_mode != 1) ||
         (a.store_mode == 1 && (a.cout % 4 || a.n_out != 4 * a.cout)) || 2 * a.wplane * 2 >= (int64_t(1) << 31))
         return 0;
+    // SCD_TUNE_X3_TILE(1..3) forces tile 0..2 here (tile study, tools/perf_convT.py --math h2)
+    const int forced = int((a.tune & SCD_TUNE_X3_TILE_MASK) >> 12);
+    if (forced >= 1 && forced <= 3) return forced;
     if (a.n_out % 128) return 2;  // 128 x 64
     const int64_t big = int64_t((a.M + 127) / 128) * (a.n_out / 128);
     return big >= 512 ? 1 : 3;  // 64 x 128 when 128 x 128 tiles leave CUs idle (two blocks per CU)
