@@ -324,6 +324,7 @@ template <class T>
 struct DaPlain {  // a materialised tensor
     const T *da;
     int ldda;
+    __device__ __forceinline__ void bind(int) {}
     __device__ __forceinline__ f4 operator()(int64_t p, int c) const { return ld4(da + p * ldda + c); }
 };
 // The encoder level's gradient, formed on the fly with the expressions of feature_grad_kernel (misc_f32.hip):
@@ -343,6 +344,7 @@ struct DaPooled {
     int ldgs2;
     int hx, wx, C;
     FastDiv div_hw, div_w, div_gsn;
+    __device__ __forceinline__ void bind(int) {}
     __device__ __forceinline__ f4 operator()(int64_t p, int c) const {
         const uint32_t img = fdiv(uint32_t(p), div_hw);
         const uint32_t rr = uint32_t(p) - img * uint32_t(hx * wx);
@@ -391,6 +393,7 @@ struct DaHead {
     const float *w;  // [n_out][C]
     int n_out, C, hw;
     FastDiv div_hw;
+    __device__ __forceinline__ void bind(int) {}
     __device__ __forceinline__ f4 operator()(int64_t p, int c) const {
         const uint32_t img = fdiv(uint32_t(p), div_hw);
         const int pix = int(uint32_t(p) - img * uint32_t(hw));
@@ -402,6 +405,37 @@ struct DaHead {
             r.y = fmaf(gv, wr[1], r.y);
             r.z = fmaf(gv, wr[2], r.z);
             r.w = fmaf(gv, wr[3], r.w);
+        }
+        return r;
+    }
+};
+
+// DaHead with the head count a compile-time constant and the thread's weight quads held in registers (bind, once per
+// thread): the per-pixel loop is branch-free and a pixel's NO gradient loads issue together.  With a runtime count
+// the loop branched per head and re-loaded the weights per pixel (the stores to dy may alias them), which held the
+// 3- and 4-head bf16 passes of the dual-stream / WhateverNet heads at 1.3-2.2 TB/s.  Same fma chain (bit-identical).
+template <int NO>
+struct DaHeadN {
+    DaHead d;
+    f4 w[NO];
+    __device__ __forceinline__ void bind(int c) {
+#pragma unroll
+        for (int o = 0; o < NO; ++o) w[o] = c < d.C ? ld4(d.w + int64_t(o) * d.C + c) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    __device__ __forceinline__ f4 operator()(int64_t p, int c) const {
+        (void)c;
+        const uint32_t img = fdiv(uint32_t(p), d.div_hw);
+        const int pix = int(uint32_t(p) - img * uint32_t(d.hw));
+        float gv[NO];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) gv[o] = d.g[(int64_t(img) * NO + o) * d.hw + pix];
+        f4 r = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            r.x = fmaf(gv[o], w[o].x, r.x);
+            r.y = fmaf(gv[o], w[o].y, r.y);
+            r.z = fmaf(gv[o], w[o].z, r.z);
+            r.w = fmaf(gv[o], w[o].w, r.w);
         }
         return r;
     }
@@ -811,6 +845,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const T *__restrict
     const int c = (blockIdx.y * qpb + q) * 4;
     const Chunk ch = chunk_of(pseg, ncps, chunk);
     f4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = s1;
+    da.bind(c);
     if (c < C) {
         const int o = ch.seg * C + c;
         const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
@@ -860,40 +895,42 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial(const T *__restrict
 //   hrec[o][c][chunk] = sum_p gout[o](p) * relu(fma(y, scale, shift))(p, c)
 // (what weighted_channel_sum's chan_sum_partial summed in a pass of its own over y; same chunks, per-thread order and
 // tree).  The gradient values g_o(p) are loaded once per pixel for both the head's dL/da and the weight grad.
-template <class T>
+template <class T, int NO>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial_head(const T *__restrict__ y, int ldy, DaHead da, int C,
                                                                   int64_t pseg, int ncps, int chunk, int nrec, int qpb,
                                                                   const float *smean, const float *sinv,
                                                                   const float *scale, const float *shift,
                                                                   float *__restrict__ rec, float *__restrict__ hrec) {
-    __shared__ f4 sh1[BN_THREADS], sh2[BN_THREADS], shh[4][BN_THREADS];
+    __shared__ f4 sh1[BN_THREADS], sh2[BN_THREADS], shh[NO][BN_THREADS];
     const int tid = threadIdx.x;
     const int q = tid % qpb, pl = tid / qpb, npl = BN_THREADS / qpb;
     const int c = (blockIdx.y * qpb + q) * 4;
     const Chunk ch = chunk_of(pseg, ncps, chunk);
     const f4 zero = {0.f, 0.f, 0.f, 0.f};
-    f4 s1 = zero, s2 = zero, hw[4] = {zero, zero, zero, zero};
+    f4 s1 = zero, s2 = zero, hw[NO];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) hw[k] = zero;
     if (c < C) {
         const int o = ch.seg * C + c;
         const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
-        f4 w4[4];
+        f4 w4[NO];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) w4[k] = k < da.n_out ? ld4(da.w + int64_t(k) * C + c) : zero;
+        for (int k = 0; k < NO; ++k) w4[k] = ld4(da.w + int64_t(k) * C + c);
         // one pixel: its n_out gradient values, dL/da (DaHead's fma chain) and the activation
-        auto px = [&](int64_t p, f4 yv, f4 (&gk)[4]) {
+        auto px = [&](int64_t p, f4 yv, f4 (&gk)[NO]) {
             const uint32_t img = fdiv(uint32_t(p), da.div_hw);
             const int pix = int(uint32_t(p) - img * uint32_t(da.hw));
+            float gv[NO];
+#pragma unroll
+            for (int k = 0; k < NO; ++k) gv[k] = da.g[(int64_t(img) * NO + k) * da.hw + pix];
             f4 r = zero;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float gv = k < da.n_out ? da.g[(int64_t(img) * da.n_out + k) * da.hw + pix] : 0.f;
-                gk[k] = f4{gv, gv, gv, gv};
-                if (k < da.n_out) {
-                    r.x = fmaf(gv, w4[k].x, r.x);
-                    r.y = fmaf(gv, w4[k].y, r.y);
-                    r.z = fmaf(gv, w4[k].z, r.z);
-                    r.w = fmaf(gv, w4[k].w, r.w);
-                }
+            for (int k = 0; k < NO; ++k) {
+                gk[k] = f4{gv[k], gv[k], gv[k], gv[k]};
+                r.x = fmaf(gv[k], w4[k].x, r.x);
+                r.y = fmaf(gv[k], w4[k].y, r.y);
+                r.z = fmaf(gv[k], w4[k].z, r.z);
+                r.w = fmaf(gv[k], w4[k].w, r.w);
             }
             return r;
         };
@@ -901,7 +938,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial_head(const T *__res
         for (; p + 3 * npl < ch.end; p += 4 * npl) {
             f4 y0 = ld4(y + p * ldy + c), y1 = ld4(y + (p + npl) * ldy + c);
             f4 y2 = ld4(y + (p + 2 * npl) * ldy + c), y3 = ld4(y + (p + 3 * npl) * ldy + c);
-            f4 k0[4], k1[4], k2[4], k3[4];
+            f4 k0[NO], k1[NO], k2[NO], k3[NO];
             f4 g0 = px(p, y0, k0), g1 = px(p + npl, y1, k1);
             f4 g2 = px(p + 2 * npl, y2, k2), g3 = px(p + 3 * npl, y3, k3);
             PIN4(y0, y1, y2, y3);
@@ -913,33 +950,30 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial_head(const T *__res
             const f4 a0 = bn_relu4(y0, sc, sf), a1 = bn_relu4(y1, sc, sf);
             const f4 a2 = bn_relu4(y2, sc, sf), a3 = bn_relu4(y3, sc, sf);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < da.n_out) hw[k] += (a0 * k0[k] + a1 * k1[k]) + (a2 * k2[k] + a3 * k3[k]);
+            for (int k = 0; k < NO; ++k) hw[k] += (a0 * k0[k] + a1 * k1[k]) + (a2 * k2[k] + a3 * k3[k]);
         }
         for (; p < ch.end; p += npl) {
             const f4 y0 = ld4(y + p * ldy + c);
-            f4 k0[4];
+            f4 k0[NO];
             const f4 z0 = relu_mask(y0, sc, sf, px(p, y0, k0));
             s1 += z0;
             s2 += z0 * ((y0 - mu) * iv);
             const f4 a0 = bn_relu4(y0, sc, sf);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < da.n_out) hw[k] += a0 * k0[k];
+            for (int k = 0; k < NO; ++k) hw[k] += a0 * k0[k];
         }
     }
     sh1[tid] = s1;
     sh2[tid] = s2;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) shh[k][tid] = hw[k];
+    for (int k = 0; k < NO; ++k) shh[k][tid] = hw[k];
     __syncthreads();
     for (int off = npl / 2; off > 0; off >>= 1) {
         if (pl < off) {
             sh1[tid] += sh1[tid + off * qpb];
             sh2[tid] += sh2[tid + off * qpb];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < da.n_out) shh[k][tid] += shh[k][tid + off * qpb];
+            for (int k = 0; k < NO; ++k) shh[k][tid] += shh[k][tid + off * qpb];
         }
         __syncthreads();
     }
@@ -952,7 +986,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial_head(const T *__res
             r[0] = av[k];
             r[1] = bv[k];
         }
-        for (int o = 0; o < da.n_out; ++o) {
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
             const f4 h = shh[o][tid];
             const float hv[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
@@ -1060,6 +1095,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply(const T *__restrict__
     const Chunk ch = chunk_of(pseg, ncps, chunk);
     f4 acc = {0.f, 0.f, 0.f, 0.f};
     f4 amax = acc;  // max |dy| of this thread (dy_bound)
+    da.bind(c);
     if (c < C) {
         const int o = ch.seg * C + c;
         const f4 mu = ld4(smean + o), iv = ld4(sinv + o), sc = ld4(scale + o), sf = ld4(shift + o);
@@ -1378,7 +1414,7 @@ static void bn_backward_run(const scd_nhwc_t &y, DA da, int nseg, const float *s
 }
 // The head's BatchNorm backward (DaHead) with the head's weight grad from the same partial pass (w_grad non-null):
 // hrec after the usual records (scd_bn_head_workspace_bytes).
-template <class T>
+template <class T, int NO>
 static void bn_backward_run_head(const scd_nhwc_t &y, const DaHead &da, int nseg, const float *save_mean,
                                  const float *save_invstd, const float *gamma, const float *scale, const float *shift,
                                  float *dgamma, float *dbeta, float *dbias_prev, const scd_nhwc_t &dy, float *dy_bound,
@@ -1389,13 +1425,13 @@ static void bn_backward_run_head(const scd_nhwc_t &y, const DaHead &da, int nseg
     float *coef = brec + size_t(g.nrec) * y.c;
     float *hrec = reinterpret_cast<float *>(static_cast<unsigned char *>(ws) +
                                             scd_bn_workspace_bytes(y.n, y.h, y.w, y.c, nseg));
-    hipLaunchKernelGGL(bn_bwd_partial_head<T>, dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+    hipLaunchKernelGGL((bn_bwd_partial_head<T, NO>), dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
                        view_ptr<const T>(y), y.ldc, da, y.c, g.pseg, g.ncps, g.chunk, g.nrec, g.qpb,
                        save_mean, save_invstd, scale, shift, rec, hrec);
     hipLaunchKernelGGL(bn_bwd_finalize, dim3(y.c), dim3(BN_THREADS), 0, s, rec, y.c, nseg, g.ncps, g.nrec, g.pseg,
                        coef, dgamma, dbeta);
-    hipLaunchKernelGGL((bn_bwd_apply<T, DaHead>), dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
-                       view_ptr<const T>(y), y.ldc, da, view_ptr<T>(dy), dy.ldc, y.c,
+    hipLaunchKernelGGL((bn_bwd_apply<T, DaHeadN<NO>>), dim3(g.nrec, g.cgroups), dim3(BN_THREADS), 0, s,
+                       view_ptr<const T>(y), y.ldc, DaHeadN<NO>{da, {}}, view_ptr<T>(dy), dy.ldc, y.c,
                        g.pseg, g.ncps, g.chunk, g.nrec, g.qpb, save_mean, save_invstd, gamma, scale, shift, coef,
                        dbias_prev ? brec : nullptr, dy_bound);
     if (dbias_prev) hipLaunchKernelGGL(sum_records, dim3(y.c), dim3(BN_THREADS), 0, s, brec, g.nrec, dbias_prev);
@@ -1541,14 +1577,23 @@ extern "C" int scd_bn_relu_backward_head(scd_nhwc_t y, const float *gout, const 
     const DaHead da{gout, w_head, n_out, y.c, y.h * y.w, make_fastdiv(uint32_t(y.h * y.w))};
     const int dt = common_dtype("bn_relu_backward_head", {&y, &dy});
     if (dt < 0) return SCD_ERR_ARG;
-    if (w_grad) {
-        SCD_WITH_T(dt, T,
-                   bn_backward_run_head<T>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta,
-                                           dbias_prev, dy, dy_bound, w_grad, ws, as_stream(stream)));
-    } else {
-        SCD_WITH_T(dt, T,
-                   bn_backward_run<T>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma, dbeta,
-                                      dbias_prev, dy, dy_bound, ws, as_stream(stream)));
+    auto run = [&](auto no) {
+        constexpr int NO = decltype(no)::value;
+        if (w_grad) {
+            SCD_WITH_T(dt, T,
+                       (bn_backward_run_head<T, NO>(y, da, nseg, save_mean, save_invstd, gamma, scale, shift, dgamma,
+                                                    dbeta, dbias_prev, dy, dy_bound, w_grad, ws, as_stream(stream))));
+        } else {
+            SCD_WITH_T(dt, T,
+                       bn_backward_run<T>(y, DaHeadN<NO>{da, {}}, nseg, save_mean, save_invstd, gamma, scale, shift,
+                                          dgamma, dbeta, dbias_prev, dy, dy_bound, ws, as_stream(stream)));
+        }
+    };
+    switch (n_out) {
+        case 1: run(std::integral_constant<int, 1>{}); break;
+        case 2: run(std::integral_constant<int, 2>{}); break;
+        case 3: run(std::integral_constant<int, 3>{}); break;
+        default: run(std::integral_constant<int, 4>{}); break;
     }
     return launch_status("scd_bn_relu_backward_head");
 }

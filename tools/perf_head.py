@@ -6,6 +6,8 @@ Cases: the Siamese head (fp32, bs=32, through the last BatchNorm), the dual-task
 two BatchNorm segments), DualStream's fusion head (bf16, bs=64, two decoders) and WhateverNet's three heads in one
 launch (bf16, bs=16 at 512^2, two decoders).  TB/s counts the bytes read (the activations) plus the logits written.
 Round 4 (the bench step, rocprof): Siamese 156 us, DualStream 505 us (2.1 TB/s), WhateverNet 780 us (1.4 TB/s).
+Then, per case and source, the head's BatchNorm backward (scd_bn_relu_backward_head with the head's weight grad, the
+call HeadsFn makes): TB/s counts y read twice (partial and apply passes), the head gradient read twice, dy written.
 """
 import argparse
 import os
@@ -55,6 +57,21 @@ def main():
         t = bench(fn, args.reps)
         nbytes = sum(y.numel() * y.element_size() for y in ys) + o.numel() * 4
         print(f'{name:40s} {t * 1e3:8.1f} us  {nbytes / t / 1e9:5.2f} TB/s', flush=True)
+        y = ys[0]
+        gout = torch.randn(n, nout, s, s, device=dev) * 1e-3
+        wh = torch.randn(nout, 64, device=dev)
+        sm, si = torch.randn(nseg * 64, device=dev), torch.rand(nseg * 64, device=dev) + 0.5
+        gm = torch.rand(64, device=dev) + 0.5
+        dg, db, dbias = torch.empty(64, device=dev), torch.empty(64, device=dev), torch.empty(64, device=dev)
+        wg = torch.empty(nout, 64, device=dev)
+        dy = torch.empty_like(y)
+        ws = torch.empty(hip.bn_head_workspace_bytes(n, s, s, 64, nseg, nout), dtype=torch.uint8, device=dev)
+        fb = lambda: hip.bn_relu_backward_head(hip.nhwc(y), gout, wh, nout, nseg, sm, si, gm, sc[0], sh[0], dg, db,  # noqa: E731
+                                               dbias, hip.nhwc(dy), ws, w_grad=wg)
+        tb = bench(fb, args.reps)
+        bb = 3 * y.numel() * y.element_size() + 2 * gout.numel() * 4
+        print(f'{"  backward (one source, " + str(nout) + " heads)":40s} {tb * 1e3:8.1f} us  {bb / tb / 1e9:5.2f} TB/s',
+              flush=True)
 
 
 if __name__ == '__main__':
