@@ -149,8 +149,10 @@ enum scd_conv_math {
  *      the 16-channel-source weight grad runs h2 when both scd_wgrad_t bounds are set.
  *   6: scd_nhwc_t.dtype: bf16 activation / gradient storage (the bf16 configs), every NHWC kernel.
  *   7: scd_bn_relu_pool_out (plain and dual-task encoder levels written into the decoders' concat buffers),
- *      scd_bn_relu_backward_pooled2 (a second, swapped skip gradient), scd_conv1x1_fwd_bn2 (two-source heads). */
-#define SCD_ABI_VERSION 7
+ *      scd_bn_relu_backward_pooled2 (a second, swapped skip gradient), scd_conv1x1_fwd_bn2 (two-source heads).
+ *   8: scd_wgrad_t.rows_out / rows_out_bound appended (the halo weight grad forms and stores a plain BatchNorm
+ *      backward's dY). */
+#define SCD_ABI_VERSION 8
 int scd_abi_version(void);
 /* The arithmetic scd_conv_igemm / scd_conv_wgrad will use for a descriptor (its `math`, or SCD_MATH_X3 / F32 where
  * the shape or the missing operand bounds keep the conv off the requested kernels); negative = invalid descriptor.
@@ -336,6 +338,12 @@ typedef struct scd_wgrad {
      * every output pixel gathered by exactly one tap) scd_wgrad_colsum_finalize turns it into the bias grad, so dOut
      * is not read again for it.  NULL = off.  Only where scd_wgrad_colsum_supported() returns 1. */
     float *src_colsum;
+    /* ABI 8, with rows_y set on the 64-channel-multiple halo weight grad: the formed dY is also stored here (same n,
+     * h, w, c and dtype as rows), every element once, exactly as scd_bn_relu_backward would write it, and
+     * rows_out_bound (device float, may be NULL) is raised to max |dY| stored -- the data grad that reads dY next
+     * then needs no BatchNorm-backward apply pass (networks.py:392-397 backward).  rows_out.data NULL = off. */
+    scd_nhwc_t rows_out;
+    float *rows_out_bound;
 } scd_wgrad_t;
 
 /* Number of K-splits the library will use and the slab bytes it needs. */
@@ -347,7 +355,9 @@ int scd_wgrad_rows_per_block(const scd_wgrad_t *d);
 int scd_conv_wgrad(const scd_wgrad_t *d, float *slabs, size_t slab_bytes, scd_stream_t stream);
 /* 1 if the weight-grad kernel scd_conv_wgrad would run for `d` applies the src_scale/src_shift transform. */
 int scd_wgrad_src_bn_supported(const scd_wgrad_t *d);
-/* 1 if it forms the rows through the fused BatchNorm backward (scd_wgrad_t.rows_y): the 16-channel-source kernel. */
+/* 1 if it forms the rows through the fused BatchNorm backward (scd_wgrad_t.rows_y): the 16-channel-source kernel,
+ * and (ABI 8) the 64-channel-multiple halo weight grad in bf16 or in h2 with 128-row blocks (both bounds set in `d`),
+ * at most 2 rows segments per launch; those also store dY (rows_out). */
 int scd_wgrad_rows_bn_supported(const scd_wgrad_t *d);
 /* Sum the slabs (deterministic fixed-order two-level reduction; the slabs are scratch and are
  * overwritten) and unpack to the parameter layout.

@@ -99,13 +99,19 @@ struct WgradArgs {
     const float *src_scale, *src_shift;  // optional fused src BN-apply + ReLU (halo16 weight grad only)
     int src_seg_imgs;
     const float *rows_bound, *src_bound;  // SCD_MATH_H2: upper bounds of |rows| and |src| (as read), both or neither
-    // optional fused BatchNorm + ReLU backward of the rows (16-channel-source weight grad only): rows hold dL/da,
-    // the kernel forms dy = bn_bwd_dy4(y, da, ...) while staging; coefficients per segment of rows_seg_imgs images
+    // optional fused BatchNorm + ReLU backward of the rows (the 16-channel-source weight grad, and the halo weight
+    // grad in its h2 / bf16 along-c layouts): rows hold dL/da, the kernel forms dy = bn_bwd_dy4(y, da, ...) while
+    // staging; coefficients per segment of rows_seg_imgs images
     const float *rows_y;
     int ldc_y;
     uint32_t y_bytes;
     const float *rbn_mean, *rbn_inv, *rbn_gamma, *rbn_scale, *rbn_shift, *rbn_coef;
     int rows_seg_imgs;
+    // optional (halo weight grad with rows_y): the formed dy also written here (ldc_o), once, by the blocks of channel
+    // tile 0, and rows_out_bound raised to max |dy| stored (the data grad's h2 operand bound)
+    void *rows_out;
+    int ldc_o;
+    float *rows_out_bound;
     int math;       // SCD_MATH_* of this launch (scd_wgrad_t.math)
     uint32_t tune;  // SCD_TUNE_* bits (scd_wgrad_t.tune)
     int sb;         // 1: rows, src and rows_y are bf16 views (ABI 6)
@@ -132,6 +138,8 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s);
 // 16x16x32-MFMA halo weight grad (conv_halo16.hip).
 const void *wgrad_halo16_fn(int math, uint32_t tune, bool bounded, int rblock);  // bounded: h2 under SCD_MATH_H2
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s);
+// Whether the halo weight grad forms its rows through the BatchNorm backward (WgradArgs.rows_y) for this arithmetic.
+bool wgrad16_rows_bn_ok(int math, uint32_t tune, bool bounded);
 // dY rows per block of the halo weight grad (64 or 128; threads = 4 * rows): plan and launch use the same value.
 int wgrad16_rblock(int math, uint32_t tune, int R, bool bounded);
 // 16-channel-source variant (the input layer), same eligibility otherwise (conv_halo16.hip).

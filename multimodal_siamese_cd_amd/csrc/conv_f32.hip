@@ -999,6 +999,13 @@ static bool wgrad_c16_ok(const scd_wgrad_t *d) {
 
 // Both operands bounded: the h2 weight grad under SCD_MATH_H2 (x3 otherwise).
 static bool wgrad_bounded(const scd_wgrad_t *d) { return d->rows_bound && d->src_bound; }
+// The halo weight grad with the rows' BatchNorm backward (rows_y) and the dY store (rows_out): its bf16 and h2 along-c
+// variants; h2 in 128-row blocks only (the 64-row h2 block would spill), at most two rows segments per launch.
+static bool wgrad_halo_rbn_ok(const scd_wgrad_t *d) {
+    if (!wgrad_halo_ok(d) || !wgrad16_rows_bn_ok(d->math, d->tune, wgrad_bounded(d))) return false;
+    if (d->math == SCD_MATH_H2 && wgrad_halo_rblock(d->math, d->tune, d->rows.c, true) != 128) return false;
+    return !d->rows_y.data || (d->rows_nseg >= 1 && d->rows_nseg <= 2);
+}
 // The generic (non-halo) weight grad in h2: bounded, SCD_MATH_H2, a tile with an h2 instantiation.
 // SCD_TUNE_NO_WGRAD_H2 keeps it on x3 (A/B).
 static bool wgrad_generic_h2(const scd_wgrad_t *d) {
@@ -1079,7 +1086,7 @@ extern "C" int scd_wgrad_src_bn_supported(const scd_wgrad_t *d) {
 extern "C" int scd_wgrad_rows_bn_supported(const scd_wgrad_t *d) {
     clear_error();
     if (wgrad_validate(d) != SCD_OK) return 0;
-    return wgrad_c16_ok(d) ? 1 : 0;
+    return wgrad_c16_ok(d) || wgrad_halo_rbn_ok(d) ? 1 : 0;
 }
 
 extern "C" int scd_wgrad_arith(const scd_wgrad_t *d) {
@@ -1136,6 +1143,7 @@ static scd_wgrad_t wgrad_slice(const scd_wgrad_t *d, int img0, int cnt) {
         c.rows_coef = d->rows_coef + 2 * o;
         c.rows_nseg = std::max(1, cnt / sg);
     }
+    if (d->rows_out.data) c.rows_out = img_slice(d->rows_out, img0, cnt);
     return c;
 }
 // Total K-splits over the image chunks (each chunk writes its own slab range; the finalize sums them all).
@@ -1265,8 +1273,8 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
             y.c != d->rows.c || y.ldc % 4 || d->rows_nseg < 1 || d->rows.n % d->rows_nseg || !d->rows_mean ||
             !d->rows_invstd || !d->rows_scale || !d->rows_shift || !d->rows_coef || !aligned16(d->rows_mean) ||
             !aligned16(d->rows_invstd) || !aligned16(d->rows_scale) || !aligned16(d->rows_shift) ||
-            !aligned16(d->rows_coef) || (d->rows_gamma && !aligned16(d->rows_gamma)) || !wgrad_c16_ok(d) ||
-            yb >= (int64_t(1) << 31)) {
+            !aligned16(d->rows_coef) || (d->rows_gamma && !aligned16(d->rows_gamma)) ||
+            !(wgrad_c16_ok(d) || wgrad_halo_rbn_ok(d)) || yb >= (int64_t(1) << 31)) {
             set_error("wgrad: the rows BatchNorm backward needs y shaped as rows, rows_nseg | rows.n, 16-byte "
                       "aligned coefficient arrays and a supported shape (check scd_wgrad_rows_bn_supported)");
             return SCD_ERR_ARG;
@@ -1281,6 +1289,22 @@ static int conv_wgrad_run(const scd_wgrad_t *d, float *slabs, size_t slab_bytes,
         a.rbn_shift = d->rows_shift;
         a.rbn_coef = d->rows_coef;
         a.rows_seg_imgs = d->rows.n / d->rows_nseg;
+    }
+    a.rows_out = nullptr;
+    a.ldc_o = 0;
+    a.rows_out_bound = nullptr;
+    if (d->rows_out.data) {
+        const scd_nhwc_t &o = d->rows_out;
+        if (!d->rows_y.data || !wgrad_halo_rbn_ok(d) || check_view(o, "wgrad.rows_out") != SCD_OK || o.n != d->rows.n ||
+            o.h != d->rows.h || o.w != d->rows.w || o.c != d->rows.c || o.dtype != d->rows.dtype || o.ldc % 4 ||
+            (reinterpret_cast<uintptr_t>(o.data) & (a.sb ? 7 : 15))) {
+            set_error("wgrad: rows_out needs rows_y on the halo weight grad (scd_wgrad_rows_bn_supported) and a view "
+                      "shaped and typed as rows, ldc %% 4 == 0, aligned");
+            return SCD_ERR_ARG;
+        }
+        a.rows_out = o.data;
+        a.ldc_o = o.ldc;
+        a.rows_out_bound = d->rows_out_bound;
     }
     if (d->src_scale || d->src_shift) {
         if (!d->src_scale || !d->src_shift || d->src_nseg < 1 || d->src.n % d->src_nseg ||

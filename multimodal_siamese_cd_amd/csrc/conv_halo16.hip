@@ -1654,9 +1654,15 @@ __device__ __forceinline__ void w16_chain(f32x4 (&acc)[9][W16L<LC>::CB][W16L<LC>
 // the partners of waves 0-3 on their SIMDs) stores the next patch BEFORE its MFMAs while the first group stores it
 // after them, so one wave of each SIMD pair stages while the other computes (a stagger: without it both reach
 // their split + LDS writes, and the matrix cores idle, together).
-template <int NP, int LC, int RG, bool SB = false, bool DB = false>
+// RBN: the rows are dL/da of a = relu(BN(y)) and every dY element is formed while staging (bn_bwd_dy4, the expression
+// of bn_bwd_apply: bit-identical values), with the BatchNorm coefficients of the block's rows held in LDS for both
+// segments; the blocks of channel tile 0 also store the formed dY (a.rows_out) for the data grad, which then reads
+// it as before: the separate BatchNorm-backward apply pass (read y and da, write dy) and this kernel's read of dy
+// become this kernel's read of y and da.
+template <int NP, int LC, int RG, bool SB = false, bool DB = false, bool RBN = false>
 __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a) {
     static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
+    static_assert(!RBN || (LC == 1 && !DB && (NP == 1 || NP == 4)), "rows transform: h2 / bf16, along-c layout");
     constexpr uint32_t EB = SB ? 2u : 4u;
     constexpr int NT = 256 * RG;
     constexpr int PH = 2, PW = 16, P = PH * PW;
@@ -1673,7 +1679,13 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
     constexpr int DP = w16_dp<NP>();  // dY planes
     constexpr int XP = w16_xp<NP>();  // X planes
     constexpr int STAGE = DP * PA + XP * PB;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[(DB ? 2 : 1) * STAGE];
+    constexpr int RBLK = 64 * RG;                      // dY rows of the block
+    constexpr int COEF = RBN ? 2 * 7 * RBLK * 4 : 0;   // RBN: [segment 2][7 coefficients][RBLK] floats
+    // RBN under h2: the y pieces come by LDS-DMA (16 B per lane) into a staging area instead of registers (the h2
+    // kernels sit at 256 VGPRs; eight more for y spilled the 64-row block)
+    constexpr bool YDMA = RBN && H2;
+    constexpr int YST = YDMA ? A_PER * NT * 16 : 0;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[(DB ? 2 : 1) * STAGE + COEF + YST];
     float ds = 1.f, ds_inv = 1.f, xs = 1.f, xs_inv = 1.f;  // h2: power-of-two operand scales
     if constexpr (H2) {
         h2_scale(*a.rows_bound, ds, ds_inv);
@@ -1696,10 +1708,16 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
 
     const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
+    const __amdgpu_buffer_rsrc_t rs_y = make_rsrc(RBN ? a.rows_y : a.rows, RBN ? a.y_bytes : 0u);
+    const bool writer = RBN && a.rows_out && ct == 0;  // block-uniform: this block stores its dY pieces
+    float omax = 0.f;                                  // RBN writer: max |dY| stored by this lane
 
-    StageT<SB> ra[A_PER], rb[B_PER];
+    StageT<SB> ra[A_PER], rb[B_PER], ya[RBN && !YDMA ? A_PER : 1];
+    unsigned char *const ystage = smem + (DB ? 2 : 1) * STAGE + COEF;  // YDMA: piece e of the patch at e * 16
+    const int wave_u = __builtin_amdgcn_readfirstlane(wid);
     f32x4 x_sc, x_sh;      // src transform coefficients of this thread's 4 channels (cq = tid & 15)
     uint32_t x_valid = 0;  // bit i: halo piece i is inside the image (the padding stays zero)
+    int st_img = 0, st_y0 = 0, st_x0 = 0;  // the patch whose pieces the staging registers hold
     auto load_patch = [&](int pi) {
         const int img = pi / pimg, pr = pi - img * pimg;
         if (a.src_scale) {
@@ -1709,12 +1727,20 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
         }
         x_valid = 0;
         const int y0 = patch_y0(pr, pw_n, ph_n, PH), x0 = patch_x0(pr, pw_n, ph_n, PW);
+        st_img = img;
+        st_y0 = y0;
+        st_x0 = x0;
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * NT, q = e / CQ, cq = e % CQ;
             const int py = q >> 4, px = q & 15;
-            const uint32_t off = uint32_t(((img * a.ho + y0 + py) * a.wo + x0 + px) * a.ldc_r + r0 + cq * 4) * EB;
-            ra[i] = bload_q<SB>(rs_rows, off);
+            const int pix = (img * a.ho + y0 + py) * a.wo + x0 + px;
+            if constexpr (YDMA)  // issued before the rows loads: waiting for those (in order) retires it too
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void *)(a.rows_y + size_t(pix) * a.ldc_y + r0 + cq * 4),
+                    (__attribute__((address_space(3))) void *)(ystage + (i * NT + wave_u * 64) * 16), 16, 0, 0);
+            ra[i] = bload_q<SB>(rs_rows, uint32_t(pix * a.ldc_r + r0 + cq * 4) * EB);
+            if constexpr (RBN && !YDMA) ya[i] = bload_q<SB>(rs_y, uint32_t(pix * a.ldc_y + r0 + cq * 4) * EB);
         }
 #pragma unroll
         for (int i = 0; i < B_PER; ++i) {
@@ -1731,11 +1757,47 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
         // h2: the scale folds into the transform exactly; applied here, not behind the coefficient loads, where the
         // compiler waited for them (vmcnt in order: the wave stalled at issue)
         const f32x4 sc = H2 ? x_sc * xs : x_sc, sh = H2 ? x_sh * xs : x_sh;
+        if constexpr (YDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this patch's y pieces have landed
 #pragma unroll
         for (int i = 0; i < A_PER; ++i) {
             const int e = tid + i * NT;
             const int o = (e / CQ) * RSD + (e % CQ) * 8;
             u32x2 h, m, l;
+            if constexpr (RBN) {
+                // dY of this piece from y and dL/da: bn_bwd_apply's expression (stored4: one rounding to the storage
+                // type), the writer blocks store it, then it is staged as a plain dY piece
+                const int cq = e % CQ, q = e / CQ;
+                const float *cf = reinterpret_cast<const float *>(smem + (DB ? 2 : 1) * STAGE) +
+                                  (st_img / a.rows_seg_imgs) * 7 * RBLK + cq * 4;
+                const f32x4 mu = *reinterpret_cast<const f32x4 *>(cf), iv = *reinterpret_cast<const f32x4 *>(cf + RBLK);
+                const f32x4 sc = *reinterpret_cast<const f32x4 *>(cf + 2 * RBLK);
+                const f32x4 sf = *reinterpret_cast<const f32x4 *>(cf + 3 * RBLK);
+                const f32x4 k1 = *reinterpret_cast<const f32x4 *>(cf + 4 * RBLK);
+                const f32x4 k2 = *reinterpret_cast<const f32x4 *>(cf + 5 * RBLK);
+                const f32x4 mul = *reinterpret_cast<const f32x4 *>(cf + 6 * RBLK);
+                f32x4 yv;
+                if constexpr (YDMA)
+                    yv = *reinterpret_cast<const f32x4 *>(ystage + e * 16);
+                else
+                    yv = stage_f32<SB>(ya[i]);
+                f32x4 dv = bn_bwd_dy4(yv, stage_f32<SB>(ra[i]), mu, iv, sc, sf, k1, k2, mul);
+                if constexpr (SB) {
+                    const u32x2 bits = pk_bf16x4(dv);
+                    ra[i] = bits;
+                    dv = unpk_bf16x4(bits);
+                } else {
+                    ra[i] = dv;
+                }
+                if (writer) {
+                    const int pix = (st_img * a.ho + st_y0 + (q >> 4)) * a.wo + st_x0 + (q & 15);
+                    const size_t idx = size_t(pix) * a.ldc_o + r0 + cq * 4;
+                    if constexpr (SB)
+                        *reinterpret_cast<u32x2 *>(static_cast<unsigned short *>(a.rows_out) + idx) = ra[i];
+                    else
+                        gstore4(static_cast<float *>(a.rows_out) + idx, dv);
+                    omax = fmaxf(omax, fmaxf(fmaxf(fabsf(dv[0]), fabsf(dv[1])), fmaxf(fabsf(dv[2]), fabsf(dv[3]))));
+                }
+            }
             if constexpr (H2) {
                 if constexpr (NP == 4)
                     split2h_pre(ra[i] * ds, h, m);
@@ -1807,6 +1869,23 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
     const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RSD + (16 * NRB * wi + 4 * (w16 & 3)) * 2;
     const uint32_t xbase = lds_addr(smem) + DP * PA + (py * HW_ + pxq) * RS + (16 * NCB * wj + 4 * (w16 & 3)) * 2;
 
+    if constexpr (RBN) {  // the block's rows' BatchNorm coefficients, both segments (launcher: at most 2 per launch)
+        float *cf = reinterpret_cast<float *>(smem + (DB ? 2 : 1) * STAGE);
+        const int nsl = a.n_img_w / a.rows_seg_imgs;
+        for (int e = tid; e < nsl * RBLK; e += NT) {
+            const int sg = e / RBLK, r = e - sg * RBLK, o = sg * a.R + r0 + r;
+            const float iv = a.rbn_inv[o];
+            float *c = cf + sg * 7 * RBLK + r;
+            c[0] = a.rbn_mean[o];
+            c[RBLK] = iv;
+            c[2 * RBLK] = a.rbn_scale[o];
+            c[3 * RBLK] = a.rbn_shift[o];
+            c[4 * RBLK] = a.rbn_coef[2 * o];
+            c[5 * RBLK] = a.rbn_coef[2 * o + 1];
+            c[6 * RBLK] = (a.rbn_gamma ? a.rbn_gamma[r0 + r] : 1.f) * iv;  // bn_bwd_apply's mul = gamma * invstd
+        }
+        __syncthreads();
+    }
     if (pbeg < pend) {
         // DB, RG 2: waves 4-7 stage the next patch before their MFMAs (loads two patches ahead), waves 0-3 after
         const bool early = DB && RG == 2 && __builtin_amdgcn_readfirstlane(wid) >= 4;
@@ -1852,6 +1931,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
 #pragma unroll
                 for (int r = 0; r < NRB; ++r) acc[t][cb][r] *= k;
     }
+    if (writer && a.rows_out_bound) wave_max_bound(a.rows_out_bound, omax);  // uniform: the whole block takes part
     // acc[t][cb][rb][q]: r = r0 + 16 NRB wi + 16rb + (lane & 15), c = c0 + 16 NCB wj + 16cb + 4g + q
     float *slab = a.slabs + size_t(split) * a.R * a.Ng;
 #pragma unroll
@@ -2223,10 +2303,32 @@ const void *wgrad_halo16_fn(int math, uint32_t tune, bool bounded, int rblock) {
         default: return reinterpret_cast<const void *>(&wgrad_halo16_x3<3, 0, 1>);
     }
 }
+// The rows transform (a.rows_y): h2 with the pre-scaled low term, or bf16, in the along-c layout
+// (wgrad16_rows_bn_ok); both row-block sizes.
+template <int NP, bool SB>
+static void w16_launch_rbn(int rb, const WgradArgs &a, dim3 grid, hipStream_t s) {
+    if (rb == 128)
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 2, SB, false, true>), grid, dim3(512), 0, s, a);
+    else
+        hipLaunchKernelGGL((wgrad_halo16_x3<NP, 1, 1, SB, false, true>), grid, dim3(256), 0, s, a);
+}
+bool wgrad16_rows_bn_ok(int math, uint32_t tune, bool bounded) {
+    const int np = wgrad16_planes(math, tune, bounded);
+    return (np == 1 || np == 4) && w16_layout(tune) && !(tune & SCD_TUNE_WGRAD16_DB);
+}
 // a.grid_r = R / wgrad16_rblock(...) (the caller plans with the same choice).
 void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
     const bool bounded = a.rows_bound && a.src_bound;
     const int lc = w16_layout(a.tune), rb = wgrad16_rblock(a.math, a.tune, a.R, bounded);
+    if (a.rows_y) {  // the caller checked wgrad16_rows_bn_ok
+        if (wgrad16_planes(a.math, a.tune, bounded) == 4)
+            w16_launch_rbn<4, false>(rb, a, grid, s);
+        else if (a.sb)
+            w16_launch_rbn<1, true>(rb, a, grid, s);
+        else
+            w16_launch_rbn<1, false>(rb, a, grid, s);
+        return;
+    }
     switch (wgrad16_planes(a.math, a.tune, bounded)) {
         case 1:
             if (a.sb)

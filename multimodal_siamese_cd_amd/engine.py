@@ -34,7 +34,12 @@ _F32 = torch.float32
 _OPTS = {'fuse_input_bn': True, 'fuse_bn_bwd': True, 'fuse_siamese_encoder': True, 'batch_pack': True,
          'pack_cache': True, 'pool_diff': True, 'pooled_bn_bwd': True, 'defer_bn_bwd': True, 'fuse_head': True,
          'convT_bias_in_wgrad': True, 'head_wgrad_in_bn_bwd': True, 'fuse_plain_encoder': True,
-         'fuse_dualtask': True, 'dt_sem_batched': True, 'fuse_heads': True}
+         'fuse_dualtask': True, 'dt_sem_batched': True, 'fuse_heads': True, 'bn_bwd_in_wgrad': 128}
+# bn_bwd_in_wgrad: the widest weight-grad source (channels) whose conv's plain BatchNorm backward is formed inside the
+# weight grad (0 = never).  Wider sources are split over more 64-channel tiles that each read the rows again, and
+# reading y and da instead of dy there cost more than the apply pass saved.  Same-process A/B
+# (profiles/r05_bn_bwd_in_wgrad_ab.txt): Siamese bs=32 off 30.05, <= 64 30.02, <= 128 29.81 ms; dual-stream bs=64 off
+# 41.89, <= 64 41.62, <= 128 41.63 ms, no limit 42.30 (vs 41.80 off).
 
 
 def conv_math_for(cfg) -> str:
@@ -75,6 +80,8 @@ def set_options(**kw) -> dict:
     instead of two calls (same per-call statistics and running-stat order; weight grads summed in another order).
     fuse_heads: the two-decoder models' heads (DualStream's outc, WhateverNet(2)'s outc_stream1/2 + outc_fusion) run as
     one launch over both decoders' last BatchNorm + ReLU (no cat, no materialised decoder outputs).
+    bn_bwd_in_wgrad (int, channels): a plain BatchNorm backward whose conv's weight-grad source has at most this many
+    channels is formed inside that weight grad, which also stores dy for the data grad (ABI 8): no apply pass; 0 = off.
     Returns the previous options."""
     prev = dict(_OPTS)
     for k, v in kw.items():
@@ -511,11 +518,13 @@ def _dc_forward(x: torch.Tensor, dc, nseg: int, training: bool, save: bool, mate
 
 
 def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor, src_bn=None, rows_bound=None,
-              src_bound=None, rows_bn=None) -> torch.Tensor:
-    """`rows_bn` (hip._rows_bn_fields): dy is dL/da, formed into the BatchNorm backward's dy while staging."""
+              src_bound=None, rows_bn=None, rows_out=None, rows_out_bound=None) -> torch.Tensor:
+    """`rows_bn` (hip._rows_bn_fields): dy is dL/da, formed into the BatchNorm backward's dy while staging;
+    `rows_out` then receives that dy (and `rows_out_bound` its max |dy|) for the data grad."""
     if rows_bound is None or src_bound is None:
         rows_bound = src_bound = None
-    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3, src_bn, rows_bound, src_bound, rows_bn)
+    d, nsplit, nbytes = hip.wgrad_plan(nhwc(dy), nhwc(x), 1, TAPS_3X3, src_bn, rows_bound, src_bound, rows_bn,
+                                       None if rows_out is None else nhwc(rows_out), rows_out_bound)
     slabs = _empty((nbytes // 4,), dy)
     hip.conv_wgrad(d, slabs)
     gw = torch.empty_like(weight)
@@ -616,6 +625,27 @@ def _dgrad_bn_bwd(dy1: torch.Tensor, wpk: torch.Tensor, n_out: int, y0: torch.Te
     return ga0, None, gb
 
 
+def _bn_backward_in_wgrad(y, g, st: _BNSaved, bn, conv, x, src_bn, x_bound, tiles, g_bound, pool):
+    """A plain BatchNorm backward whose dy is read by this conv's weight grad and then its data grad: the weight grad
+    forms dy while staging and stores it (scd_wgrad_t.rows_y / rows_out), so no apply pass runs.  Returns (dy, dgamma,
+    dbeta, dbias, weight grad, bound of dy) or None where the kernels do not take it (the caller then runs
+    _bn_backward).  Under h2 the weight grad scales dy by a bound from the statistics (_bn_backward_coef, needs
+    g_bound) and raises the exact max |dy| for the data grad."""
+    if not isinstance(g, torch.Tensor) or x.shape[3] > _OPTS['bn_bwd_in_wgrad'] or st.nseg > 2 or st.smean is None:
+        return None
+    if pool is not None and (g_bound is None or x_bound is None):
+        return None
+    rb = pool.take() if pool is not None else None
+    if not hip.wgrad_rows_bn_supported(nhwc(g), nhwc(x), 1, TAPS_3X3, src_bn, rb, x_bound if rb is not None else None):
+        return None
+    dg, db, dbias, coef = _bn_backward_coef(y, g, st, bn, conv.bias is not None, tiles, g_bound, rb)
+    dy = torch.empty_like(y)
+    ob = pool.take() if pool is not None else None
+    rows_bn = (nhwc(y), st.nseg, st.smean, st.sinv, bn.weight, st.scale, st.shift, coef)
+    gw = _wgrad3x3(g, x, conv.weight, src_bn, rb, x_bound, rows_bn, rows_out=dy, rows_out_bound=ob)
+    return dy, dg, db, dbias, gw, ob
+
+
 def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None, dy1_given: bool = False):
     """g_out: gradient of the block output (a tensor, or a _PooledGrad formed inside the BatchNorm backward).
     Returns (grad wrt DoubleConv input or None, [8 param grads in dc_params order]).  `pool` (h2): bounds of the
@@ -627,18 +657,26 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None, dy1_given: bool = F
     conv0, bn0, conv1, bn1 = s[0], s[1], s[3], s[4]
     if st1.smean is None:
         raise RuntimeError("backward through an eval-mode BatchNorm is not supported (call net.train())")
+    src_bn1 = (st0.scale, st0.shift, st0.nseg) if a0 is None else None  # fused forward: y0 through BN0 + ReLU
+    x1 = y0 if a0 is None else a0
+    fused1 = None
     if dy1_given:
         dy1, dg1, db1, dbias1 = g_out, None, None, None
         d1 = _bound_of(dy1, pool)
     else:
-        d1 = _take(pool)
-        dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None, dy_bound=d1)
-    if a0 is None:  # fused forward: the weight grad reads y0 through BN0 + ReLU as well
-        gw1 = _wgrad3x3(dy1, y0, conv1.weight, (st0.scale, st0.shift, st0.nseg), d1, b0)
-    else:
-        gw1 = _wgrad3x3(dy1, a0, conv1.weight, None, d1, b0)
+        fused1 = _bn_backward_in_wgrad(y1, g_out, st1, bn1, conv1, x1, src_bn1, b0, None,
+                                       _ACT_BOUND.get(g_out) if pool is not None and isinstance(g_out, torch.Tensor)
+                                       else None, pool)
+        if fused1 is not None:
+            dy1, dg1, db1, dbias1, gw1, d1 = fused1
+        else:
+            d1 = _take(pool)
+            dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None, dy_bound=d1)
+    if fused1 is None:
+        gw1 = _wgrad3x3(dy1, x1, conv1.weight, src_bn1, d1, b0)
+    # the bound of ga0 (h2) also for a weight grad that forms BN0's dy itself (_bn_backward_in_wgrad)
     ga0, tiles0, gb0 = _dgrad_bn_bwd(dy1, packed_conv3x3(conv1.weight, 1), conv1.in_channels, y0, st0, d1,
-                                     pool if not need_dx else None)
+                                     pool if not need_dx or _OPTS['bn_bwd_in_wgrad'] else None)
     d0 = _take(pool)
     if not need_dx and _OPTS['defer_bn_bwd'] and hip.wgrad_rows_bn_supported(nhwc(ga0), nhwc(x), 1, TAPS_3X3):
         # the input layer: dy0 has one reader, the weight grad, which forms it while staging; under h2 its bound
@@ -649,13 +687,17 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None, dy1_given: bool = F
         rows_bn = (nhwc(y0), st0.nseg, st0.smean, st0.sinv, bn0.weight, st0.scale, st0.shift, coef)
         gw0 = _wgrad3x3(ga0, x, conv0.weight, None, rb0, x_bound, rows_bn)
         return None, [gw0, dbias0, dg0, db0, gw1, dbias1, dg1, db1]
-    dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0, d0)
-    if pool is not None and x_bound is None and \
-            hip.wgrad_arith(hip.wgrad_desc(nhwc(dy0), nhwc(x), 1, TAPS_3X3, None, d0, d0)) == 'h2':
-        # a source the forward left unbounded (the channel-padded input layer, whose forward kernel is x3): bounded
-        # here, where that puts its weight grad (the generic kernel) on h2
-        x_bound = _bound_of(x, pool)
-    gw0 = _wgrad3x3(dy0, x, conv0.weight, None, d0, x_bound)
+    fused0 = _bn_backward_in_wgrad(y0, ga0, st0, bn0, conv0, x, None, x_bound, tiles0, gb0, pool) if need_dx else None
+    if fused0 is not None:
+        dy0, dg0, db0, dbias0, gw0, d0 = fused0
+    else:
+        dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0, d0)
+        if pool is not None and x_bound is None and \
+                hip.wgrad_arith(hip.wgrad_desc(nhwc(dy0), nhwc(x), 1, TAPS_3X3, None, d0, d0)) == 'h2':
+            # a source the forward left unbounded (the channel-padded input layer, whose forward kernel is x3):
+            # bounded here, where that puts its weight grad (the generic kernel) on h2
+            x_bound = _bound_of(x, pool)
+        gw0 = _wgrad3x3(dy0, x, conv0.weight, None, d0, x_bound)
     gx = None
     if need_dx:
         if x.shape[3] != conv0.in_channels:
@@ -1173,8 +1215,16 @@ class DecoderFn(torch.autograd.Function):
             # DoubleConv data grad that wrote it)
             g_cur = torch.empty_like(cur)
             gcat_bound = _bound_of(g_cat, pool)
-            hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, packed_convT2x2(convT.weight, 1), cu, None,
-                           nhwc(g_cur), src_bound=gcat_bound)
+            # h2: the kernel raises g_cur's bound as it stores (a BatchNorm backward formed inside the next weight
+            # grad scales its dy by a bound derived from it, _bn_backward_in_wgrad)
+            wT = packed_convT2x2(convT.weight, 1)
+            gcur_bound = None
+            if pool is not None and _OPTS['bn_bwd_in_wgrad'] and k > 0 and \
+                    hip.igemm_arith(g_up, hc, wc, 2, TAPS_2X2, wT, cu, nhwc(g_cur), src_bound=gcat_bound) == 'h2':
+                gcur_bound = pool.take()
+            hip.conv_igemm(g_up, hc, wc, 2, TAPS_2X2, wT, cu, None, nhwc(g_cur), src_bound=gcat_bound,
+                           dst_bound=gcur_bound)
+            _set_bound(g_cur, gcur_bound)
             # ConvT weight grad: rows = convT input, src = g_up gathered with stride 2 (h2: both bounds)
             # (and its bias grad: the kernel sums the g_up columns it stages, scd_wgrad_t.src_colsum)
             d, nsplit, nbytes = hip.wgrad_plan(nhwc(cur), g_up, 2, TAPS_2X2, None, cur_bound, gcat_bound)

@@ -87,6 +87,8 @@ class WGRAD(ctypes.Structure):
         ("math", c_int32),
         ("tune", c_uint32),
         ("src_colsum", c_void_p),
+        ("rows_out", NHWC),
+        ("rows_out_bound", c_void_p),
     ]
 
 
@@ -206,7 +208,7 @@ _SIGS = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
-ABI_VERSION = 7  # SCD_ABI_VERSION of include/scd.h
+ABI_VERSION = 8  # SCD_ABI_VERSION of include/scd.h
 
 
 def load_library(path: str = LIB_PATH):
@@ -637,14 +639,18 @@ def _rows_bn_fields(d: 'WGRAD', rows_bn):
 
 
 def wgrad_plan(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None, rows_bound=None, src_bound=None,
-               rows_bn=None):
+               rows_bn=None, rows_out: NHWC | None = None, rows_out_bound=None):
     """`src_bn` = (scale, shift, nseg): read src through its BatchNorm-apply + ReLU (see scd_wgrad_t).
     `rows_bound` / `src_bound`: device floats bounding |rows| and |src as read| (SCD_MATH_H2; both or neither).
-    `rows_bn`: see _rows_bn_fields (only where wgrad_rows_bn_supported)."""
+    `rows_bn`: see _rows_bn_fields (only where wgrad_rows_bn_supported); with it, `rows_out` (a view shaped as rows)
+    receives the formed dY and `rows_out_bound` (device float) is raised to max |dY| (ABI 8, halo weight grads)."""
     d = wgrad_desc(rows, src, stride, taps, src_bn, rows_bound, src_bound)
     if rows_bn is not None:
         _rows_bn_fields(d, rows_bn)
-    d._keep = (rows_bound, src_bound, rows_bn)
+    if rows_out is not None:
+        d.rows_out = rows_out
+        d.rows_out_bound = _ptr(rows_out_bound)
+    d._keep = (rows_bound, src_bound, rows_bn, rows_out_bound)
     ns = c_int32(0)
     nb = c_size_t(0)
     _check(lib().scd_wgrad_plan(ctypes.byref(d), ctypes.byref(ns), ctypes.byref(nb)), "scd_wgrad_plan")
@@ -656,9 +662,11 @@ def wgrad_src_bn_supported(rows: NHWC, src: NHWC, stride: int, taps, src_bn) -> 
     return lib().scd_wgrad_src_bn_supported(ctypes.byref(d)) == 1
 
 
-def wgrad_rows_bn_supported(rows: NHWC, src: NHWC, stride: int, taps) -> bool:
-    """Whether the weight grad for (rows, src) can form its rows through the fused BatchNorm backward."""
-    d = wgrad_desc(rows, src, stride, taps)
+def wgrad_rows_bn_supported(rows: NHWC, src: NHWC, stride: int, taps, src_bn=None, rows_bound=None,
+                            src_bound=None) -> bool:
+    """Whether the weight grad for (rows, src) can form its rows through the fused BatchNorm backward (with the
+    operand bounds and src transform the launch will carry: they select the arithmetic)."""
+    d = wgrad_desc(rows, src, stride, taps, src_bn, rows_bound, src_bound)
     return lib().scd_wgrad_rows_bn_supported(ctypes.byref(d)) == 1
 
 

@@ -301,3 +301,55 @@ def test_two_source_heads_equal_cat(dev, dtype):
         one = torch.empty((n, 1, h, w), device=dev)  # stream-1 head alone over a (half the lanes): same bits
         hip.conv1x1_fwd_bn(nhwc(ya), sa, ha, 1, wt[1:2, :c].contiguous(), bias[1:2], 1, one)
         assert torch.equal(one[:, 0], out2[:, 1])
+
+
+def _step_grads(cfg, dev, opts, params0, b):
+    """One training step of a freshly built model with the given parameters; returns {name: grad} (CPU)."""
+    from multimodal_siamese_cd_amd import engine, trainers
+    from multimodal_siamese_cd_amd.utils import networks
+    prev = engine.set_options(**opts)
+    try:
+        net = networks.create_network(cfg)
+        with torch.no_grad():
+            for k, p in net.module.named_parameters():
+                p.copy_(params0[k])
+        net = net.to(dev).train()
+        loss = trainers.step_loss(cfg, net(b['x_t1'], b['x_t2']), b)
+        loss.backward()
+        torch.cuda.synchronize()
+        return {k: p.grad.cpu() for k, p in net.module.named_parameters() if p.grad is not None}
+    finally:
+        engine.set_options(**prev)
+
+
+@pytest.mark.parametrize('config,math', [('baseline_siamese', 'bf16'), ('baseline_dualstream', 'bf16'),
+                                         ('dtsiamese', 'bf16'), ('baseline_siamese', 'h2')])
+def test_bn_bwd_in_wgrad_matches_apply_path(dev, config, math):
+    """ABI 8: plain BatchNorm backwards formed inside the weight grads (engine option bn_bwd_in_wgrad, the weight grad
+    stores dy for the data grad) against the apply pass they replace, on models with 64- and 128-channel layers
+    (TOPOLOGY [64, 128, 256], 64^2 crops).  bf16: every weight, gamma and beta gradient bit for bit (dy is formed with
+    bn_bwd_apply's expression and rounding; the weight grads read the same operands).  The conv biases before a
+    BatchNorm (true gradient 0) come from the statistics instead of a sum over dy: both are rounding noise, judged
+    against the weight's gradient.  h2: the weight grad scales dy by a bound from the statistics rather than its
+    max, which moves only values near the fp16 subnormal range: within 1e-6."""
+    from multimodal_siamese_cd_amd.utils import datasets, experiment_manager, networks
+    cfg = experiment_manager.load_cfg(config)
+    cfg.MODEL.TOPOLOGY = [64, 128, 256]
+    cfg.MODEL.CONV_MATH = math
+    cfg.AUGMENTATION.CROP_SIZE = 64
+    torch.manual_seed(3)
+    params0 = {k: p.detach().clone() for k, p in networks.create_network(cfg).module.named_parameters()}
+    b = datasets.synthetic_batch(cfg, 4, dev, torch.Generator(device=dev).manual_seed(11))
+    on = _step_grads(cfg, dev, {'bn_bwd_in_wgrad': 128}, params0, b)
+    off = _step_grads(cfg, dev, {'bn_bwd_in_wgrad': 0}, params0, b)
+    assert on.keys() == off.keys()
+    for k in off:
+        a, r = on[k], off[k]
+        if _pre_bn_bias(k):
+            w = off[k.replace('.bias', '.weight')]
+            assert float((a - r).abs().max()) < 1e-4 * float(w.abs().max()), k
+        elif math == 'bf16':
+            assert torch.equal(a, r), k
+        else:
+            err = float((a - r).abs().max() / r.abs().max().clamp_min(1e-30))
+            assert err < 1e-6, (k, err)

@@ -695,6 +695,75 @@ def test_wgrad_c16_deferred_bn_backward(dev, math, n, h, w, co, nseg, tiles):
     assert q[2].abs().max().item() < 1e-3 * scale_dy and o[2].abs().max().item() < 1e-3 * scale_dy
 
 
+@pytest.mark.parametrize('math,dt,co,ci,nseg,src_bn', [
+    ('h2', torch.float32, 128, 64, 2, False), ('h2', torch.float32, 256, 128, 1, True),
+    ('bf16', torch.bfloat16, 64, 64, 2, False), ('bf16', torch.bfloat16, 128, 64, 1, True),
+    ('bf16', torch.float32, 64, 128, 2, False)])
+def test_halo_wgrad_forms_and_stores_dy(dev, math, dt, co, ci, nseg, src_bn):
+    """ABI 8: the 64-channel-multiple halo weight grad with the rows' BatchNorm backward (scd_wgrad_t.rows_y) stores
+    the dY it forms (rows_out) bit for bit as scd_bn_relu_backward writes it, raises rows_out_bound to exactly max |dY|,
+    and its weight grad equals the weight grad of the materialised dY under the same operand bounds, bit for bit.  The
+    blocks of channel tile 0 store: ci = 128 has two channel tiles, so each dY element is still written once."""
+    from multimodal_siamese_cd_amd import hip
+    n, h, w = 4, 32, 32
+    g = torch.Generator().manual_seed(co + ci + nseg)
+    y = (torch.randn(n, h, w, co, generator=g) * 2 + 0.3).to(dev).to(dt)
+    da = torch.randn(n, h, w, co, generator=g).to(dev).to(dt)
+    x = torch.randn(n, h, w, ci, generator=g).to(dev).to(dt)
+    gamma = (torch.rand(co, generator=g) + 0.5).to(dev)
+    beta = torch.randn(co, generator=g).to(dev)
+    smean, sinv, scale, shift = (torch.empty(nseg * co, device=dev) for _ in range(4))
+    ws = torch.empty(hip.bn_workspace_bytes(n, h, w, co, nseg), dtype=torch.uint8, device=dev)
+    hip.bn_train_stats(hip.nhwc(y), nseg, gamma, beta, 1e-5, 0.1, False, None, None, smean, sinv, scale, shift, ws)
+    xbn = None
+    if src_bn:  # the weight grad's source read through its own BatchNorm + ReLU (the decoder's second conv)
+        xbn = ((torch.rand(2 * ci, generator=g) + 0.5).to(dev), torch.randn(2 * ci, generator=g).to(dev), 2)
+    prev = hip.set_conv_math(math)
+    try:
+        dy = torch.empty_like(y)
+        o = [torch.empty(co, device=dev) for _ in range(3)]
+        hip.bn_relu_backward(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, *o, hip.nhwc(dy), ws)
+        h2 = math == 'h2'
+        da_bound = da.float().abs().max().reshape(1) if h2 else None
+        dy_bound = torch.zeros(1, device=dev) if h2 else None
+        if h2:
+            xa = x.float()
+            if src_bn:
+                sc2, sh2 = xbn[0].reshape(2, 1, 1, 1, ci), xbn[1].reshape(2, 1, 1, 1, ci)
+                xa = torch.relu(xa.reshape(2, n // 2, h, w, ci) * sc2 + sh2)
+            x_bound = xa.abs().max().reshape(1)
+        else:
+            x_bound = None
+        assert hip.wgrad_rows_bn_supported(hip.nhwc(da), hip.nhwc(x), 1, hip.TAPS_3X3, xbn, dy_bound, x_bound)
+        coef = torch.empty(nseg * co * 2, device=dev)
+        q = [torch.empty(co, device=dev) for _ in range(3)]
+        hip.bn_relu_backward_coef(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, None, 0, coef,
+                                  *q, ws, da_bound, dy_bound)
+        dy_out = torch.full_like(y, float('nan'))
+        out_bound = torch.zeros(1, device=dev)
+
+        def wgrad(rows, rows_bn=None, rows_out=None):
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(rows), hip.nhwc(x), 1, hip.TAPS_3X3, xbn, dy_bound, x_bound,
+                                               rows_bn=rows_bn, rows_out=rows_out, rows_out_bound=out_bound)
+            assert hip.wgrad_arith(d) == math
+            slabs = torch.empty(nbytes // 4, device=dev)
+            hip.conv_wgrad(d, slabs)
+            dw = torch.empty(co, ci, 3, 3, device=dev)
+            hip.wgrad_finalize(slabs, nsplit, co, 9, ci, 0, ci, dw)
+            return dw
+
+        ref = wgrad(dy)
+        out = wgrad(da, (hip.nhwc(y), nseg, smean, sinv, gamma, scale, shift, coef), hip.nhwc(dy_out))
+        torch.cuda.synchronize()
+    finally:
+        hip.set_conv_math(prev)
+    assert torch.equal(dy_out, dy)
+    assert out_bound.item() == dy.float().abs().max().item()
+    assert torch.equal(out, ref)
+    if h2:
+        assert dy.float().abs().max().item() <= dy_bound.item()
+
+
 def test_batchnorm_eval(dev):
     from multimodal_siamese_cd_amd import hip
     g = torch.Generator().manual_seed(5)

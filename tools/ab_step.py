@@ -60,6 +60,8 @@ def apply(variant: str, model, math0: str):
             engine.set_options(defer_bn_bwd=bool(int(v)))
         elif k == 'fuse_enc':
             engine.set_options(fuse_siamese_encoder=bool(int(v)))
+        elif k == 'bn_bwd_in_wgrad':  # widest weight-grad source (channels) that forms its BatchNorm backward
+            engine.set_options(bn_bwd_in_wgrad=int(v))
         elif k in engine._OPTS:  # any other engine option by name (e.g. fuse_head=0)
             engine.set_options(**{k: bool(int(v))})
         else:
