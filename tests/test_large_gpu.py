@@ -90,3 +90,54 @@ def test_wgrad_over_2gib_matches_sum_of_halves(dev, big, math):
         assert err < 1e-5, err  # 8.5 M-term fp32 sums split differently
     finally:
         hip.set_conv_math(prev)
+
+
+def test_wgrad_rows_bn_over_2gib_stores_dy(dev, big):
+    """ABI 8 on image chunks: the halo weight grad forming a plain BatchNorm backward's dy (rows_y) and storing it
+    (rows_out) over a > 2 GiB batch with two BatchNorm segments is split into chunks like any weight grad; the stored dy
+    must equal scd_bn_relu_backward's bit for bit and its bound the exact max.  The weight grad equals the
+    materialised dy's up to fp32 summation order: with the rows transform a chunk keeps whole BatchNorm segments
+    (65 images here), without it the chunks are as large as 2 GiB allows, so the K-splits differ (bf16
+    arithmetic, fp32 storage, R = C = 64)."""
+    from multimodal_siamese_cd_amd import hip
+    prev = hip.set_conv_math('bf16')
+    try:
+        g = torch.Generator(device=dev).manual_seed(9)
+        y = torch.randn(N, H, W, CO, device=dev, generator=g) * 2 + 0.3
+        da = torch.randn(N, H, W, CO, device=dev, generator=g)
+        nseg = 2
+        gamma = torch.rand(CO, device=dev, generator=g) + 0.5
+        beta = torch.randn(CO, device=dev, generator=g)
+        smean, sinv, scale, shift = (torch.empty(nseg * CO, device=dev) for _ in range(4))
+        ws = torch.empty(hip.bn_workspace_bytes(N, H, W, CO, nseg), dtype=torch.uint8, device=dev)
+        hip.bn_train_stats(hip.nhwc(y), nseg, gamma, beta, 1e-5, 0.1, False, None, None, smean, sinv, scale, shift,
+                           ws)
+        dy = torch.empty_like(y)
+        o = [torch.empty(CO, device=dev) for _ in range(3)]
+        hip.bn_relu_backward(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, *o, hip.nhwc(dy), ws)
+        coef = torch.empty(nseg * CO * 2, device=dev)
+        q = [torch.empty(CO, device=dev) for _ in range(3)]
+        hip.bn_relu_backward_coef(hip.nhwc(y), hip.nhwc(da), nseg, smean, sinv, gamma, scale, shift, None, 0, coef,
+                                  *q, ws)
+        out = torch.empty_like(y)
+        ob = torch.zeros(1, device=dev)
+
+        def wgrad(rows, rows_bn=None, rows_out=None):
+            d, nsplit, nbytes = hip.wgrad_plan(hip.nhwc(rows), hip.nhwc(big), 1, hip.TAPS_3X3, rows_bn=rows_bn,
+                                               rows_out=rows_out, rows_out_bound=ob)
+            assert hip.wgrad_arith(d) == 'bf16'
+            slabs = torch.empty(nbytes // 4, device=dev)
+            hip.conv_wgrad(d, slabs)
+            dw = torch.empty(CO, C, 3, 3, device=dev)
+            hip.wgrad_finalize(slabs, nsplit, CO, 9, C, 0, C, dw)
+            return dw
+
+        ref = wgrad(dy)
+        fused = wgrad(da, (hip.nhwc(y), nseg, smean, sinv, gamma, scale, shift, coef), hip.nhwc(out))
+        torch.cuda.synchronize()
+        assert torch.equal(out, dy)
+        assert ob.item() == dy.abs().max().item()
+        err = ((fused.double() - ref.double()).abs().max() / ref.double().abs().max()).item()
+        assert err < 1e-5, err
+    finally:
+        hip.set_conv_math(prev)
