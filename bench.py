@@ -142,7 +142,8 @@ class KernelTimer:
             e.record()
             flops = 2.0 * d.rows.n * d.rows.h * d.rows.w * d.rows.c * d.ntaps * d.src.c
             alg = (_vbytes(d.rows) + _vbytes(d.src) + slabs.numel() * slabs.element_size()
-                   + (_vbytes(d.rows_y) if d.rows_y.data else 0))
+                   + (_vbytes(d.rows_y) if d.rows_y.data else 0)  # the rows BatchNorm backward reads y
+                   + (_vbytes(d.rows_out) if d.rows_out.data else 0))  # and stores dy for the data grad (ABI 8)
             timer.events.append(('wgrad', s, e, flops, arith, kernel_class('wgrad', d.ntaps, d.src.c), alg))
             return r
 
@@ -188,7 +189,8 @@ class KernelTimer:
 
     def alg_bytes(self, reps):
         """Algorithmic bytes of the conv launches per step: every operand read once, every output written once (src +
-        dst + split weights for igemm, dY + X + slabs for wgrad, + the y a fused BatchNorm transform reads)."""
+        dst + split weights for igemm, dY + X + slabs for wgrad, + the y a fused BatchNorm transform reads and the dy a
+        weight grad forming a BatchNorm backward stores)."""
         return sum(ev[6] for ev in self.events) / reps
 
 

@@ -11,7 +11,8 @@ algorithmic bytes (every operand read once, every output written once), FETCH (x
 correction of MI355X_MICROARCH.md) and WRITE bytes, and their ratio.  Algorithmic bytes:
   igemm: src (n h_s w_s c) + dst (n h w n_out) + the split weights (planes x K x n_out x 2 B) [+ y of a fused
          BatchNorm-backward epilogue]
-  wgrad: dY rows (n h w R) + X (n h_s w_s C) [+ y of a rows transform] + the fp32 slabs written (splits x R x taps C)
+  wgrad: dY rows (n h w R) + X (n h_s w_s C) [+ y of a rows transform] [+ the dy it stores] + the fp32 slabs written
+         (splits x R x taps C)
 FETCH counts L2 misses that the Infinity Cache may still serve, so a ratio above 1 is re-read traffic past L2.
 """
 import argparse
@@ -75,6 +76,9 @@ def log_main(a):
         if d.rows_y.data:
             alg += _px(d.rows_y) * d.rows_y.c * _eb(d.rows_y)
             extra.append('rows_bn')
+        if d.rows_out.data:  # ABI 8: the formed dy stored for the data grad
+            alg += _px(d.rows_out) * d.rows_out.c * _eb(d.rows_out)
+            extra.append('rows_out')
         if d.src_scale:
             extra.append('src_bn')
         calls.append(dict(step=step_no[0], kind='wgrad', taps=int(d.ntaps), stride=int(d.stride),
