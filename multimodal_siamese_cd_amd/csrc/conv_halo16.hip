@@ -70,6 +70,12 @@ __device__ __forceinline__ void lds_barrier() {  // a barrier that leaves LDS-DM
     asm volatile("" ::: "memory");
 }
 
+// The bf16 1 x N double-buffered tiles load their weight fragments two k-steps ahead (W2 below): dual-stream bs=64
+// 40.65 -> 40.10 ms per step, alternating processes (profiles/r05_bf16_w2_ab.txt); -DSCD_HALO16_W2=0 builds the
+// one-step lead for A/B.
+#ifndef SCD_HALO16_W2
+#define SCD_HALO16_W2 1
+#endif
 template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP, bool SB = false,
           bool WL = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
@@ -281,10 +287,67 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     }
     load_A(0);
     if constexpr (!WL) load_W(0, 0, wq);
+    // W2 (the bf16 double-buffered tiles, SCD_HALO16_W2): the weight fragments two k-steps ahead in two register sets.
+    // A bf16 k-step is 16 MFMAs per wave, a third of an h2 one, and one step of lead left the L2 latency of the next
+    // step's fragments exposed.
+    constexpr bool W2 = SCD_HALO16_W2 && NP == 1 && DB && !WL && WAVES_M == 1;  // (2 x 2 tiles: spills)
+    u32x4 wq2[W2 ? WP : 1][W2 ? TN : 1];
+    if constexpr (W2) {
+        if (nsteps > 1) load_W(a.ntaps > 1 ? 0 : 1, a.ntaps > 1 ? 1 : 0, wq2);
+    }
     store_A(0);
     __syncthreads();
     int cc = 0, t = 0;
-    for (int s = 0; s < nsteps; ++s) {
+    if constexpr (W2) {
+        // one k-step: MFMAs on wcur, then wcur refilled with step s + 2 (same sums and order as the loop below)
+        auto step = [&](int s, u32x4 (&wcur)[W2 ? WP : 1][W2 ? TN : 1]) {
+            int t1 = t + 1, cc1 = cc;
+            if (t1 == a.ntaps) {
+                t1 = 0;
+                cc1 = cc + 1;
+            }
+            int t2 = t1 + 1, cc2 = cc1;
+            if (t2 == a.ntaps) {
+                t2 = 0;
+                cc2 = cc1 + 1;
+            }
+            const bool more = s + 1 < nsteps;
+            if (t == 0 && cc + 1 < cpk) load_A(cc + 1);
+            const unsigned char *const sbuf = smem + (cc & 1) * (XP * PA);
+            const int toff = tap_at(a.tdy, t) * HWP + tap_at(a.tdx, t);
+            bf16x8 xv[TM];
+            if constexpr (PADP) {
+                const int hr = a_hr[0] + toff;
+                const unsigned char *const sb0 = sbuf + hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    xv[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(sb0 + i * (HWP * 64)));
+            } else {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int hr = a_hr[i] + toff;
+                    const int ad = hr * 64 + (((g ^ (hr >> 1)) & 3) << 4);
+                    xv[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4 *>(sbuf + ad));
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wcur[0][j]), xv[i],
+                                                                        acc[j][i], 0, 0, 0);
+            if (s + 2 < nsteps) load_W(cc2, t2, wcur);
+            if (t == T_STORE && cc + 1 < cpk) store_A((cc + 1) & 1);
+            if (more && t1 == 0) __syncthreads();
+            t = t1;
+            cc = cc1;
+        };
+        for (int s = 0; s < nsteps; s += 2) {
+            step(s, wq);
+            if (s + 1 < nsteps) step(s + 1, wq2);
+        }
+    }
+    for (int s = 0; s < (W2 ? 0 : nsteps); ++s) {
         int t1 = t + 1, cc1 = cc;
         if (t1 == a.ntaps) {
             t1 = 0;
