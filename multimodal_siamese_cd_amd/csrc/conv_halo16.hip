@@ -76,9 +76,6 @@ __device__ __forceinline__ void lds_barrier() {  // a barrier that leaves LDS-DM
 #ifndef SCD_HALO16_W2
 #define SCD_HALO16_W2 1
 #endif
-#ifndef SCD_BF16_TILE5_OCC2
-#define SCD_BF16_TILE5_OCC2 0
-#endif
 template <int WAVES_M, int WAVES_N, int TM, int TN, int TW, int OCC, bool IN_BN, bool DB, int NP, bool SB = false,
           bool WL = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(IgemmArgs a) {
@@ -293,7 +290,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     // W2 (the bf16 double-buffered tiles, SCD_HALO16_W2): the weight fragments two k-steps ahead in two register sets.
     // A bf16 k-step is 16 MFMAs per wave, a third of an h2 one, and one step of lead left the L2 latency of the next
     // step's fragments exposed.
-    constexpr bool W2 = SCD_HALO16_W2 && NP == 1 && DB && !WL && (WAVES_M == 1 || OCC == 2);  // (2 x 2 at 3: spills)
+    constexpr bool W2 = SCD_HALO16_W2 && NP == 1 && DB && !WL && WAVES_M == 1;  // (2 x 2 tiles: spills)
     u32x4 wq2[W2 ? WP : 1][W2 ? TN : 1];
     if constexpr (W2) {
         if (nsteps > 1) load_W(a.ntaps > 1 ? 0 : 1, a.ntaps > 1 ? 1 : 0, wq2);
@@ -1181,12 +1178,7 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
         switch (cfg - 1) {
             case 3: launch16_1xn_bf16<1, 4, 8, 2, 3>(a, tw, s); return;
             case 4: launch16_1xn_bf16<1, 2, 8, 2, 3>(a, tw, s); return;
-            default:
-                if (SCD_BF16_TILE5_OCC2)
-                    launch16_1xn_bf16<2, 2, 8, 2, 2>(a, tw, s);
-                else
-                    launch16_1xn_bf16<2, 2, 8, 2, 3>(a, tw, s);
-                return;
+            default: launch16_1xn_bf16<2, 2, 8, 2, 3>(a, tw, s); return;
         }
     }
     switch (cfg - 1) {
