@@ -1173,10 +1173,26 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
     }
 }
 
+// bf16 outputs of 256 channels and more on 1 x 4 waves of 128 px x 64 ch (128 x 256 per block, two blocks per CU) when
+// that grid has at least SCD_HALO16_BF16_TN4 blocks: a pixel fragment read from LDS feeds four weight fragments instead
+// of two, and the block's fixed prologue / epilogue cost covers twice the MFMAs.  Same products in the same order
+// (bit-identical).  Alternating processes (profiles/r05_bf16_tn4_ab.txt): dual-stream bs=64 40.59 -> 40.25 ms, MMCR
+// 57.71 -> 56.97 ms, bf16 Siamese bs=32 15.33 -> 15.21 ms; a 256- or 1-block threshold measured slightly less.
+// -DSCD_HALO16_BF16_TN4=0 builds the 128 x 128 tiles only.
+#ifndef SCD_HALO16_BF16_TN4
+#define SCD_HALO16_BF16_TN4 512
+#endif
 void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
     if (cfg >= 4 && bf16_1xn(a)) {
         switch (cfg - 1) {
-            case 3: launch16_1xn_bf16<1, 4, 8, 2, 3>(a, tw, s); return;
+            case 3:
+                if (SCD_HALO16_BF16_TN4 > 0 && a.n_out % 256 == 0 &&
+                    int64_t(a.n_img) * a.ho * a.wo / 128 * (a.n_out / 256) >= SCD_HALO16_BF16_TN4) {
+                    launch16_1xn_bf16<1, 4, 8, 4, 2>(a, tw, s);
+                    return;
+                }
+                launch16_1xn_bf16<1, 4, 8, 2, 3>(a, tw, s);
+                return;
             case 4: launch16_1xn_bf16<1, 2, 8, 2, 3>(a, tw, s); return;
             default: launch16_1xn_bf16<2, 2, 8, 2, 3>(a, tw, s); return;
         }
