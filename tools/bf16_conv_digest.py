@@ -8,7 +8,7 @@ hip.set_conv_math('bf16')
 dev = torch.device('cuda:0')
 h = hashlib.sha256()
 torch.manual_seed(0)
-for n, s, ci, co in [(128, 64, 256, 256), (128, 32, 512, 512), (64, 32, 1024, 256), (128, 16, 512, 512), (64, 64, 128, 256)]:
+for n, s, ci, co in [(128, 64, 256, 256), (128, 32, 512, 512), (64, 32, 1024, 256), (128, 16, 512, 512), (64, 64, 128, 256), (128, 128, 128, 128), (64, 128, 256, 128)]:
     x = torch.randn(n, s, s, ci, device=dev).to(torch.bfloat16)
     dy = torch.randn(n, s, s, co, device=dev).to(torch.bfloat16)
     w = torch.randn(co, ci, 3, 3, device=dev) * 0.05
