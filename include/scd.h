@@ -151,8 +151,9 @@ enum scd_conv_math {
  *   7: scd_bn_relu_pool_out (plain and dual-task encoder levels written into the decoders' concat buffers),
  *      scd_bn_relu_backward_pooled2 (a second, swapped skip gradient), scd_conv1x1_fwd_bn2 (two-source heads).
  *   8: scd_wgrad_t.rows_out / rows_out_bound appended (the halo weight grad forms and stores a plain BatchNorm
- *      backward's dY). */
-#define SCD_ABI_VERSION 8
+ *      backward's dY).
+ *   9: scd_igemm_t.dst_bound_seed appended (a bound seeded with another buffer's bound inside the conv launch). */
+#define SCD_ABI_VERSION 9
 int scd_abi_version(void);
 /* The arithmetic scd_conv_igemm / scd_conv_wgrad will use for a descriptor (its `math`, or SCD_MATH_X3 / F32 where
  * the shape or the missing operand bounds keep the conv off the requested kernels); negative = invalid descriptor.
@@ -160,7 +161,9 @@ int scd_abi_version(void);
 /* Kernel-variant selection, scd_igemm_t.tune / scd_wgrad_t.tune.  0 = the library's measured defaults; the other
  * values select variants kept for bit-identity tests and A/B measurements.  Every variant computes the same
  * outputs (bit-identical where the tests say so, else equal up to fp32 summation order). */
-#define SCD_TUNE_HALO16_CFG(id)   ((uint32_t)((id) + 1))  /* force 16x16x32 halo tile id 0..5 (3-5: h2 only) */
+#define SCD_TUNE_HALO16_CFG(id)   ((uint32_t)((id) + 1))  /* force 16x16x32 halo tile id 0..5 (3-5: h2 only;
+                                                             id 3 under bf16 storage: the 128x128 1x4 tile, never the
+                                                             automatic 128x256 one)                              */
 #define SCD_TUNE_HALO16_OFF       0xFu                    /* the 32x32x16 halo kernel instead                     */
 #define SCD_TUNE_HALO16_MASK      0xFu
 #define SCD_TUNE_HALO16_WRING     0x8u                    /* automatic tiles; h2 1xN tiles' weights via an LDS ring */
@@ -174,7 +177,10 @@ int scd_abi_version(void);
 #define SCD_TUNE_BF16_1XN         (1u << 11)  /* flips the bf16 arithmetic's 3x3 tile layout: 1 x N wave tiles (as h2;
                                                  the default with bf16 storage) <-> 2 x 2 (the default with fp32)     */
 #define SCD_TUNE_X3_TILE(t)       ((uint32_t)(t) << 12)   /* per-tap x3 igemm tile 1..5 (0 = automatic); on the ConvT
-                                                            gather kernel tile 1..3 (128x128, 128x64, 64x128)    */
+                                                            gather kernel tile 1..3 (128x128, 128x64, 64x128):
+                                                            the same bits, so a scope forcing an x3 tile also
+                                                            forces the ConvT tiles -- never time ConvT launches
+                                                            under an x3 tile study                              */
 #define SCD_TUNE_X3_TILE_MASK     (0xFu << 12)
 #define SCD_TUNE_C16_TILES(k)     ((uint32_t)(k) << 16)   /* input-layer forward: tiles per block (0 = 4; 15 =
                                                              one resident round)                                 */
@@ -282,6 +288,10 @@ typedef struct scd_igemm {
     float *dst_bound;
     int32_t math;  /* enum scd_conv_math: the arithmetic of this launch */
     uint32_t tune; /* SCD_TUNE_* kernel-variant bits, 0 = defaults */
+    /* ABI 9, optional (needs dst_bound): a device float whose value also enters dst_bound, folded in by the launch
+     * itself -- seeds the bound of a buffer that holds another operand too (the decoder's concat: the skip's bound
+     * and the ConvTranspose output's max) without a copy launch.  NULL = off. */
+    const float *dst_bound_seed;
 } scd_igemm_t;
 
 int scd_conv_igemm(const scd_igemm_t *d, scd_stream_t stream);

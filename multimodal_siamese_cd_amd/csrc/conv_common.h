@@ -78,10 +78,17 @@ struct IgemmArgs {
     // the weight planes in wsplit are then the fp16 two-term split with per-row inverse scales (h2_wsplit_bytes)
     const float *src_bound;
     float *dst_bound;  // optional: raised to max |stored output| (x3 / halo16 / gather16 kernels; scd_igemm_t.dst_bound)
+    const float *dst_bound_seed;  // optional (ABI 9): a value folded into dst_bound once per launch (bound_seed)
     int math;          // SCD_MATH_* of this launch (scd_igemm_t.math)
     uint32_t tune;     // SCD_TUNE_* bits (scd_igemm_t.tune)
     int sb;            // 1: src, dst and bb_y are bf16 views (ABI 6); the pointers above then address bf16 elements
 };
+
+// scd_igemm_t.dst_bound_seed: the first wave of block 0 folds the seed into its max |stored value| before
+// wave_max_bound, so dst_bound ends at max(seed, max |output|) with no separate copy or pass.
+__device__ __forceinline__ float bound_seed(const IgemmArgs &a) {
+    return (a.dst_bound_seed && blockIdx.x == 0 && threadIdx.x < 64) ? fabsf(*a.dst_bound_seed) : 0.f;
+}
 
 struct WgradArgs {
     const float *rows;

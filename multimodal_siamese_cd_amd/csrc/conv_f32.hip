@@ -652,6 +652,11 @@ static int igemm_prepare(const scd_igemm_t *d, IgemmArgs &a) {
     }
     a.src_bound = d->src_bound;
     a.dst_bound = d->dst_bound;
+    a.dst_bound_seed = d->dst_bound_seed;
+    if (d->dst_bound_seed && !d->dst_bound) {
+        set_error("igemm: dst_bound_seed needs dst_bound");
+        return SCD_ERR_ARG;
+    }
     a.math = d->math;
     a.tune = d->tune;
     if (d->wsplit && !aligned16(d->wsplit)) {

@@ -275,7 +275,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
     n0 = nn0;
     tpar ^= 1;
     }
-    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the wave takes part
+    if (a.dst_bound) wave_max_bound(a.dst_bound, fmaxf(omax, bound_seed(a)));  // uniform: every lane of the wave takes part
 }
 
 namespace {

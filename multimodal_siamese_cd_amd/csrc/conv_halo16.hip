@@ -507,7 +507,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 #pragma unroll
         for (int j = 0; j < TN; ++j) bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};  // already in acc
     }
-    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the wave takes part
+    if (a.dst_bound) wave_max_bound(a.dst_bound, fmaxf(omax, bound_seed(a)));  // uniform: every lane of the wave takes part
 
     // Fused BatchNorm statistics of this tile (BM pixels of one image) per channel: mean, then M2 about it.
     if (a.stat_rec) {
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(64 * (WAVES_N + 1), OCC) void igemm_halo16_ws(Igemm
             }
         }
     }
-    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform per wave; the producer adds 0
+    if (a.dst_bound) wave_max_bound(a.dst_bound, fmaxf(omax, bound_seed(a)));  // uniform per wave; the producer adds 0
 
     if (a.stat_rec) {
         float *red1 = reinterpret_cast<float *>(smem);  // [WME][BN] sums
@@ -1186,7 +1186,8 @@ void launch_halo16(const IgemmArgs &a, int cfg, int tw, hipStream_t s) {
     if (cfg >= 4 && bf16_1xn(a)) {
         switch (cfg - 1) {
             case 3:
-                if (SCD_HALO16_BF16_TN4 > 0 && a.n_out % 256 == 0 &&
+                // (automatic tiles only: SCD_TUNE_HALO16_CFG(3) keeps the 128 x 128 tile, the bit-identity tests' A/B)
+                if (SCD_HALO16_BF16_TN4 > 0 && halo16_mode(a.tune) == 1 && a.n_out % 256 == 0 &&
                     int64_t(a.n_img) * a.ho * a.wo / 128 * (a.n_out / 256) >= SCD_HALO16_BF16_TN4) {
                     launch16_1xn_bf16<1, 4, 8, 4, 2>(a, tw, s);
                     return;
@@ -1492,7 +1493,7 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
             // the next tile's first barrier orders these red1/red2 reads before the next writes
         }
     }
-    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the block ran every tile
+    if (a.dst_bound) wave_max_bound(a.dst_bound, fmaxf(omax, bound_seed(a)));  // uniform: every lane of the block ran every tile
 }
 
 // 0 when `a` does not take igemm_halo16_c16, else 1; *bm = 128 pixels per tile, *tw = tile width.

@@ -268,7 +268,7 @@ __global__ __launch_bounds__(64 * WAVES_M *WAVES_N) void igemm_x3(IgemmArgs a) {
             }
         }
     }
-    if (a.dst_bound) wave_max_bound(a.dst_bound, omax);  // uniform: every lane of the wave takes part
+    if (a.dst_bound) wave_max_bound(a.dst_bound, fmaxf(omax, bound_seed(a)));  // uniform: every lane of the wave takes part
 }
 
 template <int WM, int WN, int TM, int TN>

@@ -722,7 +722,7 @@ __global__ void pjaccard_bwd_kernel(const float *__restrict__ logits, const floa
 using namespace scd;
 
 // ------------------------------------------------------------------------------------------------
-extern "C" const char *scd_version(void) { return "libscd 0.8.0 (gfx950, ABI 8: halo weight grads form and store a plain BatchNorm backward's dy)"; }
+extern "C" const char *scd_version(void) { return "libscd 0.9.0 (gfx950, ABI 9: conv launches seed a bound with another buffer's bound)"; }
 extern "C" const char *scd_last_error(void) { return g_err.c_str(); }
 
 extern "C" int scd_device_check(int device) {

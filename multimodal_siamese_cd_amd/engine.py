@@ -674,14 +674,15 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None, dy1_given: bool = F
             dy1, dg1, db1, dbias1 = _bn_backward(y1, g_out, st1, bn1, conv1.bias is not None, dy_bound=d1)
     if fused1 is None:
         gw1 = _wgrad3x3(dy1, x1, conv1.weight, src_bn1, d1, b0)
-    # the bound of ga0 (h2) also for a weight grad that forms BN0's dy itself (_bn_backward_in_wgrad)
+    # the bound of ga0 (h2), only for a weight grad that forms BN0's dy itself: the input layer's (deferred) or one
+    # _bn_backward_in_wgrad can take (its source width and segment count; it still checks the kernel's shape)
+    bwd_in_wgrad0 = need_dx and x.shape[3] <= _OPTS['bn_bwd_in_wgrad'] and st0.nseg <= 2 and st0.smean is not None
     ga0, tiles0, gb0 = _dgrad_bn_bwd(dy1, packed_conv3x3(conv1.weight, 1), conv1.in_channels, y0, st0, d1,
-                                     pool if not need_dx or _OPTS['bn_bwd_in_wgrad'] else None)
-    d0 = _take(pool)
+                                     pool if not need_dx or bwd_in_wgrad0 else None)
     if not need_dx and _OPTS['defer_bn_bwd'] and hip.wgrad_rows_bn_supported(nhwc(ga0), nhwc(x), 1, TAPS_3X3):
         # the input layer: dy0 has one reader, the weight grad, which forms it while staging; under h2 its bound
         # comes from the statistics and the bound of ga0 (the h2 input-layer weight grad)
-        rb0 = d0 if gb0 is not None and x_bound is not None else None
+        rb0 = _take(pool) if gb0 is not None and x_bound is not None else None
         dg0, db0, dbias0, coef = _bn_backward_coef(y0, ga0, st0, bn0, conv0.bias is not None, tiles0,
                                                    gb0 if rb0 is not None else None, rb0)
         rows_bn = (nhwc(y0), st0.nseg, st0.smean, st0.sinv, bn0.weight, st0.scale, st0.shift, coef)
@@ -691,6 +692,7 @@ def _dc_backward(g_out, saved, dc, need_dx: bool, pool=None, dy1_given: bool = F
     if fused0 is not None:
         dy0, dg0, db0, dbias0, gw0, d0 = fused0
     else:
+        d0 = _take(pool)
         dy0, dg0, db0, dbias0 = _bn_backward(y0, ga0, st0, bn0, conv0.bias is not None, tiles0, d0)
         if pool is not None and x_bound is None and \
                 hip.wgrad_arith(hip.wgrad_desc(nhwc(dy0), nhwc(x), 1, TAPS_3X3, None, d0, d0)) == 'h2':
@@ -1121,21 +1123,24 @@ class DecoderFn(torch.autograd.Function):
             # zero border adds nothing); the skip's bound, also read by the encoder's weight grads, stays as it is.
             # The ConvT reads cur through cur's bound.
             cur_bound = _bound_of(cur, pool)
-            cat_bound = None
+            cat_bound = skip_bound = None
             if pool is not None:
-                cat_bound = pool.take()
-                cat_bound.copy_(_bound_of(skip, pool))
-            # the ConvT epilogue raises a bound on the split kernels only (src.c % 16 == 0); else one absmax pass
+                cat_bound, skip_bound = pool.take(), _bound_of(skip, pool)
+            # the ConvT epilogue raises a bound on the split kernels only (src.c % 16 == 0), seeded with the skip's
+            # inside the launch (dst_bound_seed); else a copy of the skip's bound and one absmax pass
             epi_bound = cat_bound if hip.conv_math() != 'f32' and cu % 16 == 0 else None
+            seed = skip_bound if epi_bound is not None else None
+            if cat_bound is not None and epi_bound is None:
+                cat_bound.copy_(skip_bound)
             if pad_y or pad_x:
                 # ConvT into its own map, then F.pad's zero border and placement in one window copy
                 upm = _act((b, 2 * hc, 2 * wc, cto), skip)
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(upm), store_mode=1,
-                               src_bound=cur_bound, dst_bound=epi_bound)
+                               src_bound=cur_bound, dst_bound=epi_bound, dst_bound_seed=seed)
                 hip.window_copy(nhwc(upm), nhwc(cat, cs, cto), -(pad_y // 2), -(pad_x // 2))
             else:
                 hip.conv_igemm(nhwc(cur), hc, wc, 1, TAPS_1, wT, 4 * cto, convT.bias, nhwc(cat, cs, cto),
-                               store_mode=1, src_bound=cur_bound, dst_bound=epi_bound)
+                               store_mode=1, src_bound=cur_bound, dst_bound=epi_bound, dst_bound_seed=seed)
             if cat_bound is not None and epi_bound is None:
                 hip.absmax_bound(nhwc(cat, cs, cto), cat_bound)
             last_raw = meta.raw and k == len(ups) - 1
@@ -1312,6 +1317,7 @@ class HeadsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, meta, *args):
+        meta.scope = (hip.conv_math(), hip.conv_tune())  # the backward's bounds follow the model's arithmetic
         srcs, heads = meta.srcs, meta.heads
         ns = len(srcs)
         ys = args[:ns]
@@ -1350,6 +1356,11 @@ class HeadsFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        with hip.conv_scope(*ctx.meta.scope):
+            return HeadsFn._backward(ctx, g)
+
+    @staticmethod
+    def _backward(ctx, g):
         meta = ctx.meta
         ys, wall, rows, offs, cs, K = ctx.state
         ctx.state = None

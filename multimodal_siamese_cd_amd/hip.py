@@ -60,6 +60,7 @@ class IGEMM(ctypes.Structure):
         ("dst_bound", c_void_p),
         ("math", c_int32),
         ("tune", c_uint32),
+        ("dst_bound_seed", c_void_p),  # ABI 9
     ]
 
 
@@ -208,7 +209,7 @@ _SIGS = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
-ABI_VERSION = 8  # SCD_ABI_VERSION of include/scd.h
+ABI_VERSION = 9  # SCD_ABI_VERSION of include/scd.h
 
 
 def load_library(path: str = LIB_PATH):
@@ -428,6 +429,7 @@ _MATH_NAMES = {'f32': MATH_F32, 'x3': MATH_X3, 'bf16': MATH_BF16, 'x5': MATH_X5,
 _MATH_BY_ID = {v: k for k, v in _MATH_NAMES.items()}
 
 # SCD_TUNE_* kernel-variant bits (include/scd.h): 0 = the library's measured defaults.
+# (SCD_TUNE_X3_TILE bits also force the ConvT gather kernel's tile: an x3 tile study must not time ConvT launches.)
 TUNE_HALO16_OFF = 0xF
 TUNE_HALO16_WRING = 0x8  # automatic tiles, the h2 1 x N tiles' weight fragments through an LDS ring (A/B)
 TUNE_H2_TILE_2X2 = 1 << 4
@@ -545,7 +547,7 @@ def halo16_tile_width_pref() -> int:
 
 
 def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec=None, in_bn=None,
-                bn_bwd=None, src_bound=None, dst_bound=None):
+                bn_bwd=None, src_bound=None, dst_bound=None, dst_bound_seed=None):
     nt, dy, dx = _taps(taps)
     sc, sh, nseg = in_bn if in_bn is not None else (None, None, 0)
     bb = None
@@ -555,19 +557,21 @@ def _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mo
     m, t = _cur()
     return IGEMM(src, out_h, out_w, stride, nt, dy, dx, wpk.data_ptr(), n_out, _ptr(bias), dst, store_mode,
                  _ptr(getattr(wpk, '_x3', None)), _ptr(stat_rec), _ptr(sc), _ptr(sh), nseg, bb, _ptr(src_bound),
-                 _ptr(dst_bound), m, t)
+                 _ptr(dst_bound), m, t, _ptr(dst_bound_seed))
 
 
 def conv_igemm(src: NHWC, out_h: int, out_w: int, stride: int, taps, wpk: torch.Tensor, n_out: int,
                bias, dst: NHWC, store_mode: int = 0, stat_rec: torch.Tensor | None = None, in_bn=None, bn_bwd=None,
-               src_bound: torch.Tensor | None = None, dst_bound: torch.Tensor | None = None):
+               src_bound: torch.Tensor | None = None, dst_bound: torch.Tensor | None = None,
+               dst_bound_seed: torch.Tensor | None = None):
     """`in_bn` = (scale, shift, nseg): read src through the producing layer's BatchNorm-apply + ReLU.
     `bn_bwd` = (y, nseg, save_mean, save_invstd, scale, shift, rec): also emit the BatchNorm-backward partial
     sums of the stored output into rec (see scd_bn_bwd_tiles_t).
     `src_bound`: device float >= max |src as read| (SCD_MATH_H2 operand scaling; see scd_igemm_t.src_bound).
-    `dst_bound`: device float raised to max |stored output| (ConvTranspose forward, store_mode 1)."""
+    `dst_bound`: device float raised to max |stored output| (ConvTranspose forward, store_mode 1).
+    `dst_bound_seed` (ABI 9, with dst_bound): a device float whose value the launch also folds into dst_bound."""
     d = _igemm_desc(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, stat_rec, in_bn, bn_bwd,
-                    src_bound, dst_bound)
+                    src_bound, dst_bound, dst_bound_seed)
     _check(lib().scd_conv_igemm(ctypes.byref(d), _stream()), "scd_conv_igemm")
 
 

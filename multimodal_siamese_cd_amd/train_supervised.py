@@ -43,14 +43,14 @@ def _checked_loss(value: float, cfg, step: int) -> float:
     return value
 
 
-def _check_finite(bad, cfg, step: int, device) -> None:
-    """Raise on every rank when any step since the last check produced a non-finite loss on any rank: the flag is
-    max-all-reduced, so no rank is left waiting in a DDP collective while another one stops."""
+def _check_finite(bad, cfg, first: int, step: int, device) -> None:
+    """Raise on every rank when any of the steps first..step (those since the last check) produced a non-finite loss on
+    any rank: the flag is max-all-reduced, so no rank is left waiting in a DDP collective while another one stops."""
     flag = torch.zeros(1, device=device) if bad is None else bad.float().reshape(1)
     if parallel.is_distributed():
         torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
     if flag.item() > 0:
-        raise FloatingPointError(f"non-finite training loss within the {int(cfg.LOG_FREQ)} steps up to step {step} "
+        raise FloatingPointError(f"non-finite training loss within steps {first}..{step} "
                                  f"(conv arithmetic {engine.conv_math_for(cfg)!r}; MODEL.CONV_MATH x3 is the bound-free "
                                  "fp32-class alternative)")
 
@@ -77,6 +77,7 @@ def run_training(cfg, device, max_steps: int | None = None):
                                            num_workers=int(cfg.DATALOADER.get('NUM_WORKER', 0)))
         steps_per_epoch = len(loader)
     bad = None
+    first_unchecked = 1  # the first step the next _check_finite covers
     for epoch in range(1, epochs + 1):
         start = timeit.default_timer()
         losses = []
@@ -101,8 +102,8 @@ def run_training(cfg, device, max_steps: int | None = None):
                 _evaluate(net, cfg, device, ('test',), epoch_float, global_step, rank)
                 break
             if global_step % int(cfg.LOG_FREQ) == 0:
-                _check_finite(bad, cfg, global_step, device)  # every rank raises together (max over ranks)
-                bad = None
+                _check_finite(bad, cfg, first_unchecked, global_step, device)  # every rank raises together
+                bad, first_unchecked = None, global_step + 1
             if global_step % int(cfg.LOG_FREQ) == 0 and rank == 0:
                 t = timeit.default_timer() - start
                 mean_loss = _checked_loss(torch.stack(losses).mean().item(), cfg, global_step)
@@ -113,8 +114,9 @@ def run_training(cfg, device, max_steps: int | None = None):
         # every rank checks the steps since the last log-step check (the epoch's tail when steps_per_epoch is not a
         # multiple of LOG_FREQ, a DEBUG or max_steps break) before rank 0 reports the epoch: a non-finite loss there
         # stops every rank together instead of rank 0 alone while the others enter the next collective
-        _check_finite(bad, cfg, global_step, device)
-        bad = None
+        if global_step >= first_unchecked:
+            _check_finite(bad, cfg, first_unchecked, global_step, device)
+        bad, first_unchecked = None, global_step + 1
         if not cfg.DEBUG:  # evaluation at the end of an epoch (train_supervised.py:107-110)
             _evaluate(net, cfg, device, ('training', 'validation', 'test'), global_step / steps_per_epoch,
                       global_step, rank)

@@ -492,3 +492,41 @@ def test_bf16_1xn_tiles_bit_identical(dev, st, ci, co, mode):
     assert torch.equal(outs[0][0], outs[1][0])
     if outs[0][1] is not None:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize('mode', ['stats', 'bn_bwd', 'plain'])
+def test_bf16_tn4_tile_bit_identical(dev, mode):
+    """the 128 x 256 bf16 block (1 x 4 waves of 128 px x 64 ch, the automatic choice for >= 256 outputs on
+    grids of >= 512 such blocks) against the 128 x 128 1 x 4 tile (SCD_TUNE_HALO16_CFG(3)) and the 2 x 2 tile
+    (SCD_TUNE_BF16_1XN flip): same products in the same order and 64-pixel reduction groups, so outputs and
+    statistics / BatchNorm-backward records are bit-identical.  256 -> 256 channels at 16 x 64 x 64 = 512 blocks."""
+    n, h, w, ci, co, nseg = 16, 64, 64, 256, 256, 2
+    assert n * h * w // 128 * (co // 256) >= 512
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn(n, h, w, ci, device=dev, generator=g).to(torch.bfloat16)
+    outs = []
+    for tune in (0, hip.tune_halo16_cfg(3), hip.TUNE_BF16_1XN):
+        with hip.conv_scope('bf16', tune=tune):
+            gw = torch.Generator(device=dev).manual_seed(5)
+            wpk = hip.pack_conv3x3(torch.randn(co, ci, 3, 3, device=dev, generator=gw) / (3 * ci ** 0.5), 0)
+            yb = torch.randn(n, h, w, co, device=dev, generator=gw).to(torch.bfloat16)
+            mu = torch.randn(nseg * co, device=dev, generator=gw) * 0.1
+            iv = torch.rand(nseg * co, device=dev, generator=gw) + .5
+            bsc = torch.rand(nseg * co, device=dev, generator=gw) + 0.5
+            bsh = torch.randn(nseg * co, device=dev, generator=gw)
+            y = torch.full((n, h, w, co), 7.0, device=dev).to(torch.bfloat16)
+            extra, rec = {}, None
+            if mode == 'stats':
+                nt, _ = hip.igemm_stat_tiles(nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, nhwc(y))
+                rec = extra['stat_rec'] = torch.full((nt * co * 2,), 9.0, device=dev)
+            elif mode == 'bn_bwd':
+                nt, _ = hip.igemm_bn_bwd_tiles(nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, nhwc(y))
+                rec = torch.full((co * nt * 2,), 9.0, device=dev)
+                extra['bn_bwd'] = (yb, nseg, mu, iv, bsc, bsh, rec)
+            assert hip.igemm_arith(nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, nhwc(y)) == 'bf16'
+            hip.conv_igemm(nhwc(x), h, w, 1, hip.TAPS_3X3, wpk, co, None, nhwc(y), **extra)
+            outs.append((y.cpu(), None if rec is None else rec.cpu()))
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        if outs[0][1] is not None:
+            assert torch.equal(outs[0][1], o[1])

@@ -363,11 +363,11 @@ def _worker_nonfinite(rank, world, port, out_dir):
     from multimodal_siamese_cd_amd.utils import experiment_manager as em
     cfg = em.load_cfg('debug')
     dev = torch.device('cpu')
-    train_supervised._check_finite(torch.tensor(False), cfg, 10, dev)  # all finite: no raise
+    train_supervised._check_finite(torch.tensor(False), cfg, 1, 10, dev)  # all finite: no raise
     bad = torch.tensor(rank == 1)  # only rank 1 saw a NaN loss
     raised = False
     try:
-        train_supervised._check_finite(bad, cfg, 20, dev)
+        train_supervised._check_finite(bad, cfg, 11, 20, dev)
     except FloatingPointError:
         raised = True
     torch.save({'raised': raised}, os.path.join(out_dir, f'rank{rank}.pt'))
@@ -442,5 +442,5 @@ def test_nonfinite_loss_in_epoch_tail_stops_every_rank_world2():
         mp.spawn(_worker_nonfinite_tail, args=(world, _free_port(), d), nprocs=world, join=True)
         res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
     for r in res:
-        assert r['err'] is not None and 'up to step 5' in r['err']
+        assert r['err'] is not None and 'within steps 4..5' in r['err']  # only the tail since the step-3 check
         assert r['steps'] == 5

@@ -479,6 +479,35 @@ def test_convT_gather16(dev, h2, n, h, w, ci, co):
         assert rel(gw, wr.grad) < 2e-6, arith
 
 
+@pytest.mark.parametrize('bounded', [False, True])
+def test_convT_dst_bound_seed(dev, h2, bounded):
+    """ABI 9: the ConvTranspose forward folds dst_bound_seed into dst_bound inside the launch (the decoder seeds its
+    concat bound with the skip's bound without a device copy): dst_bound ends at max(seed, max |up|), the seed float is
+    left as it was; on the x3 per-tap kernel (no source bound) and the h2 gather16 kernel; a seed without dst_bound is
+    refused."""
+    from multimodal_siamese_cd_amd import hip
+    g = torch.Generator().manual_seed(17)
+    n, h, w, ci, co = 2, 16, 16, 64, 64
+    x = torch.randn(n, h, w, ci, generator=g).to(dev)
+    wt = (torch.randn(ci, co, 2, 2, generator=g) / 8).to(dev)
+    b = torch.randn(co, generator=g).to(dev)
+    wf = hip.pack_convT2x2(wt, 0)
+    xb = absmax(x, dev) if bounded else None
+    for seed_val in (1e3, float(torch.tensor(1e-3))):  # above and below the output's max (fp32 values)
+        cat = torch.zeros(n, 2 * h, 2 * w, co + 32, device=dev)
+        seed = torch.full((1,), seed_val, device=dev)
+        bound = torch.zeros(1, device=dev)
+        assert hip.igemm_arith(hip.nhwc(x), h, w, 1, hip.TAPS_1, wf, 4 * co, hip.nhwc(cat, 32, co), store_mode=1,
+                               src_bound=xb) == ('h2' if bounded else 'x3')
+        hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_1, wf, 4 * co, b, hip.nhwc(cat, 32, co), store_mode=1,
+                       src_bound=xb, dst_bound=bound, dst_bound_seed=seed)
+        assert bound.item() == max(seed_val, cat[..., 32:].abs().max().item())
+        assert seed.item() == seed_val
+    with pytest.raises(RuntimeError, match='dst_bound_seed'):
+        hip.conv_igemm(hip.nhwc(x), h, w, 1, hip.TAPS_1, wf, 4 * co, b, hip.nhwc(cat, 32, co), store_mode=1,
+                       src_bound=xb, dst_bound_seed=seed)
+
+
 def test_halo16_dst_bound(dev, h2):
     """A bounded h2 3x3 conv raises dst_bound to exactly max |stored output| (the decoder's concat-gradient data
     grad hands it to the ConvTranspose data grad); without the halo16 kernel the request is refused."""

@@ -9,7 +9,7 @@ one() {  # name per-step-kernel bench-args...
   local name=$1 psk=$2; shift 2
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/$name" -o run -- \
     python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-kernel-timing "$@" > "$out/$name.json" 2> "$out/$name.err"
-  python3 tools/step_stats.py "$(find "$out/$name" -name 'run_kernel_stats.csv' | head -1)" --per-step-kernel "$psk" \
+  python3 tools/step_stats.py "$(find "$out/$name" -name 'run_kernel_trace.csv' | head -1)" --per-step-kernel "$psk" \
     --csv "$out/kernel_stats_$name.csv" > "$out/kernel_stats_$name.txt"
 }
 one baseline_siamese pjaccard_partial --config baseline_siamese
