@@ -197,8 +197,9 @@ int scd_abi_version(void);
                                                  of 256 x 64 (2x2 waves of 128 px x 32 ch)                          */
 #define SCD_TUNE_HALO16_WS        (1u << 29)  /* h2 1 x N tiles as warp-specialized blocks: one producer wave stages
                                                  the halo, the compute waves load only weights (128 px tiles)        */
-#define SCD_TUNE_GATHER16_PERSIST (1u << 30)  /* ConvTranspose gather kernel as persistent blocks: each walks tiles, the
-                                                 next tile's first stage loaded behind the current tile's last one   */
+#define SCD_TUNE_WGRAD16_REGSTAGE (1u << 30)  /* bf16-storage halo weight grad staged through registers, one patch in
+                                                 flight, instead of the LDS-DMA ring (A/B; until ABI 8 this bit chose
+                                                 persistent ConvT gather blocks, removed: measured slower)           */
 #define SCD_TUNE_WGRAD16_DB       (1u << 31)  /* h2 halo weight grad with two patch buffers, one barrier per patch and
                                                  (128-row blocks) the two wave groups staggered                      */
 /* dst[p*n + i] = bf16 bits of term p (h, m, l) of src[i]: the exact 3-way split used by SCD_MATH_X3.

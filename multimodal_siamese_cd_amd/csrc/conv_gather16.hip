@@ -22,10 +22,9 @@
 namespace scd {
 
 // SB: bf16 storage of src and dst (bf16 arithmetic only).
-// P: persistent blocks (SCD_TUNE_GATHER16_PERSIST): block b walks tiles b, b + gridDim.x, ... as one stream of stages,
-// so the next tile's first stage is loaded while the current tile's last stage computes and its epilogue stores (the
-// ConvTranspose forward has one or two stages per tile: one tile per block leaves every block's load latency exposed).
-template <int WM, int WN, int TM, int TN, int SK, int OCC, int NP, bool SB = false, bool P = false>
+// (Persistent blocks walking several tiles with the next tile's first stage loaded early were measured slower in round
+// 4, step 30.07 -> 30.29 ms, profiles/r04_variants_ab.txt, and removed in round 6; the tile loop below keeps one tile.)
+template <int WM, int WN, int TM, int TN, int SK, int OCC, int NP, bool SB = false>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a) {
     static_assert(NP == 1 || NP == 4, "bf16 or h2");
     static_assert(!SB || NP == 1, "bf16 storage runs the bf16 arithmetic");
@@ -173,7 +172,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
     int tpar = 0;  // tile parity (epilogue constants)
     for (;;) {
     const uint32_t qn = q + gridDim.x;
-    const bool has_next = P && qn < ntile;
+    const bool has_next = false && qn < ntile;
     int nm0 = 0, nn0 = 0;
     if (has_next) tile_of(qn, nm0, nn0);
 #pragma unroll
@@ -283,22 +282,6 @@ namespace {
 constexpr int kSK = 2;  // 32-channel k-steps per stage
 
 int gather16_enabled(uint32_t tune) { return (tune & SCD_TUNE_NO_GATHER16) ? 0 : 1; }
-int gather16_persist(uint32_t tune) { return (tune & SCD_TUNE_GATHER16_PERSIST) ? 1 : 0; }
-
-// Resident blocks of `fn` on the device (occupancy x CUs), cached per kernel by the caller.
-int resident_blocks(const void *fn, int threads, int *cache) {
-    if (*cache > 0) return *cache;
-    int per_cu = 0, cus = 0, dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess || per_cu < 1 || cus < 1) {
-        (void)hipGetLastError();
-        per_cu = 2;
-        cus = 256;
-    }
-    *cache = per_cu * cus;
-    return *cache;
-}
 
 template <int WM, int WN, int TM, int TN, int OCC, int NP, bool SB = false>
 void launch_g16(const IgemmArgs &a, hipStream_t s) {
@@ -308,15 +291,6 @@ void launch_g16(const IgemmArgs &a, hipStream_t s) {
     b.grid_n = (a.n_out + BN - 1) / BN;
     b.remap = xcd_remap_enabled(a.tune);
     const uint32_t ntile = uint32_t(b.grid_m * b.grid_n);
-    if (gather16_persist(a.tune)) {
-        // as many blocks as are resident (a multiple of 8: a block's tiles q, q + grid, ... stay on its XCD)
-        const auto fn = igemm_gather16<WM, WN, TM, TN, kSK, OCC, NP, SB, true>;
-        static int cap = 0;
-        uint32_t nb = uint32_t(resident_blocks(reinterpret_cast<const void *>(fn), 64 * WM * WN, &cap));
-        nb = ntile <= nb ? ntile : (nb >= 8 ? nb & ~7u : nb);
-        hipLaunchKernelGGL(fn, dim3(nb), dim3(64 * WM * WN), 0, s, b);
-        return;
-    }
     hipLaunchKernelGGL((igemm_gather16<WM, WN, TM, TN, kSK, OCC, NP, SB>), dim3(ntile), dim3(64 * WM * WN), 0, s, b);
 }
 

@@ -2027,6 +2027,241 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
 }
 
 // ------------------------------------------------------------------------------------------------
+// The bf16-storage halo weight grad with its patches brought into LDS by LDS-DMA (buffer_load ... lds), NB - 1
+// patches ahead.  wgrad_halo16_x3<1, 1, RG, true> holds ONE patch in flight (its next patch in staging registers):
+// at ~0.5 us of MFMAs per 32-pixel patch against an HBM latency of 1-2 us under load, every patch waited for its own
+// loads (MFMA busy 0.25-0.34 at 2.3 GHz, profiles/r05_pmc_dualstream_last).  Here a ring of NB patch buffers keeps NB - 1
+// patches in flight with no staging registers: with bf16 storage and no operand transform the staged planes are the
+// stored bits, so the global pieces land in the kernel's LDS image unchanged (the same [pixel][row] / [halo pixel]
+// [channel] planes with 32-byte row pads as wgrad_halo16_x3, filled 16 bytes per lane; pad lanes and halo pixels
+// outside the image read out of the buffer range, which returns zeros).  One barrier per patch: it retires every
+// wave's pieces of the patch about to be read and closes the reads of the buffer the next DMA overwrites.
+// Same products in the same order as wgrad_halo16_x3<1, 1, RG, true> (bit-identical slabs).
+// XT: the source is read through its BatchNorm + ReLU (src_scale / src_shift, at most two segments): the raw bf16 y
+// lands by DMA as above and each X plane is transformed in place one patch ahead of its use -- max(fma(y, sc, sh), 0)
+// rounded to bf16, zero outside the image, wgrad_halo16_x3's expressions (bit-identical) -- so a patch is waited for one
+// iteration earlier (NB - 2 patches in flight) and the transform's LDS pass overlaps the current patch's MFMAs.
+// ------------------------------------------------------------------------------------------------
+namespace {
+// dummy destination of the padding DMA pieces that even out the per-wave piece count (zeros, never read)
+constexpr int kDmaSink = 1024;
+}  // namespace
+#ifndef SCD_WGRAD16_DMA_NB
+#define SCD_WGRAD16_DMA_NB 4  // ring depth: 3 patches in flight while one is computed
+#endif
+#ifndef SCD_WGRAD16_DMA_NB_XT
+#define SCD_WGRAD16_DMA_NB_XT 5  // 128-row blocks with the source transform: 3 patches in flight (64-row: NB above)
+#endif
+
+template <int RG, int NB, bool XT = false>
+__global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a) {
+    constexpr int NT = 256 * RG, NW = NT / 64;
+    constexpr int PH = 2, PW = 16, P = PH * PW;
+    constexpr int HW_ = PW + 2, HP = (PH + 2) * HW_;  // halo: 4 x 18
+    constexpr int RS = kW16RS;                        // X row stride (64 channels + 32 bytes)
+    constexpr int RSD = 128 * RG + 32;                // dY row stride (64 RG rows + 32 bytes)
+    constexpr int PA = P * RSD, PB = HP * RS;         // plane bytes
+    constexpr int PA_K = (PA + 1023) / 1024, PB_K = (PB + 1023) / 1024;  // 1 KB DMA pieces per plane
+    constexpr int PPW = (PA_K + PB_K + NW - 1) / NW;  // pieces per wave and patch (padded with sink pieces)
+    constexpr int STAGE = (PA_K + PB_K) * 1024;
+    constexpr int DCH = 8 * RG;                       // 16-byte dY chunks per staged pixel (64 RG rows)
+    constexpr int NCB = W16L<1>::CB, NRB = W16L<1>::RB;
+    static_assert(NB >= (XT ? 3 : 2) && NB <= 6, "ring depth");
+    constexpr int CF = XT ? 2 * 2 * 64 * 4 : 0;  // XT: [segment 2][sc, sh][64 channels] floats
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NB * STAGE + kDmaSink + CF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wid);
+    const int wi = RG == 1 ? 0 : wid >> 2, wj = RG == 1 ? wid : wid & 3;
+    const uint32_t per_split = uint32_t(a.grid_r * a.grid_j);
+    const uint32_t L = a.remap ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
+    const int split = int(L / per_split);
+    const int rem = int(L - uint32_t(split) * per_split);
+    const int ct = rem / a.grid_r;
+    const int r0 = (rem - ct * a.grid_r) * 64 * RG, c0 = ct * 64;
+    const int pw_n = a.wo / PW, ph_n = a.ho / PH, pimg = pw_n * ph_n;
+    const int npatch = a.n_img_w * pimg;
+    const int pbeg = split * a.kchunk, pend = min(npatch, pbeg + a.kchunk);
+
+    const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
+    const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
+    // This lane's 16-byte chunk of each of the wave's pieces: piece k of a patch is the block's piece u = k * NW + wave
+    // (u < PA_K: dY plane bytes [1024 u, +1024); u < PA_K + PB_K: X plane; else a sink piece).  Position within its
+    // plane: row = byte / stride, chunk = (byte % stride) / 16; chunks past the data (the row pads, the tail) read out of
+    // range.  Per piece: the patch-invariant part of the global byte offset (kOOB: never loads) and the LDS offset.
+    uint32_t g_rel[PPW];  // dY: (pixel-in-patch row, chunk) offset relative to the patch's first pixel; X: unused
+    int d_row[PPW], x_hy[PPW], x_hx[PPW], chunk[PPW], kind[PPW];  // kind 0 dY, 1 X, 2 sink / pad
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) {
+        const int u = k * NW + wave_u;
+        kind[k] = 2;
+        d_row[k] = x_hy[k] = x_hx[k] = chunk[k] = 0;
+        g_rel[k] = 0;
+        if (u < PA_K) {
+            const int b = u * 1024 + lane * 16;
+            const int row = b / RSD, ch = (b - row * RSD) / 16;
+            if (row < P && ch < DCH) {
+                kind[k] = 0;
+                d_row[k] = row;
+                chunk[k] = ch;
+            }
+        } else if (u < PA_K + PB_K) {
+            const int b = (u - PA_K) * 1024 + lane * 16;
+            const int row = b / RS, ch = (b - row * RS) / 16;
+            if (row < HP && ch < 8) {
+                kind[k] = 1;
+                x_hy[k] = row / HW_;
+                x_hx[k] = row - (row / HW_) * HW_;
+                chunk[k] = ch;
+            }
+        }
+    }
+    // Issue patch pi's pieces into ring slot `slot` (wave-uniform LDS base per piece: M0 + lane * 16).
+    auto issue = [&](int pi, int slot) {
+        const int img = pi / pimg, pr = pi - img * pimg;
+        const int y0 = patch_y0(pr, pw_n, ph_n, PH), x0 = patch_x0(pr, pw_n, ph_n, PW);
+#pragma unroll
+        for (int k = 0; k < PPW; ++k) {
+            const int u = k * NW + wave_u;
+            uint32_t off = kOOB;
+            if (kind[k] == 0) {
+                const int pix = (img * a.ho + y0 + (d_row[k] >> 4)) * a.wo + x0 + (d_row[k] & 15);
+                off = uint32_t(pix * a.ldc_r + r0 + 8 * chunk[k]) * 2u;
+            } else if (kind[k] == 1) {
+                const int sy = y0 - 1 + x_hy[k], sx = x0 - 1 + x_hx[k];
+                if (unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws))
+                    off = uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + 8 * chunk[k]) * 2u;
+            }
+            unsigned char *dst = u < PA_K + PB_K ? smem + slot * STAGE + u * 1024 : smem + NB * STAGE;
+            if (u < PA_K)  // wave-uniform
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_rows, (__attribute__((address_space(3))) void *)dst, 16, off,
+                                                         0, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_src, (__attribute__((address_space(3))) void *)dst, 16, off,
+                                                         0, 0, 0);
+        }
+        asm volatile("" ::: "memory");
+    };
+
+    f32x4 acc[9][NCB][NRB];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < NCB; ++i)
+#pragma unroll
+            for (int j = 0; j < NRB; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // transposed-read lane roles of wgrad_halo16_x3
+    const int g = lane >> 4, w16 = lane & 15;
+    const int py = g >> 1, pxq = 4 * (g & 1) + (w16 >> 2);
+    const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RSD + (16 * NRB * wi + 4 * (w16 & 3)) * 2;
+    const uint32_t xbase = lds_addr(smem) + PA_K * 1024 + (py * HW_ + pxq) * RS + (16 * NCB * wj + 4 * (w16 & 3)) * 2;
+
+    // XT: the transform of patch pi's X plane in ring slot `slot`, in place: this thread's 16-byte chunks q = tid + i NT
+    // (halo pixel q >> 3, channels c0 + 8 (q & 7) ..+7); out-of-image chunks stay the DMA's zeros
+    float *const cf = reinterpret_cast<float *>(smem + NB * STAGE + kDmaSink);  // [seg][sc | sh][64]
+    auto transform = [&](int pi, int slot_) {
+        const int img = pi / pimg, pr = pi - img * pimg;
+        const int y0 = patch_y0(pr, pw_n, ph_n, PH), x0 = patch_x0(pr, pw_n, ph_n, PW);
+        const float *c_sc = cf + (img / a.src_seg_imgs) * 128, *c_sh = c_sc + 64;
+        unsigned char *const xp = smem + slot_ * STAGE + PA_K * 1024;
+#pragma unroll
+        for (int i = 0; i < (HP * 8 + NT - 1) / NT; ++i) {
+            const int q = tid + i * NT;
+            if (q >= HP * 8) break;
+            const int hp = q >> 3, j = q & 7;
+            const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
+            const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
+            if (unsigned(sy) >= unsigned(a.hs) || unsigned(sx) >= unsigned(a.ws)) continue;
+            u32x4 *const ptr = reinterpret_cast<u32x4 *>(xp + hp * RS + j * 16);
+            const u32x4 raw = *ptr;
+            u32x4 out;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                f32x4 x = unpk_bf16x4(u32x2{raw[2 * h], raw[2 * h + 1]});
+                const f32x4 sc = *reinterpret_cast<const f32x4 *>(c_sc + 8 * j + 4 * h);
+                const f32x4 sh = *reinterpret_cast<const f32x4 *>(c_sh + 8 * j + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[e] = fmaxf(fmaf(x[e], sc[e], sh[e]), 0.f);
+                const u32x2 pk = pk_bf16x4(x);
+                out[2 * h] = pk[0];
+                out[2 * h + 1] = pk[1];
+            }
+            *ptr = out;
+        }
+    };
+    if constexpr (XT) {  // both segments' coefficients of the block's 64 channels (launcher: at most two)
+        const int nsl = a.n_img_w / a.src_seg_imgs;
+        for (int e = tid; e < nsl * 64; e += NT) {
+            const int sg = e / 64, c = e - sg * 64;
+            cf[sg * 128 + c] = a.src_scale[sg * a.C + c0 + c];
+            cf[sg * 128 + 64 + c] = a.src_shift[sg * a.C + c0 + c];
+        }
+    }
+
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k)
+        if (pbeg + k < pend) issue(pbeg + k, k);
+    if constexpr (XT) {  // patch pbeg transformed before the loop (its first barrier publishes it)
+        if (pbeg < pend) {
+            const int ahead = min(NB - 2, pend - 1 - pbeg);
+            if (ahead >= 3)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW) : "memory");
+            else if (ahead == 2)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+            else if (ahead == 1)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();  // every wave's pieces of patch pbeg (and the coefficients) are in LDS
+            transform(pbeg, 0);
+        }
+    }
+    int slot = 0;
+    for (int pi = pbeg; pi < pend; ++pi) {
+        // this wave's pieces of patch pi (XT: pi + 1, transformed during this iteration): younger in flight are
+        // those of the patches after it up to min(pi + NB - 2, pend - 1)
+        const int ahead = XT ? (pi + 1 < pend ? min(NB - 3, pend - 2 - pi) : -1) : min(NB - 2, pend - 1 - pi);
+        if (ahead >= 4)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PPW) : "memory");
+        else if (ahead == 3)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW) : "memory");
+        else if (ahead == 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+        else if (ahead == 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+        else if (ahead == 0)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();  // every wave's pieces of patch pi landed; every wave left the slot of patch pi - 1
+        if (pi + NB - 1 < pend) issue(pi + NB - 1, slot == 0 ? NB - 1 : slot - 1);
+        if constexpr (XT) {
+            if (pi + 1 < pend) transform(pi + 1, slot == NB - 1 ? 0 : slot + 1);
+        }
+        const uint32_t bo = uint32_t(slot * STAGE);
+        bf16x8 dv[3][NRB];
+        w16_read_dy<0, PA_K * 1024, NRB, 1, RSD>(dv, dbase + bo);
+        s16x4 f0[6], f1[6];
+        w16_read_x<0, 0, PB_K * 1024, HW_, 1>(f0, xbase + bo);
+        w16_read_x<1, 0, PB_K * 1024, HW_, 1>(f1, xbase + bo);
+        w16_chain<0, PB_K * 1024, HW_, 1, 1>(acc, dv, f0, f1, xbase + bo);
+        slot = slot == NB - 1 ? 0 : slot + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    float *slab = a.slabs + size_t(split) * a.R * a.Ng;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int r = 0; r < NRB; ++r) {
+                const int row = r0 + 16 * NRB * wi + 16 * r + w16;
+                const int col = c0 + 16 * NCB * wj + 16 * cb + 4 * g;
+                gstore4(slab + size_t(row) * a.Ng + t * a.C + col, acc[t][cb][r]);
+            }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Halo weight gradient of a 16-channel source (the input layer: 5 bands padded to the bf16 K granule of 16).
 // Same patch walk, tap shifts and transposed-read lane roles as wgrad_halo16_x3, with the channel block cut to
 // the 16 channels that exist: a block owns 64 rows r x 16 c x 9 taps and each wave 16 r, so a patch costs
@@ -2411,7 +2646,20 @@ void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
     }
     switch (wgrad16_planes(a.math, a.tune, bounded)) {
         case 1:
-            if (a.sb)
+            if (a.sb && lc && !(a.tune & SCD_TUNE_WGRAD16_REGSTAGE) &&
+                (!a.src_scale || a.n_img_w / a.src_seg_imgs <= 2)) {
+                // bf16 storage: the LDS-DMA ring (same residency as the register-staged kernel: one 512-thread block /
+                // two 256-thread blocks per CU, so the split plan is unchanged); a source transform in place
+                if (a.src_scale) {
+                    if (rb == 128)
+                        hipLaunchKernelGGL((wgrad_halo16_dma<2, SCD_WGRAD16_DMA_NB_XT, true>), grid, dim3(512), 0, s, a);
+                    else
+                        hipLaunchKernelGGL((wgrad_halo16_dma<1, SCD_WGRAD16_DMA_NB, true>), grid, dim3(256), 0, s, a);
+                } else if (rb == 128)
+                    hipLaunchKernelGGL((wgrad_halo16_dma<2, SCD_WGRAD16_DMA_NB>), grid, dim3(512), 0, s, a);
+                else
+                    hipLaunchKernelGGL((wgrad_halo16_dma<1, SCD_WGRAD16_DMA_NB>), grid, dim3(256), 0, s, a);
+            } else if (a.sb)
                 w16_launch<1, true>(lc, rb, a, grid, s);
             else
                 w16_launch<1>(lc, rb, a, grid, s);

@@ -450,7 +450,7 @@ TUNE_NO_HALO = 1 << 26
 TUNE_HALO16_LATE_LOAD = 1 << 27
 TUNE_H2_TILE64_128 = 1 << 28
 TUNE_HALO16_WS = 1 << 29
-TUNE_GATHER16_PERSIST = 1 << 30
+TUNE_WGRAD16_REGSTAGE = 1 << 30  # bf16 halo weight grad: register staging instead of the LDS-DMA ring (A/B)
 TUNE_WGRAD16_DB = 1 << 31
 
 

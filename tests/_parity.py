@@ -244,22 +244,30 @@ def r16(t):
     return t.to(torch.bfloat16).float()
 
 
+# Accumulation type of the bf16-emulating convs: double by default; bf16_conv_oracle(torch.float32) at the shipped
+# batches (a bf16 x bf16 product is exact in fp32 as in double, so only the summation rounding differs -- the GPU's
+# own accumulation is fp32 -- at half the CPU time of double).
+_ACC16 = [torch.float64]
+
+
 class _Conv16(torch.autograd.Function):
     """A 3x3 conv with the bf16 kernels' arithmetic: bf16-rounded operands in forward, data-grad and weight-grad,
-    exact products, fp32 (here double) accumulation; the output and the data grad rounded to bf16 as bf16 storage
-    (engine.act_storage_for) keeps them in HBM."""
+    exact products, fp32 (here double, or _ACC16) accumulation; the output and the data grad rounded to bf16 as bf16
+    storage (engine.act_storage_for) keeps them in HBM."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
-        return r16(_CONV2D(r16(x).double(), r16(w).double(), None, padding=1).float() + b[None, :, None, None])
+        acc = _ACC16[0]
+        return r16(_CONV2D(r16(x).to(acc), r16(w).to(acc), None, padding=1).float() + b[None, :, None, None])
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        g16 = r16(gy).double()
-        gx = r16(torch.nn.grad.conv2d_input(x.shape, r16(w).double(), g16, padding=1).float())
-        gw = torch.nn.grad.conv2d_weight(r16(x).double(), w.shape, g16, padding=1).float()
+        acc = _ACC16[0]
+        g16 = r16(gy).to(acc)
+        gx = r16(torch.nn.grad.conv2d_input(x.shape, r16(w).to(acc), g16, padding=1).float())
+        gw = torch.nn.grad.conv2d_weight(r16(x).to(acc), w.shape, g16, padding=1).float()
         return gx, gw, gy.sum((0, 2, 3))
 
 
@@ -276,16 +284,18 @@ class _ConvT16(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.bwd16 = bwd16
         xx, ww = (r16(x), r16(w)) if fwd16 else (x, w)
-        return _CONVT2D(xx.double(), ww.double(), None, stride=2).float() + b[None, :, None, None]
+        acc = _ACC16[0]
+        return _CONVT2D(xx.to(acc), ww.to(acc), None, stride=2).float() + b[None, :, None, None]
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gg, ww = (r16(gy), r16(w)) if ctx.bwd16 else (gy, w)
-        gx = _CONV2D(gg.double(), ww.double(), None, stride=2).float()  # the transpose of the ConvT
+        acc = _ACC16[0]
+        gx = _CONV2D(gg.to(acc), ww.to(acc), None, stride=2).float()  # the transpose of the ConvT
         with torch.enable_grad():
-            wr = w.detach().double().requires_grad_(True)
-            gw, = torch.autograd.grad(_CONVT2D(r16(x.detach()).double(), wr, None, stride=2), wr, r16(gy).double())
+            wr = w.detach().to(acc).requires_grad_(True)
+            gw, = torch.autograd.grad(_CONVT2D(r16(x.detach()).to(acc), wr, None, stride=2), wr, r16(gy).to(acc))
         return gx, gw.float(), gy.sum((0, 2, 3)), None, None
 
 
@@ -301,10 +311,11 @@ def convT_bf16(x, w, b=None, stride=1, padding=0, *a, **k):
 
 
 @contextlib.contextmanager
-def bf16_conv_oracle():
+def bf16_conv_oracle(accumulate=torch.float64):
     """Inside: every 3x3 conv the bf16 kernels take (source channels a multiple of 32, or an input layer of at most
     16 bands, zero-padded to the 16-channel kernels) runs through _Conv16, every ConvTranspose through convT_bf16;
-    the rest stays fp32."""
+    the rest stays fp32.  `accumulate`: the emulated convs' summation type (see _ACC16)."""
+    prev_acc, _ACC16[0] = _ACC16[0], accumulate
     def conv(x, w, b=None, stride=1, padding=0, *a, **k):
         if (w.shape[2:] == (3, 3) and (w.shape[1] % 32 == 0 or w.shape[1] <= 16) and stride == 1
                 and padding == 1):
@@ -318,6 +329,7 @@ def bf16_conv_oracle():
     finally:
         F.conv2d = _CONV2D
         F.conv_transpose2d = _CONVT2D
+        _ACC16[0] = prev_acc
 
 
 def record_arith(monkeypatch, dev):

@@ -530,3 +530,35 @@ def test_bf16_tn4_tile_bit_identical(dev, mode):
         assert torch.equal(outs[0][0], o[0])
         if outs[0][1] is not None:
             assert torch.equal(outs[0][1], o[1])
+
+
+@pytest.mark.parametrize('src_bn', [False, True])
+@pytest.mark.parametrize('n,h,w,r,c,cs', [(4, 32, 32, 128, 64, 0), (3, 16, 48, 64, 128, 32), (2, 2, 16, 128, 128, 0),
+                                          (9, 8, 64, 256, 64, 64), (1, 64, 16, 64, 64, 0)])
+def test_weight_grad_dma_ring_bit_identical(dev, n, h, w, r, c, cs, src_bn):
+    """The bf16-storage halo weight grad with its patches brought in by LDS-DMA (the default) against the
+    register-staged kernel (SCD_TUNE_WGRAD16_REGSTAGE): identical split plan, every slab element written
+    (NaN-prefilled) and bit-identical; 128-row (8-wave) and 64-row blocks, image borders on every side (zero halo from
+    out-of-range DMA pieces), one patch row (h = 2), splits shorter than the ring, channel slices of wider buffers (the
+    decoder's concat views: ldc > c), and the source read through its BatchNorm + ReLU (two segments, transformed in
+    LDS one patch ahead: negative shifts make the zero padding differ from relu(shift))."""
+    g = torch.Generator(device=dev).manual_seed(n * h + w + r + c)
+    dyb = torch.randn(n, h, w, cs + r, device=dev, generator=g).to(torch.bfloat16)
+    xb = torch.randn(n, h, w, c + cs, device=dev, generator=g).to(torch.bfloat16)
+    rows, src = nhwc(dyb, cs, r), nhwc(xb, 0, c)
+    bn = None
+    if src_bn:
+        nseg = 2 if n % 2 == 0 else 1
+        bn = (torch.rand(nseg * c, device=dev, generator=g) + 0.5, torch.randn(nseg * c, device=dev, generator=g) * 0.5,
+              nseg)
+    out = []
+    for tune in (0, hip.TUNE_WGRAD16_REGSTAGE):
+        with hip.conv_scope('bf16', tune=tune):
+            d, nsplit, nbytes = hip.wgrad_plan(rows, src, 1, TAPS_3X3, bn)
+            assert hip.wgrad_arith(d) == 'bf16'
+            slabs = torch.full((nbytes // 4,), float('nan'), device=dev)
+            hip.conv_wgrad(d, slabs)
+            out.append((nsplit, slabs.cpu()))
+    assert out[0][0] == out[1][0]
+    assert not torch.isnan(out[0][1]).any()
+    assert torch.equal(out[0][1], out[1][1])

@@ -135,3 +135,101 @@ def test_loss_from_global_sums_kernel(dev=None):
     hip.jaccard_multi_loss_from_sums(terms(z, t, z2), acc, lm)
     assert abs(lm.item() - loss_all.item()) < 1e-6
     assert torch.equal(acc[:, 3], sums_all[:, 3])
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# The variant models of the configs that scale (baseline_dualstream, dtsiamese): 2 ranks in exact-DataParallel mode
+# against ONE process computing nn.DataParallel's function on the same GPU -- each shard's forward separately (per-shard
+# BatchNorm statistics, utils/networks.py:27), one loss over the concatenated outputs, the shards' gradients summed by
+# autograd.  Both sides run the same kernels on the same per-shard shapes, so outputs are bit-identical per shard; the
+# loss partial sums are reduced in a different order (all-reduce of per-shard sums vs one pass), so loss and
+# gradients agree to 1e-5.
+# ---------------------------------------------------------------------------------------------------------------------
+_VARIANTS = {
+    # id: (config, model, topology, tile, batch per rank)
+    'dualstream': ('baseline_dualstream', 'dualstreamunet', [64, 128], 64, 2),
+    'dtsiamese': ('dtsiamese', 'dtsiameseunet', [64, 128], 64, 2),
+}
+
+
+def _variant_setup(vid, world):
+    from multimodal_siamese_cd_amd.utils import experiment_manager as em
+    from oracle import siamese_oracle as O
+    config, model, topo, size, per = _VARIANTS[vid]
+    cfg = em.load_cfg(config)
+    cfg.MODEL.TYPE, cfg.MODEL.TOPOLOGY = model, list(topo)
+    ocfg = dict(TYPE=model, TOPOLOGY=list(topo), IN_CHANNELS=cfg.MODEL.IN_CHANNELS,
+                OUT_CHANNELS=cfg.MODEL.OUT_CHANNELS, S1_BANDS=list(cfg.DATALOADER.S1_BANDS),
+                S2_BANDS=list(cfg.DATALOADER.S2_BANDS))
+    P = O.deterministic_params(O.param_shapes(model, ocfg), 11)
+    batch = O.synthetic_batch(ocfg, per * world, size, 12)
+    return cfg, P, batch, per
+
+
+def _variant_net(cfg, P, dev):
+    from multimodal_siamese_cd_amd.utils import networks
+    net = networks.create_network(cfg)
+    with torch.no_grad():
+        for k, p in net.module.named_parameters():
+            p.copy_(P[k])
+    return net.to(dev).train()
+
+
+def _outs(o):
+    return list(o) if isinstance(o, (tuple, list)) else [o]
+
+
+def _variant_worker(rank, world, port, out_dir, vid):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR='127.0.0.1',
+                      MASTER_PORT=str(port), SCD_RANKS_SHARE_GPU='1')
+    from multimodal_siamese_cd_amd import hip, parallel, trainers
+    parallel.init_distributed('gloo')
+    dev = torch.device('cuda', parallel.device_index(rank))
+    torch.cuda.set_device(dev)
+    hip.load_library()
+    cfg, P, batch, per = _variant_setup(vid, world)
+    net = parallel.wrap_ddp(_variant_net(cfg, P, dev), dev, exact_dataparallel=True)
+    b = {k: v[rank * per:(rank + 1) * per].to(dev) for k, v in batch.items()}
+    out = net(b['x_t1'], b['x_t2'])
+    loss = trainers.step_loss(cfg, out, b, net)
+    loss.backward()
+    torch.cuda.synchronize()
+    torch.save({'loss': loss.item(), 'outs': [o.detach().cpu() for o in _outs(out)],
+                'grads': {n: p.grad.detach().cpu() for n, p in net.module.named_parameters()}},
+               os.path.join(out_dir, f'rank{rank}.pt'))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize('vid', list(_VARIANTS))
+def test_exact_dataparallel_variants_two_ranks_match_one_process(vid):
+    from multimodal_siamese_cd_amd import hip, trainers
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_variant_worker, args=(world, _free_port(), d, vid), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f'rank{r}.pt'), weights_only=True) for r in range(world)]
+    # one process: DataParallel's function (per-shard forwards, one loss over the gathered outputs, summed gradients)
+    hip.load_library()
+    dev = torch.device('cuda:0')
+    cfg, P, batch, per = _variant_setup(vid, world)
+    net = _variant_net(cfg, P, dev)
+    b = {k: v.to(dev) for k, v in batch.items()}
+    shard_outs = [_outs(net(b['x_t1'][s * per:(s + 1) * per], b['x_t2'][s * per:(s + 1) * per]))
+                  for s in range(world)]
+    outs = [torch.cat([so[i] for so in shard_outs]) for i in range(len(shard_outs[0]))]
+    loss = trainers.step_loss(cfg, outs if len(outs) > 1 else outs[0], b)
+    loss.backward()
+    torch.cuda.synchronize()
+    for r, so in zip(res, shard_outs):  # each rank's outputs: the same kernels on the same shard, bit-identical
+        for a, e in zip(r['outs'], so):
+            assert torch.equal(a, e.detach().cpu())
+        assert abs(r['loss'] - loss.item()) <= 1e-5 * abs(loss.item())
+    worst = 0.0
+    for n, p in net.named_parameters():
+        k = n.split('module.', 1)[-1]
+        ref = p.grad.detach().cpu().double()
+        for r in res:
+            e = ((r['grads'][k].double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
+            worst = max(worst, e)
+            assert e < 1e-5 or k.endswith(('conv.0.bias', 'conv.3.bias')), (k, e)
+    print(f'{vid}: exact-DataParallel 2 ranks vs one process, worst gradient max-rel {worst:.2e}')

@@ -685,42 +685,6 @@ def test_halo16_variant_training_step_bit_identical(dev, h2, variant, base):
         assert torch.equal(g0, g1)
 
 
-@pytest.mark.parametrize('arith', ['h2', 'bf16'])
-@pytest.mark.parametrize('b,hc,ci,co', [(32, 128, 64, 64), (17, 64, 128, 128), (3, 16, 512, 512)])
-def test_gather16_persistent_bit_identical(dev, arith, b, hc, ci, co):
-    """Persistent ConvTranspose gather blocks (SCD_TUNE_GATHER16_PERSIST: each block walks tiles as one stream of
-    stages, the next tile's first stage loaded behind the current tile's last) against one tile per block: the
-    pixel-shuffled forward into a concat slice (with its dst bound) and the 4-tap data grad bit-identical, on maps
-    with more tiles than resident blocks and with a ragged tile count (17 images).  bf16: bf16 storage."""
-    from multimodal_siamese_cd_amd import hip
-    st = torch.bfloat16 if arith == 'bf16' else torch.float32
-    g = torch.Generator(device=dev).manual_seed(b + hc + ci)
-    x = torch.randn(b, hc, hc, ci, device=dev, generator=g).to(st)
-    wt = torch.randn(ci, co, 2, 2, device=dev, generator=g) * 0.05
-    bias = torch.randn(co, device=dev, generator=g)
-    cs = 32
-    gcat = torch.randn(b, 2 * hc, 2 * hc, cs + co, device=dev, generator=g).to(st)
-    outs = []
-    for tune in (0, hip.TUNE_GATHER16_PERSIST):
-        with hip.conv_scope(arith, tune=tune):
-            xb = x.float().abs().max().reshape(1) if arith == 'h2' else None
-            gb = gcat.float().abs().max().reshape(1) if arith == 'h2' else None
-            wf, wb = hip.pack_convT2x2(wt, 0), hip.pack_convT2x2(wt, 1)
-            cat = torch.full((b, 2 * hc, 2 * hc, cs + co), 3.0, device=dev).to(st)
-            db = torch.zeros(1, device=dev) if arith == 'h2' else None
-            assert hip.igemm_arith(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, hip.nhwc(cat, cs, co),
-                                   store_mode=1, src_bound=xb) == arith
-            hip.conv_igemm(hip.nhwc(x), hc, hc, 1, hip.TAPS_1, wf, 4 * co, bias, hip.nhwc(cat, cs, co), store_mode=1,
-                           src_bound=xb, dst_bound=db)
-            gx = torch.full((b, hc, hc, ci), 5.0, device=dev).to(st)
-            hip.conv_igemm(hip.nhwc(gcat, cs, co), hc, hc, 2, hip.TAPS_2X2, wb, ci, None, hip.nhwc(gx), src_bound=gb)
-            outs.append((cat.cpu(), gx.cpu(), None if db is None else db.cpu()))
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-    if outs[0][2] is not None:
-        assert torch.equal(outs[0][2], outs[1][2])
-
-
 @pytest.mark.parametrize('n,h,w,ci,co,src_bn', [(4, 32, 32, 64, 128, False), (3, 16, 48, 128, 256, True),
                                                  (2, 32, 32, 128, 64, False), (5, 8, 64, 64, 64, True),
                                                  (1, 2, 16, 64, 128, False)])
