@@ -52,6 +52,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3
 BF16_MFMA_PEAK_TFLOPS = 16 * FP32_MFMA_PEAK_TFLOPS  # dense, MI355X_MICROARCH.md (1/16 ratio)
 X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6           # six bf16 products per fp32 multiply-add
 H2_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3           # three fp16 products (fp16 dense = bf16 dense)
+HBM_PEAK_TBS = 8.0  # HBM3E, MI355X_MICROARCH.md
 PEAKS = {'f32': FP32_MFMA_PEAK_TFLOPS, 'x3': X3_PEAK_TFLOPS, 'x5': BF16_MFMA_PEAK_TFLOPS / 5,
          'bf16': BF16_MFMA_PEAK_TFLOPS, 'h2': H2_PEAK_TFLOPS}
 METRIC = "image-pairs/sec training step, 256×256 SAR+optical Siamese U-Net, 1/2/4/8 MI355X"
@@ -91,18 +92,6 @@ def kernel_class(kind: str, ntaps: int, src_c: int) -> str:
     return f"{kind}_convT"
 
 
-def _eb(v) -> int:
-    return 2 if v.dtype == hip.DT_BF16 else 4
-
-
-def _vbytes(v) -> int:  # an NHWC view's payload
-    return int(v.n) * int(v.h) * int(v.w) * int(v.c) * _eb(v)
-
-
-def _tbytes(t) -> int:
-    return t.numel() * t.element_size()
-
-
 class KernelTimer:
     """HIP-event brackets around every MFMA conv launch (on torch's current stream, where libscd launches)."""
 
@@ -126,9 +115,8 @@ class KernelTimer:
             e.record()
             flops = 2.0 * src.n * out_h * out_w * n_out * len(taps[0]) * src.c
             dst = a[1] if len(a) > 1 else k['dst']
-            planes = {'h2': 2, 'x3': 3, 'x5': 2, 'bf16': 1, 'f32': 2}[arith]
-            alg = (_vbytes(src) + src.n * out_h * out_w * n_out * _eb(dst) + planes * len(taps[0]) * src.c * n_out * 2
-                   + (_tbytes(k['bn_bwd'][0]) if k.get('bn_bwd') is not None else 0))
+            alg = hip.igemm_alg_bytes(src, out_h, out_w, taps, n_out, dst, arith,
+                                      k['bn_bwd'][0] if k.get('bn_bwd') is not None else None)
             timer.events.append(('igemm', s, e, flops, arith, kernel_class('igemm', len(taps[0]), src.c), alg))
             return r
 
@@ -141,9 +129,7 @@ class KernelTimer:
             r = timer._wgrad(d, slabs)
             e.record()
             flops = 2.0 * d.rows.n * d.rows.h * d.rows.w * d.rows.c * d.ntaps * d.src.c
-            alg = (_vbytes(d.rows) + _vbytes(d.src) + slabs.numel() * slabs.element_size()
-                   + (_vbytes(d.rows_y) if d.rows_y.data else 0)  # the rows BatchNorm backward reads y
-                   + (_vbytes(d.rows_out) if d.rows_out.data else 0))  # and stores dy for the data grad (ABI 8)
+            alg = hip.wgrad_alg_bytes(d, slabs.numel() * slabs.element_size())
             timer.events.append(('wgrad', s, e, flops, arith, kernel_class('wgrad', d.ntaps, d.src.c), alg))
             return r
 
@@ -260,12 +246,15 @@ def cpu_baseline(cfg, batches=(2, 8), min_seconds=(8.0, 6.0), size: int = 256):
 
 
 def _conv_family(name: str):
+    """igemm / wgrad (the conv kernels), other (libscd's non-conv kernels: BatchNorm, pool / difference, head, loss,
+    packing, reductions) or torch (everything else in the step: the fused AdamW, torch's foreach adds)."""
     n = name.split('(')[0].replace('void ', '').replace('scd::', '').strip()
     if n.startswith('igemm'):
         return 'igemm'
     if n.startswith(('wgrad_halo', 'wgrad_x3', 'wgrad_f32')):
         return 'wgrad'
-    return None
+    return 'other' if 'scd::' in name else 'torch'
+
 
 
 def live_traffic(args, batch: int, size: int, timeout_s: int = 180):
@@ -299,22 +288,23 @@ def live_traffic(args, batch: int, size: int, timeout_s: int = 180):
             found = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs if f.endswith('counter_collection.csv')]
             if not found:
                 raise RuntimeError(f'{counter}: no counter_collection.csv')
-            fam = {'igemm': 0.0, 'wgrad': 0.0}
+            fam = {'igemm': 0.0, 'wgrad': 0.0, 'other': 0.0, 'torch': 0.0}
             with open(found[0]) as f:
                 for r in csv.DictReader(f):
-                    k = _conv_family(r['Kernel_Name'])
-                    if r['Counter_Name'] == counter and k:
-                        fam[k] += float(r['Counter_Value'])
+                    if r['Counter_Name'] == counter:
+                        fam[_conv_family(r['Kernel_Name'])] += float(r['Counter_Value'])
             tot[counter] = fam
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    by = {k: (2.0 * tot['FETCH_SIZE'][k] + tot['WRITE_SIZE'][k]) * 1024.0 / steps for k in ('igemm', 'wgrad')}
-    return {"bytes_per_step": round(sum(by.values())), "by_family": {k: round(v) for k, v in by.items()},
-            "fetch_bytes_per_step": round(2.0 * sum(tot['FETCH_SIZE'].values()) * 1024.0 / steps),
-            "write_bytes_per_step": round(sum(tot['WRITE_SIZE'].values()) * 1024.0 / steps),
+    by = {k: (2.0 * tot['FETCH_SIZE'][k] + tot['WRITE_SIZE'][k]) * 1024.0 / steps for k in tot['FETCH_SIZE']}
+    conv = ('igemm', 'wgrad')
+    return {"bytes_per_step": round(sum(by[k] for k in conv)), "by_family": {k: round(v) for k, v in by.items()},
+            "fetch_bytes_per_step": round(2.0 * sum(tot['FETCH_SIZE'][k] for k in conv) * 1024.0 / steps),
+            "write_bytes_per_step": round(sum(tot['WRITE_SIZE'][k] for k in conv) * 1024.0 / steps),
             "source": "measured by this run: two child processes of this workload (3 steps each) under rocprofv3 "
                       "--pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), FETCH x2 (gfx950 wide-read correction), "
-                      "KiB x 1024 / 3 steps; L2-miss fabric bytes of the igemm / wgrad kernels (Infinity-Cache hits "
+                      "KiB x 1024 / 3 steps; L2-miss fabric bytes of the igemm / wgrad kernels (bytes_per_step; "
+                      "by_family adds libscd's non-conv kernels ('other') and torch's ('torch': AdamW); Infinity-Cache hits "
                       "included, MI355X_MICROARCH.md HBM)"}
 
 
@@ -448,6 +438,16 @@ def main():
             traffic["algorithmic_bytes_per_step"] = round(alg)
             if traffic.get("bytes_per_step"):
                 traffic["traffic_over_algorithmic"] = round(traffic["bytes_per_step"] / alg, 3)
+            other = (traffic.get("by_family") or {}).get("other")
+            if other:
+                # the non-conv libscd kernels (HBM-bound by design): their bytes over the step time no conv kernel
+                # covers (the step has no idle between launches, profiles/r05_step_timeline.txt), an upper bound on
+                # their time, so a lower bound on their rate
+                rest_ms = ms - t_ms
+                traffic["other_family"] = {
+                    "bytes_per_step": round(other), "non_conv_ms_per_step": round(rest_ms, 3),
+                    "tb_per_s": round(other / (rest_ms * 1e-3) / 1e12, 3) if rest_ms > 0 else None,
+                    "peak_tb_per_s": HBM_PEAK_TBS}
         peak, shares = timer.peak()
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",

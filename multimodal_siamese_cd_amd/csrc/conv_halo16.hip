@@ -2041,6 +2041,9 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_x3(WgradArgs a)
 // lands by DMA as above and each X plane is transformed in place one patch ahead of its use -- max(fma(y, sc, sh), 0)
 // rounded to bf16, zero outside the image, wgrad_halo16_x3's expressions (bit-identical) -- so a patch is waited for one
 // iteration earlier (NB - 2 patches in flight) and the transform's LDS pass overlaps the current patch's MFMAs.
+// RBN: the rows are dL/da of a plain BatchNorm + ReLU (wgrad_halo16_x3's RBN, ABI 8): y and dL/da both land by DMA (y in a
+// third plane with dY's layout) and dY is formed in place in the same pass, with the writer blocks (channel tile 0)
+// storing it for the data grad; their stores are counted in the loop's vmcnt waits.
 // ------------------------------------------------------------------------------------------------
 namespace {
 // dummy destination of the padding DMA pieces that even out the per-wave piece count (zeros, never read)
@@ -2053,7 +2056,7 @@ constexpr int kDmaSink = 1024;
 #define SCD_WGRAD16_DMA_NB_XT 5  // 128-row blocks with the source transform: 3 patches in flight (64-row: NB above)
 #endif
 
-template <int RG, int NB, bool XT = false>
+template <int RG, int NB, bool XT = false, bool RBN = false>
 __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a) {
     constexpr int NT = 256 * RG, NW = NT / 64;
     constexpr int PH = 2, PW = 16, P = PH * PW;
@@ -2062,13 +2065,19 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
     constexpr int RSD = 128 * RG + 32;                // dY row stride (64 RG rows + 32 bytes)
     constexpr int PA = P * RSD, PB = HP * RS;         // plane bytes
     constexpr int PA_K = (PA + 1023) / 1024, PB_K = (PB + 1023) / 1024;  // 1 KB DMA pieces per plane
-    constexpr int PPW = (PA_K + PB_K + NW - 1) / NW;  // pieces per wave and patch (padded with sink pieces)
-    constexpr int STAGE = (PA_K + PB_K) * 1024;
+    constexpr int NPC = PA_K + PB_K + (RBN ? PA_K : 0);  // pieces per patch (RBN: y in its own plane, dY's layout)
+    constexpr int PPW = (NPC + NW - 1) / NW;          // pieces per wave and patch (padded with sink pieces)
+    constexpr int STAGE = NPC * 1024;
     constexpr int DCH = 8 * RG;                       // 16-byte dY chunks per staged pixel (64 RG rows)
+    constexpr int RBLK = 64 * RG;                     // dY rows of the block
     constexpr int NCB = W16L<1>::CB, NRB = W16L<1>::RB;
-    static_assert(NB >= (XT ? 3 : 2) && NB <= 6, "ring depth");
-    constexpr int CF = XT ? 2 * 2 * 64 * 4 : 0;  // XT: [segment 2][sc, sh][64 channels] floats
-    __shared__ __attribute__((aligned(16))) unsigned char smem[NB * STAGE + kDmaSink + CF];
+    constexpr bool TR = XT || RBN;                    // a transform pass one patch ahead
+    static_assert(NB >= (TR ? 3 : 2) && NB <= 6, "ring depth");
+    static_assert(!RBN || (P * DCH) % NT == 0, "rows transform: whole 16-byte chunks per thread");
+    constexpr int RCH = RBN ? P * DCH / NT : 0;       // RBN: dY chunks each thread forms (and the writer stores) per patch
+    constexpr int CFX = XT ? 2 * 2 * 64 * 4 : 0;      // XT: [segment 2][sc, sh][64 channels] floats
+    constexpr int CFR = RBN ? 2 * 7 * RBLK * 4 : 0;   // RBN: [segment 2][7 coefficients][RBLK] (wgrad_halo16_x3's)
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NB * STAGE + kDmaSink + CFX + CFR];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wave_u = __builtin_amdgcn_readfirstlane(wid);
@@ -2082,23 +2091,25 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
     const int pw_n = a.wo / PW, ph_n = a.ho / PH, pimg = pw_n * ph_n;
     const int npatch = a.n_img_w * pimg;
     const int pbeg = split * a.kchunk, pend = min(npatch, pbeg + a.kchunk);
+    const bool writer = RBN && a.rows_out && ct == 0;  // block-uniform: this block stores the formed dY
+    float omax = 0.f;                                  // writer: max |dY| stored by this thread
 
     const __amdgpu_buffer_rsrc_t rs_rows = make_rsrc(a.rows, a.rows_bytes);
     const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(a.src, a.src_bytes);
+    const __amdgpu_buffer_rsrc_t rs_y = make_rsrc(RBN ? a.rows_y : a.rows, RBN ? a.y_bytes : 0u);
     // This lane's 16-byte chunk of each of the wave's pieces: piece k of a patch is the block's piece u = k * NW + wave
-    // (u < PA_K: dY plane bytes [1024 u, +1024); u < PA_K + PB_K: X plane; else a sink piece).  Position within its
-    // plane: row = byte / stride, chunk = (byte % stride) / 16; chunks past the data (the row pads, the tail) read out of
-    // range.  Per piece: the patch-invariant part of the global byte offset (kOOB: never loads) and the LDS offset.
-    uint32_t g_rel[PPW];  // dY: (pixel-in-patch row, chunk) offset relative to the patch's first pixel; X: unused
-    int d_row[PPW], x_hy[PPW], x_hx[PPW], chunk[PPW], kind[PPW];  // kind 0 dY, 1 X, 2 sink / pad
+    // (u < PA_K: dY plane bytes [1024 u, +1024); then the X plane; RBN: then the y plane; else a sink piece).  Position
+    // within its plane: row = byte / stride, chunk = (byte % stride) / 16; chunks past the data (the row pads, the tail)
+    // read out of range.
+    int d_row[PPW], x_hy[PPW], x_hx[PPW], chunk[PPW], kind[PPW];  // kind 0 dY / y, 1 X, 2 sink / pad
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {
         const int u = k * NW + wave_u;
         kind[k] = 2;
         d_row[k] = x_hy[k] = x_hx[k] = chunk[k] = 0;
-        g_rel[k] = 0;
-        if (u < PA_K) {
-            const int b = u * 1024 + lane * 16;
+        const bool is_y = RBN && u >= PA_K + PB_K && u < NPC;
+        if (u < PA_K || is_y) {
+            const int b = (is_y ? u - PA_K - PB_K : u) * 1024 + lane * 16;
             const int row = b / RSD, ch = (b - row * RSD) / 16;
             if (row < P && ch < DCH) {
                 kind[k] = 0;
@@ -2123,19 +2134,23 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
 #pragma unroll
         for (int k = 0; k < PPW; ++k) {
             const int u = k * NW + wave_u;
+            const bool is_y = RBN && u >= PA_K + PB_K && u < NPC;
             uint32_t off = kOOB;
             if (kind[k] == 0) {
                 const int pix = (img * a.ho + y0 + (d_row[k] >> 4)) * a.wo + x0 + (d_row[k] & 15);
-                off = uint32_t(pix * a.ldc_r + r0 + 8 * chunk[k]) * 2u;
+                off = uint32_t(pix * (is_y ? a.ldc_y : a.ldc_r) + r0 + 8 * chunk[k]) * 2u;
             } else if (kind[k] == 1) {
                 const int sy = y0 - 1 + x_hy[k], sx = x0 - 1 + x_hx[k];
                 if (unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws))
                     off = uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + 8 * chunk[k]) * 2u;
             }
-            unsigned char *dst = u < PA_K + PB_K ? smem + slot * STAGE + u * 1024 : smem + NB * STAGE;
+            unsigned char *dst = u < NPC ? smem + slot * STAGE + u * 1024 : smem + NB * STAGE;
             if (u < PA_K)  // wave-uniform
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_rows, (__attribute__((address_space(3))) void *)dst, 16, off,
                                                          0, 0, 0);
+            else if (is_y)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_y, (__attribute__((address_space(3))) void *)dst, 16, off, 0,
+                                                         0, 0);
             else
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_src, (__attribute__((address_space(3))) void *)dst, 16, off,
                                                          0, 0, 0);
@@ -2157,52 +2172,114 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
     const uint32_t dbase = lds_addr(smem) + (py * PW + pxq) * RSD + (16 * NRB * wi + 4 * (w16 & 3)) * 2;
     const uint32_t xbase = lds_addr(smem) + PA_K * 1024 + (py * HW_ + pxq) * RS + (16 * NCB * wj + 4 * (w16 & 3)) * 2;
 
-    // XT: the transform of patch pi's X plane in ring slot `slot`, in place: this thread's 16-byte chunks q = tid + i NT
-    // (halo pixel q >> 3, channels c0 + 8 (q & 7) ..+7); out-of-image chunks stay the DMA's zeros
-    float *const cf = reinterpret_cast<float *>(smem + NB * STAGE + kDmaSink);  // [seg][sc | sh][64]
+    // The transforms of patch pi in ring slot `slot_`, in place, one patch ahead of its MFMAs:
+    //   XT  this thread's X chunks q = tid + i NT (halo pixel q >> 3, channels c0 + 8 (q & 7) ..+7): the source's
+    //       BatchNorm + ReLU, rounded to bf16; out-of-image chunks stay the DMA's zeros;
+    //   RBN this thread's dY chunks q = tid + i NT (pixel q / DCH, rows r0 + 8 (q % DCH) ..+7): dY = the BatchNorm
+    //       backward of (y, dL/da) (bn_bwd_dy4, rounded once to bf16 as bn_bwd_apply stores it), which the writer blocks
+    //       also store for the data grad.
+    float *const cfx = reinterpret_cast<float *>(smem + NB * STAGE + kDmaSink);         // [seg][sc | sh][64]
+    float *const cfr = reinterpret_cast<float *>(smem + NB * STAGE + kDmaSink + CFX);   // [seg][7][RBLK]
     auto transform = [&](int pi, int slot_) {
         const int img = pi / pimg, pr = pi - img * pimg;
         const int y0 = patch_y0(pr, pw_n, ph_n, PH), x0 = patch_x0(pr, pw_n, ph_n, PW);
-        const float *c_sc = cf + (img / a.src_seg_imgs) * 128, *c_sh = c_sc + 64;
-        unsigned char *const xp = smem + slot_ * STAGE + PA_K * 1024;
+        if constexpr (XT) {
+            const float *c_sc = cfx + (img / a.src_seg_imgs) * 128, *c_sh = c_sc + 64;
+            unsigned char *const xp = smem + slot_ * STAGE + PA_K * 1024;
 #pragma unroll
-        for (int i = 0; i < (HP * 8 + NT - 1) / NT; ++i) {
-            const int q = tid + i * NT;
-            if (q >= HP * 8) break;
-            const int hp = q >> 3, j = q & 7;
-            const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
-            const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
-            if (unsigned(sy) >= unsigned(a.hs) || unsigned(sx) >= unsigned(a.ws)) continue;
-            u32x4 *const ptr = reinterpret_cast<u32x4 *>(xp + hp * RS + j * 16);
-            const u32x4 raw = *ptr;
-            u32x4 out;
+            for (int i = 0; i < (HP * 8 + NT - 1) / NT; ++i) {
+                const int q = tid + i * NT;
+                if (q >= HP * 8) break;
+                const int hp = q >> 3, j = q & 7;
+                const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
+                const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
+                if (unsigned(sy) >= unsigned(a.hs) || unsigned(sx) >= unsigned(a.ws)) continue;
+                u32x4 *const ptr = reinterpret_cast<u32x4 *>(xp + hp * RS + j * 16);
+                const u32x4 raw = *ptr;
+                u32x4 out;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                f32x4 x = unpk_bf16x4(u32x2{raw[2 * h], raw[2 * h + 1]});
-                const f32x4 sc = *reinterpret_cast<const f32x4 *>(c_sc + 8 * j + 4 * h);
-                const f32x4 sh = *reinterpret_cast<const f32x4 *>(c_sh + 8 * j + 4 * h);
+                for (int h = 0; h < 2; ++h) {
+                    f32x4 x = unpk_bf16x4(u32x2{raw[2 * h], raw[2 * h + 1]});
+                    const f32x4 sc = *reinterpret_cast<const f32x4 *>(c_sc + 8 * j + 4 * h);
+                    const f32x4 sh = *reinterpret_cast<const f32x4 *>(c_sh + 8 * j + 4 * h);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) x[e] = fmaxf(fmaf(x[e], sc[e], sh[e]), 0.f);
-                const u32x2 pk = pk_bf16x4(x);
-                out[2 * h] = pk[0];
-                out[2 * h + 1] = pk[1];
+                    for (int e = 0; e < 4; ++e) x[e] = fmaxf(fmaf(x[e], sc[e], sh[e]), 0.f);
+                    const u32x2 pk = pk_bf16x4(x);
+                    out[2 * h] = pk[0];
+                    out[2 * h + 1] = pk[1];
+                }
+                *ptr = out;
             }
-            *ptr = out;
+        }
+        if constexpr (RBN) {
+            const float *cs = cfr + (img / a.rows_seg_imgs) * 7 * RBLK;
+            unsigned char *const dp = smem + slot_ * STAGE;
+            const unsigned char *const yp = smem + slot_ * STAGE + (PA_K + PB_K) * 1024;
+#pragma unroll
+            for (int i = 0; i < RCH; ++i) {
+                const int q = tid + i * NT;
+                const int px = q / DCH, j = q - px * DCH;
+                u32x4 *const ptr = reinterpret_cast<u32x4 *>(dp + px * RSD + j * 16);
+                const u32x4 raw = *ptr, yr = *reinterpret_cast<const u32x4 *>(yp + px * RSD + j * 16);
+                u32x4 out;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float *c = cs + 8 * j + 4 * h;
+                    const f32x4 mu = *reinterpret_cast<const f32x4 *>(c), iv = *reinterpret_cast<const f32x4 *>(c + RBLK);
+                    const f32x4 sc = *reinterpret_cast<const f32x4 *>(c + 2 * RBLK);
+                    const f32x4 sf = *reinterpret_cast<const f32x4 *>(c + 3 * RBLK);
+                    const f32x4 k1 = *reinterpret_cast<const f32x4 *>(c + 4 * RBLK);
+                    const f32x4 k2 = *reinterpret_cast<const f32x4 *>(c + 5 * RBLK);
+                    const f32x4 mul = *reinterpret_cast<const f32x4 *>(c + 6 * RBLK);
+                    const f32x4 dv = bn_bwd_dy4(unpk_bf16x4(u32x2{yr[2 * h], yr[2 * h + 1]}),
+                                                unpk_bf16x4(u32x2{raw[2 * h], raw[2 * h + 1]}), mu, iv, sc, sf, k1, k2, mul);
+                    const u32x2 pk = pk_bf16x4(dv);
+                    out[2 * h] = pk[0];
+                    out[2 * h + 1] = pk[1];
+                    if (writer) {
+                        const f32x4 r = unpk_bf16x4(pk);
+                        omax = fmaxf(omax, fmaxf(fmaxf(fabsf(r[0]), fabsf(r[1])), fmaxf(fabsf(r[2]), fabsf(r[3]))));
+                    }
+                }
+                *ptr = out;
+                if (writer) {  // one 16-byte store per chunk (vmcnt: counted in the loop's waits)
+                    const int pix = (img * a.ho + y0 + (px >> 4)) * a.wo + x0 + (px & 15);
+                    *reinterpret_cast<u32x4 *>(static_cast<unsigned short *>(a.rows_out) + size_t(pix) * a.ldc_o + r0 +
+                                               8 * j) = out;
+                }
+            }
         }
     };
     if constexpr (XT) {  // both segments' coefficients of the block's 64 channels (launcher: at most two)
         const int nsl = a.n_img_w / a.src_seg_imgs;
         for (int e = tid; e < nsl * 64; e += NT) {
             const int sg = e / 64, c = e - sg * 64;
-            cf[sg * 128 + c] = a.src_scale[sg * a.C + c0 + c];
-            cf[sg * 128 + 64 + c] = a.src_shift[sg * a.C + c0 + c];
+            cfx[sg * 128 + c] = a.src_scale[sg * a.C + c0 + c];
+            cfx[sg * 128 + 64 + c] = a.src_shift[sg * a.C + c0 + c];
+        }
+    }
+    if constexpr (RBN) {  // the block's rows' BatchNorm coefficients (wgrad_halo16_x3's table; at most two segments)
+        const int nsl = a.n_img_w / a.rows_seg_imgs;
+        for (int e = tid; e < nsl * RBLK; e += NT) {
+            const int sg = e / RBLK, r = e - sg * RBLK, o = sg * a.R + r0 + r;
+            const float iv = a.rbn_inv[o];
+            float *c = cfr + sg * 7 * RBLK + r;
+            c[0] = a.rbn_mean[o];
+            c[RBLK] = iv;
+            c[2 * RBLK] = a.rbn_scale[o];
+            c[3 * RBLK] = a.rbn_shift[o];
+            c[4 * RBLK] = a.rbn_coef[2 * o];
+            c[5 * RBLK] = a.rbn_coef[2 * o + 1];
+            c[6 * RBLK] = (a.rbn_gamma ? a.rbn_gamma[r0 + r] : 1.f) * iv;  // bn_bwd_apply's mul = gamma * invstd
         }
     }
 
+    // the writer's dY stores of the previous transform are the youngest vector-memory operations at each wait
+    const int wst = writer ? RCH : 0;
 #pragma unroll
     for (int k = 0; k < NB - 1; ++k)
         if (pbeg + k < pend) issue(pbeg + k, k);
-    if constexpr (XT) {  // patch pbeg transformed before the loop (its first barrier publishes it)
+    if constexpr (TR) {  // patch pbeg transformed before the loop (its first barrier publishes it)
         if (pbeg < pend) {
             const int ahead = min(NB - 2, pend - 1 - pbeg);
             if (ahead >= 3)
@@ -2219,22 +2296,33 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
     }
     int slot = 0;
     for (int pi = pbeg; pi < pend; ++pi) {
-        // this wave's pieces of patch pi (XT: pi + 1, transformed during this iteration): younger in flight are
-        // those of the patches after it up to min(pi + NB - 2, pend - 1)
-        const int ahead = XT ? (pi + 1 < pend ? min(NB - 3, pend - 2 - pi) : -1) : min(NB - 2, pend - 1 - pi);
-        if (ahead >= 4)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PPW) : "memory");
-        else if (ahead == 3)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW) : "memory");
-        else if (ahead == 2)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
-        else if (ahead == 1)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-        else if (ahead == 0)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // this wave's pieces of patch pi (with a transform: pi + 1, transformed during this iteration): younger in
+        // flight are those of the patches after it up to min(pi + NB - 2, pend - 1), and the writer's stores
+        const int ahead = TR ? (pi + 1 < pend ? min(NB - 3, pend - 2 - pi) : -1) : min(NB - 2, pend - 1 - pi);
+        if (wst == 0) {
+            if (ahead >= 4)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PPW) : "memory");
+            else if (ahead == 3)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW) : "memory");
+            else if (ahead == 2)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+            else if (ahead == 1)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+            else if (ahead == 0)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if constexpr (RBN) {  // RCH stores of the last transform behind the pieces
+            if (ahead >= 3)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPW + RCH) : "memory");
+            else if (ahead == 2)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + RCH) : "memory");
+            else if (ahead == 1)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW + RCH) : "memory");
+            else if (ahead == 0)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RCH) : "memory");
+        }
         lds_barrier();  // every wave's pieces of patch pi landed; every wave left the slot of patch pi - 1
         if (pi + NB - 1 < pend) issue(pi + NB - 1, slot == 0 ? NB - 1 : slot - 1);
-        if constexpr (XT) {
+        if constexpr (TR) {
             if (pi + 1 < pend) transform(pi + 1, slot == NB - 1 ? 0 : slot + 1);
         }
         const uint32_t bo = uint32_t(slot * STAGE);
@@ -2247,6 +2335,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
         slot = slot == NB - 1 ? 0 : slot + 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (writer && a.rows_out_bound) wave_max_bound(a.rows_out_bound, omax);  // uniform: the whole block takes part
 
     float *slab = a.slabs + size_t(split) * a.R * a.Ng;
 #pragma unroll
@@ -2638,7 +2727,18 @@ void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
     if (a.rows_y) {  // the caller checked wgrad16_rows_bn_ok
         if (wgrad16_planes(a.math, a.tune, bounded) == 4)
             w16_launch_rbn<4, false>(rb, a, grid, s);
-        else if (a.sb)
+        else if (a.sb && !(a.tune & SCD_TUNE_WGRAD16_REGSTAGE) && (!a.src_scale || a.n_img_w / a.src_seg_imgs <= 2)) {
+            // bf16 storage: the LDS-DMA ring with y and dL/da landed raw and dY formed in place (+ the source transform)
+            if (rb == 128) {
+                if (a.src_scale)
+                    hipLaunchKernelGGL((wgrad_halo16_dma<2, 5, true, true>), grid, dim3(512), 0, s, a);
+                else
+                    hipLaunchKernelGGL((wgrad_halo16_dma<2, 5, false, true>), grid, dim3(512), 0, s, a);
+            } else if (a.src_scale)
+                hipLaunchKernelGGL((wgrad_halo16_dma<1, 3, true, true>), grid, dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL((wgrad_halo16_dma<1, 3, false, true>), grid, dim3(256), 0, s, a);
+        } else if (a.sb)
             w16_launch_rbn<1, true>(rb, a, grid, s);
         else
             w16_launch_rbn<1, false>(rb, a, grid, s);

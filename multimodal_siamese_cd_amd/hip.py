@@ -601,6 +601,34 @@ def wgrad_arith(d: 'WGRAD') -> str:
     return _MATH_BY_ID[rc]
 
 
+# Algorithmic bytes of a conv launch: every operand read once, every output written once.  The ONE definition behind
+# bench.py's roofline.traffic.algorithmic_bytes_per_step and tools/traffic_table.py's per-launch table.
+_WEIGHT_PLANES = {'h2': 2, 'x3': 3, 'x5': 2, 'bf16': 1, 'f32': 2}
+
+
+def _view_bytes(v: NHWC) -> int:
+    return int(v.n) * int(v.h) * int(v.w) * int(v.c) * (2 if v.dtype == DT_BF16 else 4)
+
+
+def igemm_alg_bytes(src: NHWC, out_h: int, out_w: int, taps, n_out: int, dst: NHWC, arith: str,
+                    bn_bwd_y: torch.Tensor | None = None) -> int:
+    """scd_conv_igemm: src (n h_s w_s c) + the output (n out_h out_w n_out; a ConvT's pixel-shuffled store holds the
+    same elements) + the split weights (planes of the arithmetic `arith` x K x n_out x 2 B) + the y a fused
+    BatchNorm-backward epilogue reads."""
+    eb = 2 if dst.dtype == DT_BF16 else 4
+    k = len(taps[0]) * int(src.c)
+    out = int(src.n) * out_h * out_w * n_out * eb
+    yb = 0 if bn_bwd_y is None else bn_bwd_y.numel() * bn_bwd_y.element_size()
+    return _view_bytes(src) + out + _WEIGHT_PLANES[arith] * k * n_out * 2 + yb
+
+
+def wgrad_alg_bytes(d: 'WGRAD', slab_bytes: int) -> int:
+    """scd_conv_wgrad: dY rows (n h w R) + X (n h_s w_s C) + the fp32 split-K slabs written [+ the y of a rows BatchNorm
+    transform] [+ the dy it stores for the data grad (ABI 8)]."""
+    return (_view_bytes(d.rows) + _view_bytes(d.src) + int(slab_bytes)
+            + (_view_bytes(d.rows_y) if d.rows_y.data else 0) + (_view_bytes(d.rows_out) if d.rows_out.data else 0))
+
+
 def wgrad_rows_per_block(d: 'WGRAD') -> int:
     """dY rows per workgroup of the halo weight-grad kernel for this descriptor (64 / 128; 0: another kernel)."""
     rc = lib().scd_wgrad_rows_per_block(ctypes.byref(d))

@@ -562,3 +562,39 @@ def test_weight_grad_dma_ring_bit_identical(dev, n, h, w, r, c, cs, src_bn):
     assert out[0][0] == out[1][0]
     assert not torch.isnan(out[0][1]).any()
     assert torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize('n,h,w,r,c,nseg,src_bn', [(4, 32, 32, 128, 64, 2, False), (2, 16, 48, 64, 128, 2, True),
+                                                   (3, 8, 32, 256, 64, 1, True), (2, 2, 16, 64, 64, 1, False)])
+def test_weight_grad_dma_ring_rows_bn_bit_identical(dev, n, h, w, r, c, nseg, src_bn):
+    """The DMA-ring weight grad forming a plain BatchNorm backward's dY in LDS (y and dL/da landed raw, ABI 8 rows_bn)
+    against the register-staged kernel: the stored dY (rows_out, written once by the channel-tile-0 blocks), its bound
+    and every slab element bit-identical, with and without the source transform, 64- and 128-row blocks, two row tiles
+    (r = 256), one patch row."""
+    g = torch.Generator(device=dev).manual_seed(n + h + w + r + c)
+    da = torch.randn(n, h, w, r, device=dev, generator=g).to(torch.bfloat16)
+    y = (torch.randn(n, h, w, r, device=dev, generator=g) * 2 + 0.3).to(torch.bfloat16)
+    x = torch.randn(n, h, w, c, device=dev, generator=g).to(torch.bfloat16)
+    mu, iv = torch.randn(nseg * r, device=dev, generator=g) * 0.1, torch.rand(nseg * r, device=dev, generator=g) + .5
+    sc, sh = torch.rand(nseg * r, device=dev, generator=g) + 0.5, torch.randn(nseg * r, device=dev, generator=g) * 0.3
+    gamma = torch.rand(r, device=dev, generator=g) + 0.5
+    coef = torch.randn(nseg * r * 2, device=dev, generator=g) * 0.01
+    xbn = ((torch.rand(nseg * c, device=dev, generator=g) + 0.5, torch.randn(nseg * c, device=dev, generator=g) * 0.5,
+            nseg) if src_bn else None)
+    out = []
+    for tune in (0, hip.TUNE_WGRAD16_REGSTAGE):
+        with hip.conv_scope('bf16', tune=tune):
+            assert hip.wgrad_rows_bn_supported(nhwc(da), nhwc(x), 1, TAPS_3X3, xbn)
+            dy = torch.full_like(y, float('nan'))
+            bound = torch.zeros(1, device=dev)
+            d, nsplit, nbytes = hip.wgrad_plan(nhwc(da), nhwc(x), 1, TAPS_3X3, xbn,
+                                               rows_bn=(nhwc(y), nseg, mu, iv, gamma, sc, sh, coef), rows_out=nhwc(dy),
+                                               rows_out_bound=bound)
+            slabs = torch.full((nbytes // 4,), float('nan'), device=dev)
+            hip.conv_wgrad(d, slabs)
+            out.append((nsplit, slabs.cpu(), dy.cpu(), bound.item()))
+    assert out[0][0] == out[1][0]
+    assert not torch.isnan(out[0][1]).any() and not torch.isnan(out[0][2].float()).any()
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
+    assert out[0][3] == out[1][3] == out[0][2].float().abs().max().item()

@@ -698,6 +698,7 @@ def test_wgrad_c16_deferred_bn_backward(dev, math, n, h, w, co, nseg, tiles):
 @pytest.mark.parametrize('math,dt,co,ci,nseg,src_bn', [
     ('h2', torch.float32, 128, 64, 2, False), ('h2', torch.float32, 256, 128, 1, True),
     ('bf16', torch.bfloat16, 64, 64, 2, False), ('bf16', torch.bfloat16, 128, 64, 1, True),
+    ('bf16', torch.bfloat16, 256, 128, 2, True), ('bf16', torch.bfloat16, 64, 128, 1, True),
     ('bf16', torch.float32, 64, 128, 2, False)])
 def test_halo_wgrad_forms_and_stores_dy(dev, math, dt, co, ci, nseg, src_bn):
     """ABI 8: the 64-channel-multiple halo weight grad with the rows' BatchNorm backward (scd_wgrad_t.rows_y) stores

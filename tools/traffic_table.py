@@ -9,11 +9,13 @@ order with its operand shapes; `table` pairs them with the conv dispatches of ea
 launches more than one dispatch -- > 2 GiB image chunks -- is refused) and prints, per launch of the last step:
 algorithmic bytes (every operand read once, every output written once), FETCH (x2, the gfx950 wide-read
 correction of MI355X_MICROARCH.md) and WRITE bytes, and their ratio.  Algorithmic bytes:
-  igemm: src (n h_s w_s c) + dst (n h w n_out) + the split weights (planes x K x n_out x 2 B) [+ y of a fused
-         BatchNorm-backward epilogue]
+  igemm: src (n h_s w_s c) + the output (n h w n_out elements: a ConvT's pixel-shuffled store holds as many) + the
+         split weights (planes of the launch's arithmetic x K x n_out x 2 B) [+ y of a fused BatchNorm-backward epilogue]
   wgrad: dY rows (n h w R) + X (n h_s w_s C) [+ y of a rows transform] [+ the dy it stores] + the fp32 slabs written
          (splits x R x taps C)
 FETCH counts L2 misses that the Infinity Cache may still serve, so a ratio above 1 is re-read traffic past L2.
+The per-launch algorithmic bytes are hip.igemm_alg_bytes / hip.wgrad_alg_bytes, the same functions bench.py sums for
+roofline.traffic.algorithmic_bytes_per_step (one definition; round 5's table had counted a ConvT forward's output 4x).
 """
 import argparse
 import csv
@@ -23,14 +25,6 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-
-
-def _eb(v):
-    return 2 if v.dtype == 1 else 4
-
-
-def _px(v):
-    return int(v.n) * int(v.h) * int(v.w)
 
 
 def log_main(a):
@@ -51,33 +45,31 @@ def log_main(a):
     step_no = [0]
     orig_ig, orig_wg = hip.conv_igemm, hip.conv_wgrad
 
-    def igemm(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, **kw):
-        planes = {'h2': 2, 'x3': 3, 'x5': 2, 'bf16': 1, 'f32': 2}.get(hip.conv_math(), 2)
-        k = len(taps[0]) * int(src.c)
-        alg = _px(src) * src.c * _eb(src) + _px(dst) * n_out * _eb(dst) + planes * k * n_out * 2
+    def igemm(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode=0, **kw):
+        # bench.py's definition (hip.igemm_alg_bytes, the launch's own arithmetic)
+        arith = hip.igemm_arith(src, out_h, out_w, stride, taps, wpk, n_out, dst, store_mode,
+                                src_bound=kw.get('src_bound'))
+        alg = hip.igemm_alg_bytes(src, out_h, out_w, taps, n_out, dst, arith,
+                                  kw['bn_bwd'][0] if kw.get('bn_bwd') is not None else None)
         extra = []
         if kw.get('in_bn') is not None:
             extra.append('in_bn')
         if kw.get('bn_bwd') is not None:
-            y = kw['bn_bwd'][0]
-            alg += y.numel() * y.element_size()
             extra.append('bn_bwd')
         if kw.get('stat_rec') is not None:
             extra.append('stats')
         calls.append(dict(step=step_no[0], kind='igemm', taps=len(taps[0]), stride=stride,
                           shape=f'{src.n}x{src.h}x{src.w}x{src.c} -> {dst.n}x{out_h}x{out_w}x{n_out}',
                           extra=','.join(extra), alg_bytes=int(alg)))
-        return orig_ig(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, **kw)
+        return orig_ig(src, out_h, out_w, stride, taps, wpk, n_out, bias, dst, store_mode, **kw)
 
     def wgrad(d, slabs):
         r, x = d.rows, d.src
-        alg = _px(r) * r.c * _eb(r) + _px(x) * x.c * _eb(x) + slabs.numel() * slabs.element_size()
+        alg = hip.wgrad_alg_bytes(d, slabs.numel() * slabs.element_size())  # bench.py's definition
         extra = []
         if d.rows_y.data:
-            alg += _px(d.rows_y) * d.rows_y.c * _eb(d.rows_y)
             extra.append('rows_bn')
         if d.rows_out.data:  # ABI 8: the formed dy stored for the data grad
-            alg += _px(d.rows_out) * d.rows_out.c * _eb(d.rows_out)
             extra.append('rows_out')
         if d.src_scale:
             extra.append('src_bn')
