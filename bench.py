@@ -275,6 +275,8 @@ def live_traffic(args, batch: int, size: int, timeout_s: int = 180):
         child += ['--math', args.math]
     if args.storage:
         child += ['--storage', args.storage]
+    if int(args.tune, 0):
+        child += ['--tune', args.tune]
     steps = 3
     tot = {}
     tmp = tempfile.mkdtemp(prefix='scd_pmc_', dir='/tmp')
@@ -322,6 +324,7 @@ def main():
                     help='skip the live PMC traffic passes (two rocprofv3 child runs of this workload)')
     ap.add_argument('--math', default=None, choices=['f32', 'x3', 'x5', 'bf16', 'h2'],
                     help='conv arithmetic (default: from the config, engine.conv_math_for: MODEL.PRECISION fp32 -> h2)')
+    ap.add_argument('--tune', default='0', help='process-default SCD_TUNE_* bits (hex or decimal; A/B of kernel variants)')
     ap.add_argument('--storage', default=None, choices=['fp32', 'bf16'],
                     help='activation / gradient storage (default: engine.act_storage_for: bf16 for the bf16 arithmetic)')
     args = ap.parse_args()
@@ -330,6 +333,8 @@ def main():
     dev = torch.device('cuda', parallel.device_index(local_rank))
     torch.cuda.set_device(dev)
     hip.load_library()
+    if int(args.tune, 0):
+        hip.set_tune(int(args.tune, 0))
 
     cfg = experiment_manager.load_cfg(args.config)
     if args.math:
