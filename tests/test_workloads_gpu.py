@@ -12,10 +12,12 @@ bf16 workloads: bf16 roundings amplify through depth, so no bf16 implementation 
 model level (the kernel tests pin the arithmetic exactly).  Outputs within 3e-2 of the fp32 oracle and closer to an
 oracle with the bf16 conv arithmetic emulated than to the fp32 one; loss within 1e-2; every weight gradient's cosine
 similarity to the fp32 oracle's at most 0.05 below what the bf16-emulating oracle itself reaches, and > 0.85 (the
-emulating oracle itself reaches 0.897 on the WhateverNet BatchNorm shifts of the deepest levels at 512x512).
+emulating oracle itself reaches 0.897 on the WhateverNet BatchNorm shifts of the deepest levels at 512x512) wherever
+the emulating oracle reaches 0.9 -- at the shipped bs=64 the large-map ConvTranspose bias sums do not (round 6).
 
-Sizes: the workloads' own tiles and topologies ([64, 128, 256, 512], 256x256; WhateverNet 512x512) at bs=2, and the
-headline baseline_siamese at its bench batch, bs=32 (the BatchNorm-derived h2 bounds grow with the batch).
+Sizes: the workloads' own tiles and topologies ([64, 128, 256, 512], 256x256; WhateverNet 512x512) at bs=2, the
+headline baseline_siamese at its bench batch, bs=32 (the BatchNorm-derived h2 bounds grow with the batch), and every
+workload at its shipped batch, forward and backward (siamese and dtsiamese bs=64, dual-stream bs=64, MMCR bs=4).
 """
 import contextlib
 
@@ -157,8 +159,9 @@ def test_fp32_workload_matches_oracle(dev, monkeypatch, wid, config, model, topo
 
 BF16_WORKLOADS = [
     # id, config file, model, topology, tile, batch, labelled samples
+    # (siamese_mmcr_alpha0500 runs at its shipped batch, bs=4, in test_mmcr_shipped_batch: one oracle pass of each kind
+    # there instead of a bs=2 pass here as well)
     ('baseline_dualstream', 'baseline_dualstream', 'dualstreamunet', FULL, 256, 2, None),
-    ('siamese_mmcr_alpha0500', 'siamese_mmcr_alpha0500', 'whatevernet', FULL, 512, 2, [True, False]),
 ]
 
 
