@@ -2052,6 +2052,9 @@ constexpr int kDmaSink = 1024;
 #ifndef SCD_WGRAD16_DMA_NB
 #define SCD_WGRAD16_DMA_NB 4  // ring depth: 3 patches in flight while one is computed
 #endif
+#ifndef SCD_WGRAD16_DMA_TRANSFORMS
+#define SCD_WGRAD16_DMA_TRANSFORMS 1  // 0: the ring for untransformed operands only (A/B build)
+#endif
 #ifndef SCD_WGRAD16_DMA_NB_XT
 #define SCD_WGRAD16_DMA_NB_XT 5  // 128-row blocks with the source transform: 3 patches in flight (64-row: NB above)
 #endif
@@ -2101,20 +2104,23 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
     // (u < PA_K: dY plane bytes [1024 u, +1024); then the X plane; RBN: then the y plane; else a sink piece).  Position
     // within its plane: row = byte / stride, chunk = (byte % stride) / 16; chunks past the data (the row pads, the tail)
     // read out of range.
-    int d_row[PPW], x_hy[PPW], x_hx[PPW], chunk[PPW], kind[PPW];  // kind 0 dY / y, 1 X, 2 sink / pad
+    // Per piece, precomputed once: rel = its element offset relative to the patch's first pixel (dY / y: that pixel's
+    // row start; X: the halo's, one row and column up-left, so the validity test per patch is two compares) -- issue()
+    // then adds one patch base per plane and tests the halo piece's bounds: a few VALU per piece instead of the index
+    // arithmetic that made the first DMA ring (round 6, profiles/r06_wgrad_dma_pmc) 2.3 VALU per MFMA.
+    int rel[PPW], x_hy[PPW], x_hx[PPW], kind[PPW];  // kind 0 dY / y, 1 X, 2 sink / pad
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {
         const int u = k * NW + wave_u;
         kind[k] = 2;
-        d_row[k] = x_hy[k] = x_hx[k] = chunk[k] = 0;
+        rel[k] = x_hy[k] = x_hx[k] = 0;
         const bool is_y = RBN && u >= PA_K + PB_K && u < NPC;
         if (u < PA_K || is_y) {
             const int b = (is_y ? u - PA_K - PB_K : u) * 1024 + lane * 16;
             const int row = b / RSD, ch = (b - row * RSD) / 16;
             if (row < P && ch < DCH) {
                 kind[k] = 0;
-                d_row[k] = row;
-                chunk[k] = ch;
+                rel[k] = ((row >> 4) * a.wo + (row & 15)) * (is_y ? a.ldc_y : a.ldc_r) + r0 + 8 * ch;
             }
         } else if (u < PA_K + PB_K) {
             const int b = (u - PA_K) * 1024 + lane * 16;
@@ -2123,27 +2129,44 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
                 kind[k] = 1;
                 x_hy[k] = row / HW_;
                 x_hx[k] = row - (row / HW_) * HW_;
-                chunk[k] = ch;
+                rel[k] = ((x_hy[k] - 1) * a.ws + (x_hx[k] - 1)) * a.ldc_s + c0 + 8 * ch;
             }
         }
     }
-    // Issue patch pi's pieces into ring slot `slot` (wave-uniform LDS base per piece: M0 + lane * 16).
-    auto issue = [&](int pi, int slot) {
+    // The patch walk as a cursor (image, first row, first column): down each 16-pixel column strip (patch_y0 / x0's
+    // order), advanced by compares instead of divisions.
+    struct Cursor {
+        int img, y0, x0;
+    };
+    auto cursor_at = [&](int pi) {
         const int img = pi / pimg, pr = pi - img * pimg;
-        const int y0 = patch_y0(pr, pw_n, ph_n, PH), x0 = patch_x0(pr, pw_n, ph_n, PW);
+        return Cursor{img, patch_y0(pr, pw_n, ph_n, PH), patch_x0(pr, pw_n, ph_n, PW)};
+    };
+    auto advance = [&](Cursor &c) {
+        if constexpr (SCD_WGRAD_ROW_WALK) {
+            if ((c.x0 += PW) == a.wo) {
+                c.x0 = 0;
+                if ((c.y0 += PH) == a.ho) c.y0 = 0, ++c.img;
+            }
+        } else if ((c.y0 += PH) == a.ho) {
+            c.y0 = 0;
+            if ((c.x0 += PW) == a.wo) c.x0 = 0, ++c.img;
+        }
+    };
+    // Issue the pieces of the patch at cursor `c` into ring slot `slot` (wave-uniform LDS base per piece: M0 + lane * 16).
+    auto issue = [&](const Cursor &c, int slot) {
+        const int img = c.img, y0 = c.y0, x0 = c.x0;
+        const int pix0 = (img * a.ho + y0) * a.wo + x0;  // the patch's first pixel (rows and src share h, w)
+        const int br = pix0 * a.ldc_r, by = RBN ? pix0 * a.ldc_y : 0, bs = pix0 * a.ldc_s;
 #pragma unroll
         for (int k = 0; k < PPW; ++k) {
             const int u = k * NW + wave_u;
             const bool is_y = RBN && u >= PA_K + PB_K && u < NPC;
-            uint32_t off = kOOB;
-            if (kind[k] == 0) {
-                const int pix = (img * a.ho + y0 + (d_row[k] >> 4)) * a.wo + x0 + (d_row[k] & 15);
-                off = uint32_t(pix * (is_y ? a.ldc_y : a.ldc_r) + r0 + 8 * chunk[k]) * 2u;
-            } else if (kind[k] == 1) {
-                const int sy = y0 - 1 + x_hy[k], sx = x0 - 1 + x_hx[k];
-                if (unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws))
-                    off = uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + c0 + 8 * chunk[k]) * 2u;
-            }
+            const int base = u < PA_K ? br : is_y ? by : bs;  // wave-uniform: the piece's plane
+            // branch-free: dY / y pieces always load, halo pieces inside the image, pads and sinks never
+            const bool ok = kind[k] == 0 || (kind[k] == 1 && unsigned(y0 - 1 + x_hy[k]) < unsigned(a.hs) &&
+                                             unsigned(x0 - 1 + x_hx[k]) < unsigned(a.ws));
+            const uint32_t off = ok ? uint32_t(base + rel[k]) * 2u : kOOB;
             unsigned char *dst = u < NPC ? smem + slot * STAGE + u * 1024 : smem + NB * STAGE;
             if (u < PA_K)  // wave-uniform
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_rows, (__attribute__((address_space(3))) void *)dst, 16, off,
@@ -2180,9 +2203,8 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
     //       also store for the data grad.
     float *const cfx = reinterpret_cast<float *>(smem + NB * STAGE + kDmaSink);         // [seg][sc | sh][64]
     float *const cfr = reinterpret_cast<float *>(smem + NB * STAGE + kDmaSink + CFX);   // [seg][7][RBLK]
-    auto transform = [&](int pi, int slot_) {
-        const int img = pi / pimg, pr = pi - img * pimg;
-        const int y0 = patch_y0(pr, pw_n, ph_n, PH), x0 = patch_x0(pr, pw_n, ph_n, PW);
+    auto transform = [&](const Cursor &cur, int slot_) {
+        const int img = cur.img, y0 = cur.y0, x0 = cur.x0;
         if constexpr (XT) {
             const float *c_sc = cfx + (img / a.src_seg_imgs) * 128, *c_sh = c_sc + 64;
             unsigned char *const xp = smem + slot_ * STAGE + PA_K * 1024;
@@ -2276,9 +2298,13 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
 
     // the writer's dY stores of the previous transform are the youngest vector-memory operations at each wait
     const int wst = writer ? RCH : 0;
+    Cursor ci = cursor_at(pbeg), ct1 = ci;  // the next patch to issue; the patch the next transform forms
 #pragma unroll
     for (int k = 0; k < NB - 1; ++k)
-        if (pbeg + k < pend) issue(pbeg + k, k);
+        if (pbeg + k < pend) {
+            issue(ci, k);
+            advance(ci);
+        }
     if constexpr (TR) {  // patch pbeg transformed before the loop (its first barrier publishes it)
         if (pbeg < pend) {
             const int ahead = min(NB - 2, pend - 1 - pbeg);
@@ -2291,7 +2317,8 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
             else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_barrier();  // every wave's pieces of patch pbeg (and the coefficients) are in LDS
-            transform(pbeg, 0);
+            transform(ct1, 0);
+            advance(ct1);
         }
     }
     int slot = 0;
@@ -2321,9 +2348,15 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RCH) : "memory");
         }
         lds_barrier();  // every wave's pieces of patch pi landed; every wave left the slot of patch pi - 1
-        if (pi + NB - 1 < pend) issue(pi + NB - 1, slot == 0 ? NB - 1 : slot - 1);
+        if (pi + NB - 1 < pend) {
+            issue(ci, slot == 0 ? NB - 1 : slot - 1);
+            advance(ci);
+        }
         if constexpr (TR) {
-            if (pi + 1 < pend) transform(pi + 1, slot == NB - 1 ? 0 : slot + 1);
+            if (pi + 1 < pend) {
+                transform(ct1, slot == NB - 1 ? 0 : slot + 1);
+                advance(ct1);
+            }
         }
         const uint32_t bo = uint32_t(slot * STAGE);
         bf16x8 dv[3][NRB];
@@ -2727,7 +2760,8 @@ void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
     if (a.rows_y) {  // the caller checked wgrad16_rows_bn_ok
         if (wgrad16_planes(a.math, a.tune, bounded) == 4)
             w16_launch_rbn<4, false>(rb, a, grid, s);
-        else if (a.sb && !(a.tune & SCD_TUNE_WGRAD16_REGSTAGE) && (!a.src_scale || a.n_img_w / a.src_seg_imgs <= 2)) {
+        else if (SCD_WGRAD16_DMA_TRANSFORMS && a.sb && !(a.tune & SCD_TUNE_WGRAD16_REGSTAGE) &&
+                 (!a.src_scale || a.n_img_w / a.src_seg_imgs <= 2)) {
             // bf16 storage: the LDS-DMA ring with y and dL/da landed raw and dY formed in place (+ the source transform)
             if (rb == 128) {
                 if (a.src_scale)
@@ -2747,7 +2781,7 @@ void launch_wgrad_halo16_x3(const WgradArgs &a, dim3 grid, hipStream_t s) {
     switch (wgrad16_planes(a.math, a.tune, bounded)) {
         case 1:
             if (a.sb && lc && !(a.tune & SCD_TUNE_WGRAD16_REGSTAGE) &&
-                (!a.src_scale || a.n_img_w / a.src_seg_imgs <= 2)) {
+                (!a.src_scale || (SCD_WGRAD16_DMA_TRANSFORMS && a.n_img_w / a.src_seg_imgs <= 2))) {
                 // bf16 storage: the LDS-DMA ring (same residency as the register-staged kernel: one 512-thread block /
                 // two 256-thread blocks per CU, so the split plan is unchanged); a source transform in place
                 if (a.src_scale) {
