@@ -98,9 +98,12 @@ def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 16, find_unused_paramete
     of fp32 gradients, the decoder's 21 MB ready together, then down4 19 MB, down3 14 MB, ...) let the all-reduce of
     each bucket run on RCCL's stream while the shallower, costlier levels' backward continues; only the last bucket
     (the shallow levels, < 4 MB) is exposed.
-    `find_unused_parameters=None` turns DDP's unused-parameter search on only for a model that declares
-    parameters outside its forward graph (`params_outside_forward`).  Without it, the bucket holding such a
-    parameter is never reduced, the replicas drift apart and the next step raises.
+    Parameters a model declares outside its forward graph (`params_outside_forward`, e.g. the dual-task model's
+    outc_sem_change) are excluded from DDP (never bucketed, never reduced: they never get a gradient), so the default
+    `find_unused_parameters=None` runs without DDP's per-step unused-parameter search; without the exclusion, the
+    bucket holding such a parameter would never be reduced and the next step would raise.  (Until round 6 the search
+    was turned on for such models instead; with it dtsiamese's last bucket, ready 5 ms before the backward's end,
+    measured 17.9 MB: profiles/r06_rehearsal_2rank/.)
 
     Loss semantics.  Default (the throughput mode): every rank takes power_jaccard_loss over its own shard and DDP
     averages the gradients, i.e. the gradient of the MEAN of the per-shard losses.  The reference's nn.DataParallel
@@ -119,7 +122,13 @@ def wrap_ddp(wrapper, device=None, bucket_cap_mb: int = 16, find_unused_paramete
         return wrapper
     module = wrapper.module if hasattr(wrapper, 'module') else wrapper
     if find_unused_parameters is None:
-        find_unused_parameters = bool(params_outside_forward(module))
+        # parameters the model declares outside its forward (never a gradient) are left out of DDP's buckets, so no
+        # per-step unused-parameter search runs and the gradient buckets follow the readiness order of the others
+        outside = params_outside_forward(module)
+        ignore = [n for n, _ in module.named_parameters() if n.split('.')[0] in outside]
+        if ignore:
+            torch.nn.parallel.DistributedDataParallel._set_params_and_buffers_to_ignore_for_model(module, ignore)
+        find_unused_parameters = False
     ids = [device.index] if (device is not None and device.type == 'cuda') else None
     ddp = torch.nn.parallel.DistributedDataParallel(module, device_ids=ids, broadcast_buffers=True,
                                                     bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,

@@ -145,7 +145,8 @@ def _worker_spare(rank, world, port, out_dir):
     torch.manual_seed(0)
     model = OracleReplicaSpare(orc.deterministic_params(shapes, 5), orc.fresh_buffers(shapes))
     net = parallel.wrap_ddp(model, device=None)
-    assert net.find_unused_parameters
+    assert not net.find_unused_parameters  # the declared parameters are excluded from DDP instead
+    assert set(getattr(model, '_ddp_params_and_buffers_to_ignore', ())) == {'spare.weight', 'spare.bias'}
     opt = torch.optim.AdamW(net.parameters(), lr=1e-3, weight_decay=0.01)
     for step in range(2):  # the second step is where an unreduced bucket raises
         b = orc.synthetic_batch(CFG, PER_RANK, HW, parallel.rank_seed(11 + step, rank))
