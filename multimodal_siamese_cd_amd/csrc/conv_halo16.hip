@@ -2202,6 +2202,18 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
     //       backward of (y, dL/da) (bn_bwd_dy4, rounded once to bf16 as bn_bwd_apply stores it), which the writer blocks
     //       also store for the data grad.
     float *const cfx = reinterpret_cast<float *>(smem + NB * STAGE + kDmaSink);         // [seg][sc | sh][64]
+    // XT: this thread's 16-byte chunks of the X plane, by linear LDS position (chunk tid + i NT: consecutive lanes read
+    // and write consecutive 16 bytes, no bank conflicts): halo row / column and channel octet (-1: a row pad or past the
+    // plane), fixed for the kernel
+    constexpr int XTI = XT ? (PB / 16 + NT - 1) / NT : 1;
+    int xt_hy[XTI], xt_hx[XTI], xt_j[XTI];
+#pragma unroll
+    for (int i = 0; i < XTI; ++i) {
+        const int L = tid + i * NT, row = L / (RS / 16), col = L - row * (RS / 16);
+        xt_j[i] = (XT && L < PB / 16 && col < 8) ? col : -1;
+        xt_hy[i] = row / HW_;
+        xt_hx[i] = row - (row / HW_) * HW_;
+    }
     float *const cfr = reinterpret_cast<float *>(smem + NB * STAGE + kDmaSink + CFX);   // [seg][7][RBLK]
     auto transform = [&](const Cursor &cur, int slot_) {
         const int img = cur.img, y0 = cur.y0, x0 = cur.x0;
@@ -2209,14 +2221,12 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
             const float *c_sc = cfx + (img / a.src_seg_imgs) * 128, *c_sh = c_sc + 64;
             unsigned char *const xp = smem + slot_ * STAGE + PA_K * 1024;
 #pragma unroll
-            for (int i = 0; i < (HP * 8 + NT - 1) / NT; ++i) {
-                const int q = tid + i * NT;
-                if (q >= HP * 8) break;
-                const int hp = q >> 3, j = q & 7;
-                const int hy = hp / HW_, hx = hp - (hp / HW_) * HW_;
-                const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
-                if (unsigned(sy) >= unsigned(a.hs) || unsigned(sx) >= unsigned(a.ws)) continue;
-                u32x4 *const ptr = reinterpret_cast<u32x4 *>(xp + hp * RS + j * 16);
+            for (int i = 0; i < XTI; ++i) {
+                if (xt_j[i] < 0 || unsigned(y0 - 1 + xt_hy[i]) >= unsigned(a.hs) ||
+                    unsigned(x0 - 1 + xt_hx[i]) >= unsigned(a.ws))
+                    continue;  // a row pad, past the plane, or outside the image (the DMA's zeros stay)
+                const int j = xt_j[i];
+                u32x4 *const ptr = reinterpret_cast<u32x4 *>(xp + (tid + i * NT) * 16);
                 const u32x4 raw = *ptr;
                 u32x4 out;
 #pragma unroll
