@@ -1101,10 +1101,17 @@ bool bf16_1xn(const IgemmArgs &a) {
     return a.math == SCD_MATH_BF16 && (bool(a.sb) != bool(a.tune & SCD_TUNE_BF16_1XN));
 }
 
-// The 1 x N tiles in the bf16 arithmetic (fp32 or bf16 storage, double-buffered: one plane always fits).
+// The 1 x N tiles in the bf16 arithmetic (fp32 or bf16 storage).  Double-buffered halo on the tiles of 128 and more
+// channels; the 64-channel tiles (256 x 64, 128 x 64) single-buffered: there the second buffer cost resident blocks
+// (256 x 64: 41 KB per block, 3 blocks per CU; 5 single-buffered) and every block covers only two to eight 32-channel
+// chunks.  Round 6, tools/perf_conv.py bf16 storage: enc0b fwd 0.516 -> 0.459 ms, up1b 0.236 -> 0.203, enc1a data grad
+// 0.231 -> 0.198 single-buffered, while the 128-channel up3a forward lost 6% (profiles/r06_bf16_halo_db_study.txt).
+// SCD_TUNE_HALO16_DB_ON / _OFF force one choice for every tile.
 template <int WM, int WN, int TM, int TN, int OCC>
 void launch16_1xn_bf16(const IgemmArgs &a, int tw, hipStream_t s) {
-    if (halo16_db(a.tune, false))
+    const bool db = (a.tune & (SCD_TUNE_HALO16_DB_ON | SCD_TUNE_HALO16_DB_OFF)) ? halo16_db(a.tune, false) != 0
+                                                                                  : WN * TN * 16 >= 128;
+    if (db)
         launch16c<WM, WN, TM, TN, OCC, true, 1>(a, tw, s);
     else
         launch16c<WM, WN, TM, TN, OCC, false, 1>(a, tw, s);
