@@ -1106,6 +1106,8 @@ bool bf16_1xn(const IgemmArgs &a) {
 // (256 x 64: 41 KB per block, 3 blocks per CU; 5 single-buffered) and every block covers only two to eight 32-channel
 // chunks.  Round 6, tools/perf_conv.py bf16 storage: enc0b fwd 0.516 -> 0.459 ms, up1b 0.236 -> 0.203, enc1a data grad
 // 0.231 -> 0.198 single-buffered, while the 128-channel up3a forward lost 6% (profiles/r06_bf16_halo_db_study.txt).
+// Steps (one process, profiles/r06_bf16_halo_db_ab.txt): dual-stream bs=64 40.29 -> 39.75 ms, MMCR 56.94 -> 56.28,
+// bf16 Siamese 15.17 -> 15.02 (every tile single-buffered: 40.00, 56.49, 15.18).
 // SCD_TUNE_HALO16_DB_ON / _OFF force one choice for every tile.
 template <int WM, int WN, int TM, int TN, int OCC>
 void launch16_1xn_bf16(const IgemmArgs &a, int tw, hipStream_t s) {
