@@ -193,8 +193,8 @@ int scd_abi_version(void);
 #define SCD_TUNE_NO_HALO16_C16    (1u << 25)  /* input-layer forward on the per-tap x3 kernel                     */
 #define SCD_TUNE_NO_HALO          (1u << 26)  /* no halo kernels at all (per-tap kernels)                         */
 #define SCD_TUNE_HALO16_LATE_LOAD (1u << 27)  /* single-buffered halo16: next chunk's halo loaded at the last tap  */
-#define SCD_TUNE_H2_TILE64_128    (1u << 28)  /* h2, 64..127 outputs of 64-channel sources: 128 x 64 tiles instead
-                                                 of 256 x 64 (2x2 waves of 128 px x 32 ch)                          */
+#define SCD_TUNE_H2_TILE64_128    (1u << 28)  /* 64..127 outputs of 64-channel sources (h2, bf16 storage): 128 x 64
+                                                 tiles instead of 256 x 64 (2x2 waves of 128 px x 32 ch)             */
 #define SCD_TUNE_HALO16_WS        (1u << 29)  /* h2 1 x N tiles as warp-specialized blocks: one producer wave stages
                                                  the halo, the compute waves load only weights (128 px tiles)        */
 #define SCD_TUNE_WGRAD16_REGSTAGE (1u << 30)  /* bf16-storage halo weight grad staged through registers, one patch in

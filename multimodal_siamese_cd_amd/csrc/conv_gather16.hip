@@ -236,35 +236,46 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
         buf ^= 1;
     }
 
-    // h2: undo the operand scales (powers of two: exact); add the bias, store 4 channels per lane
+    // h2: undo the operand scales (powers of two: exact); add the bias, store 4 channels per lane.  A lane's pixel
+    // addresses depend on i only (store_mode 1: the upsampled pixel (2y, 2x); tap (di, dj) of channel tile j adds
+    // di rows + dj pixels), so they are formed once per i, not once per (i, j).
+    constexpr uint32_t EB = SB ? 2u : 4u;
+    size_t e_pix[TM];  // element offset of pixel tile i's pixel (store_mode 1: of its (2y, 2x) pixel)
+    bool m_ok[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * WPX + i * 16 + l16;
+        m_ok[i] = m < a.M;
+        size_t pix = size_t(m);
+        if (a.store_mode == 1) {
+            const uint32_t mm = m_ok[i] ? uint32_t(m) : 0u;
+            const uint32_t img = fdiv(mm, a.div_hw);
+            const uint32_t r = mm - img * uint32_t(a.ho * a.wo);
+            const uint32_t oy = fdiv(r, a.div_w);
+            const uint32_t ox = r - oy * uint32_t(a.wo);
+            pix = size_t(int(img) * a.dst_h + 2 * int(oy)) * a.dst_w + 2 * int(ox);
+        }
+        e_pix[i] = pix * a.ldc_d;
+    }
+    unsigned char *const dst_b = reinterpret_cast<unsigned char *>(a.dst);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * WCH + j * 16 + 4 * g;
         if (n >= a.n_out) continue;  // n_out % 4 == 0: a lane's 4 channels are all in or all out
         const int nl = wn * WCH + j * 16 + 4 * g;
         const f32x4 sc = *reinterpret_cast<const f32x4 *>(&ep_sc[tpar][nl]);
-        int oc = n, di = 0, dj = 0;
+        size_t e_j = size_t(n);  // element offset of channel tile j within a pixel tile's row
         if (a.store_mode == 1) {
             const int ij = n / a.cout;
-            oc = n - ij * a.cout;
-            di = ij >> 1;
-            dj = ij & 1;
+            const int oc = n - ij * a.cout, di = ij >> 1, dj = ij & 1;
+            e_j = size_t(di * a.dst_w + dj) * a.ldc_d + oc;
         }
         const f32x4 b4 = *reinterpret_cast<const f32x4 *>(&ep_b[tpar][nl]);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-            const int m = m0 + wm * WPX + i * 16 + l16;
-            if (m >= a.M) continue;
+            if (!m_ok[i]) continue;
             const f32x4 v = acc[j][i] * sc + b4;
-            size_t pix = size_t(m);
-            if (a.store_mode == 1) {
-                const uint32_t img = fdiv(uint32_t(m), a.div_hw);
-                const uint32_t r = uint32_t(m) - img * uint32_t(a.ho * a.wo);
-                const uint32_t oy = fdiv(r, a.div_w);
-                const uint32_t ox = r - oy * uint32_t(a.wo);
-                pix = size_t(int(img) * a.dst_h + 2 * int(oy) + di) * a.dst_w + 2 * int(ox) + dj;
-            }
-            store_q<SB>(a.dst, pix * a.ldc_d + oc, v);
+            store_qb<SB>(dst_b + (e_pix[i] + e_j) * EB, v);
             omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
         }
     }

@@ -35,6 +35,36 @@ __device__ __forceinline__ float row16_sum(float x) {
     return x;
 }
 
+// row16_sum of the four components of v, bit-identical to four row16_sum calls (x + perm(x) is perm(x) + x).  The
+// four chains are interleaved in one asm block so each DPP add reads a value written four VALU instructions earlier
+// (the DPP read-after-VALU-write hazard needs two wait states; the leading s_nop covers the producers of v).  Written
+// out because, on vector inputs, the compiler packs the four chains' adds into v_pk_add_f32 and can then no longer
+// fold each DPP move into its add: 2.5 instructions per step instead of one.
+__device__ __forceinline__ f32x4 row16_sum4(f32x4 v) {
+    float a, b, c, d;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %0, %4, %4 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %5, %5 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %6, %6 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %3, %7, %7 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %3, %3, %3 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %3, %3, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %2, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %3, %3, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+    return f32x4{a, b, c, d};
+}
+
 __device__ __forceinline__ void gstore4(float *p, f32x4 v) { *(__attribute__((address_space(1))) f32x4 *)(p) = v; }
 
 // WAVES_M x WAVES_N waves; a wave computes TM*16 pixels x TN*16 channels (TM x TN MFMA tiles).
@@ -489,19 +519,29 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         bias4[j] = (a.bias && n < a.n_out) ? *reinterpret_cast<const f32x4 *>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     float omax = 0.f;  // max |stored value| of this lane (dst_bound)
+    // 16-wide tiles: pixel tile i of the wave is output row y0 + (wm WPX) / 16 + i, column x0 + l16, so a lane's
+    // addresses are one base plus i rows plus 16 j channels (one 64-bit multiply per lane instead of one per tile;
+    // the 64-bit index products had made the epilogue the kernel's largest VALU block on the K = 576 layers)
+    const int nq = n0 + wn * WCH + 4 * g;  // the lane's first channel (tile j adds 16 j)
+    auto row_pix = [&](int i) -> size_t {  // output pixel of pixel tile i of this lane
+        const int p = wm * WPX + i * 16 + l16;
+        return size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+    };
+    unsigned char *const dst_b = reinterpret_cast<unsigned char *>(a.dst);
+    const size_t d_row = size_t(a.wo) * a.ldc_d * EB;  // TW == 16: bytes from pixel tile i to i + 1
+    unsigned char *d_p = dst_b + (row_pix(0) * a.ldc_d + nq) * EB;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-        const int p = wm * WPX + i * 16 + l16;
-        const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+        if constexpr (TW != 16) d_p = dst_b + (row_pix(i) * a.ldc_d + nq) * EB;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wn * WCH + j * 16 + 4 * g;
-            if (n < a.n_out) {
-                const f32x4 v = store_q<SB>(a.dst, pix * a.ldc_d + n, acc[j][i] + bias4[j]);
+            if (nq + j * 16 < a.n_out) {
+                const f32x4 v = store_qb<SB>(d_p + j * 16 * EB, acc[j][i] + bias4[j]);
                 if constexpr (SB) acc[j][i] = v;  // the statistics / BN-backward sums see the stored values
                 omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
             }
         }
+        if constexpr (TW == 16) d_p += d_row;
     }
     if constexpr (SB) {
 #pragma unroll
@@ -509,45 +549,50 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
     }
     if (a.dst_bound) wave_max_bound(a.dst_bound, fmaxf(omax, bound_seed(a)));  // uniform: every lane of the wave takes part
 
+    // The epilogue reductions below run on channel quads (f32x4: the adds, multiplies and fmas issue as packed
+    // two-float instructions); every component follows the scalar order of bn_bwd_partial / the statistics merge, so
+    // the records are unchanged.  The stored value of tile (j, i): acc + bias (bf16 storage: acc already holds it, and
+    // x + 0 would only turn -0 into +0, which neither a sum nor a squared deviation can see).
+    auto stored = [&](int j, int i) -> f32x4 {
+        if constexpr (SB)
+            return acc[j][i];
+        else
+            return acc[j][i] + bias4[j];
+    };
     // Fused BatchNorm statistics of this tile (BM pixels of one image) per channel: mean, then M2 about it.
     if (a.stat_rec) {
         float *red1 = reinterpret_cast<float *>(smem);  // [WME][BN] sums
         float *red2 = red1 + WME * BN;                  // [WME][BN] M2
-        float mean[TN][4];
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int q = 0; q < RG; ++q) {
+                f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int q = 0; q < RG; ++q) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int i = q * TMG; i < (q + 1) * TMG; ++i) s += acc[j][i][r] + bias4[j][r];
-                    s = row16_sum(s);
-                    if (l16 == 0) red1[(wm * RG + q) * BN + wn * WCH + j * 16 + 4 * g + r] = s;
-                }
+                for (int i = q * TMG; i < (q + 1) * TMG; ++i) s4 += stored(j, i);
+                const f32x4 t = row16_sum4(s4);
+                if (l16 == 0) *reinterpret_cast<f32x4 *>(&red1[(wm * RG + q) * BN + wn * WCH + j * 16 + 4 * g]) = t;
+            }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TN; ++j) {
+            const int nl = wn * WCH + j * 16 + 4 * g;
+            f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int nl = wn * WCH + j * 16 + 4 * g + r;
-                float s = 0.f;
+            for (int w = 0; w < WME; ++w) s4 += *reinterpret_cast<const f32x4 *>(&red1[w * BN + nl]);
+            const f32x4 mean4 = s4 * (1.f / float(BM));
 #pragma unroll
-                for (int w = 0; w < WME; ++w) s += red1[w * BN + nl];
-                mean[j][r] = s * (1.f / float(BM));
+            for (int qg = 0; qg < RG; ++qg) {
+                f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int qg = 0; qg < RG; ++qg) {
-                    float q = 0.f;
-#pragma unroll
-                    for (int i = qg * TMG; i < (qg + 1) * TMG; ++i) {
-                        const float d = (acc[j][i][r] + bias4[j][r]) - mean[j][r];
-                        q = fmaf(d, d, q);
-                    }
-                    q = row16_sum(q);
-                    if (l16 == 0) red2[(wm * RG + qg) * BN + nl] = q;
+                for (int i = qg * TMG; i < (qg + 1) * TMG; ++i) {
+                    const f32x4 d = stored(j, i) - mean4;
+                    q4 = __builtin_elementwise_fma(d, d, q4);
                 }
+                const f32x4 t = row16_sum4(q4);
+                if (l16 == 0) *reinterpret_cast<f32x4 *>(&red2[(wm * RG + qg) * BN + nl]) = t;
             }
+        }
         __syncthreads();
         for (int nl = tid; nl < BN; nl += NT) {
             if (n0 + nl >= a.n_out) continue;
@@ -569,9 +614,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         float *red1 = reinterpret_cast<float *>(smem);  // [WME][BN]
         float *red2 = red1 + WME * BN;
         const int co = (img / a.bb_seg_imgs) * a.n_out;
+        const unsigned char *const y_b = reinterpret_cast<const unsigned char *>(a.bb_y);
+        const size_t y_row = size_t(a.wo) * a.bb_ldy * EB;  // TW == 16: as the stores above
+        const unsigned char *const y_p0 = y_b + (row_pix(0) * a.bb_ldy + nq) * EB;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wn * WCH + j * 16 + 4 * g;
+            const int n = nq + j * 16;
             const bool nok = n < a.n_out;
             const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
             const f32x4 mu = nok ? gload4(a.bb_mean + co + n) : z4, iv = nok ? gload4(a.bb_inv + co + n) : z4;
@@ -581,23 +629,20 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
                 f32x4 s1 = z4, s2 = z4;
 #pragma unroll
                 for (int i = qg * TMG; i < (qg + 1) * TMG; ++i) {
-                    const int p = wm * WPX + i * 16 + l16;
-                    const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
-                    const f32x4 y4 = nok ? load_q<SB>(a.bb_y, pix * a.bb_ldy + n) : z4;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float dz = fmaf(y4[r], sc[r], sf[r]) > 0.f ? acc[j][i][r] : 0.f;
-                        s1[r] += dz;
-                        s2[r] += dz * ((y4[r] - mu[r]) * iv[r]);
-                    }
+                    const unsigned char *const yp = TW == 16 ? y_p0 + size_t(i) * y_row + j * 16 * EB
+                                                             : y_b + (row_pix(i) * a.bb_ldy + n) * EB;
+                    const f32x4 y4 = nok ? load_qb<SB>(yp) : z4;
+                    const f32x4 t = __builtin_elementwise_fma(y4, sc, sf);  // the forward's exact ReLU test
+                    const f32x4 dz = {t[0] > 0.f ? acc[j][i][0] : 0.f, t[1] > 0.f ? acc[j][i][1] : 0.f,
+                                      t[2] > 0.f ? acc[j][i][2] : 0.f, t[3] > 0.f ? acc[j][i][3] : 0.f};
+                    s1 += dz;
+                    s2 = __builtin_elementwise_fma(dz, (y4 - mu) * iv, s2);  // s2 += dz * xhat, contracted
                 }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float t1 = row16_sum(s1[r]), t2 = row16_sum(s2[r]);
-                    if (l16 == 0) {
-                        red1[(wm * RG + qg) * BN + wn * WCH + j * 16 + 4 * g + r] = t1;
-                        red2[(wm * RG + qg) * BN + wn * WCH + j * 16 + 4 * g + r] = t2;
-                    }
+                const f32x4 t1 = row16_sum4(s1);
+                const f32x4 t2 = row16_sum4(s2);
+                if (l16 == 0) {
+                    *reinterpret_cast<f32x4 *>(&red1[(wm * RG + qg) * BN + wn * WCH + j * 16 + 4 * g]) = t1;
+                    *reinterpret_cast<f32x4 *>(&red2[(wm * RG + qg) * BN + wn * WCH + j * 16 + 4 * g]) = t2;
                 }
             }
         }
@@ -1162,6 +1207,8 @@ int halo16_pick(const IgemmArgs &a, bool eligible, int *bm, int *tw) {
         // 128 x 64 at 3 waves/SIMD: +3..9% on the 64-channel layers
         // h2 on 1 x 2 waves; 64-channel sources (K = 576, two 32-channel chunks) on the 256 x 64 tile of 2 x 2 such
         // waves (enc0b fwd / dgrad -4..-5%, up2b -2%; 128- and 256-channel sources measured neutral or slower)
+        // (bf16 storage too: the 128 x 64 tile ran its layers 10-14% faster in isolation but the step 0.6% slower,
+        // profiles/r06_bf16_tile64_study.txt)
         id = ((wide_1xn_ok(a) && h2_tile64(a.tune)) || bf16_1xn(a))
                  ? ((a.c == 64 && !(a.tune & SCD_TUNE_H2_TILE64_128)) ? 5 : 4)
                  : 1;
@@ -1436,56 +1483,61 @@ __global__ __launch_bounds__(256, 2) void igemm_halo16_c16(IgemmArgs a) {
                 for (int i = 0; i < TM; ++i) acc[j][i] *= sc;
             }
         }
-        // acc[j][i][r]: channel n0 + wn*WCH + 16j + 4g + r, pixel wm*WPX + 16i + l16
+        // acc[j][i][r]: channel n0 + wn*WCH + 16j + 4g + r, pixel wm*WPX + 16i + l16 (igemm_halo16_x3's epilogue:
+        // 16-wide tiles address pixel tile i as one base plus i rows; channel-quad reductions, same order)
+        const int nq = n0 + wn * WCH + 4 * g;
+        auto row_pix = [&](int i) -> size_t {
+            const int p = wm * WPX + i * 16 + l16;
+            return size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+        };
+        unsigned char *const dst_b = reinterpret_cast<unsigned char *>(a.dst);
+        const size_t d_row = size_t(a.wo) * a.ldc_d * EB;
+        unsigned char *d_p = dst_b + (row_pix(0) * a.ldc_d + nq) * EB;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-            const int p = wm * WPX + i * 16 + l16;
-            const size_t pix = size_t(img * a.ho + y0 + p / TW) * a.wo + x0 + (p % TW);
+            if constexpr (TW != 16) d_p = dst_b + (row_pix(i) * a.ldc_d + nq) * EB;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int n = n0 + wn * WCH + j * 16 + 4 * g;
-                if (n < a.n_out) {
-                    const f32x4 v = store_q<SB>(a.dst, pix * a.ldc_d + n, acc[j][i] + bias4[j]);
+                if (nq + j * 16 < a.n_out) {
+                    const f32x4 v = store_qb<SB>(d_p + j * 16 * EB, acc[j][i] + bias4[j]);
                     if constexpr (SB) acc[j][i] = v;  // statistics of the stored values
                     omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
                 }
             }
+            if constexpr (TW == 16) d_p += d_row;
         }
-        if constexpr (SB) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};  // already in acc
-        }
+        auto stored = [&](int j, int i) -> f32x4 {  // bf16 storage: acc holds the stored value (see igemm_halo16_x3)
+            if constexpr (SB)
+                return acc[j][i];
+            else
+                return acc[j][i] + bias4[j];
+        };
         if (a.stat_rec) {  // as igemm_halo16_x3: tile mean, then M2 about it
-            float mean[TN][4];
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
+            for (int j = 0; j < TN; ++j) {
+                f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float sm = 0.f;
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) sm += acc[j][i][r] + bias4[j][r];
-                    sm = row16_sum(sm);
-                    if (l16 == 0) red1[wm * BN + wn * WCH + j * 16 + 4 * g + r] = sm;
-                }
+                for (int i = 0; i < TM; ++i) s4 += stored(j, i);
+                const f32x4 t = row16_sum4(s4);
+                if (l16 == 0) *reinterpret_cast<f32x4 *>(&red1[wm * BN + wn * WCH + j * 16 + 4 * g]) = t;
+            }
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
+            for (int j = 0; j < TN; ++j) {
+                const int nl = wn * WCH + j * 16 + 4 * g;
+                f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int nl = wn * WCH + j * 16 + 4 * g + r;
-                    float sm = 0.f;
+                for (int w = 0; w < WAVES_M; ++w) s4 += *reinterpret_cast<const f32x4 *>(&red1[w * BN + nl]);
+                const f32x4 mean4 = s4 * (1.f / float(BM));
+                f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int w = 0; w < WAVES_M; ++w) sm += red1[w * BN + nl];
-                    mean[j][r] = sm * (1.f / float(BM));
-                    float q = 0.f;
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) {
-                        const float d = (acc[j][i][r] + bias4[j][r]) - mean[j][r];
-                        q = fmaf(d, d, q);
-                    }
-                    q = row16_sum(q);
-                    if (l16 == 0) red2[wm * BN + nl] = q;
+                for (int i = 0; i < TM; ++i) {
+                    const f32x4 d = stored(j, i) - mean4;
+                    q4 = __builtin_elementwise_fma(d, d, q4);
                 }
+                const f32x4 t = row16_sum4(q4);
+                if (l16 == 0) *reinterpret_cast<f32x4 *>(&red2[wm * BN + nl]) = t;
+            }
             __syncthreads();
             for (int nl = tid; nl < BN; nl += NT) {
                 if (n0 + nl >= a.n_out) continue;

@@ -157,6 +157,25 @@ __device__ __forceinline__ f32x4 store_q(float *dst, size_t e, f32x4 v) {
         return v;
     }
 }
+// store_q / load_q at a byte address (the epilogues' incrementally formed row addresses)
+template <bool SB>
+__device__ __forceinline__ f32x4 store_qb(unsigned char *p, f32x4 v) {
+    if constexpr (SB) {
+        const u32x2 pk = pk_bf16x4(v);
+        gstore2u(p, pk);
+        return unpk_bf16x4(pk);
+    } else {
+        *(__attribute__((address_space(1))) f32x4 *)(p) = v;
+        return v;
+    }
+}
+template <bool SB>
+__device__ __forceinline__ f32x4 load_qb(const unsigned char *p) {
+    if constexpr (SB)
+        return unpk_bf16x4(*(const __attribute__((address_space(1))) u32x2 *)(p));
+    else
+        return *(const __attribute__((address_space(1))) f32x4 *)(p);
+}
 template <bool SB>
 __device__ __forceinline__ f32x4 load_q(const float *src, size_t e) {
     if constexpr (SB)
