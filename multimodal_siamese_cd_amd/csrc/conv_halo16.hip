@@ -180,16 +180,33 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 
     uint32_t a_boff[A_PER];
     int a_off[A_PER];
+    {
+        // this thread's pieces: halo pixel (tid >> 3) + i NT / 8, channel piece tid & 7 (NT % 8 == 0).  The halo
+        // position and byte offset advance by a constant step per piece (one compare for the row wrap), instead of
+        // a division and three 32-bit products per piece
+        static_assert(NT % 8 == 0, "a thread's pieces share one channel piece");
+        constexpr int S = NT / 8, DQ = S / HWD, DR = S % HWD;
+        const int col = tid & 7;
+        int hy = (tid >> 3) / HWD, hx = (tid >> 3) - ((tid >> 3) / HWD) * HWD;
+        const int pix_b = a.ldc_s * int(EB), row_b = a.ws * pix_b;
+        // byte offset of halo pixel (0, 0) = source pixel (y0 - 1, x0 - 1), channel piece col (may wrap below zero:
+        // only in-range pieces use the sum, whose true value fits)
+        const uint32_t base = uint32_t(((img * a.hs + y0 - 1) * a.ws + x0 - 1) * a.ldc_s + col * 4) * EB;
+        int off = hy * row_b + hx * pix_b;
+        const int step = DQ * row_b + DR * pix_b, wrap = row_b - HWD * pix_b;
 #pragma unroll
-    for (int i = 0; i < A_PER; ++i) {
-        const int e = tid + i * NT;
-        const bool in = e < A_CH;
-        const int hp = in ? (e >> 3) : 0, col = e & 7;
-        const int hy = hp / HWD, hx = hp - (hp / HWD) * HWD;
-        const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
-        const bool ok = in && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
-        a_boff[i] = ok ? uint32_t(((img * a.hs + sy) * a.ws + sx) * a.ldc_s + col * 4) * EB : kOOB;
-        a_off[i] = in ? soff(hy * HWP + hx, col) : -1;
+        for (int i = 0; i < A_PER; ++i) {
+            const bool in = tid + i * NT < A_CH;
+            const int sy = y0 - 1 + hy, sx = x0 - 1 + hx;
+            const bool ok = in && unsigned(sy) < unsigned(a.hs) && unsigned(sx) < unsigned(a.ws);
+            a_boff[i] = ok ? base + uint32_t(off) : kOOB;
+            a_off[i] = in ? soff(hy * HWP + hx, col) : -1;
+            hx += DR;
+            const bool w = hx >= HWD;  // selects, not a branch
+            hx = w ? hx - HWD : hx;
+            hy += DQ + int(w);
+            off += step + (w ? wrap : 0);
+        }
     }
     // Weight fragments from the 32-row fragment-major split (scd_split_bf16x3_frag): the 16 rows x 8 k of
     // one 16-lane group are 256 contiguous bytes of a 1 KB 32x16 fragment.
