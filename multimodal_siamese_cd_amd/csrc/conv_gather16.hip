@@ -276,7 +276,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_gather16(IgemmArgs a)
             if (!m_ok[i]) continue;
             const f32x4 v = acc[j][i] * sc + b4;
             store_qb<SB>(dst_b + (e_pix[i] + e_j) * EB, v);
-            omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+            if (a.dst_bound)  // uniform; no bound in the bf16 arithmetic
+                omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
         }
     }
     if (!has_next) break;

@@ -535,7 +535,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
         const int n = n0 + wn * WCH + j * 16 + 4 * g;
         bias4[j] = (a.bias && n < a.n_out) ? *reinterpret_cast<const f32x4 *>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    float omax = 0.f;  // max |stored value| of this lane (dst_bound)
     // 16-wide tiles: pixel tile i of the wave is output row y0 + (wm WPX) / 16 + i, column x0 + l16, so a lane's
     // addresses are one base plus i rows plus 16 j channels (one 64-bit multiply per lane instead of one per tile;
     // the 64-bit index products had made the epilogue the kernel's largest VALU block on the K = 576 layers)
@@ -555,7 +554,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
             if (nq + j * 16 < a.n_out) {
                 const f32x4 v = store_qb<SB>(d_p + j * 16 * EB, acc[j][i] + bias4[j]);
                 if constexpr (SB) acc[j][i] = v;  // the statistics / BN-backward sums see the stored values
-                omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
             }
         }
         if constexpr (TW == 16) d_p += d_row;
@@ -564,18 +562,30 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, OCC) void igemm_halo16_x3(I
 #pragma unroll
         for (int j = 0; j < TN; ++j) bias4[j] = f32x4{0.f, 0.f, 0.f, 0.f};  // already in acc
     }
-    if (a.dst_bound) wave_max_bound(a.dst_bound, fmaxf(omax, bound_seed(a)));  // uniform: every lane of the wave takes part
-
-    // The epilogue reductions below run on channel quads (f32x4: the adds, multiplies and fmas issue as packed
-    // two-float instructions); every component follows the scalar order of bn_bwd_partial / the statistics merge, so
-    // the records are unchanged.  The stored value of tile (j, i): acc + bias (bf16 storage: acc already holds it, and
-    // x + 0 would only turn -0 into +0, which neither a sum nor a squared deviation can see).
+    // The stored value of tile (j, i): acc + bias (bf16 storage: acc already holds it, and x + 0 would only turn -0
+    // into +0, which neither a sum, a squared deviation nor a magnitude can see).
     auto stored = [&](int j, int i) -> f32x4 {
         if constexpr (SB)
             return acc[j][i];
         else
             return acc[j][i] + bias4[j];
     };
+    if (a.dst_bound) {  // uniform: every lane of the wave takes part; skipped where no consumer needs a bound (bf16)
+        float omax = 0.f;  // max |stored value| of this lane
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                if (nq + j * 16 < a.n_out) {
+                    const f32x4 v = stored(j, i);
+                    omax = fmaxf(omax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+                }
+        wave_max_bound(a.dst_bound, fmaxf(omax, bound_seed(a)));
+    }
+
+    // The epilogue reductions below run on channel quads (f32x4: the adds, multiplies and fmas issue as packed
+    // two-float instructions); every component follows the scalar order of bn_bwd_partial / the statistics merge, so
+    // the records are unchanged.
     // Fused BatchNorm statistics of this tile (BM pixels of one image) per channel: mean, then M2 about it.
     if (a.stat_rec) {
         float *red1 = reinterpret_cast<float *>(smem);  // [WME][BN] sums
@@ -2346,7 +2356,7 @@ __global__ __launch_bounds__(256 * RG, 2 / RG) void wgrad_halo16_dma(WgradArgs a
                     const u32x2 pk = pk_bf16x4(dv);
                     out[2 * h] = pk[0];
                     out[2 * h + 1] = pk[1];
-                    if (writer) {
+                    if (writer && a.rows_out_bound) {  // (no bound in the bf16 arithmetic)
                         const f32x4 r = unpk_bf16x4(pk);
                         omax = fmaxf(omax, fmaxf(fmaxf(fabsf(r[0]), fabsf(r[1])), fmaxf(fabsf(r[2]), fabsf(r[3]))));
                     }
